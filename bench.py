@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident encode+decode GiB/s of liberasurecode_rs_vand on MI355X.
+
+One step = one pass of the hot path over one batch: RS(k=10, m=4) encode of S stripes of 1 MiB
+fragments (BASELINE.json configs[2], "C3"), then decode of the same S stripes with data fragments
+{0,1,2,3} erased (every rebuilt fragment needs a full 10-term GF(2^16) dot product).  Inputs are
+resident in HBM before the timed region.  value = object bytes (2 * S * k * F per step per GPU,
+summed over GPUs) / wall time of the K timed steps (max over ranks), in GiB/s.
+
+Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent, each rank owns
+its own S stripes (weak scaling) and there is no data-path collective -- the process group is used
+for the start barrier and the max-over-ranks of the elapsed time only.
+
+Extra fields: "roofline" (gf16_apply_kernel, HIP-event timed per launch on the launch stream) and
+"cpu_baseline" (the oracle restatement of the same algorithm on the host cores; rank 0 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (before libecamd: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from liberasurecode_amd import device as D  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+
+CONFIGS = {
+    # name: (k, m, fragment bytes, stripes per GPU, decode erasures, description)
+    "c3": (10, 4, 1 << 20, 256, [0, 1, 2, 3],
+           "C3 liberasurecode_rs_vand k=10 m=4, 1 MiB fragments, encode + decode(4 data missing)"),
+    "c2": (4, 2, 64 << 10, 4096, [0, 1],
+           "C2 liberasurecode_rs_vand k=4 m=2, 64 KiB fragments, encode + decode(2 data missing)"),
+    "c5": (20, 8, 4 << 20, 32, list(range(8)),
+           "C5 liberasurecode_rs_vand k=20 m=8, 4 MiB fragments, encode + decode(8 data missing)"),
+}
+
+
+def cpu_baseline(k, m, F, missing, threads, stripes):
+    """The oracle (same log/antilog algorithm as the reference) on `threads` host cores."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as orc
+    from ecdata import stripe_fragments
+
+    lib = orc.lib()
+    G = orc.ints(orc.generator(k, m))
+    miss = orc.ints(list(missing) + [-1])
+
+    def job(t, count):
+        data = stripe_fragments(t, k, F)
+        frags = [np.array(x) for x in data] + [np.zeros(F, np.uint8) for _ in range(m)]
+        dp, pp = orc.ptr_array(frags[:k]), orc.ptr_array(frags[k:])
+        n = 0
+        t0 = time.perf_counter()
+        for _ in range(count):
+            lib.orc_rs_encode(G, dp, pp, k, m, F)
+            lib.orc_rs_decode(G, dp, pp, k, m, miss, F, 1)
+            n += 1
+        return n, time.perf_counter() - t0
+
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(job, range(threads), [1] * threads))  # warm (allocations, page faults)
+        t0 = time.perf_counter()
+        res = list(ex.map(job, range(threads), [stripes] * threads))
+        wall = time.perf_counter() - t0
+    total = sum(n for n, _ in res)
+    return {"value": round(2 * total * k * F / GIB / wall, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{total} stripes x (encode + decode {list(missing)}) of k={k} m={m} F={F} "
+                      f"on {threads} threads (oracle/ec_oracle.c log/antilog tables, -O2)",
+            "cpu_seconds": round(sum(t for _, t in res), 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-stripes", type=int, default=8, help="stripes per CPU thread")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    k, m, F, S, missing, desc = CONFIGS[args.config]
+    if args.stripes:
+        S = args.stripes
+    assert D.available(), "no HIP device"
+    lay = D.Layout.alloc(k + m, F, S)
+    stream = D.Stream()
+    lay.fill_splitmix(nfrags=k, stripe0=rank * S, stream=stream)
+    D.rs_encode(k, m, lay, stream=stream)
+    stream.synchronize()
+
+    ev = [(D.Event(), D.Event(), D.Event()) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        D.rs_encode(k, m, lay, stream=stream)
+        if i is not None:
+            ev[i][1].record(stream)
+        D.rs_decode(k, m, missing, lay, stream=stream)
+        if i is not None:
+            ev[i][2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+
+    def barrier():
+        D.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    D.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+
+    enc_ms = [a.elapsed_ms(b) for a, b, _ in ev]
+    dec_ms = [b.elapsed_ms(c) for _, b, c in ev]
+    obj_bytes = S * k * F  # object bytes per stripe batch per GPU
+    value = 2 * obj_bytes * args.steps * world / GIB / elapsed
+    # dominant kernel: gf16_apply_kernel<4> (encode: 10 in, 4 out; decode: 10 in, 4 out)
+    launch_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
+    # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
+    algo_bytes = S * (2 * k + m + len(missing)) * F // 2
+    achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": "device-resident encode+decode GiB/s (RS k=10 m=4, 1 MiB frags), 1/2/4/8 GPU"
+            if args.config == "c3" else f"device-resident encode+decode GiB/s ({desc})",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16 (GF(2^16) words)",
+            "data": "synthetic (splitmix64 fragments generated in HBM)",
+            "config": {"workload": desc, "k": k, "m": m, "fragment_bytes": F,
+                       "stripes_per_gpu": S, "decode_missing": missing,
+                       "parallelism": f"stripe-sharded x{world} (no data-path collective)"},
+            "encode_gibs_per_gpu": round(obj_bytes / GIB / (sum(enc_ms) / len(enc_ms) / 1e3), 3),
+            "decode_gibs_per_gpu": round(obj_bytes / GIB / (sum(dec_ms) / len(dec_ms) / 1e3), 3),
+            "roofline": {"bound": "hbm", "kernel": "gf16_apply_kernel<4,false>",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "launch_ms": round(launch_ms, 4),
+                         "algorithmic_bytes_per_launch": algo_bytes},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(k, m, F, missing, args.cpu_threads,
+                                               args.cpu_stripes)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

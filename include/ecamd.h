@@ -1,0 +1,109 @@
+/*
+ * ecamd.h -- MI355X device-resident erasure-code engine (libecamd.so), C ABI.
+ *
+ * This is the batched extension the reference does not have ("B2 ... A batched,
+ * device-pointer extension API is new"): S independent stripes whose fragments already live in
+ * HBM are encoded / decoded / reconstructed by one kernel launch.  The per-call drop-in ABIs of
+ * the reference (liberasurecode_rs_vand.h, xor_code.h, erasurecode.h) are layered on top of it.
+ *
+ * All pointers named d_* are device pointers; `stream` is a hipStream_t (NULL = default stream).
+ * Calls are asynchronous on `stream` unless stated.  Every entry point returns 0 on success and a
+ * negative value on failure (ecamd_last_error() gives the reason).  There is no CPU fallback: with
+ * no HIP device every call fails with ECAMD_ENODEV.
+ *
+ * Fragment layout ("strided"): fragment f of stripe s starts at
+ *     base + s * stripe_stride + f * frag_stride
+ * so both [S][k+m][F] (frag_stride = F, stripe_stride = (k+m)*F) and fragment-major
+ * [k+m][S][F] layouts are expressible.  base, strides and offsets must be 16-byte aligned;
+ * blocksize (bytes per fragment payload) may be any value >= 1.
+ */
+#ifndef ECAMD_H
+#define ECAMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECAMD_ENODEV (-19)
+#define ECAMD_EINVAL (-22)
+#define ECAMD_ENOMEM (-12)
+#define ECAMD_EHIP (-5)
+
+/* 0 if a HIP device is usable, ECAMD_ENODEV otherwise. */
+int ecamd_init(void);
+int ecamd_device_count(void);
+const char *ecamd_last_error(void);
+
+/* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
+typedef struct ecamd_map ecamd_map;
+
+/* Prepare the R x K coefficient matrix for the current device (split tables in HBM). */
+int ecamd_map_create(const int *coeff, int R, int K, ecamd_map **out);
+void ecamd_map_destroy(ecamd_map *map);
+
+/* Input j of stripe s at in_base + s*in_stripe_stride + in_off[j] (K host-side offsets), output r
+ * at out_base + s*out_stripe_stride + out_off[r] (R offsets). */
+int ecamd_map_apply_strided(const ecamd_map *map, const void *in_base, int64_t in_stripe_stride,
+                            const int64_t *in_off, void *out_base, int64_t out_stripe_stride,
+                            const int64_t *out_off, int64_t blocksize, int nstripes, void *stream);
+
+/* Pointer tables in device memory: input j of stripe s is d_in_ptrs[s*in_row + in_col[j]],
+ * output r is d_out_ptrs[s*out_row + out_col[r]] (in_col / out_col are host arrays). */
+int ecamd_map_apply_ptrs(const ecamd_map *map, const void *const *d_in_ptrs, int in_row,
+                         const int *in_col, void *const *d_out_ptrs, int out_row,
+                         const int *out_col, int64_t blocksize, int nstripes, void *stream);
+
+/* ---- GF(2) (flat XOR) fragment maps: outputs[r] = XOR of inputs j with bit j of mask[r] ---- */
+int ecamd_xor_apply_strided(const uint32_t *masks, int R, int K, const void *in_base,
+                            int64_t in_stripe_stride, const int64_t *in_off, void *out_base,
+                            int64_t out_stripe_stride, const int64_t *out_off, int64_t blocksize,
+                            int nstripes, void *stream);
+int ecamd_xor_apply_ptrs(const uint32_t *masks, int R, int K, const void *const *d_in_ptrs,
+                         int in_row, const int *in_col, void *const *d_out_ptrs, int out_row,
+                         const int *out_col, int64_t blocksize, int nstripes, void *stream);
+
+/* ---- liberasurecode_rs_vand on strided batches (maps cached per (k, m, pattern)) ---- */
+/* Encode: parity fragments k..k+m-1 from data 0..k-1. */
+int ecamd_rs_encode(int k, int m, void *base, int64_t stripe_stride, int64_t frag_stride,
+                    int64_t blocksize, int nstripes, void *stream);
+/* Decode: rebuild every fragment in the -1 terminated `missing` list in place (data, and parity
+ * if rebuild_parity) from the first k available, as liberasurecode_rs_vand_decode does. */
+int ecamd_rs_decode(int k, int m, const int *missing, int rebuild_parity, void *base,
+                    int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
+                    void *stream);
+/* Reconstruct one destination, as liberasurecode_rs_vand_reconstruct does. */
+int ecamd_rs_reconstruct(int k, int m, const int *missing, int dest, void *base,
+                         int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
+                         int nstripes, void *stream);
+
+/* ---- synthetic data: splitmix64 stream per fragment, seed = seed_base ^ (s<<8) ^ f ---- */
+int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, int nfrags,
+                        int64_t blocksize, int nstripes, int stripe0, uint64_t seed_base,
+                        void *stream);
+
+/* ---- device memory helpers for C / ctypes callers ---- */
+int ecamd_malloc(void **d_ptr, int64_t bytes);
+int ecamd_free(void *d_ptr);
+int ecamd_memcpy_h2d(void *d_dst, const void *h_src, int64_t bytes);
+int ecamd_memcpy_d2h(void *h_dst, const void *d_src, int64_t bytes);
+int ecamd_memset(void *d_ptr, int value, int64_t bytes);
+/* kind: 0 host->device, 1 device->host, 2 device->device; asynchronous on stream */
+int ecamd_memcpy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream);
+int ecamd_host_alloc(void **h_ptr, int64_t bytes); /* pinned host memory */
+int ecamd_host_free(void *h_ptr);
+int ecamd_synchronize(void);
+int ecamd_stream_create(void **stream);
+int ecamd_stream_destroy(void *stream);
+int ecamd_stream_synchronize(void *stream);
+/* HIP-event timing on a stream: records start/stop around nothing; use ecamd_timer_* below. */
+int ecamd_event_create(void **ev);
+int ecamd_event_destroy(void *ev);
+int ecamd_event_record(void *ev, void *stream);
+int ecamd_event_elapsed_ms(void *start, void *stop, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

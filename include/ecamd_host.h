@@ -1,0 +1,55 @@
+/*
+ * ecamd_host.h -- host-side planning for the MI355X erasure-code backend (libecamd_host.so).
+ *
+ * Pure host C ABI (no HIP types): GF(2^16) arithmetic, the reference generator matrix, and the
+ * "fragment maps" (which fragments to read, which to write, with which coefficients) that the
+ * device kernels apply.  Each entry point restates a piece of the reference's built-in
+ * liberasurecode_rs_vand codec:
+ *
+ *   ecamd_gf16_mul / ecamd_gf16_inv   rs_galois_mult / rs_galois_inverse
+ *                                     (src/builtin/rs_vand/rs_galois.c:90-117)
+ *   ecamd_rs_generator                make_systematic_matrix (liberasurecode_rs_vand.c:240-289)
+ *   ecamd_gf16_invert                 gaussj_inversion (liberasurecode_rs_vand.c:293-334)
+ *   ecamd_rs_decode_map               coefficient rows of liberasurecode_rs_vand_decode
+ *                                     (liberasurecode_rs_vand.c:426-481); missing parity is
+ *                                     expressed directly over the first k available fragments
+ *   ecamd_rs_reconstruct_map          coefficient row of liberasurecode_rs_vand_reconstruct
+ *                                     (liberasurecode_rs_vand.c:483-558)
+ */
+#ifndef ECAMD_HOST_H
+#define ECAMD_HOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int ecamd_gf16_mul(int a, int b);
+int ecamd_gf16_inv(int a);
+
+/* (k+m) x k row-major systematic generator into out; 0 on success. */
+int ecamd_rs_generator(int k, int m, int *out);
+
+/* Inverse of the n x n matrix a into inv; 0 on success, -1 if singular. */
+int ecamd_gf16_invert(const int *a, int *inv, int n);
+
+/* Decode map for a -1 terminated missing list.  inputs[k] receives the first k available
+ * fragment indices; outputs[*nout] the rebuilt fragment indices (missing data, then missing
+ * parity if rebuild_parity); coeff[*nout * k] the rows.  Returns -1 if more than m are missing. */
+int ecamd_rs_decode_map(const int *G, int k, int m, const int *missing, int rebuild_parity,
+                        int *inputs, int *outputs, int *coeff, int *nout);
+
+/* Reconstruct map for one destination: inputs[*ninputs] and coeff[*ninputs]. */
+int ecamd_rs_reconstruct_map(const int *G, int k, int m, const int *missing, int dest, int *inputs,
+                             int *ninputs, int *coeff);
+
+/* LDS split-table image for rows [row0,row0+width) x inputs [col0,col0+ncols) of the R x K
+ * matrix coeff; width in {2,4,8}.  Returns the byte count written (ncols*512*width*2). */
+int ecamd_split_tables(const int *coeff, int R, int K, int row0, int width, int col0, int ncols,
+                       uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

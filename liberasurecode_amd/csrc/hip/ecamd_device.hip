@@ -1,0 +1,602 @@
+// ecamd_device.hip -- host side of libecamd.so: device discovery, fragment-map planning
+// (row groups / column chunks sized to the 160 KiB LDS of a gfx950 CU), launch geometry and
+// the cached liberasurecode_rs_vand encode/decode/reconstruct maps.  C ABI in include/ecamd.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../host/gf16.hpp"
+#include "../host/tables.hpp"
+#include "ecamd.h"
+#include "ecamd_kernels.hpp"
+
+using namespace ecamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(ECAMD_EHIP, "%s: %s", #expr, hipGetErrorString(e_));               \
+    } while (0)
+
+struct DeviceInfo {
+    int cus = 0;
+    bool lds_attr_set = false;
+};
+
+std::mutex g_dev_mu;
+int g_ndev = -1;
+std::vector<DeviceInfo> g_dev;
+
+int ensure_device(int* dev_out)
+{
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_ndev < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_ndev = n;
+        g_dev.assign(std::max(n, 0), DeviceInfo());
+    }
+    if (g_ndev <= 0)
+        return fail(ECAMD_ENODEV, "liberasurecode_amd: no HIP device (MI355X) available; "
+                                  "this backend has no CPU fallback");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    DeviceInfo& di = g_dev[dev];
+    if (di.cus == 0) {
+        HIP_TRY(hipDeviceGetAttribute(&di.cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (di.cus <= 0) di.cus = 256;
+    }
+    if (!di.lds_attr_set) {
+        // Allow the full 160 KiB of gfx950 LDS as dynamic shared memory.
+        const void* ks[] = {
+            reinterpret_cast<const void*>(&gf16_apply_kernel<2, false>),
+            reinterpret_cast<const void*>(&gf16_apply_kernel<4, false>),
+            reinterpret_cast<const void*>(&gf16_apply_kernel<8, false>),
+            reinterpret_cast<const void*>(&gf16_apply_kernel<2, true>),
+            reinterpret_cast<const void*>(&gf16_apply_kernel<4, true>),
+            reinterpret_cast<const void*>(&gf16_apply_kernel<8, true>),
+        };
+        for (const void* k : ks)
+            HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+        di.lds_attr_set = true;
+    }
+    if (dev_out) *dev_out = dev;
+    return 0;
+}
+
+int cu_count(int dev)
+{
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    return g_dev[dev].cus;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+struct ecamd_map {
+    struct Pass {
+        int row0, width, col0, ncols;
+        size_t offset;  // into d_tables
+        size_t bytes;
+    };
+    int device = 0;
+    int R = 0, K = 0;
+    std::vector<Pass> passes;
+    uint8_t* d_tables = nullptr;
+};
+
+namespace {
+
+// Row groups of width 2/4/8 and column chunks that fit the LDS of one workgroup.
+std::vector<ecamd_map::Pass> plan_passes(int R, int K)
+{
+    int width;
+    if (R <= 2)
+        width = 2;
+    else if (R <= 4)
+        width = 4;
+    else
+        width = (K <= kLdsBytes / (512 * 16)) ? 8 : 4;
+    const int maxcols = std::min(kMaxCols, kLdsBytes / (512 * 2 * width));
+    std::vector<ecamd_map::Pass> passes;
+    size_t off = 0;
+    for (int row0 = 0; row0 < R; row0 += width) {
+        for (int col0 = 0; col0 < K; col0 += maxcols) {
+            ecamd_map::Pass p;
+            p.row0 = row0;
+            p.width = width;
+            p.col0 = col0;
+            p.ncols = std::min(maxcols, K - col0);
+            p.offset = off;
+            p.bytes = static_cast<size_t>(p.ncols) * 512 * 2 * width;
+            off += p.bytes;
+            passes.push_back(p);
+        }
+    }
+    return passes;
+}
+
+struct Geometry {
+    int threads;
+    int grid;
+    size_t lds;
+    uint32_t tiles_per_stripe;
+    uint32_t ntiles;
+};
+
+int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g)
+{
+    int wgs = lds ? static_cast<int>(std::min<size_t>(8, std::max<size_t>(1, kLdsBytes / lds))) : 8;
+    int threads = lds ? std::min(1024, std::max(256, (1024 / wgs) / 64 * 64)) : 256;
+    int64_t span = static_cast<int64_t>(threads) * 16;
+    int64_t tps = (bs + span - 1) / span;
+    int64_t nt = tps * nstripes;
+    if (nt >= (1ll << 32)) return fail(ECAMD_EINVAL, "batch too large: %lld tiles", (long long)nt);
+    g.threads = threads;
+    g.lds = lds;
+    g.tiles_per_stripe = static_cast<uint32_t>(tps);
+    g.ntiles = static_cast<uint32_t>(nt);
+    int64_t grid = std::min<int64_t>(nt, static_cast<int64_t>(cu_count(dev)) * wgs);
+    g.grid = static_cast<int>(std::max<int64_t>(grid, 1));
+    return 0;
+}
+
+template <bool PTRS>
+int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off,
+                const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st)
+{
+    for (const auto& p : map->passes) {
+        ApplyArgs a = base_args;
+        a.tables = map->d_tables + p.offset;
+        a.bs = bs;
+        a.ncols = p.ncols;
+        a.nrows = std::min(p.width, map->R - p.row0);
+        a.accumulate = p.col0 > 0;
+        for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[p.col0 + j];
+        for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
+        Geometry g;
+        int rc = geometry(map->device, p.bytes, bs, nstripes, g);
+        if (rc) return rc;
+        a.ntiles = g.ntiles;
+        a.tiles_per_stripe = g.tiles_per_stripe;
+        dim3 grid(g.grid), block(g.threads);
+        switch (p.width) {
+        case 2: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS>), grid, block, g.lds, st, a); break;
+        case 4: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS>), grid, block, g.lds, st, a); break;
+        default: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS>), grid, block, g.lds, st, a); break;
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+template <bool PTRS>
+int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const int64_t* in_off,
+               const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st)
+{
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    for (int row0 = 0; row0 < R; row0 += kMaxRows) {
+        for (int col0 = 0; col0 < K; col0 += 32) {
+            ApplyArgs a = base_args;
+            a.bs = bs;
+            a.ncols = std::min(32, K - col0);
+            a.nrows = std::min(kMaxRows, R - row0);
+            a.accumulate = col0 > 0;
+            for (int j = 0; j < a.ncols; j++) a.in_off[j] = in_off[col0 + j];
+            for (int r = 0; r < a.nrows; r++) {
+                a.out_off[r] = out_off[row0 + r];
+                a.masks[r] = col0 < 32 ? (masks[row0 + r] >> col0) : 0u;
+            }
+            Geometry g;
+            int rc = geometry(dev, 0, bs, nstripes, g);
+            if (rc) return rc;
+            a.ntiles = g.ntiles;
+            a.tiles_per_stripe = g.tiles_per_stripe;
+            hipLaunchKernelGGL((xor_apply_kernel<8, PTRS>), dim3(g.grid), dim3(g.threads), 0, st,
+                               a);
+            HIP_TRY(hipGetLastError());
+        }
+    }
+    return 0;
+}
+
+// ---- cached liberasurecode_rs_vand maps ------------------------------------------------
+
+struct RsEntry {
+    std::unique_ptr<ecamd_map, void (*)(ecamd_map*)> map{nullptr, ecamd_map_destroy};
+    std::vector<int> inputs, outputs;
+};
+
+std::mutex g_cache_mu;
+std::map<std::vector<int>, std::shared_ptr<RsEntry>> g_cache;
+
+int rs_entry(int kind, int k, int m, const int* missing, int rebuild, int dest,
+             std::shared_ptr<RsEntry>& out)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (k <= 0 || m < 0 || k + m > 65536) return fail(ECAMD_EINVAL, "bad k=%d m=%d", k, m);
+    std::vector<int> miss;
+    if (missing)
+        for (int i = 0; missing[i] > -1; i++) miss.push_back(missing[i]);
+    std::vector<int> key = {dev, kind, k, m, rebuild, dest};
+    key.insert(key.end(), miss.begin(), miss.end());
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto it = g_cache.find(key);
+        if (it != g_cache.end()) {
+            out = it->second;
+            return 0;
+        }
+    }
+    std::vector<int> G = rs_generator(k, m);
+    if (G.empty()) return fail(ECAMD_EINVAL, "no generator for k=%d m=%d", k, m);
+    FragmentMap fm;
+    if (kind == 0)
+        fm = rs_encode_map(G, k, m);
+    else if (kind == 1) {
+        if (rs_decode_map(G, k, m, miss, rebuild != 0, fm) != 0)
+            return fail(ECAMD_EINVAL, "too many missing fragments (%zu > m=%d)", miss.size(), m);
+    } else {
+        if (rs_reconstruct_map(G, k, m, miss, dest, fm) != 0)
+            return fail(ECAMD_EINVAL, "cannot reconstruct %d", dest);
+    }
+    auto e = std::make_shared<RsEntry>();
+    e->inputs = fm.inputs;
+    e->outputs = fm.outputs;
+    if (!fm.outputs.empty() && !fm.inputs.empty()) {
+        ecamd_map* mp = nullptr;
+        rc = ecamd_map_create(fm.coeff.data(), static_cast<int>(fm.outputs.size()),
+                              static_cast<int>(fm.inputs.size()), &mp);
+        if (rc) return rc;
+        e->map.reset(mp);
+    }
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    auto ins = g_cache.emplace(key, e);
+    out = ins.first->second;
+    return 0;
+}
+
+int rs_run(const RsEntry& e, void* base, int64_t stripe_stride, int64_t frag_stride, int64_t bs,
+           int nstripes, void* stream)
+{
+    if (e.outputs.empty() || nstripes <= 0 || bs <= 0) return 0;
+    if (e.inputs.empty()) {  // every input aliased away: the output is all zeros
+        for (int s = 0; s < nstripes; s++)
+            for (int o : e.outputs)
+                HIP_TRY(hipMemsetAsync(static_cast<uint8_t*>(base) + s * stripe_stride +
+                                           o * frag_stride, 0, bs,
+                                       static_cast<hipStream_t>(stream)));
+        return 0;
+    }
+    std::vector<int64_t> in_off, out_off;
+    for (int i : e.inputs) in_off.push_back(i * frag_stride);
+    for (int o : e.outputs) out_off.push_back(o * frag_stride);
+    return ecamd_map_apply_strided(e.map.get(), base, stripe_stride, in_off.data(), base,
+                                   stripe_stride, out_off.data(), bs, nstripes, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ecamd_init(void) { return ensure_device(nullptr); }
+
+int ecamd_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* ecamd_last_error(void) { return g_err.c_str(); }
+
+int ecamd_map_create(const int* coeff, int R, int K, ecamd_map** out)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!coeff || !out || R <= 0 || K <= 0) return fail(ECAMD_EINVAL, "bad map R=%d K=%d", R, K);
+    std::vector<int> c(coeff, coeff + static_cast<size_t>(R) * K);
+    for (int& v : c) v &= 0xffff;
+    auto passes = plan_passes(R, K);
+    size_t total = passes.back().offset + passes.back().bytes;
+    std::vector<uint8_t> img(total);
+    for (const auto& p : passes) {
+        auto t = build_split_tables(c, R, K, p.row0, p.width, p.col0, p.ncols);
+        std::memcpy(img.data() + p.offset, t.data(), t.size());
+    }
+    auto* map = new ecamd_map();
+    map->device = dev;
+    map->R = R;
+    map->K = K;
+    map->passes = passes;
+    if (hipMalloc(&map->d_tables, total) != hipSuccess) {
+        delete map;
+        return fail(ECAMD_ENOMEM, "hipMalloc(%zu) for tables failed", total);
+    }
+    if (hipMemcpy(map->d_tables, img.data(), total, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(map->d_tables);
+        delete map;
+        return fail(ECAMD_EHIP, "table upload failed");
+    }
+    *out = map;
+    return 0;
+}
+
+void ecamd_map_destroy(ecamd_map* map)
+{
+    if (!map) return;
+    if (map->d_tables) (void)hipFree(map->d_tables);
+    delete map;
+}
+
+int ecamd_map_apply_strided(const ecamd_map* map, const void* in_base, int64_t in_stripe_stride,
+                            const int64_t* in_off, void* out_base, int64_t out_stripe_stride,
+                            const int64_t* out_off, int64_t blocksize, int nstripes, void* stream)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    if (!map || !in_off || !out_off) return fail(ECAMD_EINVAL, "null argument");
+    if (nstripes <= 0 || blocksize <= 0) return 0;
+    bool ok = aligned16(in_base) && aligned16(out_base) && (in_stripe_stride % 16) == 0 &&
+              (out_stripe_stride % 16) == 0;
+    for (int j = 0; j < map->K; j++) ok = ok && (in_off[j] % 16) == 0;
+    for (int r = 0; r < map->R; r++) ok = ok && (out_off[r] % 16) == 0;
+    if (!ok) return fail(ECAMD_EINVAL, "fragment addresses must be 16-byte aligned");
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(in_base);
+    a.out_base = static_cast<uint8_t*>(out_base);
+    a.in_stride = in_stripe_stride;
+    a.out_stride = out_stripe_stride;
+    return launch_gf16<false>(map, a, in_off, out_off, blocksize, nstripes,
+                              static_cast<hipStream_t>(stream));
+}
+
+int ecamd_map_apply_ptrs(const ecamd_map* map, const void* const* d_in_ptrs, int in_row,
+                         const int* in_col, void* const* d_out_ptrs, int out_row,
+                         const int* out_col, int64_t blocksize, int nstripes, void* stream)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    if (!map || !d_in_ptrs || !d_out_ptrs || !in_col || !out_col)
+        return fail(ECAMD_EINVAL, "null argument");
+    if (nstripes <= 0 || blocksize <= 0) return 0;
+    ApplyArgs a{};
+    a.in_ptrs = reinterpret_cast<const uint8_t* const*>(d_in_ptrs);
+    a.out_ptrs = reinterpret_cast<uint8_t* const*>(d_out_ptrs);
+    a.in_stride = in_row;
+    a.out_stride = out_row;
+    std::vector<int64_t> io(in_col, in_col + map->K), oo(out_col, out_col + map->R);
+    return launch_gf16<true>(map, a, io.data(), oo.data(), blocksize, nstripes,
+                             static_cast<hipStream_t>(stream));
+}
+
+int ecamd_xor_apply_strided(const uint32_t* masks, int R, int K, const void* in_base,
+                            int64_t in_stripe_stride, const int64_t* in_off, void* out_base,
+                            int64_t out_stripe_stride, const int64_t* out_off, int64_t blocksize,
+                            int nstripes, void* stream)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    if (!masks || !in_off || !out_off || R <= 0 || K <= 0 || K > 32)
+        return fail(ECAMD_EINVAL, "bad xor map R=%d K=%d", R, K);
+    if (nstripes <= 0 || blocksize <= 0) return 0;
+    bool ok = aligned16(in_base) && aligned16(out_base) && (in_stripe_stride % 16) == 0 &&
+              (out_stripe_stride % 16) == 0;
+    for (int j = 0; j < K; j++) ok = ok && (in_off[j] % 16) == 0;
+    for (int r = 0; r < R; r++) ok = ok && (out_off[r] % 16) == 0;
+    if (!ok) return fail(ECAMD_EINVAL, "fragment addresses must be 16-byte aligned");
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(in_base);
+    a.out_base = static_cast<uint8_t*>(out_base);
+    a.in_stride = in_stripe_stride;
+    a.out_stride = out_stripe_stride;
+    return launch_xor<false>(masks, R, K, a, in_off, out_off, blocksize, nstripes,
+                             static_cast<hipStream_t>(stream));
+}
+
+int ecamd_xor_apply_ptrs(const uint32_t* masks, int R, int K, const void* const* d_in_ptrs,
+                         int in_row, const int* in_col, void* const* d_out_ptrs, int out_row,
+                         const int* out_col, int64_t blocksize, int nstripes, void* stream)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    if (!masks || !d_in_ptrs || !d_out_ptrs || !in_col || !out_col || R <= 0 || K <= 0 || K > 32)
+        return fail(ECAMD_EINVAL, "bad xor map R=%d K=%d", R, K);
+    if (nstripes <= 0 || blocksize <= 0) return 0;
+    ApplyArgs a{};
+    a.in_ptrs = reinterpret_cast<const uint8_t* const*>(d_in_ptrs);
+    a.out_ptrs = reinterpret_cast<uint8_t* const*>(d_out_ptrs);
+    a.in_stride = in_row;
+    a.out_stride = out_row;
+    std::vector<int64_t> io(in_col, in_col + K), oo(out_col, out_col + R);
+    return launch_xor<true>(masks, R, K, a, io.data(), oo.data(), blocksize, nstripes,
+                            static_cast<hipStream_t>(stream));
+}
+
+int ecamd_rs_encode(int k, int m, void* base, int64_t stripe_stride, int64_t frag_stride,
+                    int64_t blocksize, int nstripes, void* stream)
+{
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
+    if (rc) return rc;
+    return rs_run(*e, base, stripe_stride, frag_stride, blocksize, nstripes, stream);
+}
+
+int ecamd_rs_decode(int k, int m, const int* missing, int rebuild_parity, void* base,
+                    int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
+                    void* stream)
+{
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(1, k, m, missing, rebuild_parity ? 1 : 0, -1, e);
+    if (rc) return rc;
+    return rs_run(*e, base, stripe_stride, frag_stride, blocksize, nstripes, stream);
+}
+
+int ecamd_rs_reconstruct(int k, int m, const int* missing, int dest, void* base,
+                         int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
+                         int nstripes, void* stream)
+{
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(2, k, m, missing, 0, dest, e);
+    if (rc) return rc;
+    return rs_run(*e, base, stripe_stride, frag_stride, blocksize, nstripes, stream);
+}
+
+int ecamd_fill_splitmix(void* base, int64_t stripe_stride, int64_t frag_stride, int nfrags,
+                        int64_t blocksize, int nstripes, int stripe0, uint64_t seed_base,
+                        void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!aligned16(base) || stripe_stride % 8 || frag_stride % 8)
+        return fail(ECAMD_EINVAL, "fill: base must be 16-byte and strides 8-byte aligned");
+    FillArgs f{static_cast<uint8_t*>(base), stripe_stride, frag_stride, blocksize, nfrags,
+               nstripes, stripe0, seed_base};
+    int64_t total = ((blocksize + 7) / 8) * nfrags * static_cast<int64_t>(nstripes);
+    int64_t grid = std::min<int64_t>((total + 255) / 256, static_cast<int64_t>(cu_count(dev)) * 16);
+    hipLaunchKernelGGL(splitmix_fill_kernel, dim3(static_cast<int>(std::max<int64_t>(grid, 1))),
+                       dim3(256), 0, static_cast<hipStream_t>(stream), f);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_malloc(void** d_ptr, int64_t bytes)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipMalloc(d_ptr, static_cast<size_t>(bytes)));
+    return 0;
+}
+
+int ecamd_free(void* d_ptr)
+{
+    HIP_TRY(hipFree(d_ptr));
+    return 0;
+}
+
+int ecamd_memcpy_h2d(void* d_dst, const void* h_src, int64_t bytes)
+{
+    HIP_TRY(hipMemcpy(d_dst, h_src, static_cast<size_t>(bytes), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int ecamd_memcpy_d2h(void* h_dst, const void* d_src, int64_t bytes)
+{
+    HIP_TRY(hipMemcpy(h_dst, d_src, static_cast<size_t>(bytes), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int ecamd_memset(void* d_ptr, int value, int64_t bytes)
+{
+    HIP_TRY(hipMemset(d_ptr, value, static_cast<size_t>(bytes)));
+    return 0;
+}
+
+int ecamd_memcpy_async(void* dst, const void* src, int64_t bytes, int kind, void* stream)
+{
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                      : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(dst, src, static_cast<size_t>(bytes), k, static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int ecamd_host_alloc(void** h_ptr, int64_t bytes)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipHostMalloc(h_ptr, static_cast<size_t>(bytes), hipHostMallocDefault));
+    return 0;
+}
+
+int ecamd_host_free(void* h_ptr)
+{
+    HIP_TRY(hipHostFree(h_ptr));
+    return 0;
+}
+
+int ecamd_synchronize(void)
+{
+    HIP_TRY(hipDeviceSynchronize());
+    return 0;
+}
+
+int ecamd_stream_create(void** stream)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return 0;
+}
+
+int ecamd_stream_destroy(void* stream)
+{
+    HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int ecamd_stream_synchronize(void* stream)
+{
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int ecamd_event_create(void** ev)
+{
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    *ev = e;
+    return 0;
+}
+
+int ecamd_event_destroy(void* ev)
+{
+    HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(ev)));
+    return 0;
+}
+
+int ecamd_event_record(void* ev, void* stream)
+{
+    HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int ecamd_event_elapsed_ms(void* start, void* stop, float* ms)
+{
+    HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(stop)));
+    HIP_TRY(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)));
+    return 0;
+}
+
+}  // extern "C"

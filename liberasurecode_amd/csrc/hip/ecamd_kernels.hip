@@ -1,0 +1,287 @@
+// ecamd_kernels.hip -- gfx950 (MI355X / CDNA4) kernels for the erasure-code hot path.
+//
+// gf16_apply_kernel: out[r] = sum_j A[r][j] * in[j] over GF(2^16) on little-endian 16-bit words,
+// for many independent stripes in one launch.  This is the GPU form of the reference's
+// region_dot_product / region_multiply / region_xor (src/builtin/rs_vand/liberasurecode_rs_vand.c:
+// 336-397), which encode, decode and reconstruct all reduce to (:399-558).
+//
+//   * HBM: every lane moves 16 B per fragment per tile (global_load_dwordx4), a wave covers a
+//     contiguous 1 KiB of each fragment; inputs are read once and all outputs written once per
+//     tile, so algorithmic traffic = (K + R) * blocksize per stripe.
+//   * LDS: multiply-by-constant is GF(2)-linear, so c*x = T_lo[x & 0xff] ^ T_hi[x >> 8].  The
+//     tables of one input pack all W outputs of the row group into one W*2-byte entry, so one
+//     16-bit input word costs two ds_read_b{32,64,128} for every output at once (W = 2, 4, 8).
+//     The whole image (K * 512 * 2W bytes) is staged into LDS once per workgroup; workgroups are
+//     persistent and grid-stride over tiles, so the staging cost is amortised.
+//   * Inputs are fetched one group of 4 fragments ahead of the lookups (software pipeline) so
+//     each wave keeps >= 4 KiB of loads in flight while its LDS lookups run.
+//
+// xor_apply_kernel: out[r] = XOR of the inputs selected by mask[r] (flat-XOR HD codes,
+// src/builtin/xor_codes/xor_code.c:141-207); pure streaming.
+//
+// splitmix_fill_kernel: synthetic fragment bytes (bench / tests), same stream as tests/ecdata.py.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ecamd_kernels.hpp"
+
+namespace ecamd {
+
+namespace {
+
+__device__ __forceinline__ uint4 load16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+// Partial 16-byte chunk at the end of a fragment: bytes [0, rem) of p, zero filled.
+__device__ __forceinline__ uint4 load_tail(const uint8_t* p, int rem)
+{
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        uint32_t b = (i < rem) ? static_cast<uint32_t>(p[i]) : 0u;
+        w[i >> 2] |= b << (8 * (i & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_tail(uint8_t* p, uint4 v, int rem)
+{
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+        if (i < rem) p[i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+}
+
+template <bool PTRS>
+__device__ __forceinline__ const uint8_t* in_frag(const ApplyArgs& a, uint32_t s, int j)
+{
+    if constexpr (PTRS)
+        return a.in_ptrs[static_cast<int64_t>(s) * a.in_stride + a.in_off[j]];
+    else
+        return a.in_base + static_cast<int64_t>(s) * a.in_stride + a.in_off[j];
+}
+
+template <bool PTRS>
+__device__ __forceinline__ uint8_t* out_frag(const ApplyArgs& a, uint32_t s, int r)
+{
+    if constexpr (PTRS)
+        return a.out_ptrs[static_cast<int64_t>(s) * a.out_stride + a.out_off[r]];
+    else
+        return a.out_base + static_cast<int64_t>(s) * a.out_stride + a.out_off[r];
+}
+
+// One LDS table entry of D dwords (D = W/2): ds_read_b32 / b64 / b128.
+template <int D>
+__device__ __forceinline__ void lds_entry(const uint8_t* p, uint32_t (&e)[D])
+{
+    if constexpr (D == 1) {
+        e[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (D == 2) {
+        uint2 v = *reinterpret_cast<const uint2*>(p);
+        e[0] = v.x;
+        e[1] = v.y;
+    } else {
+        uint4 v = *reinterpret_cast<const uint4*>(p);
+        e[0] = v.x;
+        e[1] = v.y;
+        e[2] = v.z;
+        e[3] = v.w;
+    }
+}
+
+// acc[w] ^= T_lo[j][lo(x_w)] ^ T_hi[j][hi(x_w)] for the 8 words of one 16-byte chunk.
+template <int W>
+__device__ __forceinline__ void mac_chunk(const uint8_t* tl, uint4 x, uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    const uint8_t* th = tl + 256 * EB;
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const uint32_t v = xs[w >> 1] >> ((w & 1) * 16);
+        uint32_t e0[D], e1[D];
+        lds_entry<D>(tl + (v & 0xffu) * EB, e0);
+        lds_entry<D>(th + ((v >> 8) & 0xffu) * EB, e1);
+#pragma unroll
+        for (int d = 0; d < D; d++) acc[w][d] ^= e0[d] ^ e1[d];
+    }
+}
+
+template <int W, bool PTRS, bool TAIL>
+__device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* lds, uint32_t s,
+                                           int64_t off, int rem)
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    const int K = a.ncols;
+    uint32_t acc[8][D];
+#pragma unroll
+    for (int w = 0; w < 8; w++)
+#pragma unroll
+        for (int d = 0; d < D; d++) acc[w][d] = 0u;
+
+    auto fetch = [&](int j) -> uint4 {
+        const uint8_t* p = in_frag<PTRS>(a, s, j) + off;
+        return TAIL ? load_tail(p, rem) : load16(p);
+    };
+    uint4 cur[4], nxt[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) cur[i] = (i < K) ? fetch(i) : make_uint4(0, 0, 0, 0);
+    for (int j0 = 0; j0 < K; j0 += 4) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            nxt[i] = (j0 + 4 + i < K) ? fetch(j0 + 4 + i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (j0 + i < K) mac_chunk<W>(lds + static_cast<size_t>(j0 + i) * 512 * EB, cur[i], acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+    }
+
+#pragma unroll
+    for (int r = 0; r < W; r++) {
+        if (r >= a.nrows) break;
+        uint32_t o[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const uint32_t A = acc[2 * d][r >> 1], B = acc[2 * d + 1][r >> 1];
+            o[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+        }
+        uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
+        uint8_t* q = out_frag<PTRS>(a, s, r) + off;
+        if (a.accumulate) {
+            uint4 prev = TAIL ? load_tail(q, rem) : load16(q);
+            v.x ^= prev.x;
+            v.y ^= prev.y;
+            v.z ^= prev.z;
+            v.w ^= prev.w;
+        }
+        if (TAIL)
+            store_tail(q, v, rem);
+        else
+            *reinterpret_cast<uint4*>(q) = v;
+    }
+}
+
+}  // namespace
+
+template <int W, bool PTRS>
+__global__ void __launch_bounds__(1024) gf16_apply_kernel(const ApplyArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int EB = 2 * W;
+    const int tbytes = a.ncols * 512 * EB;
+    for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
+        *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
+    __syncthreads();
+
+    const int64_t span = static_cast<int64_t>(blockDim.x) * 16;
+    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int64_t off = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span +
+                            static_cast<int64_t>(threadIdx.x) * 16;
+        const int64_t rem = a.bs - off;
+        if (rem <= 0) continue;
+        if (rem >= 16)
+            apply_tile<W, PTRS, false>(a, lds, s, off, 16);
+        else
+            apply_tile<W, PTRS, true>(a, lds, s, off, static_cast<int>(rem));
+    }
+}
+
+template __global__ void gf16_apply_kernel<2, false>(const ApplyArgs);
+template __global__ void gf16_apply_kernel<4, false>(const ApplyArgs);
+template __global__ void gf16_apply_kernel<8, false>(const ApplyArgs);
+template __global__ void gf16_apply_kernel<2, true>(const ApplyArgs);
+template __global__ void gf16_apply_kernel<4, true>(const ApplyArgs);
+template __global__ void gf16_apply_kernel<8, true>(const ApplyArgs);
+
+// ---------------------------------------------------------------- flat XOR ----
+
+template <int W, bool PTRS, bool TAIL>
+__device__ __forceinline__ void xor_tile(const ApplyArgs& a, uint32_t s, int64_t off, int rem)
+{
+    const int K = a.ncols;
+    uint4 acc[W];
+#pragma unroll
+    for (int r = 0; r < W; r++) acc[r] = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < K; j++) {
+        const uint8_t* p = in_frag<PTRS>(a, s, j) + off;
+        const uint4 x = TAIL ? load_tail(p, rem) : load16(p);
+#pragma unroll
+        for (int r = 0; r < W; r++) {
+            const uint32_t m = 0u - ((a.masks[r] >> j) & 1u);  // wave-uniform select
+            acc[r].x ^= x.x & m;
+            acc[r].y ^= x.y & m;
+            acc[r].z ^= x.z & m;
+            acc[r].w ^= x.w & m;
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < W; r++) {
+        if (r >= a.nrows) break;
+        uint8_t* q = out_frag<PTRS>(a, s, r) + off;
+        uint4 v = acc[r];
+        if (a.accumulate) {
+            uint4 prev = TAIL ? load_tail(q, rem) : load16(q);
+            v.x ^= prev.x;
+            v.y ^= prev.y;
+            v.z ^= prev.z;
+            v.w ^= prev.w;
+        }
+        if (TAIL)
+            store_tail(q, v, rem);
+        else
+            *reinterpret_cast<uint4*>(q) = v;
+    }
+}
+
+template <int W, bool PTRS>
+__global__ void __launch_bounds__(256) xor_apply_kernel(const ApplyArgs a)
+{
+    const int64_t span = static_cast<int64_t>(blockDim.x) * 16;
+    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int64_t off = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span +
+                            static_cast<int64_t>(threadIdx.x) * 16;
+        const int64_t rem = a.bs - off;
+        if (rem <= 0) continue;
+        if (rem >= 16)
+            xor_tile<W, PTRS, false>(a, s, off, 16);
+        else
+            xor_tile<W, PTRS, true>(a, s, off, static_cast<int>(rem));
+    }
+}
+
+template __global__ void xor_apply_kernel<8, false>(const ApplyArgs);
+template __global__ void xor_apply_kernel<8, true>(const ApplyArgs);
+
+// ---------------------------------------------------------------- synthetic data ----
+
+__global__ void __launch_bounds__(256) splitmix_fill_kernel(FillArgs f)
+{
+    const int64_t words = (f.bs + 7) / 8;
+    const int64_t total = words * f.nfrags * static_cast<int64_t>(f.nstripes);
+    for (int64_t g = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; g < total;
+         g += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t i = g % words;
+        const int64_t fs = g / words;
+        const int frag = static_cast<int>(fs % f.nfrags);
+        const int64_t s = fs / f.nfrags;
+        const uint64_t seed = f.seed_base ^ (static_cast<uint64_t>(s + f.stripe0) << 8) ^
+                              static_cast<uint64_t>(frag);
+        uint64_t z = seed + static_cast<uint64_t>(i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        uint8_t* p = f.base + s * f.stripe_stride + frag * f.frag_stride + i * 8;
+        const int64_t left = f.bs - i * 8;
+        if (left >= 8) {
+            *reinterpret_cast<uint64_t*>(p) = z;
+        } else {
+            for (int b = 0; b < left; b++) p[b] = static_cast<uint8_t>(z >> (8 * b));
+        }
+    }
+}
+
+}  // namespace ecamd

@@ -1,0 +1,48 @@
+// ecamd_kernels.hpp -- kernel argument blocks shared by ecamd_kernels.hip and ecamd_device.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ecamd {
+
+constexpr int kMaxCols = 80;      // inputs per launch: 80 * 512 * 4 B = 160 KiB of LDS at W = 2
+constexpr int kMaxRows = 8;       // outputs per launch
+constexpr int kLdsBytes = 163840; // gfx950: 160 KiB per workgroup
+
+struct ApplyArgs {
+    const uint8_t* tables;            // split-table image (gf16) -- unused by xor
+    const uint8_t* in_base;           // strided form
+    uint8_t* out_base;
+    const uint8_t* const* in_ptrs;    // pointer-table form
+    uint8_t* const* out_ptrs;
+    int64_t in_stride;                // bytes per stripe (strided) / pointers per stripe (table)
+    int64_t out_stride;
+    int64_t bs;                       // bytes per fragment payload
+    uint32_t ntiles;
+    uint32_t tiles_per_stripe;
+    int ncols;                        // inputs in this launch
+    int nrows;                        // outputs in this launch
+    int accumulate;                   // 1: out ^= result (later column chunks)
+    uint32_t masks[kMaxRows];         // xor kernel: input selection per output
+    int64_t in_off[kMaxCols];         // byte offset (strided) / column (table) of input j
+    int64_t out_off[kMaxRows];
+};
+
+struct FillArgs {
+    uint8_t* base;
+    int64_t stripe_stride;
+    int64_t frag_stride;
+    int64_t bs;
+    int nfrags;
+    int nstripes;
+    int stripe0;
+    uint64_t seed_base;
+};
+
+template <int W, bool PTRS>
+__global__ void gf16_apply_kernel(const ApplyArgs a);
+template <int W, bool PTRS>
+__global__ void xor_apply_kernel(const ApplyArgs a);
+__global__ void splitmix_fill_kernel(FillArgs f);
+
+}  // namespace ecamd

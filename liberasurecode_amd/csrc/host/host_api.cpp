@@ -1,0 +1,86 @@
+// host_api.cpp -- extern "C" surface of libecamd_host.so (include/ecamd_host.h).
+#include "ecamd_host.h"
+
+#include <cstring>
+#include <vector>
+
+#include "gf16.hpp"
+#include "tables.hpp"
+
+using namespace ecamd;
+
+namespace {
+std::vector<int> minus1_list(const int* missing)
+{
+    std::vector<int> v;
+    if (!missing) return v;
+    for (int i = 0; missing[i] > -1; i++) v.push_back(missing[i]);
+    return v;
+}
+}  // namespace
+
+extern "C" {
+
+int ecamd_gf16_mul(int a, int b) { return GF16::get().mul(a & 0xffff, b & 0xffff); }
+
+int ecamd_gf16_inv(int a) { return GF16::get().inv(a & 0xffff); }
+
+int ecamd_rs_generator(int k, int m, int* out)
+{
+    std::vector<int> g = rs_generator(k, m);
+    if (g.empty() || !out) return -1;
+    std::memcpy(out, g.data(), g.size() * sizeof(int));
+    return 0;
+}
+
+int ecamd_gf16_invert(const int* a, int* inv, int n)
+{
+    if (!a || !inv || n <= 0) return -1;
+    std::vector<int> m(a, a + static_cast<size_t>(n) * n), r;
+    if (!gf16_invert(m, r, n)) return -1;
+    std::memcpy(inv, r.data(), r.size() * sizeof(int));
+    return 0;
+}
+
+int ecamd_rs_decode_map(const int* G, int k, int m, const int* missing, int rebuild_parity,
+                        int* inputs, int* outputs, int* coeff, int* nout)
+{
+    if (!G || k <= 0 || m < 0) return -1;
+    std::vector<int> g(G, G + static_cast<size_t>(k + m) * k);
+    FragmentMap fm;
+    if (rs_decode_map(g, k, m, minus1_list(missing), rebuild_parity != 0, fm) != 0) return -1;
+    std::memcpy(inputs, fm.inputs.data(), fm.inputs.size() * sizeof(int));
+    if (!fm.outputs.empty()) {
+        std::memcpy(outputs, fm.outputs.data(), fm.outputs.size() * sizeof(int));
+        std::memcpy(coeff, fm.coeff.data(), fm.coeff.size() * sizeof(int));
+    }
+    *nout = static_cast<int>(fm.outputs.size());
+    return 0;
+}
+
+int ecamd_rs_reconstruct_map(const int* G, int k, int m, const int* missing, int dest, int* inputs,
+                             int* ninputs, int* coeff)
+{
+    if (!G || k <= 0 || m < 0) return -1;
+    std::vector<int> g(G, G + static_cast<size_t>(k + m) * k);
+    FragmentMap fm;
+    if (rs_reconstruct_map(g, k, m, minus1_list(missing), dest, fm) != 0) return -1;
+    if (!fm.inputs.empty()) {
+        std::memcpy(inputs, fm.inputs.data(), fm.inputs.size() * sizeof(int));
+        std::memcpy(coeff, fm.coeff.data(), fm.coeff.size() * sizeof(int));
+    }
+    *ninputs = static_cast<int>(fm.inputs.size());
+    return 0;
+}
+
+int ecamd_split_tables(const int* coeff, int R, int K, int row0, int width, int col0, int ncols,
+                       uint8_t* out)
+{
+    if (!coeff || !out || (width != 2 && width != 4 && width != 8)) return -1;
+    std::vector<int> c(coeff, coeff + static_cast<size_t>(R) * K);
+    std::vector<uint8_t> img = build_split_tables(c, R, K, row0, width, col0, ncols);
+    std::memcpy(out, img.data(), img.size());
+    return static_cast<int>(img.size());
+}
+
+}  // extern "C"

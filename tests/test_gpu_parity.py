@@ -1,0 +1,257 @@
+"""GPU parity: the HIP path (libecamd.so, liberasurecode_rs_vand.so.1) against the reference's
+golden vectors, the C oracle and the independent numpy GF(2^16).  Needs an MI355X."""
+import ctypes as C
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import gfnp
+import oracle_lib as orc
+from ecdata import EDGE_PATTERNS, stripe_fragments
+from liberasurecode_amd import _lib
+from liberasurecode_amd import device as D
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "rs_vand.json")))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    assert D.available(), _lib.dev().ecamd_last_error()
+
+
+def _upload(frags_sfb):
+    S, F, bs = frags_sfb.shape
+    lay = D.Layout.alloc(F, bs, S)
+    lay.upload_stripes(frags_sfb)
+    return lay
+
+
+def test_fill_splitmix_matches_numpy():
+    lay = D.Layout.alloc(5, 1000, 3)
+    lay.fill_splitmix(stripe0=7)
+    D.synchronize()
+    got = lay.download_stripes()
+    for s in range(3):
+        assert (got[s] == stripe_fragments(7 + s, 5, 1000)).all()
+
+
+def _case_data(case):
+    k, bs = case["k"], case["bs"]
+    if case.get("pattern"):
+        return np.stack([EDGE_PATTERNS[case["pattern"]](bs) for _ in range(k)])
+    return stripe_fragments(case["stripe"], k, bs)
+
+
+@pytest.mark.parametrize("case", GOLD["encode"],
+                         ids=lambda c: f"{c['k']}-{c['m']}-{c['bs']}-{c['pattern']}")
+def test_encode_golden(case):
+    k, m, bs = case["k"], case["m"], case["bs"]
+    frags = np.zeros((1, k + m, bs), dtype=np.uint8)
+    frags[0, :k] = _case_data(case)
+    frags[0, k:] = 0xA5  # parity must be overwritten
+    lay = _upload(frags)
+    D.rs_encode(k, m, lay)
+    out = lay.download_stripes()[0]
+    assert [sha(out[k + p]) for p in range(m)] == case["parity_sha256"]
+
+
+def _decode_frags(case):
+    k, m, bs = case["k"], case["m"], case["bs"]
+    data = stripe_fragments(case["stripe"], k, bs)
+    par = (stripe_fragments(case["stripe"], m, bs, base=0xBAD0) if case["garbage"]
+           else orc.encode(k, m, data))
+    frags = np.concatenate([data, par])[None].copy()
+    for i in case["missing"]:
+        frags[0, i] = 0x5A  # missing slots are overwritten, whatever they hold
+    return frags
+
+
+@pytest.mark.parametrize("case", GOLD["decode"],
+                         ids=lambda c: f"{c['k']}-{c['m']}-{c['bs']}-{c['missing']}-{c['garbage']}")
+def test_decode_golden(case):
+    k, m = case["k"], case["m"]
+    lay = _upload(_decode_frags(case))
+    if case["ret"] != 0:
+        with pytest.raises(_lib.ECAmdError):
+            D.rs_decode(k, m, case["missing"], lay)
+        return
+    D.rs_decode(k, m, case["missing"], lay)
+    out = lay.download_stripes()[0]
+    assert {str(i): sha(out[i]) for i in case["missing"]} == case["out_sha256"]
+
+
+@pytest.mark.parametrize("case", GOLD["reconstruct"],
+                         ids=lambda c: f"{c['k']}-{c['m']}-{c['missing']}-{c['dest']}-{c['garbage']}")
+def test_reconstruct_golden(case):
+    k, m = case["k"], case["m"]
+    frags = _decode_frags(case)
+    for i in case["missing"]:
+        frags[0, i] = 0  # the reference test zeroes missing buffers
+    lay = _upload(frags)
+    D.rs_reconstruct(k, m, case["missing"], case["dest"], lay)
+    out = lay.download_stripes()[0]
+    assert sha(out[case["dest"]]) == case["out_sha256"]
+
+
+@pytest.mark.parametrize("k,m,bs,S", [(4, 2, 65536, 64), (10, 4, 1 << 20, 8), (10, 4, 4096, 257),
+                                      (20, 8, 1 << 18, 6), (12, 6, 3000, 33)])
+def test_batched_encode_matches_oracle(k, m, bs, S):
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix(nfrags=k, stripe0=100)
+    D.rs_encode(k, m, lay)
+    out = lay.download_stripes()
+    for s in sorted({0, S // 2, S - 1}):
+        data = stripe_fragments(100 + s, k, bs)
+        assert (out[s, :k] == data).all()
+        assert (out[s, k:] == orc.encode(k, m, data)).all()
+
+
+@pytest.mark.parametrize("k,m,bs,S,missing", [
+    (10, 4, 1 << 20, 16, [0, 1, 2, 3]), (10, 4, 1 << 20, 16, [0, 5, 10, 13]),
+    (20, 8, 1 << 22, 4, list(range(8))), (20, 8, 1 << 20, 4, [0, 2, 4, 6, 20, 22, 24, 26]),
+    (4, 2, 65536, 128, [1, 3])])
+def test_roundtrip_encode_erase_decode(k, m, bs, S, missing):
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix(nfrags=k, stripe0=5)
+    D.rs_encode(k, m, lay)
+    ref = lay.download_stripes()
+    host = ref.copy()
+    host[:, missing] = 0xEE
+    lay.upload_stripes(host)
+    D.rs_decode(k, m, missing, lay)
+    assert (lay.download_stripes() == ref).all()
+    # reconstruct each erased fragment on its own, as liberasurecode_reconstruct_fragment does
+    for d in missing[:3]:
+        lay.upload_stripes(host)
+        D.rs_reconstruct(k, m, missing, d, lay)
+        assert (lay.download_stripes()[:, d] == ref[:, d]).all()
+
+
+@pytest.mark.parametrize("bs", [1, 2, 3, 15, 16, 17, 31, 33, 255, 1000, 4097])
+@pytest.mark.parametrize("R,K", [(1, 3), (2, 5), (3, 4), (4, 10), (6, 7), (8, 20), (9, 25), (5, 45)])
+def test_map_tails_and_shapes(bs, R, K):
+    rng = np.random.default_rng(bs * 1000 + R * 10 + K)
+    coeff = rng.integers(0, 65536, size=(R, K))
+    coeff[0, 0] = 1
+    ins = [rng.integers(0, 256, size=bs, dtype=np.uint8) for _ in range(K)]
+    frags = np.zeros((2, K + R, bs), dtype=np.uint8)
+    frags[:, :K] = np.stack(ins)
+    frags[:, K:] = 0x77
+    lay = _upload(frags)
+    D.GF16Map(coeff).apply(lay, list(range(K)), list(range(K, K + R)))
+    out = lay.download_stripes()
+    want = gfnp.apply_map(coeff, ins)
+    for r in range(R):
+        assert (out[0, K + r] == want[r]).all(), (r, bs)
+        assert (out[1, K + r] == want[r]).all()
+
+
+def test_map_apply_pointer_tables():
+    k, m, bs, S = 10, 4, 8192, 5
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix(nfrags=k)
+    G = np.array(orc.generator(k, m)).reshape(k + m, k)
+    mp = D.GF16Map(G[k:])
+    ptrs = np.array([lay.buf.ptr + s * lay.stripe_stride + f * lay.frag_stride
+                     for s in range(S) for f in range(k + m)], dtype=np.uint64)
+    pbuf = D.DeviceBuffer(ptrs.nbytes)
+    pbuf.upload(ptrs.view(np.uint8))
+    rc = _lib.dev().ecamd_map_apply_ptrs(mp.handle, pbuf.ptr, k + m, _lib.ints(range(k)), pbuf.ptr,
+                                         k + m, _lib.ints(range(k, k + m)), bs, S, None)
+    assert rc == 0
+    out = lay.download_stripes()
+    for s in range(S):
+        assert (out[s, k:] == orc.encode(k, m, out[s, :k])).all()
+
+
+@pytest.mark.parametrize("bs", [16, 1000, 4096, 65536 + 3])
+def test_xor_apply(bs):
+    rng = np.random.default_rng(bs)
+    K, R, S = 6, 3, 4
+    frags = rng.integers(0, 256, size=(S, K + R, bs), dtype=np.uint8)
+    lay = _upload(frags)
+    masks = [0b101001, 0b010110, 0b111111]
+    D.xor_apply(masks, lay, list(range(K)), list(range(K, K + R)))
+    out = lay.download_stripes()
+    for r, mk in enumerate(masks):
+        want = np.zeros((S, bs), dtype=np.uint8)
+        for j in range(K):
+            if mk >> j & 1:
+                want ^= frags[:, j]
+        assert (out[:, K + r] == want).all()
+
+
+# ---------------------------------------------------------------- drop-in B1 .so ----
+
+def _b1():
+    lib = C.CDLL(os.path.join(ROOT, "liberasurecode_amd", "lib", "liberasurecode_rs_vand.so.1"))
+    IP = C.POINTER(C.c_int)
+    lib.make_systematic_matrix.restype = IP
+    lib.make_systematic_matrix.argtypes = [C.c_int, C.c_int]
+    lib.liberasurecode_rs_vand_encode.argtypes = [IP, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    lib.liberasurecode_rs_vand_decode.argtypes = [IP, C.c_void_p, C.c_void_p, C.c_int, C.c_int, IP,
+                                                  C.c_int, C.c_int]
+    lib.liberasurecode_rs_vand_reconstruct.argtypes = [IP, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                       IP, C.c_int, C.c_int]
+    return lib
+
+
+def test_b1_abi_golden():
+    lib = _b1()
+    for case in GOLD["encode"][:12]:
+        k, m, bs = case["k"], case["m"], case["bs"]
+        lib.init_liberasurecode_rs_vand(k, m)
+        G = lib.make_systematic_matrix(k, m)
+        assert bool(G)
+        data = [np.array(x) for x in _case_data(case)]
+        par = [np.full(bs, 0xA5, dtype=np.uint8) for _ in range(m)]
+        lib.liberasurecode_rs_vand_encode(G, orc.ptr_array(data), orc.ptr_array(par), k, m, bs)
+        assert [sha(p) for p in par] == case["parity_sha256"]
+    for case in GOLD["decode"]:
+        if case["bs"] > 65536:
+            continue
+        k, m = case["k"], case["m"]
+        G = lib.make_systematic_matrix(k, m)
+        frags = [np.array(x) for x in _decode_frags(case)[0]]
+        rc = lib.liberasurecode_rs_vand_decode(G, orc.ptr_array(frags[:k]), orc.ptr_array(frags[k:]),
+                                               k, m, orc.ints(case["missing"] + [-1]), case["bs"], 1)
+        assert rc == case["ret"]
+        if rc == 0:
+            assert {str(i): sha(frags[i]) for i in case["missing"]} == case["out_sha256"]
+    for case in GOLD["reconstruct"]:
+        if case["bs"] > 65536:
+            continue
+        k, m = case["k"], case["m"]
+        G = lib.make_systematic_matrix(k, m)
+        frags = [np.array(x) for x in _decode_frags(case)[0]]
+        for i in case["missing"]:
+            frags[i][:] = 0
+        rc = lib.liberasurecode_rs_vand_reconstruct(G, orc.ptr_array(frags[:k]),
+                                                    orc.ptr_array(frags[k:]), k, m,
+                                                    orc.ints(case["missing"] + [-1]), case["dest"],
+                                                    case["bs"])
+        assert rc == case["ret"]
+        assert sha(frags[case["dest"]]) == case["out_sha256"]
+
+
+def test_reference_unit_test_runs_on_our_codec():
+    """The reference's own test/builtin/rs_vand/liberasurecode_rs_vand_test.c, compiled from its
+    source by oracle/Makefile, run against OUR liberasurecode_rs_vand.so.1 via LD_LIBRARY_PATH."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "liberasurecode_rs_vand_test")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built (needs the reference sources at build time)")
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(ROOT, "liberasurecode_amd", "lib"))
+    probe = subprocess.run(["ldd", exe], env=env, capture_output=True, text=True).stdout
+    assert os.path.join("liberasurecode_amd", "lib", "liberasurecode_rs_vand.so.1") in probe
+    r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
