@@ -81,6 +81,23 @@ def cpu_baseline(k, m, F, missing, threads, stripes):
             "cpu_seconds": round(sum(t for _, t in res), 2)}
 
 
+def pmc_traffic(cfg, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this same
+    command (profiles/<round>_<cfg>_summary.json, built by tools/summarize_prof.py from separate
+    FETCH_SIZE / WRITE_SIZE passes with the gfx950 FETCH_SIZE x2 correction)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_summary.json")),
+                       reverse=True):
+        try:
+            summ = json.load(open(path))
+        except Exception:
+            continue
+        for name, d in summ.get("kernels", {}).items():
+            if kernel in name and "hbm_bytes_per_launch" in d:
+                return int(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -90,7 +107,7 @@ def main():
     ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-stripes", type=int, default=8, help="stripes per CPU thread")
+    ap.add_argument("--cpu-stripes", type=int, default=32, help="stripes per CPU thread")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,6 +171,9 @@ def main():
     # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+    width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
+    kernel = f"gf16_apply_kernel<{width}, false, true>"
+    traffic, traffic_src = pmc_traffic(args.config, kernel)
 
     if rank == 0:
         out = {
@@ -175,9 +195,10 @@ def main():
                        "parallelism": f"stripe-sharded x{world} (no data-path collective)"},
             "encode_gibs_per_gpu": round(obj_bytes / GIB / (sum(enc_ms) / len(enc_ms) / 1e3), 3),
             "decode_gibs_per_gpu": round(obj_bytes / GIB / (sum(dec_ms) / len(dec_ms) / 1e3), 3),
-            "roofline": {"bound": "hbm", "kernel": "gf16_apply_kernel<4,false>",
+            "roofline": {"bound": "hbm", "kernel": kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "launch_ms": round(launch_ms, 4),
                          "algorithmic_bytes_per_launch": algo_bytes},
         }

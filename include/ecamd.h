@@ -35,6 +35,8 @@ extern "C" {
 int ecamd_init(void);
 int ecamd_device_count(void);
 const char *ecamd_last_error(void);
+/* Launch-geometry knobs for sweeps ("threads", "wgs_per_cu", "nt"); 0 restores the default. */
+int ecamd_tune(const char *key, int value);
 
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
 typedef struct ecamd_map ecamd_map;
@@ -83,6 +85,9 @@ int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, 
                         int64_t blocksize, int nstripes, int stripe0, uint64_t seed_base,
                         void *stream);
 
+/* ---- measurement helper: non-temporal 16 B/lane streaming copy (HBM ceiling probe) ---- */
+int ecamd_debug_stream_copy(void *d_dst, const void *d_src, int64_t bytes, void *stream);
+
 /* ---- device memory helpers for C / ctypes callers ---- */
 int ecamd_malloc(void **d_ptr, int64_t bytes);
 int ecamd_free(void *d_ptr);
@@ -97,7 +102,7 @@ int ecamd_synchronize(void);
 int ecamd_stream_create(void **stream);
 int ecamd_stream_destroy(void *stream);
 int ecamd_stream_synchronize(void *stream);
-/* HIP-event timing on a stream: records start/stop around nothing; use ecamd_timer_* below. */
+/* HIP events for timing work on a stream (elapsed_ms waits for `stop`). */
 int ecamd_event_create(void **ev);
 int ecamd_event_destroy(void *ev);
 int ecamd_event_record(void *ev, void *stream);

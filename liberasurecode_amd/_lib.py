@@ -66,6 +66,7 @@ def dev():
         _proto(d, "ecamd_init", C.c_int, [])
         _proto(d, "ecamd_device_count", C.c_int, [])
         _proto(d, "ecamd_last_error", C.c_char_p, [])
+        _proto(d, "ecamd_tune", C.c_int, [C.c_char_p, C.c_int])
         _proto(d, "ecamd_map_create", C.c_int, [IP, C.c_int, C.c_int, C.POINTER(VP)])
         _proto(d, "ecamd_map_destroy", None, [VP])
         _proto(d, "ecamd_map_apply_strided", C.c_int,
@@ -85,6 +86,7 @@ def dev():
                [C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
         _proto(d, "ecamd_fill_splitmix", C.c_int,
                [VP, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_uint64, VP])
+        _proto(d, "ecamd_debug_stream_copy", C.c_int, [VP, VP, C.c_int64, VP])
         _proto(d, "ecamd_malloc", C.c_int, [C.POINTER(VP), C.c_int64])
         _proto(d, "ecamd_free", C.c_int, [VP])
         _proto(d, "ecamd_memcpy_h2d", C.c_int, [VP, VP, C.c_int64])

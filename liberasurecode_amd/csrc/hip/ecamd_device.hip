@@ -72,14 +72,16 @@ int ensure_device(int* dev_out)
     }
     if (!di.lds_attr_set) {
         // Allow the full 160 KiB of gfx950 LDS as dynamic shared memory.
-        const void* ks[] = {
-            reinterpret_cast<const void*>(&gf16_apply_kernel<2, false>),
-            reinterpret_cast<const void*>(&gf16_apply_kernel<4, false>),
-            reinterpret_cast<const void*>(&gf16_apply_kernel<8, false>),
-            reinterpret_cast<const void*>(&gf16_apply_kernel<2, true>),
-            reinterpret_cast<const void*>(&gf16_apply_kernel<4, true>),
-            reinterpret_cast<const void*>(&gf16_apply_kernel<8, true>),
-        };
+#define K_(W, P, N) reinterpret_cast<const void*>(&gf16_apply_kernel<W, P, N>)
+        const void* ks[] = {K_(2, false, false), K_(4, false, false), K_(8, false, false),
+                            K_(2, true, false),  K_(4, true, false),  K_(8, true, false),
+                            K_(2, false, true),  K_(4, false, true),  K_(8, false, true),
+                            K_(2, true, true),   K_(4, true, true),   K_(8, true, true),
+                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<1, false>),
+                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<1, true>),
+                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<2, false>),
+                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<2, true>)};
+#undef K_
         for (const void* k : ks)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         di.lds_attr_set = true;
@@ -95,6 +97,17 @@ int cu_count(int dev)
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Launch-geometry knobs (0 = automatic).  Set through ecamd_tune() for sweeps; defaults are the
+// measured best on MI355X ("Tuning").
+struct Tuning {
+    int threads = 0;     // threads per workgroup of the gf16 kernel
+    int wgs_per_cu = 0;  // resident workgroups per CU the grid is sized for
+    int nt = 1;          // 1: non-temporal global loads/stores in the gf16 kernel (+7% on MI355X)
+    int exp_ch = 0;      // sweeps: experimental W=4 kernel with 1 or 2 chunks per lane
+    int ablate = 0;      // sweeps: experimental kernel without LDS lookups (wrong results)
+};
+Tuning g_tune;
 
 }  // namespace
 
@@ -149,11 +162,13 @@ struct Geometry {
     uint32_t ntiles;
 };
 
-int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g)
+int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chunks = 1)
 {
     int wgs = lds ? static_cast<int>(std::min<size_t>(8, std::max<size_t>(1, kLdsBytes / lds))) : 8;
     int threads = lds ? std::min(1024, std::max(256, (1024 / wgs) / 64 * 64)) : 256;
-    int64_t span = static_cast<int64_t>(threads) * 16;
+    if (lds && g_tune.threads > 0) threads = g_tune.threads;
+    if (lds && g_tune.wgs_per_cu > 0) wgs = std::min<int>(g_tune.wgs_per_cu, std::max<size_t>(1, kLdsBytes / lds));
+    int64_t span = static_cast<int64_t>(threads) * 16 * chunks;
     int64_t tps = (bs + span - 1) / span;
     int64_t nt = tps * nstripes;
     if (nt >= (1ll << 32)) return fail(ECAMD_EINVAL, "batch too large: %lld tiles", (long long)nt);
@@ -180,15 +195,31 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
         for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[p.col0 + j];
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
         Geometry g;
-        int rc = geometry(map->device, p.bytes, bs, nstripes, g);
+        const bool exp = g_tune.exp_ch > 0 && p.width == 4 && !PTRS;
+        int rc = geometry(map->device, p.bytes, bs, nstripes, g, exp ? g_tune.exp_ch : 1);
         if (rc) return rc;
         a.ntiles = g.ntiles;
         a.tiles_per_stripe = g.tiles_per_stripe;
         dim3 grid(g.grid), block(g.threads);
-        switch (p.width) {
-        case 2: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS>), grid, block, g.lds, st, a); break;
-        case 4: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS>), grid, block, g.lds, st, a); break;
-        default: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS>), grid, block, g.lds, st, a); break;
+        if (exp) {
+            const int v = (g_tune.exp_ch == 2 ? 2 : 0) + (g_tune.ablate ? 1 : 0);
+            switch (v) {
+            case 0: hipLaunchKernelGGL((gf16_apply_exp_kernel<1, false>), grid, block, g.lds, st, a); break;
+            case 1: hipLaunchKernelGGL((gf16_apply_exp_kernel<1, true>), grid, block, g.lds, st, a); break;
+            case 2: hipLaunchKernelGGL((gf16_apply_exp_kernel<2, false>), grid, block, g.lds, st, a); break;
+            default: hipLaunchKernelGGL((gf16_apply_exp_kernel<2, true>), grid, block, g.lds, st, a); break;
+            }
+            HIP_TRY(hipGetLastError());
+            continue;
+        }
+        const bool nt = g_tune.nt != 0;
+        switch (p.width * 2 + (nt ? 1 : 0)) {
+        case 4: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, false>), grid, block, g.lds, st, a); break;
+        case 5: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, true>), grid, block, g.lds, st, a); break;
+        case 8: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, false>), grid, block, g.lds, st, a); break;
+        case 9: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, true>), grid, block, g.lds, st, a); break;
+        case 16: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, false>), grid, block, g.lds, st, a); break;
+        default: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, true>), grid, block, g.lds, st, a); break;
         }
         HIP_TRY(hipGetLastError());
     }
@@ -308,6 +339,28 @@ int rs_run(const RsEntry& e, void* base, int64_t stripe_stride, int64_t frag_str
 extern "C" {
 
 int ecamd_init(void) { return ensure_device(nullptr); }
+
+int ecamd_tune(const char* key, int value)
+{
+    if (!key) return fail(ECAMD_EINVAL, "null key");
+    std::string k(key);
+    if (k == "threads") {
+        if (value != 0 && (value < 64 || value > 1024 || value % 64))
+            return fail(ECAMD_EINVAL, "threads must be a multiple of 64 in [64,1024]");
+        g_tune.threads = value;
+    } else if (k == "wgs_per_cu") {
+        g_tune.wgs_per_cu = std::max(0, std::min(value, 8));
+    } else if (k == "nt") {
+        g_tune.nt = value != 0;  // note: the default is 1; ecamd_tune("nt", 0) turns it off
+    } else if (k == "exp_ch") {
+        g_tune.exp_ch = (value == 1 || value == 2) ? value : 0;
+    } else if (k == "ablate") {
+        g_tune.ablate = value != 0;
+    } else {
+        return fail(ECAMD_EINVAL, "unknown tuning key %s", key);
+    }
+    return 0;
+}
 
 int ecamd_device_count(void)
 {
@@ -486,6 +539,20 @@ int ecamd_fill_splitmix(void* base, int64_t stripe_stride, int64_t frag_stride, 
     int64_t grid = std::min<int64_t>((total + 255) / 256, static_cast<int64_t>(cu_count(dev)) * 16);
     hipLaunchKernelGGL(splitmix_fill_kernel, dim3(static_cast<int>(std::max<int64_t>(grid, 1))),
                        dim3(256), 0, static_cast<hipStream_t>(stream), f);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_debug_stream_copy(void* dst, const void* src, int64_t bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!aligned16(dst) || !aligned16(src) || bytes % 16)
+        return fail(ECAMD_EINVAL, "stream copy needs 16-byte aligned pointers and size");
+    hipLaunchKernelGGL(stream_copy_kernel, dim3(cu_count(dev) * 8), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), static_cast<uint4*>(dst),
+                       static_cast<const uint4*>(src), bytes / 16);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -31,6 +31,30 @@ namespace {
 
 __device__ __forceinline__ uint4 load16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 stream_load16(const uint8_t* p)
+{
+    if constexpr (NT) {
+        u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *reinterpret_cast<const uint4*>(p);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ void stream_store16(uint8_t* p, uint4 v)
+{
+    if constexpr (NT) {
+        u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+    } else {
+        *reinterpret_cast<uint4*>(p) = v;
+    }
+}
+
 // Partial 16-byte chunk at the end of a fragment: bytes [0, rem) of p, zero filled.
 __device__ __forceinline__ uint4 load_tail(const uint8_t* p, int rem)
 {
@@ -107,7 +131,7 @@ __device__ __forceinline__ void mac_chunk(const uint8_t* tl, uint4 x, uint32_t (
     }
 }
 
-template <int W, bool PTRS, bool TAIL>
+template <int W, bool PTRS, bool NT, bool TAIL>
 __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* lds, uint32_t s,
                                            int64_t off, int rem)
 {
@@ -122,7 +146,7 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
 
     auto fetch = [&](int j) -> uint4 {
         const uint8_t* p = in_frag<PTRS>(a, s, j) + off;
-        return TAIL ? load_tail(p, rem) : load16(p);
+        return TAIL ? load_tail(p, rem) : stream_load16<NT>(p);
     };
     uint4 cur[4], nxt[4];
 #pragma unroll
@@ -159,13 +183,13 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
         if (TAIL)
             store_tail(q, v, rem);
         else
-            *reinterpret_cast<uint4*>(q) = v;
+            stream_store16<NT>(q, v);
     }
 }
 
 }  // namespace
 
-template <int W, bool PTRS>
+template <int W, bool PTRS, bool NT>
 __global__ void __launch_bounds__(1024) gf16_apply_kernel(const ApplyArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -183,18 +207,18 @@ __global__ void __launch_bounds__(1024) gf16_apply_kernel(const ApplyArgs a)
         const int64_t rem = a.bs - off;
         if (rem <= 0) continue;
         if (rem >= 16)
-            apply_tile<W, PTRS, false>(a, lds, s, off, 16);
+            apply_tile<W, PTRS, NT, false>(a, lds, s, off, 16);
         else
-            apply_tile<W, PTRS, true>(a, lds, s, off, static_cast<int>(rem));
+            apply_tile<W, PTRS, NT, true>(a, lds, s, off, static_cast<int>(rem));
     }
 }
 
-template __global__ void gf16_apply_kernel<2, false>(const ApplyArgs);
-template __global__ void gf16_apply_kernel<4, false>(const ApplyArgs);
-template __global__ void gf16_apply_kernel<8, false>(const ApplyArgs);
-template __global__ void gf16_apply_kernel<2, true>(const ApplyArgs);
-template __global__ void gf16_apply_kernel<4, true>(const ApplyArgs);
-template __global__ void gf16_apply_kernel<8, true>(const ApplyArgs);
+#define ECAMD_INST(W, P, N) template __global__ void gf16_apply_kernel<W, P, N>(const ApplyArgs);
+ECAMD_INST(2, false, false) ECAMD_INST(4, false, false) ECAMD_INST(8, false, false)
+ECAMD_INST(2, true, false) ECAMD_INST(4, true, false) ECAMD_INST(8, true, false)
+ECAMD_INST(2, false, true) ECAMD_INST(4, false, true) ECAMD_INST(8, false, true)
+ECAMD_INST(2, true, true) ECAMD_INST(4, true, true) ECAMD_INST(8, true, true)
+#undef ECAMD_INST
 
 // ---------------------------------------------------------------- flat XOR ----
 

@@ -39,10 +39,13 @@ struct FillArgs {
     uint64_t seed_base;
 };
 
-template <int W, bool PTRS>
+template <int W, bool PTRS, bool NT>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
+template <int CH, bool ABLATE>
+__global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);
 __global__ void splitmix_fill_kernel(FillArgs f);
+__global__ void stream_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n);
 
 }  // namespace ecamd

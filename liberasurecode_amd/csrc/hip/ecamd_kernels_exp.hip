@@ -1,0 +1,147 @@
+// ecamd_kernels_exp.hip -- tuning variants of the W=4 strided GF(2^16) kernel (sweeps only).
+//
+// CH     : 16-byte chunks per lane per tile (1 or 2); 2 doubles the bytes each lane has in
+//          flight and halves the tile bookkeeping.
+// ABLATE : skip the LDS lookups (acc ^= input) -- WRONG RESULTS, used only to price the LDS
+//          work against pure streaming on the same launch geometry (cdna_hip_programming.md §7
+//          "ablate").  Never reachable from the codec entry points: only ecamd_tune("ablate").
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ecamd_kernels.hpp"
+
+namespace ecamd {
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ldnt(const uint8_t* p)
+{
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void stnt(uint8_t* p, uint4 v)
+{
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
+template <bool ABLATE>
+__device__ __forceinline__ void mac4(const uint8_t* tl, uint4 x, uint32_t (&acc)[8][2])
+{
+    const uint8_t* th = tl + 256 * 8;
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const uint32_t v = xs[w >> 1] >> ((w & 1) * 16);
+        if constexpr (ABLATE) {
+            acc[w][0] ^= v;
+            acc[w][1] ^= v;
+        } else {
+            uint2 e0 = *reinterpret_cast<const uint2*>(tl + (v & 0xffu) * 8);
+            uint2 e1 = *reinterpret_cast<const uint2*>(th + ((v >> 8) & 0xffu) * 8);
+            acc[w][0] ^= e0.x ^ e1.x;
+            acc[w][1] ^= e0.y ^ e1.y;
+        }
+    }
+}
+
+}  // namespace
+
+template <int CH, bool ABLATE>
+__global__ void __launch_bounds__(1024) gf16_apply_exp_kernel(const ApplyArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int tbytes = a.ncols * 512 * 8;
+    for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
+        *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
+    __syncthreads();
+    const int K = a.ncols;
+    const int64_t cstride = static_cast<int64_t>(blockDim.x) * 16;
+    const int64_t span = cstride * CH;
+    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int64_t off = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span +
+                            static_cast<int64_t>(threadIdx.x) * 16;
+        // sweeps run on 16-byte multiples of the tile span only
+        if (off + (CH - 1) * cstride + 16 > a.bs) continue;
+        const uint8_t* ib = a.in_base + static_cast<int64_t>(s) * a.in_stride + off;
+        uint32_t acc[CH][8][2];
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+#pragma unroll
+            for (int w = 0; w < 8; w++) acc[c][w][0] = acc[c][w][1] = 0u;
+        uint4 cur[4][CH], nxt[4][CH];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                cur[i][c] = (i < K) ? ldnt(ib + a.in_off[i] + c * cstride) : make_uint4(0, 0, 0, 0);
+        for (int j0 = 0; j0 < K; j0 += 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < CH; c++)
+                    nxt[i][c] = (j0 + 4 + i < K) ? ldnt(ib + a.in_off[j0 + 4 + i] + c * cstride)
+                                                 : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (j0 + i < K)
+#pragma unroll
+                    for (int c = 0; c < CH; c++)
+                        mac4<ABLATE>(lds + static_cast<size_t>(j0 + i) * 4096, cur[i][c], acc[c]);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
+        }
+        uint8_t* ob = a.out_base + static_cast<int64_t>(s) * a.out_stride + off;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            if (r >= a.nrows) break;
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                uint32_t o[4];
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const uint32_t A = acc[c][2 * d][r >> 1], B = acc[c][2 * d + 1][r >> 1];
+                    o[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+                }
+                stnt(ob + a.out_off[r] + c * cstride, make_uint4(o[0], o[1], o[2], o[3]));
+            }
+        }
+    }
+}
+
+template __global__ void gf16_apply_exp_kernel<1, false>(const ApplyArgs);
+template __global__ void gf16_apply_exp_kernel<2, false>(const ApplyArgs);
+template __global__ void gf16_apply_exp_kernel<1, true>(const ApplyArgs);
+template __global__ void gf16_apply_exp_kernel<2, true>(const ApplyArgs);
+
+}  // namespace ecamd
+
+namespace ecamd {
+
+// Streaming copy at 16 B per lane, 4 chunks in flight, non-temporal: the measured HBM ceiling
+// for one read + one write stream (DESIGN.md reports the roofline against it and the spec).
+__global__ void __launch_bounds__(256) stream_copy_kernel(uint4* __restrict__ dst,
+                                                          const uint4* __restrict__ src, int64_t n)
+{
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        v4 a = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src + i));
+        v4 b = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src + i + stride));
+        v4 c = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src + i + 2 * stride));
+        v4 d = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src + i + 3 * stride));
+        __builtin_nontemporal_store(a, reinterpret_cast<v4*>(dst + i));
+        __builtin_nontemporal_store(b, reinterpret_cast<v4*>(dst + i + stride));
+        __builtin_nontemporal_store(c, reinterpret_cast<v4*>(dst + i + 2 * stride));
+        __builtin_nontemporal_store(d, reinterpret_cast<v4*>(dst + i + 3 * stride));
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+}  // namespace ecamd
