@@ -80,6 +80,16 @@ int ecamd_rs_reconstruct(int k, int m, const int *missing, int dest, void *base,
                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
                          int nstripes, void *stream);
 
+/* ---- synchronous host-buffer execution (used by the per-call drop-in ABIs) ----
+ * Pooled pinned staging + two streams, chunked so host copies overlap PCIe and the kernel.
+ * ecamd_host_map_apply: out[r] = sum_j coeff[r*K+j] * in[j] over GF(2^16).
+ * ecamd_host_xor_apply: out[r] = XOR of bufs[b] for bits b of sources[r] (nbuf <= 64, at most 32
+ * distinct buffers referenced); outputs may alias bufs, every output sees the original inputs. */
+int ecamd_host_map_apply(const int *coeff, int R, int K, const void *const *in, void *const *out,
+                         int64_t blocksize);
+int ecamd_host_xor_apply(const uint64_t *sources, int R, int nbuf, const void *const *bufs,
+                         void *const *out, int64_t blocksize);
+
 /* ---- synthetic data: splitmix64 stream per fragment, seed = seed_base ^ (s<<8) ^ f ---- */
 int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, int nfrags,
                         int64_t blocksize, int nstripes, int stripe0, uint64_t seed_base,

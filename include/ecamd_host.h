@@ -49,6 +49,25 @@ int ecamd_rs_reconstruct_map(const int *G, int k, int m, const int *missing, int
 int ecamd_split_tables(const int *coeff, int R, int K, int row0, int width, int col0, int ncols,
                        uint8_t *out);
 
+/* ---- flat-XOR HD codes (src/builtin/xor_codes/) ---- */
+
+/* Parity / data bitmaps of a supported (k, m, hd) code (include/xor_codes/xor_hd_code_defs.h);
+ * -1 if the code is not one init_xor_hd_code accepts (xor_hd_code.c:664-693). */
+int ecamd_xor_code_tables(int k, int m, int hd, unsigned int *parity_bms, unsigned int *data_bms);
+
+/* Exact plan of a reference operation on k+m buffers: op 0 = xor_code_encode, 1 = xor_hd_decode
+ * (arg = decode_parity), 2 = xor_reconstruct_one (arg = index).  outputs[*nout] are the buffers
+ * the reference modifies, sources[i] the bitmask of ORIGINAL buffers whose XOR output i ends up
+ * holding.  Returns the reference's return code (-100 for bad arguments). */
+int ecamd_xor_plan(int op, int k, int m, int hd, const unsigned int *parity_bms,
+                   const unsigned int *data_bms, const int *missing, int arg, int *outputs,
+                   uint64_t *sources, int *nout);
+
+/* xor_hd_fragments_needed (xor_hd_code.c:209-412); needed ends with -1. */
+int ecamd_xor_fragments_needed(int k, int m, int hd, const unsigned int *parity_bms,
+                               const unsigned int *data_bms, const int *to_reconstruct,
+                               const int *to_exclude, int *needed);
+
 #ifdef __cplusplus
 }
 #endif

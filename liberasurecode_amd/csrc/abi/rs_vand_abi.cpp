@@ -10,8 +10,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <map>
-#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -28,111 +26,14 @@ void report(const char* what)
     std::fprintf(stderr, "liberasurecode_rs_vand (MI355X): %s: %s\n", what, ecamd_last_error());
 }
 
-// ---- device maps, cached by content (callers may free() and re-make matrices freely) ----
-struct MapHolder {
-    ecamd_map* map = nullptr;
-    ~MapHolder() { ecamd_map_destroy(map); }
-};
-std::mutex g_map_mu;
-std::map<std::vector<int>, std::shared_ptr<MapHolder>> g_maps;
-
-std::shared_ptr<MapHolder> get_map(const std::vector<int>& coeff, int R, int K)
-{
-    std::vector<int> key = {R, K};
-    key.insert(key.end(), coeff.begin(), coeff.end());
-    {
-        std::lock_guard<std::mutex> lk(g_map_mu);
-        auto it = g_maps.find(key);
-        if (it != g_maps.end()) return it->second;
-    }
-    auto h = std::make_shared<MapHolder>();
-    if (ecamd_map_create(coeff.data(), R, K, &h->map) != 0) {
-        report("map create");
-        return nullptr;
-    }
-    std::lock_guard<std::mutex> lk(g_map_mu);
-    if (g_maps.size() > 4096) g_maps.clear();  // holders in flight keep their map alive
-    return g_maps.emplace(key, h).first->second;
-}
-
-// ---- staging contexts: one stream + one device slab each, pooled across threads ----
-struct Staging {
-    void* stream = nullptr;
-    void* d_slab = nullptr;
-    int64_t cap = 0;
-};
-std::mutex g_pool_mu;
-std::vector<Staging*> g_pool;
-
-Staging* acquire(int64_t bytes)
-{
-    Staging* s = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (!g_pool.empty()) {
-            s = g_pool.back();
-            g_pool.pop_back();
-        }
-    }
-    if (!s) {
-        s = new Staging();
-        if (ecamd_stream_create(&s->stream) != 0) {
-            report("stream create");
-            delete s;
-            return nullptr;
-        }
-    }
-    if (s->cap < bytes) {
-        if (s->d_slab) ecamd_free(s->d_slab);
-        s->d_slab = nullptr;
-        s->cap = 0;
-        if (ecamd_malloc(&s->d_slab, bytes) != 0) {
-            report("device slab");
-            std::lock_guard<std::mutex> lk(g_pool_mu);
-            g_pool.push_back(s);
-            return nullptr;
-        }
-        s->cap = bytes;
-    }
-    return s;
-}
-
-void release(Staging* s)
-{
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.push_back(s);
-}
-
-// out[r] = sum_j coeff[r][j] * in[j] for host buffers, through the GPU.
+// out[r] = sum_j coeff[r][j] * in[j] for host buffers, through the GPU (libecamd hostio).
 int run_map(const std::vector<int>& coeff, const std::vector<char*>& in,
             const std::vector<char*>& out, int blocksize)
 {
-    const int K = static_cast<int>(in.size()), R = static_cast<int>(out.size());
-    if (R == 0 || blocksize <= 0) return 0;
-    if (K == 0) {  // only possible after aliasing folds every input away
-        for (char* o : out) std::memset(o, 0, blocksize);
-        return 0;
-    }
-    auto map = get_map(coeff, R, K);
-    if (!map) return -1;
-    const int64_t pitch = (static_cast<int64_t>(blocksize) + 15) / 16 * 16;
-    Staging* st = acquire(pitch * (K + R));
-    if (!st) return -1;
-    char* slab = static_cast<char*>(st->d_slab);
-    std::vector<int64_t> in_off(K), out_off(R);
-    int rc = 0;
-    for (int j = 0; j < K && rc == 0; j++) {
-        in_off[j] = j * pitch;
-        rc = ecamd_memcpy_async(slab + in_off[j], in[j], blocksize, 0, st->stream);
-    }
-    for (int r = 0; r < R; r++) out_off[r] = (K + r) * pitch;
-    if (rc == 0)
-        rc = ecamd_map_apply_strided(map->map, slab, 0, in_off.data(), slab, 0, out_off.data(),
-                                     blocksize, 1, st->stream);
-    for (int r = 0; r < R && rc == 0; r++)
-        rc = ecamd_memcpy_async(out[r], slab + out_off[r], blocksize, 1, st->stream);
-    if (rc == 0) rc = ecamd_stream_synchronize(st->stream);
-    release(st);
+    int rc = ecamd_host_map_apply(coeff.data(), static_cast<int>(out.size()),
+                                  static_cast<int>(in.size()),
+                                  reinterpret_cast<const void* const*>(in.data()),
+                                  reinterpret_cast<void* const*>(out.data()), blocksize);
     if (rc) report("region kernel");
     return rc ? -1 : 0;
 }

@@ -6,6 +6,7 @@
 
 #include "gf16.hpp"
 #include "tables.hpp"
+#include "xor_plan.hpp"
 
 using namespace ecamd;
 
@@ -81,6 +82,57 @@ int ecamd_split_tables(const int* coeff, int R, int K, int row0, int width, int 
     std::vector<uint8_t> img = build_split_tables(c, R, K, row0, width, col0, ncols);
     std::memcpy(out, img.data(), img.size());
     return static_cast<int>(img.size());
+}
+
+int ecamd_xor_code_tables(int k, int m, int hd, unsigned int* parity_bms, unsigned int* data_bms)
+{
+    XorCode c;
+    if (!xor_code_lookup(k, m, hd, c)) return -1;
+    if (parity_bms) std::memcpy(parity_bms, c.parity_bms, sizeof(unsigned int) * m);
+    if (data_bms) std::memcpy(data_bms, c.data_bms, sizeof(unsigned int) * k);
+    return 0;
+}
+
+int ecamd_xor_plan(int op, int k, int m, int hd, const unsigned int* parity_bms,
+                   const unsigned int* data_bms, const int* missing, int arg, int* outputs,
+                   uint64_t* sources, int* nout)
+{
+    XorCode c;
+    c.k = k;
+    c.m = m;
+    c.hd = hd;
+    c.parity_bms = parity_bms;
+    c.data_bms = data_bms;
+    if (!parity_bms || !data_bms || k <= 0 || m <= 0 || k + m > 63 || !nout) return -100;
+    XorPlan p;
+    if (op == 0)
+        p = xor_plan_encode(c);
+    else if (op == 1)
+        p = xor_plan_decode(c, minus1_list(missing), arg);
+    else
+        p = xor_plan_reconstruct_one(c, minus1_list(missing), arg);
+    for (size_t i = 0; i < p.outputs.size(); i++) {
+        outputs[i] = p.outputs[i];
+        sources[i] = p.sources[i];
+    }
+    *nout = static_cast<int>(p.outputs.size());
+    return p.rc;
+}
+
+int ecamd_xor_fragments_needed(int k, int m, int hd, const unsigned int* parity_bms,
+                               const unsigned int* data_bms, const int* to_reconstruct,
+                               const int* to_exclude, int* needed)
+{
+    XorCode c;
+    c.k = k;
+    c.m = m;
+    c.hd = hd;
+    c.parity_bms = parity_bms;
+    c.data_bms = data_bms;
+    std::vector<int> out;
+    int rc = xor_fragments_needed(c, minus1_list(to_reconstruct), minus1_list(to_exclude), out);
+    if (rc >= 0 && needed) std::memcpy(needed, out.data(), out.size() * sizeof(int));
+    return rc;
 }
 
 }  // extern "C"

@@ -1,0 +1,255 @@
+// hostio.cpp -- synchronous host-buffer execution for the per-call drop-in ABIs
+// (liberasurecode_rs_vand.so.1, libXorcode.so.1): the reference contract is "caller-owned host
+// fragments in, results complete on return", called concurrently from many threads
+// (src/erasurecode.c:414, 543, 769 hold only a shared read lock around the codec calls).
+//
+// Each call borrows a pooled staging context (2 HIP streams, 2 pinned host slabs, 2 device slabs)
+// and walks the fragments in chunks: while the GPU runs chunk c (H2D -> kernel -> D2H on stream
+// c&1), the CPU packs chunk c+1 into the other pinned slab and unpacks chunk c-1.  Fragment maps
+// are cached by content, so callers may free() and rebuild matrices at will.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "ecamd.h"
+
+namespace {
+
+constexpr int64_t kChunkTarget = 8 << 20;  // bytes of all fragments per chunk (both directions)
+
+struct MapHolder {
+    ecamd_map* map = nullptr;
+    ~MapHolder() { ecamd_map_destroy(map); }
+};
+std::mutex g_map_mu;
+std::map<std::vector<int>, std::shared_ptr<MapHolder>> g_maps;
+
+std::shared_ptr<MapHolder> cached_map(const int* coeff, int R, int K, int* rc)
+{
+    std::vector<int> key = {R, K};
+    key.insert(key.end(), coeff, coeff + static_cast<size_t>(R) * K);
+    {
+        std::lock_guard<std::mutex> lk(g_map_mu);
+        auto it = g_maps.find(key);
+        if (it != g_maps.end()) return it->second;
+    }
+    auto h = std::make_shared<MapHolder>();
+    *rc = ecamd_map_create(coeff, R, K, &h->map);
+    if (*rc) return nullptr;
+    std::lock_guard<std::mutex> lk(g_map_mu);
+    if (g_maps.size() > 4096) g_maps.clear();  // holders in flight keep their map alive
+    return g_maps.emplace(key, h).first->second;
+}
+
+struct Slot {
+    void* stream = nullptr;
+    void* event = nullptr;
+    char* h_pin = nullptr;
+    char* d_buf = nullptr;
+};
+
+struct Staging {
+    Slot slot[2];
+    int64_t cap = 0;  // bytes per slab
+    bool ok = false;
+    ~Staging()
+    {
+        for (auto& s : slot) {
+            if (s.h_pin) ecamd_host_free(s.h_pin);
+            if (s.d_buf) ecamd_free(s.d_buf);
+        }
+    }
+};
+
+std::mutex g_pool_mu;
+std::vector<Staging*> g_pool;
+
+int grow(Staging* st, int64_t bytes)
+{
+    if (st->cap >= bytes) return 0;
+    for (auto& s : st->slot) {
+        if (s.h_pin) ecamd_host_free(s.h_pin);
+        if (s.d_buf) ecamd_free(s.d_buf);
+        s.h_pin = s.d_buf = nullptr;
+        void* p = nullptr;
+        int rc = ecamd_host_alloc(&p, bytes);
+        if (rc) return rc;
+        s.h_pin = static_cast<char*>(p);
+        rc = ecamd_malloc(&p, bytes);
+        if (rc) return rc;
+        s.d_buf = static_cast<char*>(p);
+    }
+    st->cap = bytes;
+    return 0;
+}
+
+Staging* acquire(int64_t bytes, int* rc)
+{
+    Staging* st = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (!g_pool.empty()) {
+            st = g_pool.back();
+            g_pool.pop_back();
+        }
+    }
+    if (!st) {
+        st = new Staging();
+        for (auto& s : st->slot) {
+            if ((*rc = ecamd_stream_create(&s.stream)) || (*rc = ecamd_event_create(&s.event))) {
+                delete st;
+                return nullptr;
+            }
+        }
+    }
+    if ((*rc = grow(st, bytes))) {
+        delete st;
+        return nullptr;
+    }
+    return st;
+}
+
+void release(Staging* st)
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back(st);
+}
+
+// Kernel launcher for one chunk: inputs at d + j*pitch, outputs at d + (K+r)*pitch.
+using Launch = int (*)(const void* ctx, char* d, int64_t pitch, int64_t bytes, void* stream);
+
+int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t bs,
+                const void* ctx, Launch launch)
+{
+    const int64_t nfr = K + R;
+    int64_t chunk = std::max<int64_t>(16, (kChunkTarget / nfr) / 16 * 16);
+    const int64_t padded = (bs + 15) / 16 * 16;
+    chunk = std::min(chunk, padded);
+    int rc = 0;
+    Staging* st = acquire(chunk * nfr, &rc);
+    if (!st) return rc;
+    const int64_t nchunks = (bs + chunk - 1) / chunk;
+    int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
+    auto drain = [&](int s) -> int {
+        if (pending[s] < 0) return 0;
+        int r = ecamd_stream_synchronize(st->slot[s].stream);
+        if (r) return r;
+        const int64_t off = pending[s] * chunk;
+        const int64_t n = std::min(chunk, bs - off);
+        for (int o = 0; o < R; o++)
+            std::memcpy(out[o] + off, st->slot[s].h_pin + (K + o) * chunk, static_cast<size_t>(n));
+        pending[s] = -1;
+        return 0;
+    };
+    for (int64_t c = 0; c < nchunks && rc == 0; c++) {
+        const int s = static_cast<int>(c & 1);
+        Slot& sl = st->slot[s];
+        if ((rc = drain(s))) break;
+        const int64_t off = c * chunk;
+        const int64_t n = std::min(chunk, bs - off);
+        for (int j = 0; j < K; j++)
+            std::memcpy(sl.h_pin + j * chunk, in[j] + off, static_cast<size_t>(n));
+        for (int j = 0; j < K && rc == 0; j++)
+            rc = ecamd_memcpy_async(sl.d_buf + j * chunk, sl.h_pin + j * chunk, n, 0, sl.stream);
+        if (rc == 0) rc = launch(ctx, sl.d_buf, chunk, n, sl.stream);
+        for (int o = 0; o < R && rc == 0; o++)
+            rc = ecamd_memcpy_async(sl.h_pin + (K + o) * chunk, sl.d_buf + (K + o) * chunk, n, 1,
+                                    sl.stream);
+        pending[s] = c;
+    }
+    for (int s = 0; s < 2; s++) {
+        int r = drain(s);
+        if (rc == 0) rc = r;
+    }
+    release(st);
+    return rc;
+}
+
+struct MapCtx {
+    const ecamd_map* map;
+    int K, R;
+};
+
+int launch_map(const void* vctx, char* d, int64_t pitch, int64_t bytes, void* stream)
+{
+    const MapCtx* c = static_cast<const MapCtx*>(vctx);
+    std::vector<int64_t> io(c->K), oo(c->R);
+    for (int j = 0; j < c->K; j++) io[j] = j * pitch;
+    for (int r = 0; r < c->R; r++) oo[r] = (c->K + r) * pitch;
+    return ecamd_map_apply_strided(c->map, d, 0, io.data(), d, 0, oo.data(), bytes, 1, stream);
+}
+
+struct XorCtx {
+    std::vector<uint32_t> masks;
+    int K, R;
+};
+
+int launch_xor(const void* vctx, char* d, int64_t pitch, int64_t bytes, void* stream)
+{
+    const XorCtx* c = static_cast<const XorCtx*>(vctx);
+    std::vector<int64_t> io(c->K), oo(c->R);
+    for (int j = 0; j < c->K; j++) io[j] = j * pitch;
+    for (int r = 0; r < c->R; r++) oo[r] = (c->K + r) * pitch;
+    return ecamd_xor_apply_strided(c->masks.data(), c->R, c->K, d, 0, io.data(), d, 0, oo.data(),
+                                   bytes, 1, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ecamd_host_map_apply(const int* coeff, int R, int K, const void* const* in,
+                         void* const* out, int64_t blocksize)
+{
+    if (R <= 0 || blocksize <= 0) return 0;
+    if (K <= 0) {
+        for (int r = 0; r < R; r++) std::memset(out[r], 0, static_cast<size_t>(blocksize));
+        return 0;
+    }
+    int rc = 0;
+    auto mh = cached_map(coeff, R, K, &rc);
+    if (!mh) return rc ? rc : ECAMD_EINVAL;
+    MapCtx ctx{mh->map, K, R};
+    return run_chunked(K, R, reinterpret_cast<const char* const*>(in),
+                       reinterpret_cast<char* const*>(out), blocksize, &ctx, launch_map);
+}
+
+int ecamd_host_xor_apply(const uint64_t* sources, int R, int nbuf, const void* const* bufs,
+                         void* const* out, int64_t blocksize)
+{
+    if (R <= 0 || blocksize <= 0) return 0;
+    // compact the referenced originals into input slots 0..K-1
+    uint64_t used = 0;
+    for (int r = 0; r < R; r++) used |= sources[r];
+    std::vector<const char*> in;
+    std::vector<int> slot(64, -1);
+    for (int b = 0; b < nbuf && b < 64; b++)
+        if ((used >> b) & 1u) {
+            slot[b] = static_cast<int>(in.size());
+            in.push_back(static_cast<const char*>(bufs[b]));
+        }
+    if (in.size() > 32) return ECAMD_EINVAL;
+    XorCtx ctx;
+    ctx.K = static_cast<int>(in.size());
+    ctx.R = R;
+    for (int r = 0; r < R; r++) {
+        uint32_t mk = 0;
+        for (int b = 0; b < nbuf && b < 64; b++)
+            if ((sources[r] >> b) & 1u) mk |= 1u << slot[b];
+        ctx.masks.push_back(mk);
+    }
+    if (ctx.K == 0) {
+        for (int r = 0; r < R; r++) std::memset(out[r], 0, static_cast<size_t>(blocksize));
+        return 0;
+    }
+    // outputs may alias inputs: results land in pinned memory first and are copied back only
+    // after the whole chunk's inputs were packed, so every output sees the ORIGINAL inputs.
+    return run_chunked(ctx.K, R, in.data(), reinterpret_cast<char* const*>(out), blocksize, &ctx,
+                       launch_xor);
+}
+
+}  // extern "C"

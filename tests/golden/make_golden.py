@@ -229,12 +229,118 @@ def rs_cases(lib):
     return out
 
 
+class XorCodeT(C.Structure):
+    # include/xor_codes/xor_code.h:54-65
+    _fields_ = [("k", C.c_int), ("m", C.c_int), ("hd", C.c_int),
+                ("parity_bms", C.POINTER(C.c_uint)), ("data_bms", C.POINTER(C.c_uint)),
+                ("decode", C.c_void_p), ("encode", C.c_void_p), ("fragments_needed", C.c_void_p)]
+
+
+XOR_CODES = ([(3, 3, 3)] + [(k, 6, 3) for k in range(6, 16)] + [(k, 5, 3) for k in range(5, 11)]
+             + [(k, 6, 4) for k in range(6, 21)] + [(k, 5, 4) for k in range(5, 11)])
+
+
+def load_xor():
+    lib = C.CDLL(os.path.join(REF, "libXorcode.so.1"))
+    XP = C.POINTER(XorCodeT)
+    lib.init_xor_hd_code.restype = XP
+    lib.init_xor_hd_code.argtypes = [C.c_int, C.c_int, C.c_int]
+    lib.xor_code_encode.argtypes = [XP, C.c_void_p, C.c_void_p, C.c_int]
+    lib.xor_hd_decode.argtypes = [XP, C.c_void_p, C.c_void_p, IP, C.c_int, C.c_int]
+    lib.xor_reconstruct_one.argtypes = [XP, C.c_void_p, C.c_void_p, IP, C.c_int, C.c_int]
+    lib.xor_hd_fragments_needed.argtypes = [XP, IP, IP, IP]
+    return lib
+
+
+def xor_patterns(n, seed):
+    """Deterministic erasure patterns: all of size 1 and 2, a sample of size 3 and 4 (the
+    reference's own test covers every pattern below hd, test/builtin/xor_codes/test_xor_hd_code.c)."""
+    import random
+    rnd = random.Random(seed)
+    pats = [list(p) for r in (1, 2) for p in itertools.combinations(range(n), r)]
+    threes = [list(p) for p in itertools.combinations(range(n), 3)]
+    pats += threes if len(threes) <= 400 else rnd.sample(threes, 400)
+    fours = [list(p) for p in itertools.combinations(range(n), 4)]
+    pats += rnd.sample(fours, min(40, len(fours)))
+    # order inside a missing list matters to the reference (it walks the list): shuffle some
+    for p in pats[::3]:
+        rnd.shuffle(p)
+    return pats
+
+
+def xor_case_buffers(k, m, bs, seed):
+    return [np.array(x) for x in stripe_fragments(seed, k + m, bs, base=0x50A)]
+
+
+def xor_cases(lib, bs=48):
+    """Per code: tables, encode (accumulating into non-zero parity), decode / reconstruct on
+    INCONSISTENT random buffers for every listed pattern, fragments_needed."""
+    out = []
+    for k, m, hd in XOR_CODES:
+        code = lib.init_xor_hd_code(k, m, hd)
+        rec = {"k": k, "m": m, "hd": hd, "bs": bs,
+               "parity_bms": [code.contents.parity_bms[i] for i in range(m)],
+               "data_bms": [code.contents.data_bms[i] for i in range(k)]}
+        bufs = xor_case_buffers(k, m, bs, k * 100 + m * 10 + hd)
+        b = Bufs(bufs)
+        lib.xor_code_encode(code, b.array(0, k), b.array(k, k + m), bs)
+        rec["encode_sha256"] = sha(b"".join(x.tobytes() for x in b.arrs))
+        pats = xor_patterns(k + m, k * 1000 + m * 10 + hd)
+        rec["patterns_seed"] = k * 1000 + m * 10 + hd
+        rcs, h = [], hashlib.sha256()
+        for p in pats:
+            bb = Bufs(xor_case_buffers(k, m, bs, 7 + len(rcs)))
+            rc = lib.xor_hd_decode(code, bb.array(0, k), bb.array(k, k + m), as_ip(p + [-1]), bs, 1)
+            rcs.append(rc)
+            for x in bb.arrs:
+                h.update(x.tobytes())
+        rec["decode_rc"] = rcs
+        rec["decode_sha256"] = h.hexdigest()
+        rcs, h = [], hashlib.sha256()
+        for p in pats:
+            if len(p) > 3:
+                continue
+            for idx in sorted(set(p)):
+                bb = Bufs(xor_case_buffers(k, m, bs, 11 + len(rcs)))
+                rc = lib.xor_reconstruct_one(code, bb.array(0, k), bb.array(k, k + m),
+                                             as_ip(p + [-1]), idx, bs)
+                rcs.append(rc)
+                for x in bb.arrs:
+                    h.update(x.tobytes())
+        rec["reconstruct_rc"] = rcs
+        rec["reconstruct_sha256"] = h.hexdigest()
+        fn = []
+        for p in pats:
+            if len(p) > 3:
+                continue
+            for split in range(len(p)):
+                recon, excl = p[:split + 1], p[split + 1:]
+                needed = (C.c_int * (k + m + 1))(*([-7] * (k + m + 1)))
+                rc = lib.xor_hd_fragments_needed(code, as_ip(recon + [-1]), as_ip(excl + [-1]),
+                                                 needed)
+                lst = []
+                if rc >= 0:
+                    for i in range(k + m + 1):
+                        if needed[i] == -1:
+                            break
+                        lst.append(needed[i])
+                fn.append([rc, lst])
+        rec["fragments_needed_head"] = fn[:40]
+        rec["fragments_needed_sha256"] = sha(json.dumps(fn, separators=(",", ":")).encode())
+        out.append(rec)
+    return out
+
+
 def main():
     rs = load_rs()
     data = rs_cases(rs)
     with open(os.path.join(HERE, "rs_vand.json"), "w") as f:
         json.dump(data, f, separators=(",", ":"))
     print("rs_vand.json:", {k: len(v) for k, v in data.items()})
+    xd = xor_cases(load_xor())
+    with open(os.path.join(HERE, "xor_codes.json"), "w") as f:
+        json.dump(xd, f, separators=(",", ":"))
+    print("xor_codes.json:", len(xd), "codes")
 
 
 if __name__ == "__main__":
