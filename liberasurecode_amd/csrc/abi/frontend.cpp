@@ -1,0 +1,1007 @@
+// frontend.cpp -- liberasurecode.so.1 (boundary B2): the liberasurecode C API over the MI355X
+// codec libraries of this repo.
+//
+// Restates the reference frontend (src/erasurecode.c, erasurecode_helpers.c,
+// erasurecode_preprocessing.c, erasurecode_postprocessing.c): instance registry under one
+// reader/writer lock, 80-byte fragment framing with zlib CRC-32 (and the legacy sign-extending
+// variant), the systematic decode fast path, and the two built-in backend shims:
+//   flat_xor_hd             -> libXorcode.so.1            (src/backends/xor/flat_xor_hd.c)
+//   liberasurecode_rs_vand  -> liberasurecode_rs_vand.so.1 (src/backends/rs_vand/liberasurecode_rs_vand.c)
+// Both libraries are the GPU drop-ins built next to this one (RUNPATH $ORIGIN), so every region
+// operation of encode / decode / reconstruct runs on the GPU.
+#include <dlfcn.h>
+#include <pthread.h>
+#include <syslog.h>
+#include <zlib.h>
+
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "erasurecode.h"
+#include "erasurecode_backend.h"
+#include "xor_code.h"
+
+#define LOGE(...) syslog(LOG_ERR, __VA_ARGS__)
+#define LOGW(...) syslog(LOG_WARNING, __VA_ARGS__)
+
+namespace {
+
+constexpr size_t kHdr = sizeof(fragment_header_t);
+static_assert(sizeof(fragment_metadata_t) == 59, "packed metadata");
+static_assert(sizeof(fragment_header_t) == 80, "packed header");
+
+uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+fragment_header_t* hdr(char* buf) { return reinterpret_cast<fragment_header_t*>(buf); }
+bool has_magic(char* buf) { return hdr(buf)->magic == LIBERASURECODE_FRAG_HEADER_MAGIC; }
+
+bool env_legacy_crc()
+{
+    const char* f = getenv("LIBERASURECODE_WRITE_LEGACY_CRC");
+    return f && !(f[0] == '\0' || (f[0] == '0' && f[1] == '\0'));
+}
+
+uint32_t zcrc(const void* p, size_t n)
+{
+    return static_cast<uint32_t>(crc32(0, static_cast<const Bytef*>(p), static_cast<uInt>(n)));
+}
+
+// ---------------------------------------------------------------- fragment buffers ----
+
+// 16-byte aligned, zeroed (get_aligned_buffer16, erasurecode_helpers.c:61-76)
+void* aligned_zero(size_t n)
+{
+    void* p = nullptr;
+    if (posix_memalign(&p, 16, n ? n : 1) != 0) return nullptr;
+    std::memset(p, 0, n);
+    return p;
+}
+
+// header + payload, zeroed, magic set (alloc_fragment_buffer, :124-138)
+char* new_fragment(int payload)
+{
+    char* f = static_cast<char*>(aligned_zero(static_cast<size_t>(payload) + kHdr));
+    if (f) hdr(f)->magic = LIBERASURECODE_FRAG_HEADER_MAGIC;
+    return f;
+}
+
+int frag_idx(char* f) { return has_magic(f) ? static_cast<int>(hdr(f)->meta.idx) : -1; }
+int frag_size(char* f) { return has_magic(f) ? static_cast<int>(hdr(f)->meta.size) : -1; }
+int frag_orig_size(char* f) { return has_magic(f) ? static_cast<int>(hdr(f)->meta.orig_data_size) : -1; }
+char* payload(char* f) { return f + kHdr; }
+
+// ---------------------------------------------------------------- registry ----
+
+pthread_rwlock_t g_lock = PTHREAD_RWLOCK_INITIALIZER;
+ec_backend* g_instances = nullptr;  // singly linked through link.sle_next
+int g_next_desc = 0;
+
+struct ReadLock {
+    int rc;
+    ReadLock() : rc(pthread_rwlock_rdlock(&g_lock)) {}
+    ~ReadLock()
+    {
+        if (rc == 0) pthread_rwlock_unlock(&g_lock);
+    }
+};
+
+ec_backend* find(int desc)
+{
+    for (ec_backend* b = g_instances; b; b = b->link.sle_next)
+        if (b->idesc == desc) return b;
+    return nullptr;
+}
+
+int new_desc()
+{
+    for (;;) {
+        if (++g_next_desc <= 0) g_next_desc = 1;
+        if (!find(g_next_desc)) return g_next_desc;
+    }
+}
+
+size_t zero_metadata(void*, int) { return 0; }
+size_t zero_offset(void*, int) { return 0; }
+
+// ------------------------------------------------ flat_xor_hd shim (flat_xor_hd.c:65-226) ----
+
+struct XorDesc {
+    xor_code_t* code;
+};
+
+int fx_encode(void* d, char** data, char** parity, int bs)
+{
+    xor_code_t* c = static_cast<XorDesc*>(d)->code;
+    c->encode(c, data, parity, bs);
+    return 0;
+}
+
+int fx_decode(void* d, char** data, char** parity, int* missing, int bs)
+{
+    xor_code_t* c = static_cast<XorDesc*>(d)->code;
+    return c->decode(c, data, parity, missing, bs, 1);
+}
+
+int fx_reconstruct(void* d, char** data, char** parity, int* missing, int dest, int bs)
+{
+    return xor_reconstruct_one(static_cast<XorDesc*>(d)->code, data, parity, missing, dest, bs);
+}
+
+int fx_needed(void* d, int* missing, int* exclude, int* needed)
+{
+    xor_code_t* c = static_cast<XorDesc*>(d)->code;
+    c->fragments_needed(c, missing, exclude, needed);
+    return 0;  // the reference shim ignores the library's return code
+}
+
+int fx_check_reconstruct(void* d, int* missing, int)
+{
+    const xor_code_t* c = static_cast<XorDesc*>(d)->code;
+    bool seen[EC_MAX_FRAGMENTS] = {};
+    for (int i = 0; missing[i] >= 0; i++)
+        if (missing[i] < EC_MAX_FRAGMENTS) seen[missing[i]] = true;
+    int avail = c->k + c->m;
+    for (bool s : seen) avail -= s ? 1 : 0;
+    const int k = c->k, m = c->m;
+    if (c->hd == 3) {
+        if (avail < 2) return -EINSUFFFRAGS;
+        if (m == 5 && ((k == 8 || k == 9) && avail < 3)) return -EINSUFFFRAGS;
+        if (m == 5 && k == 10 && avail < 4) return -EINSUFFFRAGS;
+        if (m == 6 && k >= 9 && k <= 11 && avail < 3) return -EINSUFFFRAGS;
+        if (m == 6 && k >= 12 && k <= 14 && avail < 4) return -EINSUFFFRAGS;
+        if (m == 6 && k == 15 && avail < 5) return -EINSUFFFRAGS;
+    } else {
+        if (avail < 3) return -EINSUFFFRAGS;
+        if (m == 5 && (k == 7 || k == 8) && avail < 4) return -EINSUFFFRAGS;
+        if (m == 5 && k + m - avail > 9) return -EINSUFFFRAGS;
+        if (m == 6 && avail < (k + m) / 2 - 3) return -EINSUFFFRAGS;
+    }
+    return 0;
+}
+
+int fx_element_size(void*) { return 32; }
+
+void* fx_init(ec_backend_args* args, void*)
+{
+    args->uargs.w = 32;
+    xor_code_t* c = init_xor_hd_code(args->uargs.k, args->uargs.m, args->uargs.hd);
+    if (!c) return nullptr;
+    auto* d = static_cast<XorDesc*>(std::malloc(sizeof(XorDesc)));
+    if (!d) {
+        std::free(c);
+        return nullptr;
+    }
+    d->code = c;
+    return d;
+}
+
+int fx_exit(void* d)
+{
+    std::free(static_cast<XorDesc*>(d)->code);
+    std::free(d);
+    return 0;
+}
+
+bool fx_compatible(uint32_t v) { return v == _VERSION(1, 0, 0); }
+
+ec_backend_op_stubs g_xor_ops = {fx_init, fx_exit, true, fx_encode, fx_decode, fx_needed,
+                                 fx_reconstruct, fx_element_size, fx_compatible, zero_metadata,
+                                 zero_offset, fx_check_reconstruct};
+
+// ---------------------------------- liberasurecode_rs_vand shim (rs_vand.c:82-311) ----
+
+struct RsDesc {
+    void (*init)(int, int);
+    void (*deinit)(void);
+    void (*free_matrix)(int*);
+    int* (*make_matrix)(int, int);
+    int (*encode)(int*, char**, char**, int, int, int);
+    int (*decode)(int*, char**, char**, int, int, int*, int, int);
+    int (*reconstruct)(int*, char**, char**, int, int, int*, int, int);
+    int* matrix;
+    int k, m, w;
+};
+
+int rs_encode(void* d, char** data, char** parity, int bs)
+{
+    auto* r = static_cast<RsDesc*>(d);
+    r->encode(r->matrix, data, parity, r->k, r->m, bs);
+    return 0;  // the reference shim discards the codec's return code
+}
+
+int rs_decode(void* d, char** data, char** parity, int* missing, int bs)
+{
+    auto* r = static_cast<RsDesc*>(d);
+    r->decode(r->matrix, data, parity, r->k, r->m, missing, bs, 1);
+    return 0;
+}
+
+int rs_reconstruct(void* d, char** data, char** parity, int* missing, int dest, int bs)
+{
+    auto* r = static_cast<RsDesc*>(d);
+    r->reconstruct(r->matrix, data, parity, r->k, r->m, missing, dest, bs);
+    return 0;
+}
+
+int rs_needed(void* d, int* missing, int* exclude, int* needed)
+{
+    auto* r = static_cast<RsDesc*>(d);
+    bool gone[EC_MAX_FRAGMENTS] = {};
+    for (int i = 0; exclude[i] >= 0; i++)
+        if (exclude[i] < EC_MAX_FRAGMENTS) gone[exclude[i]] = true;
+    for (int i = 0; missing[i] >= 0; i++)
+        if (missing[i] < EC_MAX_FRAGMENTS) gone[missing[i]] = true;
+    int j = 0;
+    for (int i = 0; i < r->k + r->m; i++) {
+        if (!gone[i]) needed[j++] = i;
+        if (j == r->k) {
+            needed[j] = -1;
+            return 0;
+        }
+    }
+    return -1;
+}
+
+int rs_element_size(void* d) { return static_cast<RsDesc*>(d)->w; }
+
+template <typename F>
+bool bind(void* so, const char* name, F& fn)
+{
+    fn = reinterpret_cast<F>(dlsym(so, name));
+    return fn != nullptr;
+}
+
+void* rs_init(ec_backend_args* args, void* so)
+{
+    auto* r = static_cast<RsDesc*>(std::calloc(1, sizeof(RsDesc)));
+    if (!r) return nullptr;
+    r->k = args->uargs.k;
+    r->m = args->uargs.m;
+    args->uargs.w = r->w = 16;
+    bool ok = r->k + r->m <= 65536 && bind(so, "init_liberasurecode_rs_vand", r->init) &&
+              bind(so, "deinit_liberasurecode_rs_vand", r->deinit) &&
+              bind(so, "make_systematic_matrix", r->make_matrix) &&
+              bind(so, "free_systematic_matrix", r->free_matrix) &&
+              bind(so, "liberasurecode_rs_vand_encode", r->encode) &&
+              bind(so, "liberasurecode_rs_vand_decode", r->decode) &&
+              bind(so, "liberasurecode_rs_vand_reconstruct", r->reconstruct);
+    if (ok) {
+        r->init(r->k, r->m);
+        r->matrix = r->make_matrix(r->k, r->m);
+        ok = r->matrix != nullptr;
+    }
+    if (!ok) {
+        std::free(r);
+        return nullptr;
+    }
+    return r;
+}
+
+int rs_exit(void* d)
+{
+    auto* r = static_cast<RsDesc*>(d);
+    r->free_matrix(r->matrix);
+    r->deinit();
+    std::free(r);
+    return 0;
+}
+
+bool rs_compatible(uint32_t v) { return v == _VERSION(1, 0, 0); }
+
+ec_backend_op_stubs g_rs_ops = {rs_init, rs_exit, true, rs_encode, rs_decode, rs_needed,
+                                rs_reconstruct, rs_element_size, rs_compatible, zero_metadata,
+                                zero_offset, nullptr};
+
+// ------------------------------------------------------------ backend table (:58-71) ----
+
+struct TableEntry {
+    ec_backend_id_t id;
+    const char* name;
+    const char* soname;
+    ec_backend_op_stubs* ops;  // nullptr: no shim in this build (reported as not available)
+};
+
+const TableEntry kBackends[EC_BACKENDS_MAX] = {
+    {EC_BACKEND_NULL, "null", "libnullcode.so.1", nullptr},
+    {EC_BACKEND_JERASURE_RS_VAND, "jerasure_rs_vand", "libJerasure.so.2", nullptr},
+    {EC_BACKEND_JERASURE_RS_CAUCHY, "jerasure_rs_cauchy", "libJerasure.so.2", nullptr},
+    {EC_BACKEND_FLAT_XOR_HD, "flat_xor_hd", "libXorcode.so.1", &g_xor_ops},
+    {EC_BACKEND_ISA_L_RS_VAND, "isa_l_rs_vand", "libisal.so.2", nullptr},
+    {EC_BACKEND_SHSS, "shss", "libshss.so.1", nullptr},
+    {EC_BACKEND_LIBERASURECODE_RS_VAND, "liberasurecode_rs_vand", "liberasurecode_rs_vand.so.1",
+     &g_rs_ops},
+    {EC_BACKEND_ISA_L_RS_CAUCHY, "isa_l_rs_cauchy", "libisal.so.2", nullptr},
+    {EC_BACKEND_LIBPHAZR, "libphazr", "libphazr.so.1", nullptr},
+    {EC_BACKEND_ISA_L_RS_VAND_INV, "isa_l_rs_vand_inv", "libisal.so.2", nullptr},
+    {EC_BACKEND_ISA_L_RS_LRC, "isa_l_rs_lrc", "libisal.so.2", nullptr},
+};
+
+void fill_common(ec_backend_common& c, const TableEntry& e)
+{
+    std::memset(&c, 0, sizeof(c));
+    c.id = e.id;
+    std::snprintf(c.name, sizeof(c.name), "%s", e.name);
+    c.soname = e.soname;
+    std::snprintf(c.soversion, sizeof(c.soversion), "1.0");
+    c.ops = e.ops;
+    c.ec_backend_version = _VERSION(1, 0, 0);
+}
+
+void* open_backend(const TableEntry& e)
+{
+    if (!e.ops) return nullptr;
+    return dlopen(e.soname, RTLD_LAZY | RTLD_LOCAL);
+}
+
+// ------------------------------------------------------------ framing ----
+
+// get_aligned_data_size (erasurecode_helpers.c:186-208): round up to k * w/8, in int.
+int aligned_size(ec_backend* be, int data_len)
+{
+    const int a = be->args.uargs.k * (be->args.uargs.w / 8);
+    return ((data_len + a - 1) / a) * a;
+}
+
+void write_checksum(char* f, ec_checksum_type_t ct, int bs)
+{
+    fragment_header_t* h = hdr(f);
+    h->meta.chksum_type = static_cast<uint8_t>(ct);
+    h->meta.chksum_mismatch = 0;
+    if (ct == CHKSUM_CRC32)
+        h->meta.chksum[0] = env_legacy_crc()
+                                ? static_cast<uint32_t>(liberasurecode_crc32_alt(0, payload(f), bs))
+                                : zcrc(payload(f), static_cast<size_t>(bs));
+}
+
+// add_fragment_metadata (erasurecode_postprocessing.c:37-69)
+void stamp(ec_backend* be, char* f, int idx, uint64_t orig, int bs, ec_checksum_type_t ct,
+           bool with_payload_crc)
+{
+    if (!has_magic(f)) return;
+    fragment_header_t* h = hdr(f);
+    h->libec_version = LIBERASURECODE_VERSION;
+    h->meta.idx = static_cast<uint32_t>(idx);
+    h->meta.orig_data_size = orig;
+    h->meta.size = static_cast<uint32_t>(bs);
+    h->meta.backend_id = static_cast<uint8_t>(be->common.id);
+    h->meta.backend_version = be->common.ec_backend_version;
+    h->meta.frag_backend_metadata_size =
+        static_cast<uint32_t>(be->common.ops->get_backend_metadata_size(be->desc.backend_desc, bs));
+    if (with_payload_crc) write_checksum(f, ct, bs);
+    h->metadata_chksum = env_legacy_crc() ? static_cast<uint32_t>(liberasurecode_crc32_alt(
+                                                0, &h->meta, sizeof(fragment_metadata_t)))
+                                          : zcrc(&h->meta, sizeof(fragment_metadata_t));
+}
+
+// fragments_to_string (erasurecode_preprocessing.c:269-370): concatenate data payloads.
+int assemble(int k, char** frags, int n, char** out, uint64_t* out_len)
+{
+    *out = nullptr;
+    if (n < k) return -1;
+    std::vector<char*> data(k, nullptr);
+    int orig = -1, have = 0;
+    for (int i = 0; i < n; i++) {
+        int idx = frag_idx(frags[i]), sz = frag_size(frags[i]);
+        if (idx < 0 || sz < 0) {
+            LOGE("Invalid fragment header information!");
+            return -EBADHEADER;
+        }
+        if (orig < 0) {
+            orig = frag_orig_size(frags[i]);
+        } else if (frag_orig_size(frags[i]) != orig) {
+            LOGE("Inconsistent orig_data_size in fragment header!");
+            return -EBADHEADER;
+        }
+        if (idx < k && !data[idx]) {
+            data[idx] = frags[i];
+            have++;
+        }
+    }
+    if (have != k) return -1;
+    char* s = static_cast<char*>(aligned_zero(static_cast<size_t>(orig > 0 ? orig : 0)));
+    if (!s) return -ENOMEM;
+    *out_len = static_cast<uint64_t>(orig);
+    int off = 0, left = orig;
+    for (int i = 0; i < k && left > 0; i++) {
+        int take = std::min(frag_size(data[i]), left);
+        std::memcpy(s + off, payload(data[i]), static_cast<size_t>(take));
+        left -= take;
+        off += take;
+    }
+    *out = s;
+    return 0;
+}
+
+// prepare_fragments_for_decode (erasurecode_preprocessing.c:117-217)
+int prepare_decode(int k, int m, char** data, char** parity, const int* missing, int* orig,
+                   int* bs, uint64_t frag_len, std::vector<char*>& owned)
+{
+    bool gone[EC_MAX_FRAGMENTS] = {};
+    for (int i = 0; missing[i] >= 0; i++) gone[missing[i]] = true;
+    int o = -1, p = -1;
+    auto fix = [&](char*& slot, int idx) -> int {
+        if (!slot) {
+            slot = new_fragment(static_cast<int>(frag_len - kHdr));
+            if (!slot) return -ENOMEM;
+            owned.push_back(slot);
+        } else if (reinterpret_cast<uintptr_t>(slot) & 15u) {
+            char* t = new_fragment(static_cast<int>(frag_len - kHdr));
+            if (!t) return -ENOMEM;
+            std::memcpy(t, slot, frag_len);
+            slot = t;
+            owned.push_back(t);
+        }
+        if (!gone[idx] && o < 0) {
+            o = frag_orig_size(slot);
+            if (o < 0) return -EBADHEADER;
+            p = frag_size(slot);
+            if (p < 0) return -EBADHEADER;
+        }
+        return 0;
+    };
+    for (int i = 0; i < k; i++)
+        if (int rc = fix(data[i], i)) return rc;
+    for (int i = 0; i < m; i++)
+        if (int rc = fix(parity[i], k + i)) return rc;
+    *orig = o;
+    *bs = p;
+    return 0;
+}
+
+// is_invalid_fragment_metadata (erasurecode.c:1156-1187), caller holds the read lock
+int check_metadata(int desc, fragment_metadata_t* md)
+{
+    ec_backend* be = find(desc);
+    if (!be) {
+        LOGE("Unable to verify fragment metadata: invalid backend id %d.", desc);
+        return -EINVALIDPARAMS;
+    }
+    if (liberasurecode_verify_fragment_metadata(be, md) != 0) return -EBADHEADER;
+    if (!be->common.ops->is_compatible_with(md->backend_version)) return -EBADHEADER;
+    if (md->chksum_mismatch == 1) return -EBADCHKSUM;
+    return 0;
+}
+
+// is_invalid_fragment (erasurecode.c:1189-1222), caller holds the read lock
+int invalid_fragment(int desc, char* f)
+{
+    if (!find(desc) || !f) return 1;
+    uint32_t ver = 0;
+    if (get_libec_version(f, &ver) != 0 || ver > LIBERASURECODE_VERSION) return 1;
+    fragment_metadata_t md;
+    if (liberasurecode_get_fragment_metadata(f, &md) != 0) return 1;
+    return check_metadata(desc, &md) != 0 ? 1 : 0;
+}
+
+void free_owned(std::vector<char*>& owned)
+{
+    for (char* p : owned) std::free(p);
+    owned.clear();
+}
+
+}  // namespace
+
+extern "C" {
+
+__attribute__((constructor)) void liberasurecode_init(void)
+{
+    openlog("liberasurecode", LOG_PID | LOG_CONS, LOG_USER);
+}
+
+__attribute__((destructor)) void liberasurecode_exit(void) { closelog(); }
+
+int liberasurecode_crc32_alt(int crc, const void* buf, size_t size)
+{
+    // The legacy checksum of bug 1666320 (src/utils/chksum/crc32.c:79-91): reflected CRC-32
+    // whose 8-bit shift sign-extends from bit 23.
+    static uint32_t tab[256];
+    static bool ready = false;
+    if (!ready) {
+        for (uint32_t n = 0; n < 256; n++) {
+            uint32_t c = n;
+            for (int b = 0; b < 8; b++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+            tab[n] = c;
+        }
+        ready = true;
+    }
+    const signed char* p = static_cast<const signed char*>(buf);
+    int32_t c = crc ^ ~0;
+    while (size--) {
+        int32_t shifted = ((((c >> 8) & 0x00FFFFFF) ^ 0x00800000) - 0x00800000);
+        c = static_cast<int32_t>(tab[(c ^ *p++) & 0xFF]) ^ shifted;
+    }
+    return c ^ ~0;
+}
+
+void* alloc_and_set_buffer(int size, int value)
+{
+    void* b = std::malloc(static_cast<size_t>(size));
+    if (b) std::memset(b, value, static_cast<size_t>(size));
+    return b;
+}
+
+char* get_data_ptr_from_fragment(char* buf) { return buf + kHdr; }
+
+int get_libec_version(char* buf, uint32_t* ver)
+{
+    if (!has_magic(buf)) return -1;
+    *ver = hdr(buf)->libec_version;
+    return 0;
+}
+
+int get_backend_id(char* buf, ec_backend_id_t* id)
+{
+    if (!has_magic(buf)) return -1;
+    *id = static_cast<ec_backend_id_t>(hdr(buf)->meta.backend_id);
+    return 0;
+}
+
+int get_backend_version(char* buf, uint32_t* version)
+{
+    if (!has_magic(buf)) return -1;
+    *version = hdr(buf)->meta.backend_version;
+    return 0;
+}
+
+int get_fragment_partition(int k, int m, char** fragments, int num_fragments, char** data,
+                           char** parity, int* missing)
+{
+    for (int i = 0; i < k; i++) data[i] = nullptr;
+    for (int i = 0; i < m; i++) parity[i] = nullptr;
+    for (int i = 0; i < num_fragments; i++) {
+        int idx = frag_idx(fragments[i]);
+        if (idx < 0 || idx >= k + m) return -EBADHEADER;
+        if (idx < k)
+            data[idx] = fragments[i];
+        else
+            parity[idx - k] = fragments[i];
+    }
+    int n = 0;
+    for (int i = 0; i < k; i++)
+        if (!data[i]) missing[n++] = i;
+    for (int i = 0; i < m; i++)
+        if (!parity[i]) missing[n++] = k + i;
+    return 0;
+}
+
+ec_backend_t liberasurecode_backend_instance_get_by_desc(int desc) { return find(desc); }
+
+int liberasurecode_backend_available(const ec_backend_id_t backend_id)
+{
+    if (backend_id >= EC_BACKENDS_MAX) return 0;
+    void* so = open_backend(kBackends[backend_id]);
+    if (!so) return 0;
+    dlclose(so);
+    return 1;
+}
+
+int liberasurecode_instance_create(const ec_backend_id_t id, struct ec_args* args)
+{
+    if (!args) return -EINVALIDPARAMS;
+    if (id >= EC_BACKENDS_MAX) return -EBACKENDNOTSUPP;
+    if (args->k < 0 || args->m < 0) return -EINVALIDPARAMS;
+    if (args->k + args->m > EC_MAX_FRAGMENTS) {
+        LOGE("Total number of fragments (k + m) must be less than %d\n", EC_MAX_FRAGMENTS);
+        return -EINVALIDPARAMS;
+    }
+    auto* be = static_cast<ec_backend*>(std::calloc(1, sizeof(ec_backend)));
+    if (!be) return -ENOMEM;
+    fill_common(be->common, kBackends[id]);
+    std::memcpy(&be->args.uargs, args, sizeof(ec_args));
+    be->desc.backend_sohandle = open_backend(kBackends[id]);
+    if (!be->desc.backend_sohandle) {
+        const char* e = dlerror();
+        LOGE("%s: dynamic linking error %s\n", __func__, e ? e : "(backend not built)");
+        std::free(be);
+        return -EBACKENDNOTAVAIL;
+    }
+    int desc = -1;
+    if (pthread_rwlock_wrlock(&g_lock) != 0) {
+        std::free(be);
+        return -1;
+    }
+    be->desc.backend_desc = be->common.ops->init(&be->args, be->desc.backend_sohandle);
+    if (!be->desc.backend_desc) {
+        std::free(be);
+        desc = -EBACKENDINITERR;
+    } else {
+        be->idesc = new_desc();
+        be->link.sle_next = g_instances;
+        g_instances = be;
+        desc = be->idesc;
+    }
+    pthread_rwlock_unlock(&g_lock);
+    return desc;
+}
+
+int liberasurecode_instance_destroy(int desc)
+{
+    int rc = pthread_rwlock_wrlock(&g_lock);
+    if (rc != 0) return rc;
+    ec_backend** pp = &g_instances;
+    while (*pp && (*pp)->idesc != desc) pp = &(*pp)->link.sle_next;
+    ec_backend* be = *pp;
+    if (!be) {
+        pthread_rwlock_unlock(&g_lock);
+        return -EBACKENDNOTAVAIL;
+    }
+    be->common.ops->exit(be->desc.backend_desc);
+    if (be->desc.backend_sohandle) {
+        dlclose(be->desc.backend_sohandle);
+        dlerror();
+    }
+    *pp = be->link.sle_next;
+    std::free(be);
+    pthread_rwlock_unlock(&g_lock);
+    return 0;
+}
+
+int liberasurecode_encode_cleanup(int desc, char** encoded_data, char** encoded_parity)
+{
+    int k, m;
+    {
+        ReadLock lk;
+        if (lk.rc) return lk.rc;
+        ec_backend* be = find(desc);
+        if (!be) return -EBACKENDNOTAVAIL;
+        k = be->args.uargs.k;
+        m = be->args.uargs.m;
+    }
+    if (encoded_data) {
+        for (int i = 0; i < k; i++) std::free(encoded_data[i]);
+        std::free(encoded_data);
+    }
+    if (encoded_parity) {
+        for (int i = 0; i < m; i++) std::free(encoded_parity[i]);
+        std::free(encoded_parity);
+    }
+    return 0;
+}
+
+int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_size,
+                          char*** encoded_data, char*** encoded_parity, uint64_t* fragment_len)
+{
+    if (!orig_data || !encoded_data || !encoded_parity || !fragment_len) {
+        LOGE("liberasurecode_encode: null argument");
+        return -EINVALIDPARAMS;
+    }
+    int ret = 0;
+    char** data = nullptr;
+    char** parity = nullptr;
+    int k = 0, m = 0;
+    {
+        ReadLock lk;
+        if (lk.rc) return lk.rc < 0 ? lk.rc : -lk.rc;
+        ec_backend* be = find(desc);
+        if (!be) return -EBACKENDNOTAVAIL;
+        k = be->args.uargs.k;
+        m = be->args.uargs.m;
+        data = static_cast<char**>(alloc_and_set_buffer(static_cast<int>(sizeof(char*)) * k, 0));
+        parity = static_cast<char**>(alloc_and_set_buffer(static_cast<int>(sizeof(char*)) * m, 0));
+        if (!data || !parity) {
+            ret = -ENOMEM;
+        } else {
+            // prepare_fragments_for_encode (erasurecode_preprocessing.c:36-108)
+            const int total = static_cast<int>(orig_data_size);
+            const int bs = aligned_size(be, total) / k;
+            const int meta = static_cast<int>(
+                be->common.ops->get_backend_metadata_size(be->desc.backend_desc, bs));
+            const int off = static_cast<int>(be->common.ops->get_encode_offset(be->desc.backend_desc, meta));
+            int left = total;
+            const char* src = orig_data;
+            for (int i = 0; i < k + m && ret == 0; i++) {
+                char* f = new_fragment(bs + meta);
+                if (!f) {
+                    ret = -ENOMEM;
+                    break;
+                }
+                if (i < k) {
+                    data[i] = f;
+                    const int take = left > bs ? bs : left;
+                    if (left > 0) std::memcpy(payload(f) + off, src, static_cast<size_t>(take));
+                    src += take;
+                    left -= take;
+                } else {
+                    parity[i - k] = f;
+                }
+            }
+            if (ret == 0) {
+                std::vector<char*> dp(k), pp(m);
+                for (int i = 0; i < k; i++) dp[i] = payload(data[i]);
+                for (int i = 0; i < m; i++) pp[i] = payload(parity[i]);
+                ret = be->common.ops->encode(be->desc.backend_desc, dp.data(), pp.data(), bs);
+                if (ret > 0) ret = 0;  // only negative returns are failures (erasurecode.c:454-461)
+            }
+            if (ret == 0) {
+                // finalize_fragments_after_encode (erasurecode_postprocessing.c:71-93)
+                const ec_checksum_type_t ct = be->args.uargs.ct;
+                for (int i = 0; i < k; i++) stamp(be, data[i], i, orig_data_size, bs, ct, true);
+                for (int i = 0; i < m; i++) stamp(be, parity[i], k + i, orig_data_size, bs, ct, true);
+                *fragment_len = static_cast<uint64_t>(frag_size(data[0])) +
+                                hdr(data[0])->meta.frag_backend_metadata_size + kHdr;
+            }
+        }
+    }
+    if (ret) {
+        LOGE("Error in liberasurecode_encode %d", ret);
+        liberasurecode_encode_cleanup(desc, data, parity);
+        data = parity = nullptr;
+    }
+    *encoded_data = data;
+    *encoded_parity = parity;
+    return ret;
+}
+
+int liberasurecode_decode_cleanup(int desc, char* data)
+{
+    {
+        ReadLock lk;
+        if (lk.rc) return lk.rc;
+        if (!find(desc)) return -EBACKENDNOTAVAIL;
+    }
+    std::free(data);
+    return 0;
+}
+
+int liberasurecode_decode(int desc, char** available_fragments, int num_fragments,
+                          uint64_t fragment_len, int force_metadata_checks, char** out_data,
+                          uint64_t* out_data_len)
+{
+    ReadLock lk;
+    if (lk.rc) return lk.rc;
+    ec_backend* be = find(desc);
+    if (!be) return -EBACKENDNOTAVAIL;
+    if (!available_fragments || !out_data || !out_data_len) {
+        LOGE("liberasurecode_decode: null argument");
+        return -EINVALIDPARAMS;
+    }
+    const int k = be->args.uargs.k, m = be->args.uargs.m;
+    if (num_fragments < k) {
+        LOGE("Not enough fragments to decode, got %d, need %d!", num_fragments, k);
+        return -EINSUFFFRAGS;
+    }
+    if (fragment_len < kHdr) {
+        LOGE("Fragments not long enough to include headers!");
+        return -EBADHEADER;
+    }
+    for (int i = 0; i < num_fragments; i++)
+        if (is_invalid_fragment_header(hdr(available_fragments[i]))) {
+            LOGE("Invalid fragment header information!");
+            return -EBADHEADER;
+        }
+    if (be->common.ops->is_systematic &&
+        assemble(k, available_fragments, num_fragments, out_data, out_data_len) == 0)
+        return 0;  // every data fragment present: no backend work
+
+    std::vector<char*> data(k), parity(m), owned;
+    std::vector<int> missing(k + m, -1);
+    if (force_metadata_checks) {
+        int bad = 0;
+        for (int i = 0; i < num_fragments; i++) bad += invalid_fragment(desc, available_fragments[i]);
+        if (num_fragments - bad < k) {
+            LOGE("Not enough valid fragments available for decode!");
+            return -EINSUFFFRAGS;
+        }
+    }
+    int ret = get_fragment_partition(k, m, available_fragments, num_fragments, data.data(),
+                                     parity.data(), missing.data());
+    int orig = 0, bs = 0;
+    if (ret == 0)
+        ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
+                             fragment_len, owned);
+    if (ret == 0) {
+        std::vector<char*> dp(k), pp(m);
+        for (int i = 0; i < k; i++) dp[i] = payload(data[i]);
+        for (int i = 0; i < m; i++) pp[i] = payload(parity[i]);
+        ret = be->common.ops->decode(be->desc.backend_desc, dp.data(), pp.data(), missing.data(), bs);
+        if (ret < 0) LOGE("Encountered error in backend decode function!");
+    }
+    if (ret == 0) {
+        for (int j = 0; missing[j] >= 0; j++) {
+            if (missing[j] >= k) continue;
+            char* f = data[missing[j]];
+            hdr(f)->magic = LIBERASURECODE_FRAG_HEADER_MAGIC;  // init_fragment_header
+            stamp(be, f, missing[j], static_cast<uint64_t>(orig), bs, be->args.uargs.ct, false);
+        }
+        ret = assemble(k, data.data(), k, out_data, out_data_len);
+        if (ret < 0) LOGE("Could not convert decoded fragments to a string!");
+    }
+    free_owned(owned);
+    return ret;
+}
+
+int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, int num_fragments,
+                                        uint64_t fragment_len, int destination_idx,
+                                        char* out_fragment)
+{
+    ReadLock lk;
+    if (lk.rc) return lk.rc;
+    ec_backend* be = find(desc);
+    if (!be) return -EBACKENDNOTAVAIL;
+    if (!available_fragments || !out_fragment) {
+        LOGE("Can not reconstruct fragment: null argument");
+        return -EINVALIDPARAMS;
+    }
+    const int k = be->args.uargs.k, m = be->args.uargs.m;
+    if (destination_idx < 0 || destination_idx >= k + m) return -EINVALIDPARAMS;
+    for (int i = 0; i < num_fragments; i++)
+        if (is_invalid_fragment_header(hdr(available_fragments[i]))) {
+            LOGE("Invalid fragment header information!");
+            return -EBADHEADER;
+        }
+    std::vector<char*> data(k), parity(m), owned;
+    std::vector<int> missing(k + m, -1);
+    int ret = get_fragment_partition(k, m, available_fragments, num_fragments, data.data(),
+                                     parity.data(), missing.data());
+    if (ret < 0) return ret;
+    bool dest_missing = false;
+    for (int i = 0; missing[i] > -1; i++) dest_missing |= missing[i] == destination_idx;
+    auto slot = [&](int idx) -> char* { return idx < k ? data[idx] : parity[idx - k]; };
+    if (!dest_missing) {
+        LOGW("Dest idx for reconstruction was supplied as available buffer!");
+        std::memcpy(out_fragment, slot(destination_idx), fragment_len);
+        return 0;
+    }
+    if (!be->common.ops->check_reconstruct_fragments) {
+        if (num_fragments < k) return -EINSUFFFRAGS;
+    } else {
+        ret = be->common.ops->check_reconstruct_fragments(be->desc.backend_desc, missing.data(),
+                                                          destination_idx);
+        if (ret < 0) return ret;
+    }
+    int orig = 0, bs = 0;
+    ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
+                         fragment_len, owned);
+    if (ret == 0) {
+        std::vector<char*> dp(k), pp(m);
+        for (int i = 0; i < k; i++) dp[i] = payload(data[i]);
+        for (int i = 0; i < m; i++) pp[i] = payload(parity[i]);
+        ret = be->common.ops->reconstruct(be->desc.backend_desc, dp.data(), pp.data(),
+                                          missing.data(), destination_idx, bs);
+        if (ret < 0) LOGE("Could not reconstruct fragment!");
+    }
+    if (ret == 0) {
+        char* f = slot(destination_idx);
+        hdr(f)->magic = LIBERASURECODE_FRAG_HEADER_MAGIC;
+        stamp(be, f, destination_idx, static_cast<uint64_t>(orig), bs, be->args.uargs.ct, true);
+        std::memcpy(out_fragment, f, fragment_len);
+    }
+    free_owned(owned);
+    return ret;
+}
+
+int liberasurecode_fragments_needed(int desc, int* fragments_to_reconstruct,
+                                    int* fragments_to_exclude, int* fragments_needed)
+{
+    ReadLock lk;
+    if (lk.rc) return lk.rc;
+    ec_backend* be = find(desc);
+    if (!be) return -EBACKENDNOTAVAIL;
+    if (!fragments_to_reconstruct || !fragments_to_exclude || !fragments_needed) {
+        LOGE("Unable to determine list of fragments needed: null argument");
+        return -EINVALIDPARAMS;
+    }
+    return be->common.ops->fragments_needed(be->desc.backend_desc, fragments_to_reconstruct,
+                                            fragments_to_exclude, fragments_needed);
+}
+
+int liberasurecode_get_fragment_metadata(char* fragment, fragment_metadata_t* md)
+{
+    if (!fragment || !md) {
+        LOGE("liberasurecode_get_fragment_metadata: null argument");
+        return -EINVALIDPARAMS;
+    }
+    if (is_invalid_fragment_header(hdr(fragment))) {
+        LOGE("Invalid fragment header information!");
+        return -EBADHEADER;
+    }
+    std::memcpy(md, fragment, sizeof(fragment_metadata_t));
+    if (hdr(fragment)->magic != LIBERASURECODE_FRAG_HEADER_MAGIC) {
+        if (bswap32(hdr(fragment)->magic) != LIBERASURECODE_FRAG_HEADER_MAGIC) {
+            LOGE("Invalid fragment, illegal magic value");
+            return -EINVALIDPARAMS;
+        }
+        // written on an opposite-endian host (erasurecode.c:1050-1068); the reference swaps the
+        // one-byte chksum_type through a 32-bit swap, which always leaves it 0
+        md->idx = bswap32(md->idx);
+        md->size = bswap32(md->size);
+        md->frag_backend_metadata_size = bswap32(md->frag_backend_metadata_size);
+        md->orig_data_size = bswap64(md->orig_data_size);
+        md->chksum_type = static_cast<uint8_t>(bswap32(md->chksum_type));
+        for (int i = 0; i < LIBERASURECODE_MAX_CHECKSUM_LEN; i++) md->chksum[i] = bswap32(md->chksum[i]);
+        md->backend_version = bswap32(md->backend_version);
+    }
+    if (md->chksum_type == CHKSUM_CRC32) {
+        const uint32_t stored = md->chksum[0];
+        char* p = payload(fragment);
+        const size_t n = md->size;
+        md->chksum_mismatch =
+            (stored != zcrc(p, n) &&
+             stored != static_cast<uint32_t>(liberasurecode_crc32_alt(0, p, n))) ? 1 : 0;
+    }
+    return 0;
+}
+
+int is_invalid_fragment_header(fragment_header_t* header)
+{
+    if (header->libec_version == 0) return 1;
+    uint32_t stored = header->metadata_chksum, ver = header->libec_version;
+    if (header->magic != LIBERASURECODE_FRAG_HEADER_MAGIC) {
+        if (bswap32(header->magic) != LIBERASURECODE_FRAG_HEADER_MAGIC) {
+            LOGE("Invalid fragment header (get meta chksum)!");
+            return 1;
+        }
+        stored = bswap32(stored);
+        ver = bswap32(ver);
+    }
+    if (ver < _VERSION(1, 2, 0)) return 0;  // no metadata checksum before 1.2.0
+    if (stored == zcrc(&header->meta, sizeof(fragment_metadata_t))) return 0;
+    return stored != static_cast<uint32_t>(
+                         liberasurecode_crc32_alt(0, &header->meta, sizeof(fragment_metadata_t)));
+}
+
+int liberasurecode_verify_fragment_metadata(ec_backend_t be, fragment_metadata_t* md)
+{
+    if (md->idx >= static_cast<uint32_t>(be->args.uargs.k + be->args.uargs.m)) return 1;
+    if (md->backend_id != be->common.id) return 1;
+    if (!be->common.ops->is_compatible_with(md->backend_version)) return 1;
+    return 0;
+}
+
+int is_invalid_fragment(int desc, char* fragment)
+{
+    ReadLock lk;
+    if (lk.rc) return lk.rc;
+    return invalid_fragment(desc, fragment);
+}
+
+int liberasurecode_verify_stripe_metadata(int desc, char** fragments, int num_fragments)
+{
+    if (!fragments) {
+        LOGE("Unable to verify stripe metadata: fragments missing.");
+        return -EINVALIDPARAMS;
+    }
+    if (num_fragments <= 0) {
+        LOGE("Unable to verify stripe metadata: number of fragments must be greater than 0.");
+        return -EINVALIDPARAMS;
+    }
+    ReadLock lk;
+    if (lk.rc) return lk.rc;
+    for (int i = 0; i < num_fragments; i++) {
+        int ret = check_metadata(desc, reinterpret_cast<fragment_metadata_t*>(fragments[i]));
+        if (ret < 0) return ret;
+    }
+    return 0;
+}
+
+int liberasurecode_get_aligned_data_size(int desc, uint64_t data_len)
+{
+    ReadLock lk;
+    if (lk.rc) return lk.rc < 0 ? lk.rc : -lk.rc;
+    ec_backend* be = find(desc);
+    if (!be) return -EBACKENDNOTAVAIL;
+    const uint64_t a = static_cast<uint64_t>(be->args.uargs.k) *
+                       static_cast<uint64_t>(be->common.ops->element_size(be->desc.backend_desc) / 8);
+    return static_cast<int>(((data_len + a - 1) / a) * a);
+}
+
+int liberasurecode_get_minimum_encode_size(int desc) { return liberasurecode_get_aligned_data_size(desc, 1); }
+
+int liberasurecode_get_fragment_size(int desc, int data_len)
+{
+    ReadLock lk;
+    if (lk.rc) return lk.rc < 0 ? lk.rc : -lk.rc;
+    ec_backend* be = find(desc);
+    if (!be) return -EBACKENDNOTAVAIL;
+    const int bs = aligned_size(be, data_len) / be->args.uargs.k;
+    return bs + static_cast<int>(be->common.ops->get_backend_metadata_size(be->desc.backend_desc, bs));
+}
+
+uint32_t liberasurecode_get_version(void) { return LIBERASURECODE_VERSION; }
+
+}  // extern "C"

@@ -14,7 +14,17 @@ HEADERS = {
     "ecamd_host.h": "libecamd_host.so",
     "ecamd.h": "libecamd.so",
     "liberasurecode_rs_vand.h": "liberasurecode_rs_vand.so.1",
+    "xor_code.h": "libXorcode.so.1",
 }
+
+# libXorcode.sym:1-5 of the reference
+REF_XORCODE_SYMS = sorted("""init_xor_hd_code xor_code_encode xor_hd_decode xor_hd_fragments_needed
+xor_reconstruct_one""".split())
+
+
+def test_xorcode_exports_exactly_reference_symbols():
+    assert exported(os.path.join(LIB, "libXorcode.so.1")) == REF_XORCODE_SYMS
+    assert declared("xor_code.h") == REF_XORCODE_SYMS
 
 # liberasurecode_rs_vand.sym:1-13 of the reference (the CI symbol contract, check-symbols.sh)
 REF_RS_VAND_SYMS = sorted("""create_decoding_matrix deinit_liberasurecode_rs_vand

@@ -88,4 +88,4 @@ def test_reference_xor_unit_test_runs_on_our_library():
     assert os.path.join("liberasurecode_amd", "lib", "libXorcode.so.1") in probe
     r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
-    assert r.stdout.count("Running") == 38
+    assert (r.stdout + r.stderr).count("Running") == 38
