@@ -24,9 +24,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402  (before libecamd: one HIP runtime per process)
-import torch.distributed as dist  # noqa: E402
 
 from liberasurecode_amd import device as D  # noqa: E402
+from liberasurecode_amd.shard import Coordinator, stripe_range  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
@@ -110,20 +110,17 @@ def main():
     ap.add_argument("--cpu-stripes", type=int, default=32, help="stripes per CPU thread")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    co = Coordinator()  # one process per GPU; RCCL only for the barrier and time reductions
+    world, rank = co.world, co.rank
 
     k, m, F, S, missing, desc = CONFIGS[args.config]
     if args.stripes:
         S = args.stripes
     assert D.available(), "no HIP device"
+    first, S = stripe_range(rank, world, S)  # this rank's shard of independent stripes
     lay = D.Layout.alloc(k + m, F, S)
     stream = D.Stream()
-    lay.fill_splitmix(nfrags=k, stripe0=rank * S, stream=stream)
+    lay.fill_splitmix(nfrags=k, stripe0=first, stream=stream)
     D.rs_encode(k, m, lay, stream=stream)
     stream.synchronize()
 
@@ -143,24 +140,19 @@ def main():
         step()
     stream.synchronize()
 
-    def barrier():
+    def sync_all():
         D.synchronize()
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
 
-    barrier()
+    sync_all()
+    co.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-    D.synchronize()
-    torch.cuda.synchronize()
+    sync_all()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
+    elapsed = co.reduce([elapsed], op="max")[0]
+    co.barrier()
 
     enc_ms = [a.elapsed_ms(b) for a, b, _ in ev]
     dec_ms = [b.elapsed_ms(c) for _, b, c in ev]
@@ -206,8 +198,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(k, m, F, missing, args.cpu_threads,
                                                args.cpu_stripes)
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    co.close()
 
 
 if __name__ == "__main__":
