@@ -166,6 +166,8 @@ def main():
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
     kernel = f"gf16_apply_kernel<{width}, false, true>"
     traffic, traffic_src = pmc_traffic(args.config, kernel)
+    if traffic is not None and S != CONFIGS[args.config][3]:
+        traffic = int(traffic * S / CONFIGS[args.config][3])  # profile ran at the default S
 
     if rank == 0:
         out = {

@@ -97,6 +97,10 @@ int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, 
 
 /* ---- measurement helper: non-temporal 16 B/lane streaming copy (HBM ceiling probe) ---- */
 int ecamd_debug_stream_copy(void *d_dst, const void *d_src, int64_t bytes, void *stream);
+/* kind 0 copy / 1 read-only / 2 write-only over `bytes`, unroll in {1,4,8} 16-B loads per lane in
+ * flight, grid = CUs x wgs_per_cu workgroups of 256 lanes (bandwidth ceilings for DESIGN.md). */
+int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void *d_dst, const void *d_src,
+                         int64_t bytes, void *stream);
 
 /* ---- device memory helpers for C / ctypes callers ---- */
 int ecamd_malloc(void **d_ptr, int64_t bytes);

@@ -557,6 +557,27 @@ int ecamd_debug_stream_copy(void* dst, const void* src, int64_t bytes, void* str
     return 0;
 }
 
+int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void* dst, const void* src,
+                         int64_t bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    static uint32_t* sink = nullptr;
+    if (!sink) HIP_TRY(hipMalloc(&sink, 1024 * sizeof(uint32_t)));
+    dim3 grid(cu_count(dev) * std::max(1, wgs_per_cu)), block(256);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    auto* d = static_cast<uint8_t*>(dst);
+    auto* s = static_cast<const uint8_t*>(src);
+    switch (unroll) {
+    case 1: hipLaunchKernelGGL(bw_probe_kernel<1>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    case 4: hipLaunchKernelGGL(bw_probe_kernel<4>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    default: hipLaunchKernelGGL(bw_probe_kernel<8>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 int ecamd_malloc(void** d_ptr, int64_t bytes)
 {
     int rc = ensure_device(nullptr);

@@ -46,6 +46,9 @@ __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);
 __global__ void splitmix_fill_kernel(FillArgs f);
+template <int U>
+__global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int kind,
+                                uint32_t* sink);
 __global__ void stream_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n);
 
 }  // namespace ecamd

@@ -145,3 +145,45 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(uint4* __restrict__ ds
 }
 
 }  // namespace ecamd
+
+namespace ecamd {
+
+// Bandwidth probes for DESIGN.md (not used by the codec): kind 0 copy, 1 read-only (XOR-reduce,
+// one dword written per lane at the end), 2 write-only.  Each workgroup owns contiguous tiles of
+// blockDim * 16 * U bytes; U loads per lane are in flight before any store.
+template <int U>
+__global__ void __launch_bounds__(256) bw_probe_kernel(uint8_t* dst, const uint8_t* src,
+                                                       int64_t bytes, int kind, uint32_t* sink)
+{
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const int64_t tile = static_cast<int64_t>(blockDim.x) * 16 * U;
+    const int64_t ntiles = bytes / tile;
+    v4 acc = {0u, 0u, 0u, 0u};
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int64_t base = t * tile + static_cast<int64_t>(threadIdx.x) * 16;
+        v4 r[U];
+        if (kind != 2) {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                r[u] = __builtin_nontemporal_load(reinterpret_cast<const v4*>(src + base + u * blockDim.x * 16));
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) r[u] = v4{static_cast<unsigned>(t), 1u, 2u, static_cast<unsigned>(u)};
+        }
+        if (kind == 1) {
+#pragma unroll
+            for (int u = 0; u < U; u++) acc ^= r[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                __builtin_nontemporal_store(r[u], reinterpret_cast<v4*>(dst + base + u * blockDim.x * 16));
+        }
+    }
+    if (kind == 1 && (acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x9e3779b9u) sink[threadIdx.x] = acc.x;
+}
+
+template __global__ void bw_probe_kernel<1>(uint8_t*, const uint8_t*, int64_t, int, uint32_t*);
+template __global__ void bw_probe_kernel<4>(uint8_t*, const uint8_t*, int64_t, int, uint32_t*);
+template __global__ void bw_probe_kernel<8>(uint8_t*, const uint8_t*, int64_t, int, uint32_t*);
+
+}  // namespace ecamd

@@ -35,12 +35,15 @@ class Coordinator:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.on_gpu = False
+        if torch.cuda.is_available() and torch.cuda.device_count() > 0:
+            # one GPU per rank; ranks beyond the visible GPUs share them (rehearsal only)
+            torch.cuda.set_device(self.local % torch.cuda.device_count())
         if self.world > 1:
+            backend = backend or os.environ.get("ECAMD_DIST_BACKEND")
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
             self.on_gpu = backend == "nccl"
             if self.on_gpu:
-                torch.cuda.set_device(self.local)
                 dist.init_process_group(backend=backend,
                                         device_id=torch.device("cuda", self.local))
             else:
