@@ -11,8 +11,9 @@ Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent,
 its own S stripes (weak scaling) and there is no data-path collective -- the process group is used
 for the start barrier and the max-over-ranks of the elapsed time only.
 
-Extra fields: "roofline" (gf16_apply_kernel, HIP-event timed per launch on the launch stream) and
-"cpu_baseline" (the oracle restatement of the same algorithm on the host cores; rank 0 only).
+Extra fields: "roofline" (gf16_apply_kernel, HIP-event timed per launch on the launch stream; peak =
+8 TB/s spec, plus a copy peak measured live) and "cpu_baseline" (the reference codec compiled from
+its sources -- or the oracle restatement when that build is absent -- on the host cores; rank 0).
 """
 import argparse
 import json
@@ -43,7 +44,13 @@ CONFIGS = {
 
 
 def cpu_baseline(k, m, F, missing, threads, stripes):
-    """The oracle (same log/antilog algorithm as the reference) on `threads` host cores."""
+    """Host-CPU baseline of the same hot path on this machine.
+
+    Uses the REFERENCE codec itself (oracle/_ref/liberasurecode_rs_vand.so.1, compiled from the
+    reference sources by oracle/Makefile, kind "reference") when it is present, else the oracle
+    restatement (oracle/ec_oracle.c, same log/antilog algorithm, kind "port").  One stripe per task,
+    `threads` threads (ctypes releases the GIL), and separately one thread."""
+    import ctypes as C
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
@@ -52,33 +59,85 @@ def cpu_baseline(k, m, F, missing, threads, stripes):
     import oracle_lib as orc
     from ecdata import stripe_fragments
 
-    lib = orc.lib()
-    G = orc.ints(orc.generator(k, m))
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "liberasurecode_rs_vand.so.1")
+    IP = C.POINTER(C.c_int)
+    if os.path.exists(ref_path):
+        lib = C.CDLL(ref_path)
+        lib.make_systematic_matrix.restype = IP
+        lib.make_systematic_matrix.argtypes = [C.c_int, C.c_int]
+        lib.liberasurecode_rs_vand_encode.argtypes = [IP, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                      C.c_int]
+        lib.liberasurecode_rs_vand_decode.argtypes = [IP, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                      IP, C.c_int, C.c_int]
+        lib.init_liberasurecode_rs_vand(k, m)
+        G = lib.make_systematic_matrix(k, m)
+        enc, dec, kind = lib.liberasurecode_rs_vand_encode, lib.liberasurecode_rs_vand_decode, "reference"
+        what = "reference liberasurecode_rs_vand.so.1 built from /root/reference sources, gcc -O2"
+    else:
+        lib = orc.lib()
+        G = orc.ints(orc.generator(k, m))
+        enc, dec, kind = lib.orc_rs_encode, lib.orc_rs_decode, "port"
+        what = "oracle/ec_oracle.c (log/antilog tables as the reference), gcc -O2"
     miss = orc.ints(list(missing) + [-1])
 
     def job(t, count):
         data = stripe_fragments(t, k, F)
         frags = [np.array(x) for x in data] + [np.zeros(F, np.uint8) for _ in range(m)]
         dp, pp = orc.ptr_array(frags[:k]), orc.ptr_array(frags[k:])
-        n = 0
         t0 = time.perf_counter()
         for _ in range(count):
-            lib.orc_rs_encode(G, dp, pp, k, m, F)
-            lib.orc_rs_decode(G, dp, pp, k, m, miss, F, 1)
-            n += 1
-        return n, time.perf_counter() - t0
+            enc(G, dp, pp, k, m, F)
+            dec(G, dp, pp, k, m, miss, F, 1)
+        return count, time.perf_counter() - t0
 
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(job, range(threads), [1] * threads))  # warm (allocations, page faults)
-        t0 = time.perf_counter()
-        res = list(ex.map(job, range(threads), [stripes] * threads))
-        wall = time.perf_counter() - t0
-    total = sum(n for n, _ in res)
-    return {"value": round(2 * total * k * F / GIB / wall, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{total} stripes x (encode + decode {list(missing)}) of k={k} m={m} F={F} "
-                      f"on {threads} threads (oracle/ec_oracle.c log/antilog tables, -O2)",
-            "cpu_seconds": round(sum(t for _, t in res), 2)}
+    def run(nthreads, per):
+        with ThreadPoolExecutor(nthreads) as ex:
+            list(ex.map(job, range(nthreads), [1] * nthreads))  # warm (allocations, page faults)
+            t0 = time.perf_counter()
+            res = list(ex.map(job, range(nthreads), [per] * nthreads))
+            wall = time.perf_counter() - t0
+        total = sum(n for n, _ in res)
+        return 2 * total * k * F / GIB / wall, total, sum(t for _, t in res)
+
+    value, total, cpu_s = run(threads, stripes)
+    one, one_total, one_s = run(1, max(2, stripes // 4))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(value, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "value_1core": round(one, 4),
+            "sample": f"{total} stripes x (encode + decode {list(missing)}) of k={k} m={m} F={F} on "
+                      f"{threads} threads, plus {one_total} on 1 thread; {what}",
+            "cpu_seconds": round(cpu_s + one_s, 2), "cpu_model": model,
+            "host_cpus_visible": os.cpu_count()}
+
+
+def measured_copy_peak(stream, nbytes=1 << 30):
+    """Second roofline denominator: non-temporal 16 B/lane copy of 1 GiB on this GPU (GB/s)."""
+    import ctypes as C
+
+    from liberasurecode_amd import _lib
+    d = _lib.dev()
+    d.ecamd_debug_bw_probe.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                       C.c_int64, C.c_void_p]
+    buf = D.DeviceBuffer(2 * nbytes)
+    a, b = D.Event(), D.Event()
+    best = 0.0
+    for _ in range(3):
+        _lib.check(d.ecamd_debug_bw_probe(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes,
+                                          stream.handle), "copy probe")
+        a.record(stream)
+        for _ in range(4):
+            d.ecamd_debug_bw_probe(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes, stream.handle)
+        b.record(stream)
+        best = max(best, 2 * nbytes * 4 / (a.elapsed_ms(b) * 1e-3) / 1e9)
+    buf.free()
+    return best
 
 
 def pmc_traffic(cfg, kernel):
@@ -169,6 +228,8 @@ def main():
     if traffic is not None and S != CONFIGS[args.config][3]:
         traffic = int(traffic * S / CONFIGS[args.config][3])  # profile ran at the default S
 
+    copy_gbs = measured_copy_peak(stream)
+
     if rank == 0:
         out = {
             "metric": "device-resident encode+decode GiB/s (RS k=10 m=4, 1 MiB frags), 1/2/4/8 GPU"
@@ -194,6 +255,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "launch_ms": round(launch_ms, 4),
+                         "copy_peak_measured": round(copy_gbs, 1),
+                         "frac_of_measured_copy": round(achieved / copy_gbs, 4),
                          "algorithmic_bytes_per_launch": algo_bytes},
         }
         if not args.no_cpu_baseline and world == 1:
