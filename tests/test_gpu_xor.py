@@ -89,3 +89,36 @@ def test_reference_xor_unit_test_runs_on_our_library():
     r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert (r.stdout + r.stderr).count("Running") == 38
+
+
+@pytest.mark.parametrize("k,m,hd,bs", [(10, 6, 4, (1 << 20) + 13), (20, 6, 4, 3), (15, 6, 3, 65537),
+                                       (5, 5, 4, 1), (3, 3, 3, 777777)])
+def test_libxorcode_vs_oracle_ragged(lib, k, m, hd, bs):
+    """Large and odd blocksizes on inconsistent random buffers: every byte equals the buffer-level
+    oracle (oracle/xor_oracle.py) for a sample of decode and reconstruct patterns."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import xor_oracle as XO
+    code = lib.init_xor_hd_code(k, m, hd)
+    oc = XO.XorCode(k, m, hd)
+    rng = np.random.default_rng(k * 7 + bs)
+    pats = X.xor_patterns(k + m, 99)
+    sample = [pats[i] for i in sorted(set(rng.integers(0, len(pats), 12).tolist()))]
+    base = [rng.integers(0, 256, bs, dtype=np.uint8) for _ in range(k + m)]
+    bb, ob = [x.copy() for x in base], [x.copy() for x in base]
+    lib.xor_code_encode(code, ptrs(bb, 0, k), ptrs(bb, k, k + m), bs)
+    oc.encode(ob)
+    assert all((a == b).all() for a, b in zip(bb, ob))
+    for p in sample:
+        bb, ob = [x.copy() for x in base], [x.copy() for x in base]
+        rc = lib.xor_hd_decode(code, ptrs(bb, 0, k), ptrs(bb, k, k + m), ints(p + [-1]), bs, 1)
+        assert rc == oc.decode(ob, p, 1)
+        assert all((a == b).all() for a, b in zip(bb, ob)), p
+        if len(p) <= 3:
+            idx = p[-1]
+            bb, ob = [x.copy() for x in base], [x.copy() for x in base]
+            rc = lib.xor_reconstruct_one(code, ptrs(bb, 0, k), ptrs(bb, k, k + m), ints(p + [-1]),
+                                         idx, bs)
+            assert rc == oc.reconstruct_one(ob, p, idx)
+            assert all((a == b).all() for a, b in zip(bb, ob)), (p, idx)
