@@ -90,6 +90,45 @@ int ecamd_host_map_apply(const int *coeff, int R, int K, const void *const *in, 
 int ecamd_host_xor_apply(const uint64_t *sources, int R, int nbuf, const void *const *bufs,
                          void *const *out, int64_t blocksize);
 
+/* ---- on-device framing: the wire format of liberasurecode_encode, in HBM ----
+ * backend 6 = liberasurecode_rs_vand, 3 = flat_xor_hd (hd used only there); checksum is the
+ * ec_checksum_type_t of the instance (1 none, 2 CRC32; anything else is stored, not computed, as the
+ * reference does).  Object s lives at d_obj + s*obj_stride (obj_size bytes, all stripes the same
+ * size); fragment f of stripe s at d_frags + s*stripe_stride + f*frag_stride: the 80-byte
+ * fragment_header_t followed by the payload.  frag_stride >= 80 + blocksize rounded up to 16, all
+ * fragment addresses 16-byte aligned.  LIBERASURECODE_WRITE_LEGACY_CRC selects the legacy checksum
+ * exactly as in the reference.  Asynchronous on `stream`. */
+
+/* blocksize = get_aligned_data_size(obj_size) / k; fragment_len = 80 + blocksize. */
+int ecamd_frame_geometry(int backend, int k, int m, int hd, uint64_t obj_size, int64_t *blocksize,
+                         int64_t *fragment_len);
+/* liberasurecode_encode (src/erasurecode.c:383-477) for nstripes objects at once: split + pad,
+ * parity, payload CRC32 and headers; fragments byte-identical to the reference's. */
+int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const void *d_obj,
+                       int64_t obj_stride, uint64_t obj_size, void *d_frags, int64_t stripe_stride,
+                       int64_t frag_stride, int nstripes, void *stream);
+/* liberasurecode_decode (src/erasurecode.c:523-734) with fragments already in their index slots:
+ * rebuild the missing (-1 terminated) data payloads in place, then write the objects. */
+int ecamd_frame_decode(int backend, int k, int m, int hd, const int *missing, void *d_frags,
+                       int64_t stripe_stride, int64_t frag_stride, int nstripes, void *d_obj,
+                       int64_t obj_stride, uint64_t obj_size, void *stream);
+/* liberasurecode_reconstruct_fragment (src/erasurecode.c:748-949): rebuild fragment `dest` of
+ * every stripe in its slot, header and checksum included. */
+int ecamd_frame_reconstruct(int backend, int k, int m, int hd, int checksum, const int *missing,
+                            int dest, void *d_frags, int64_t stripe_stride, int64_t frag_stride,
+                            uint64_t obj_size, int nstripes, void *stream);
+/* Header / checksum audit of nfrag fragments per stripe: d_status[s*nfrag+f] bit 0 bad magic, 1 bad
+ * metadata checksum (neither zlib nor legacy), 2 idx != f, 3 size != blocksize, 4 payload CRC32
+ * mismatch (when the header says CRC32; `legacy` picks the machine).  d_crc (optional) receives the
+ * computed payload CRCs. */
+int ecamd_frame_verify(int nfrag, int64_t blocksize, int legacy, const void *d_frags,
+                       int64_t stripe_stride, int64_t frag_stride, int nstripes, uint32_t *d_status,
+                       uint32_t *d_crc, void *stream);
+/* zlib crc32(0, buf, len) (legacy = 0) or liberasurecode_crc32_alt(0, buf, len) (legacy = 1) of
+ * every buffer d_base + s*stripe_stride + f*frag_stride, f < nfrag: d_crc[s*nfrag + f]. */
+int ecamd_crc32(int legacy, const void *d_base, int64_t stripe_stride, int64_t frag_stride,
+                int nfrag, int64_t len, int nstripes, uint32_t *d_crc, void *stream);
+
 /* ---- synthetic data: splitmix64 stream per fragment, seed = seed_base ^ (s<<8) ^ f ---- */
 int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, int nfrags,
                         int64_t blocksize, int nstripes, int stripe0, uint64_t seed_base,

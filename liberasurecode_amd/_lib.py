@@ -86,6 +86,21 @@ def dev():
                [C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
         _proto(d, "ecamd_fill_splitmix", C.c_int,
                [VP, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_uint64, VP])
+        _proto(d, "ecamd_frame_geometry", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, I64P, I64P])
+        _proto(d, "ecamd_frame_encode", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_uint64, VP,
+                C.c_int64, C.c_int64, C.c_int, VP])
+        _proto(d, "ecamd_frame_decode", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, IP, VP, C.c_int64, C.c_int64, C.c_int, VP,
+                C.c_int64, C.c_uint64, VP])
+        _proto(d, "ecamd_frame_reconstruct", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64,
+                C.c_int64, C.c_uint64, C.c_int, VP])
+        _proto(d, "ecamd_frame_verify", C.c_int,
+               [C.c_int, C.c_int64, C.c_int, VP, C.c_int64, C.c_int64, C.c_int, VP, VP, VP])
+        _proto(d, "ecamd_crc32", C.c_int,
+               [C.c_int, VP, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int, VP, VP])
         _proto(d, "ecamd_debug_stream_copy", C.c_int, [VP, VP, C.c_int64, VP])
         _proto(d, "ecamd_malloc", C.c_int, [C.POINTER(VP), C.c_int64])
         _proto(d, "ecamd_free", C.c_int, [VP])

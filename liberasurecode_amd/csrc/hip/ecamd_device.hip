@@ -16,6 +16,7 @@
 #include "../host/gf16.hpp"
 #include "../host/tables.hpp"
 #include "ecamd.h"
+#include "ecamd_internal.hpp"
 #include "ecamd_kernels.hpp"
 
 using namespace ecamd;
@@ -106,10 +107,36 @@ struct Tuning {
     int nt = 1;          // 1: non-temporal global loads/stores in the gf16 kernel (+7% on MI355X)
     int exp_ch = 0;      // sweeps: experimental W=4 kernel with 1 or 2 chunks per lane
     int ablate = 0;      // sweeps: experimental kernel without LDS lookups (wrong results)
+    int crc_bits = 8;    // CRC32 kernel: 8 (byte tables) or 4 (conflict-free nibble tables)
+    int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
 };
 Tuning g_tune;
 
 }  // namespace
+
+namespace ecamd {
+
+int dev_ensure(int* dev_out) { return ensure_device(dev_out); }
+int dev_cu_count(int dev) { return cu_count(dev); }
+int dev_fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+int dev_tune(const char* key)
+{
+    const std::string k(key);
+    if (k == "crc_bits") return g_tune.crc_bits;
+    if (k == "crc_wgs") return g_tune.crc_wgs;
+    return 0;
+}
+
+}  // namespace ecamd
 
 struct ecamd_map {
     struct Pass {
@@ -356,6 +383,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.exp_ch = (value == 1 || value == 2) ? value : 0;
     } else if (k == "ablate") {
         g_tune.ablate = value != 0;
+    } else if (k == "crc_bits") {
+        g_tune.crc_bits = value == 4 ? 4 : 8;
+    } else if (k == "crc_wgs") {
+        g_tune.crc_wgs = std::max(0, std::min(value, 4));
     } else {
         return fail(ECAMD_EINVAL, "unknown tuning key %s", key);
     }

@@ -1,0 +1,284 @@
+// ecamd_frame.hip -- on-device fragment framing for the device-resident path:
+// the 80-byte fragment headers and the zlib-compatible payload / metadata CRC32 of the reference
+// (src/erasurecode_postprocessing.c:37-93, src/erasurecode_helpers.c:463-496; wire format
+// include/erasurecode.h fragment_header_t), plus the object <-> payload copies of
+// prepare_fragments_for_encode (src/erasurecode_preprocessing.c:36-108) and fragments_to_string
+// (:269-370).
+//
+// CRC32 of a payload (host/crc.hpp has the algebra) runs in two kernels:
+//   crc_partial_kernel<B>  one wave per "span" of J KiB of one payload.  Lane l owns the 16-byte
+//     pieces l, l+64, l+128, ... of the span (so every wave load is a coalesced 1 KiB), and keeps
+//     state s = A^1024 s ^ r0(piece): r0(piece) is 128/B lookups of B-bit fields in LDS tables and
+//     A^1024 (the 1008-byte gap to the lane's next piece, plus the piece) 32/B lookups.  A 6-level
+//     shuffle butterfly (A^(16*2^t) tables) folds the 64 lane states into r0(span).  Spans are
+//     aligned to the END of the payload's 16-byte body, so the first one is padded with leading
+//     zeros, which do not change r0.
+//   crc_finalize_kernel    one thread per payload: Horner over its spans with A^(J KiB), the last
+//     len % 16 bytes through the byte table, crc = ~(A^len ~0 ^ r0), and -- when asked -- the
+//     whole 80-byte header with its metadata checksum.
+// B = 8 (byte tables, 20 KiB + 24 KiB) or B = 4 (nibble tables: 16 entries span 16 distinct LDS
+// banks, so lookups never conflict, at twice the lookups).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ecamd_frame.hpp"
+
+namespace ecamd {
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ u32x4 nt_load16(const uint8_t* p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t lmap(const uint32_t* tab, uint32_t x)
+{
+    constexpr int E = 1 << B;
+    constexpr uint32_t M = E - 1;
+    uint32_t r = 0;
+#pragma unroll
+    for (int f = 0; f < 32 / B; ++f) r ^= tab[f * E + ((x >> (f * B)) & M)];
+    return r;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t piece_r0(const uint32_t* tab, u32x4 v)
+{
+    constexpr int S = (32 / B) << B;  // words of one data word's tables
+    return lmap<B>(tab, v.x) ^ lmap<B>(tab + S, v.y) ^ lmap<B>(tab + 2 * S, v.z) ^
+           lmap<B>(tab + 3 * S, v.w);
+}
+
+__device__ __forceinline__ uint32_t byte_step(const uint32_t* T, uint32_t s, uint32_t b, int legacy)
+{
+    uint32_t sh = s >> 8;
+    if (legacy && (s & 0x80000000u)) sh |= 0xff000000u;
+    return T[(s ^ b) & 0xffu] ^ sh;
+}
+
+__device__ __forceinline__ const uint8_t* item_ptr(const CrcArgs& a, int64_t item)
+{
+    const int64_t s = item / a.nfrag;
+    const int f = static_cast<int>(item - s * a.nfrag);
+    return a.base + s * a.stripe_stride + f * a.frag_stride;
+}
+
+}  // namespace
+
+template <int B>
+__global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
+                                                          uint32_t* __restrict__ partial)
+{
+    constexpr int E = 1 << B, NF = 32 / B;
+    constexpr int PIECE = 4 * NF * E, FIELDS = NF * E, WORDS = PIECE + 7 * FIELDS;
+    __shared__ uint32_t tab[WORDS];
+    for (int i = threadIdx.x; i < WORDS; i += blockDim.x) tab[i] = img[i];
+    __syncthreads();
+    const uint32_t* gap = tab + PIECE;
+    const int lane = threadIdx.x & 63;
+    const int nw = blockDim.x >> 6;
+    const int64_t total = static_cast<int64_t>(a.items) * a.nspans;
+    const int64_t span = static_cast<int64_t>(a.J) * 1024;
+    for (int64_t ws = static_cast<int64_t>(blockIdx.x) * nw + (threadIdx.x >> 6); ws < total;
+         ws += static_cast<int64_t>(gridDim.x) * nw) {
+        const int64_t item = ws / a.nspans;
+        const int q = static_cast<int>(ws - item * a.nspans);
+        const uint8_t* p = item_ptr(a, item) + a.payload_off;
+        const int64_t start = a.body - static_cast<int64_t>(a.nspans - q) * span + lane * 16;
+        uint32_t st = 0;
+        for (int j = 0; j < a.J; j += 4) {
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t off = start + static_cast<int64_t>(j + u) * 1024;
+                v[u] = off >= 0 ? nt_load16(p + off) : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) st = lmap<B>(gap, st) ^ piece_r0<B>(tab, v[u]);
+        }
+        // Lane l's state sits (63 - l) pieces before the span end: fold pairs, quads, ...
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const uint32_t right = __shfl_down(st, 1 << t, 64);
+            st = lmap<B>(tab + PIECE + FIELDS * (1 + t), st) ^ right;
+        }
+        if (lane == 0) partial[ws] = st;
+    }
+}
+
+template __global__ void crc_partial_kernel<8>(const CrcArgs, const uint32_t* __restrict__,
+                                               uint32_t* __restrict__);
+template __global__ void crc_partial_kernel<4>(const CrcArgs, const uint32_t* __restrict__,
+                                               uint32_t* __restrict__);
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void put(uint8_t* h, int off, uint64_t v)
+{
+#pragma unroll
+    for (int i = 0; i < N; ++i) h[off + i] = static_cast<uint8_t>(v >> (8 * i));
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t get(const uint8_t* h, int off)
+{
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) v |= static_cast<uint32_t>(h[off + i]) << (8 * i);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t meta_crc(const uint32_t* T, const uint8_t* h, int legacy)
+{
+    uint32_t s = ~0u;
+#pragma unroll
+    for (int i = 0; i < kMetaBytes; ++i) s = byte_step(T, s, h[i], legacy);
+    return ~s;
+}
+
+}  // namespace
+
+__global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
+                                    const uint32_t* __restrict__ partial, uint32_t* __restrict__ crc_out,
+                                    const HeaderArgs h)
+{
+    const int64_t item = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (item >= a.items) return;
+    const uint32_t* span = img + a.span_off;
+    const uint32_t* T = img + a.t_off;
+    const uint8_t* frag = item_ptr(a, item);
+    uint32_t crc = 0;
+    if (a.nspans > 0) {
+        uint32_t acc = 0;
+        const uint32_t* pp = partial + item * a.nspans;
+        for (int q = 0; q < a.nspans; ++q) {
+            acc = span[acc & 0xff] ^ span[256 + ((acc >> 8) & 0xff)] ^
+                  span[512 + ((acc >> 16) & 0xff)] ^ span[768 + (acc >> 24)] ^ pp[q];
+        }
+        const uint8_t* p = frag + a.payload_off;
+        for (int64_t i = a.body; i < a.len; ++i) acc = byte_step(T, acc, p[i], a.legacy);
+        crc = ~(a.c0 ^ acc);
+        if (crc_out) crc_out[item] = crc;
+    }
+    if (!h.write) return;
+    // add_fragment_metadata (src/erasurecode_postprocessing.c:37-69) on a zeroed header
+    // (alloc_fragment_buffer, src/erasurecode_helpers.c:124-138).
+    uint8_t hd[kHeaderBytes];
+#pragma unroll
+    for (int i = 0; i < kHeaderBytes; ++i) hd[i] = 0;
+    const int f = static_cast<int>(item % a.nfrag);
+    put<4>(hd, 0, static_cast<uint32_t>(h.idx0 + f));
+    put<4>(hd, 4, h.size);
+    put<4>(hd, 8, h.backend_meta_size);
+    put<8>(hd, 12, h.orig_data_size);
+    put<1>(hd, 20, h.chksum_type);
+    if (h.chksum_type == kChksumCrc32) put<4>(hd, 21, crc);
+    put<1>(hd, 54, h.backend_id);
+    put<4>(hd, 55, h.backend_version);
+    put<4>(hd, 59, kFragMagic);
+    put<4>(hd, 63, h.libec_version);
+    put<4>(hd, 67, meta_crc(T, hd, a.legacy));
+    uint8_t* out = const_cast<uint8_t*>(frag);
+#pragma unroll
+    for (int c = 0; c < kHeaderBytes / 16; ++c) {
+        uint4 v = make_uint4(get<4>(hd, 16 * c), get<4>(hd, 16 * c + 4), get<4>(hd, 16 * c + 8),
+                             get<4>(hd, 16 * c + 12));
+        *reinterpret_cast<uint4*>(out + 16 * c) = v;
+    }
+}
+
+// prepare_fragments_for_encode: data payload j of stripe s = object bytes [j*bs, (j+1)*bs), zero
+// padded past the object's end (and through the 16-byte slack after the payload).
+__global__ void frame_split_kernel(const SplitArgs a)
+{
+    const int64_t per_frag = (a.bs + 15) / 16;
+    const int64_t total = per_frag * a.k * a.nstripes;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+         t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t sj = t / per_frag;
+        const int64_t c = t - sj * per_frag;
+        const int64_t s = sj / a.k;
+        const int j = static_cast<int>(sj - s * a.k);
+        const int64_t src_off = j * a.bs + c * 16;
+        int64_t n = a.size - src_off;
+        n = n < 0 ? 0 : n;
+        n = n > a.bs - c * 16 ? a.bs - c * 16 : n;
+        const uint8_t* src = a.obj + s * a.obj_stride + src_off;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (n >= 16 && a.aligned) {
+            u32x4 w = nt_load16(src);
+            v = make_uint4(w.x, w.y, w.z, w.w);
+        } else if (n > 0) {
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (int i = 0; i < (n < 16 ? n : 16); ++i) w[i >> 2] |= static_cast<uint32_t>(src[i]) << (8 * (i & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        uint8_t* dst = a.frags + s * a.stripe_stride + j * a.frag_stride + kHeaderBytes + c * 16;
+        u32x4 o = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(o, reinterpret_cast<u32x4*>(dst));
+    }
+}
+
+// fragments_to_string: object bytes [0, size) = data payloads 0..k-1 concatenated.
+__global__ void frame_join_kernel(const JoinArgs a)
+{
+    const int64_t per_obj = (a.size + 15) / 16;
+    const int64_t total = per_obj * a.nstripes;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+         t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t s = t / per_obj;
+        const int64_t o = (t - s * per_obj) * 16;
+        const uint8_t* fr = a.frags + s * a.stripe_stride + kHeaderBytes;
+        uint8_t* dst = a.obj + s * a.obj_stride + o;
+        const int64_t n = a.size - o < 16 ? a.size - o : 16;
+        if (n == 16 && a.aligned) {
+            const int64_t j = o / a.bs;
+            u32x4 w = nt_load16(fr + j * a.frag_stride + (o - j * a.bs));
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
+        } else {
+            for (int i = 0; i < n; ++i) {
+                const int64_t b = o + i;
+                const int64_t j = b / a.bs;
+                dst[i] = fr[j * a.frag_stride + (b - j * a.bs)];
+            }
+        }
+    }
+}
+
+// is_invalid_fragment_header / checksum verification (src/erasurecode.c:1050-1140): per fragment
+// bit 0 bad magic, bit 1 metadata checksum (neither zlib nor legacy), bit 2 idx != slot, bit 3
+// size != blocksize, bit 4 payload CRC32 mismatch (only when chksum_type says CRC32).
+__global__ void frame_verify_kernel(const CrcArgs a, const uint32_t* __restrict__ img_zlib,
+                                    const uint32_t* __restrict__ img_legacy,
+                                    const uint32_t* __restrict__ crc, int64_t bs,
+                                    uint32_t* __restrict__ status)
+{
+    const int64_t item = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (item >= a.items) return;
+    const uint8_t* frag = item_ptr(a, item);
+    uint8_t hd[kHeaderBytes];
+#pragma unroll
+    for (int c = 0; c < kHeaderBytes / 16; ++c) {
+        uint4 v = *reinterpret_cast<const uint4*>(frag + 16 * c);
+        put<4>(hd, 16 * c, v.x);
+        put<4>(hd, 16 * c + 4, v.y);
+        put<4>(hd, 16 * c + 8, v.z);
+        put<4>(hd, 16 * c + 12, v.w);
+    }
+    uint32_t st = 0;
+    if (get<4>(hd, 59) != kFragMagic) st |= 1u;
+    const uint32_t stored = get<4>(hd, 67);
+    if (stored != meta_crc(img_zlib + a.t_off, hd, 0) && stored != meta_crc(img_legacy + a.t_off, hd, 1))
+        st |= 2u;
+    if (get<4>(hd, 0) != static_cast<uint32_t>(item % a.nfrag)) st |= 4u;
+    if (get<4>(hd, 4) != static_cast<uint32_t>(bs)) st |= 8u;
+    if (hd[20] == kChksumCrc32 && crc && get<4>(hd, 21) != crc[item]) st |= 16u;
+    status[item] = st;
+}
+
+}  // namespace ecamd

@@ -1,0 +1,82 @@
+// ecamd_frame.hpp -- argument blocks of the framing / CRC kernels (hip/ecamd_frame.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ecamd {
+
+constexpr int kHeaderBytes = 80;           // sizeof(fragment_header_t), include/erasurecode.h
+constexpr int kMetaBytes = 59;             // sizeof(fragment_metadata_t)
+constexpr uint32_t kFragMagic = 0xb0c5ecc;  // LIBERASURECODE_FRAG_HEADER_MAGIC
+constexpr uint8_t kChksumCrc32 = 2;        // CHKSUM_CRC32
+
+// Items = nstripes * nfrag payloads; item (s, f) fragment at base + s*stripe_stride + f*frag_stride,
+// its payload at + payload_off, len bytes (body = len & ~15 handled by the partial kernel).
+struct CrcArgs {
+    const uint8_t* base;
+    int64_t stripe_stride;
+    int64_t frag_stride;
+    int64_t payload_off;
+    int64_t len;
+    int64_t body;
+    int64_t items;
+    int nfrag;
+    int nspans;      // spans per item (0: no checksum, header only)
+    int J;           // KiB per span
+    int legacy;      // 1: liberasurecode_crc32_alt machine
+    uint32_t c0;     // A^len(~0)
+    uint32_t span_off;
+    uint32_t t_off;
+};
+
+struct HeaderArgs {
+    int write;
+    int idx0;
+    uint32_t size;
+    uint32_t backend_meta_size;
+    uint64_t orig_data_size;
+    uint32_t backend_version;
+    uint32_t libec_version;
+    uint8_t chksum_type;
+    uint8_t backend_id;
+};
+
+struct SplitArgs {
+    const uint8_t* obj;
+    int64_t obj_stride;
+    int64_t size;
+    uint8_t* frags;
+    int64_t stripe_stride;
+    int64_t frag_stride;
+    int64_t bs;
+    int k;
+    int nstripes;
+    int aligned;     // object base / stride / bs all 16-byte multiples
+};
+
+struct JoinArgs {
+    const uint8_t* frags;
+    int64_t stripe_stride;
+    int64_t frag_stride;
+    int64_t bs;
+    uint8_t* obj;
+    int64_t obj_stride;
+    int64_t size;
+    int nstripes;
+    int aligned;
+};
+
+template <int B>
+__global__ void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
+                                   uint32_t* __restrict__ partial);
+__global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
+                                    const uint32_t* __restrict__ partial,
+                                    uint32_t* __restrict__ crc_out, const HeaderArgs h);
+__global__ void frame_split_kernel(const SplitArgs a);
+__global__ void frame_join_kernel(const JoinArgs a);
+__global__ void frame_verify_kernel(const CrcArgs a, const uint32_t* __restrict__ img_zlib,
+                                    const uint32_t* __restrict__ img_legacy,
+                                    const uint32_t* __restrict__ crc, int64_t bs,
+                                    uint32_t* __restrict__ status);
+
+}  // namespace ecamd

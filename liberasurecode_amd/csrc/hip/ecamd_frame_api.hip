@@ -1,0 +1,450 @@
+// ecamd_frame_api.hip -- C ABI of the device-resident framed path (include/ecamd.h, "framing"):
+// whole liberasurecode_encode / _decode / _reconstruct_fragment equivalents over S stripes whose
+// objects and fragments live in HBM, byte-identical to the reference's wire format.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "../host/crc.hpp"
+#include "ecamd.h"
+#include "ecamd_frame.hpp"
+#include "ecamd_host.h"
+#include "ecamd_internal.hpp"
+
+using namespace ecamd;
+
+namespace {
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return dev_fail(ECAMD_EHIP, "%s: %s", #expr, hipGetErrorString(e_));           \
+    } while (0)
+
+constexpr int kBackendXor = 3;   // EC_BACKEND_FLAT_XOR_HD
+constexpr int kBackendRs = 6;    // EC_BACKEND_LIBERASURECODE_RS_VAND
+constexpr uint32_t kLibecVersion = (1u << 16) | (8u << 8);  // LIBERASURECODE_VERSION 1.8.0
+constexpr uint32_t kBackendVersion = 1u << 16;              // ec_backend_version 1.0.0
+
+// LIBERASURECODE_WRITE_LEGACY_CRC, read per call as the reference does
+// (src/erasurecode_postprocessing.c:59-60, src/erasurecode_helpers.c:479-480).
+bool legacy_crc()
+{
+    const char* f = std::getenv("LIBERASURECODE_WRITE_LEGACY_CRC");
+    return f && !(f[0] == '\0' || (f[0] == '0' && f[1] == '\0'));
+}
+
+struct DevImage {
+    uint32_t* d = nullptr;
+    CrcImage img;
+};
+
+std::mutex g_mu;
+std::map<std::tuple<int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J
+std::map<std::pair<int, void*>, std::pair<uint32_t*, size_t>> g_scratch;     // dev, stream
+
+int image(int dev, bool legacy, int B, int J, const DevImage** out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_tuple(dev, legacy ? 1 : 0, B, J);
+    auto it = g_images.find(key);
+    if (it == g_images.end()) {
+        auto di = std::make_unique<DevImage>();
+        di->img = build_crc_image(CrcMachine(legacy), B, J);
+        const size_t bytes = di->img.words.size() * sizeof(uint32_t);
+        HIP_TRY(hipMalloc(&di->d, bytes));
+        HIP_TRY(hipMemcpy(di->d, di->img.words.data(), bytes, hipMemcpyHostToDevice));
+        it = g_images.emplace(key, std::move(di)).first;
+    }
+    *out = it->second.get();
+    return 0;
+}
+
+// Per-(device, stream) scratch for span partials; calls on one stream are ordered, so reuse is safe.
+int scratch(int dev, void* stream, size_t words, uint32_t** out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& e = g_scratch[{dev, stream}];
+    if (e.second < words) {
+        if (e.first) {
+            HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+            HIP_TRY(hipFree(e.first));
+            e.first = nullptr;
+            e.second = 0;
+        }
+        HIP_TRY(hipMalloc(&e.first, std::max<size_t>(words, 1) * sizeof(uint32_t)));
+        e.second = std::max<size_t>(words, 1);
+    }
+    *out = e.first;
+    return 0;
+}
+
+struct Code {
+    int backend, k, m, hd, w;
+};
+
+int check_code(const Code& c)
+{
+    if (c.backend == kBackendRs) {
+        if (c.k < 1 || c.m < 1 || c.k + c.m > 32)
+            return dev_fail(ECAMD_EINVAL, "rs_vand: need k >= 1, m >= 1, k + m <= 32");
+    } else if (c.backend == kBackendXor) {
+        unsigned pb[32], db[32];
+        if (c.k < 1 || c.m < 1 || c.k > 32 || c.m > 32 ||
+            ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db) != 0)
+            return dev_fail(ECAMD_EINVAL, "flat_xor_hd: (k=%d, m=%d, hd=%d) is not a supported code",
+                            c.k, c.m, c.hd);
+    } else {
+        return dev_fail(ECAMD_EINVAL, "backend %d has no device path (3 flat_xor_hd, 6 rs_vand)",
+                        c.backend);
+    }
+    return 0;
+}
+
+Code make_code(int backend, int k, int m, int hd)
+{
+    return Code{backend, k, m, hd, backend == kBackendXor ? 32 : 16};
+}
+
+// get_aligned_data_size (src/erasurecode_helpers.c:186-208) / k, in int as the reference.
+int64_t blocksize_of(const Code& c, uint64_t size)
+{
+    const int64_t a = static_cast<int64_t>(c.k) * (c.w / 8);
+    const int64_t aligned = ((static_cast<int64_t>(size) + a - 1) / a) * a;
+    return aligned / c.k;
+}
+
+bool a16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int check_frames(const void* frags, int64_t stripe_stride, int64_t frag_stride, int64_t bs,
+                 int nfrag, int nstripes)
+{
+    if (!frags || nstripes < 0) return dev_fail(ECAMD_EINVAL, "null fragments or nstripes < 0");
+    if (!a16(frags) || stripe_stride % 16 || frag_stride % 16)
+        return dev_fail(ECAMD_EINVAL, "fragment base and strides must be 16-byte aligned");
+    if (frag_stride < kHeaderBytes + ((bs + 15) & ~int64_t(15)))
+        return dev_fail(ECAMD_EINVAL, "frag_stride %lld < 80 + blocksize rounded to 16 (%lld)",
+                        (long long)frag_stride, (long long)(kHeaderBytes + ((bs + 15) & ~int64_t(15))));
+    return 0;
+}
+
+// CRC32 of nfrag payloads per stripe (fragment f at base + s*ss + f*fs, payload at +payload_off)
+// and, if h.write, the headers.  crc_out may be null.
+int run_crc(int dev, bool legacy, bool with_crc, const uint8_t* base, int64_t ss, int64_t fs,
+            int64_t payload_off, int nfrag, int64_t len, int nstripes, uint32_t* crc_out,
+            const HeaderArgs& h, void* stream)
+{
+    const int64_t items = static_cast<int64_t>(nfrag) * nstripes;
+    if (items == 0) return 0;
+    const int B = dev_tune("crc_bits") == 4 ? 4 : 8;
+    const int64_t body = len & ~int64_t(15);
+    int J = static_cast<int>(std::min<int64_t>(16, std::max<int64_t>(4, ((body / 1024 + 3) / 4) * 4)));
+    const DevImage* di = nullptr;
+    int rc = image(dev, legacy, B, J, &di);
+    if (rc) return rc;
+    CrcArgs a{};
+    a.base = base;
+    a.stripe_stride = ss;
+    a.frag_stride = fs;
+    a.payload_off = payload_off;
+    a.len = len;
+    a.body = body;
+    a.items = items;
+    a.nfrag = nfrag;
+    a.J = J;
+    a.legacy = legacy ? 1 : 0;
+    a.span_off = static_cast<uint32_t>(di->img.span_off);
+    a.t_off = static_cast<uint32_t>(di->img.t_off);
+    a.nspans = 0;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint32_t* partial = nullptr;
+    if (with_crc) {
+        const int64_t span = static_cast<int64_t>(J) * 1024;
+        a.nspans = static_cast<int>(std::max<int64_t>(1, (body + span - 1) / span));
+        a.c0 = zero_shift(CrcMachine(legacy), static_cast<uint64_t>(len)).apply(~0u);
+        const int64_t waves = items * a.nspans;
+        rc = scratch(dev, stream, static_cast<size_t>(waves), &partial);
+        if (rc) return rc;
+        int wpc = dev_tune("crc_wgs");
+        // Measured on MI355X (C3 payloads, 3.5 GiB): B=8 at 2 workgroups/CU 6.35 TB/s, 3: 5.94,
+        // 4 (LDS-capped to 3): 5.95; B=4 at 4: 5.36 ("Framing").
+        if (wpc <= 0) wpc = B == 8 ? 2 : 4;
+        const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(
+                                                      static_cast<int64_t>(dev_cu_count(dev)) * wpc,
+                                                      (waves + 7) / 8));
+        if (B == 8)
+            hipLaunchKernelGGL(crc_partial_kernel<8>, dim3(static_cast<unsigned>(grid)), dim3(512), 0,
+                               st, a, di->d, partial);
+        else
+            hipLaunchKernelGGL(crc_partial_kernel<4>, dim3(static_cast<unsigned>(grid)), dim3(512), 0,
+                               st, a, di->d, partial);
+        HIP_TRY(hipGetLastError());
+    }
+    if (with_crc || h.write) {
+        hipLaunchKernelGGL(crc_finalize_kernel, dim3(static_cast<unsigned>((items + 127) / 128)),
+                           dim3(128), 0, st, a, di->d, partial, crc_out, h);
+        HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+HeaderArgs header_args(const Code& c, int checksum, int64_t bs, uint64_t obj_size, int idx0)
+{
+    HeaderArgs h{};
+    h.write = 1;
+    h.idx0 = idx0;
+    h.size = static_cast<uint32_t>(bs);
+    h.backend_meta_size = 0;  // get_backend_metadata_size is 0 for both backends
+    h.orig_data_size = obj_size;
+    h.backend_version = kBackendVersion;
+    h.libec_version = kLibecVersion;
+    h.chksum_type = static_cast<uint8_t>(checksum);
+    h.backend_id = static_cast<uint8_t>(c.backend);
+    return h;
+}
+
+int grid_for(int dev, int64_t work)
+{
+    return static_cast<int>(std::max<int64_t>(
+        1, std::min<int64_t>((work + 255) / 256, static_cast<int64_t>(dev_cu_count(dev)) * 16)));
+}
+
+// XOR plan of a reference operation applied in place on the payloads of every stripe.
+int xor_plan_apply(const Code& c, int op, const int* missing, int arg, uint8_t* payload0,
+                   int64_t ss, int64_t fs, int64_t bs, int nstripes, void* stream)
+{
+    unsigned pb[32], db[32];
+    ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db);
+    std::vector<int> outs(c.k + c.m);
+    std::vector<uint64_t> srcs(c.k + c.m);
+    int n = 0;
+    const int prc = ecamd_xor_plan(op, c.k, c.m, c.hd, pb, db, missing, arg, outs.data(),
+                                   srcs.data(), &n);
+    if (prc < 0)
+        return dev_fail(ECAMD_EINVAL, "flat_xor_hd: erasure pattern not recoverable (rc %d)", prc);
+    if (n == 0) return 0;
+    // The frontend hands the codec zero-filled buffers for missing fragments
+    // (src/erasurecode_preprocessing.c:141-147, 180-186) and the XOR code accumulates into them,
+    // so whatever the missing slots hold here counts as zero.
+    uint64_t lost = 0;
+    for (int i = 0; missing[i] >= 0; i++) lost |= uint64_t(1) << missing[i];
+    uint64_t used = 0;
+    for (int i = 0; i < n; i++) {
+        srcs[i] &= ~lost;
+        used |= srcs[i];
+    }
+    std::vector<int> col(64, -1);
+    std::vector<int64_t> in_off, out_off;
+    for (int b = 0; b < c.k + c.m; b++)
+        if (used >> b & 1u) {
+            col[b] = static_cast<int>(in_off.size());
+            in_off.push_back(b * fs);
+        }
+    if (in_off.empty()) in_off.push_back(0);  // every output is all-zero: one unused input
+    std::vector<uint32_t> masks;
+    for (int i = 0; i < n; i++) {
+        uint32_t mk = 0;
+        for (int b = 0; b < c.k + c.m; b++)
+            if (srcs[i] >> b & 1u) mk |= 1u << col[b];
+        masks.push_back(mk);
+        out_off.push_back(outs[i] * fs);
+    }
+    return ecamd_xor_apply_strided(masks.data(), n, static_cast<int>(in_off.size()), payload0, ss,
+                                   in_off.data(), payload0, ss, out_off.data(), bs, nstripes, stream);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ecamd_frame_geometry(int backend, int k, int m, int hd, uint64_t obj_size, int64_t* blocksize,
+                         int64_t* fragment_len)
+{
+    const Code c = make_code(backend, k, m, hd);
+    int rc = check_code(c);
+    if (rc) return rc;
+    if (obj_size > 0x7fffffffull) return dev_fail(ECAMD_EINVAL, "object larger than INT_MAX");
+    const int64_t bs = blocksize_of(c, obj_size);
+    if (blocksize) *blocksize = bs;
+    if (fragment_len) *fragment_len = kHeaderBytes + bs;
+    return 0;
+}
+
+int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const void* d_obj,
+                       int64_t obj_stride, uint64_t obj_size, void* d_frags, int64_t stripe_stride,
+                       int64_t frag_stride, int nstripes, void* stream)
+{
+    int dev = 0;
+    int rc = dev_ensure(&dev);
+    if (rc) return rc;
+    const Code c = make_code(backend, k, m, hd);
+    if ((rc = check_code(c))) return rc;
+    if (obj_size > 0x7fffffffull) return dev_fail(ECAMD_EINVAL, "object larger than INT_MAX");
+    const int64_t bs = blocksize_of(c, obj_size);
+    if ((rc = check_frames(d_frags, stripe_stride, frag_stride, bs, k + m, nstripes))) return rc;
+    if (nstripes == 0) return 0;
+    if (!d_obj && obj_size) return dev_fail(ECAMD_EINVAL, "null object buffer");
+    auto* frags = static_cast<uint8_t*>(d_frags);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SplitArgs sa{static_cast<const uint8_t*>(d_obj), obj_stride, static_cast<int64_t>(obj_size),
+                 frags, stripe_stride, frag_stride, bs, k, nstripes,
+                 (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
+    hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),
+                       dim3(256), 0, st, sa);
+    HIP_TRY(hipGetLastError());
+    uint8_t* p0 = frags + kHeaderBytes;
+    if (backend == kBackendRs) {
+        rc = ecamd_rs_encode(k, m, p0, stripe_stride, frag_stride, bs, nstripes, stream);
+    } else {
+        // xor_code_encode accumulates into zeroed parity (src/builtin/xor_codes/xor_code.c:180-191):
+        // parity j = XOR of the data fragments in parity_bms[j].
+        unsigned pb[32], db[32];
+        ecamd_xor_code_tables(k, m, hd, pb, db);
+        std::vector<int64_t> in_off(k), out_off(m);
+        for (int j = 0; j < k; j++) in_off[j] = j * frag_stride;
+        for (int r = 0; r < m; r++) out_off[r] = (k + r) * frag_stride;
+        rc = ecamd_xor_apply_strided(pb, m, k, p0, stripe_stride, in_off.data(), p0, stripe_stride,
+                                     out_off.data(), bs, nstripes, stream);
+    }
+    if (rc) return rc;
+    const bool legacy = legacy_crc();
+    return run_crc(dev, legacy, checksum == kChksumCrc32, frags, stripe_stride, frag_stride,
+                   kHeaderBytes, k + m, bs, nstripes, nullptr, header_args(c, checksum, bs, obj_size, 0),
+                   stream);
+}
+
+int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, void* d_frags,
+                       int64_t stripe_stride, int64_t frag_stride, int nstripes, void* d_obj,
+                       int64_t obj_stride, uint64_t obj_size, void* stream)
+{
+    int dev = 0;
+    int rc = dev_ensure(&dev);
+    if (rc) return rc;
+    const Code c = make_code(backend, k, m, hd);
+    if ((rc = check_code(c))) return rc;
+    if (!missing) return dev_fail(ECAMD_EINVAL, "null missing list");
+    const int64_t bs = blocksize_of(c, obj_size);
+    if ((rc = check_frames(d_frags, stripe_stride, frag_stride, bs, k + m, nstripes))) return rc;
+    if (nstripes == 0) return 0;
+    int nmiss = 0, data_missing = 0;
+    for (; missing[nmiss] >= 0; nmiss++) {
+        if (missing[nmiss] >= k + m) return dev_fail(ECAMD_EINVAL, "missing index out of range");
+        data_missing += missing[nmiss] < k;
+    }
+    if (nmiss > m) return dev_fail(ECAMD_EINVAL, "%d fragments missing, at most m = %d", nmiss, m);
+    auto* frags = static_cast<uint8_t*>(d_frags);
+    uint8_t* p0 = frags + kHeaderBytes;
+    if (data_missing) {  // the systematic fast path (src/erasurecode.c:597-607) skips this
+        if (backend == kBackendRs)
+            rc = ecamd_rs_decode(k, m, missing, 0, p0, stripe_stride, frag_stride, bs, nstripes, stream);
+        else
+            rc = xor_plan_apply(c, 1, missing, 0, p0, stripe_stride, frag_stride, bs, nstripes, stream);
+        if (rc) return rc;
+    }
+    if (obj_size == 0) return 0;
+    if (!d_obj) return dev_fail(ECAMD_EINVAL, "null object buffer");
+    JoinArgs ja{frags, stripe_stride, frag_stride, bs, static_cast<uint8_t*>(d_obj), obj_stride,
+                static_cast<int64_t>(obj_size), nstripes,
+                (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
+    hipLaunchKernelGGL(frame_join_kernel,
+                       dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),
+                       dim3(256), 0, static_cast<hipStream_t>(stream), ja);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_frame_reconstruct(int backend, int k, int m, int hd, int checksum, const int* missing,
+                            int dest, void* d_frags, int64_t stripe_stride, int64_t frag_stride,
+                            uint64_t obj_size, int nstripes, void* stream)
+{
+    int dev = 0;
+    int rc = dev_ensure(&dev);
+    if (rc) return rc;
+    const Code c = make_code(backend, k, m, hd);
+    if ((rc = check_code(c))) return rc;
+    if (!missing || dest < 0 || dest >= k + m) return dev_fail(ECAMD_EINVAL, "bad missing / dest");
+    const int64_t bs = blocksize_of(c, obj_size);
+    if ((rc = check_frames(d_frags, stripe_stride, frag_stride, bs, k + m, nstripes))) return rc;
+    if (nstripes == 0) return 0;
+    int nmiss = 0;
+    while (missing[nmiss] >= 0) nmiss++;
+    if (nmiss > m) return dev_fail(ECAMD_EINVAL, "%d fragments missing, at most m = %d", nmiss, m);
+    auto* frags = static_cast<uint8_t*>(d_frags);
+    uint8_t* p0 = frags + kHeaderBytes;
+    if (backend == kBackendRs)
+        rc = ecamd_rs_reconstruct(k, m, missing, dest, p0, stripe_stride, frag_stride, bs, nstripes,
+                                  stream);
+    else
+        rc = xor_plan_apply(c, 2, missing, dest, p0, stripe_stride, frag_stride, bs, nstripes, stream);
+    if (rc) return rc;
+    // liberasurecode_reconstruct_fragment stamps the rebuilt fragment with its checksum
+    // (src/erasurecode.c:907-915 -> add_fragment_metadata).
+    return run_crc(dev, legacy_crc(), checksum == kChksumCrc32, frags + dest * frag_stride,
+                   stripe_stride, frag_stride, kHeaderBytes, 1, bs, nstripes, nullptr,
+                   header_args(c, checksum, bs, obj_size, dest), stream);
+}
+
+int ecamd_frame_verify(int nfrag, int64_t blocksize, int legacy, const void* d_frags,
+                       int64_t stripe_stride, int64_t frag_stride, int nstripes,
+                       uint32_t* d_status, uint32_t* d_crc, void* stream)
+{
+    int dev = 0;
+    int rc = dev_ensure(&dev);
+    if (rc) return rc;
+    if (nfrag < 1 || nfrag > 64 || blocksize < 0 || !d_status)
+        return dev_fail(ECAMD_EINVAL, "bad nfrag / blocksize / status");
+    if ((rc = check_frames(d_frags, stripe_stride, frag_stride, blocksize, nfrag, nstripes))) return rc;
+    if (nstripes == 0) return 0;
+    const int64_t items = static_cast<int64_t>(nfrag) * nstripes;
+    uint32_t* crc = d_crc;
+    std::unique_ptr<void, int (*)(void*)> tmp(nullptr, [](void* p) { return static_cast<int>(hipFree(p)); });
+    if (!crc) {
+        void* t = nullptr;
+        HIP_TRY(hipMalloc(&t, items * sizeof(uint32_t)));
+        tmp.reset(t);
+        crc = static_cast<uint32_t*>(t);
+    }
+    const auto* frags = static_cast<const uint8_t*>(d_frags);
+    HeaderArgs none{};
+    rc = run_crc(dev, legacy != 0, true, frags, stripe_stride, frag_stride, kHeaderBytes, nfrag,
+                 blocksize, nstripes, crc, none, stream);
+    if (rc) return rc;
+    const DevImage *iz = nullptr, *il = nullptr;
+    if ((rc = image(dev, false, 8, 4, &iz)) || (rc = image(dev, true, 8, 4, &il))) return rc;
+    CrcArgs a{};
+    a.base = frags;
+    a.stripe_stride = stripe_stride;
+    a.frag_stride = frag_stride;
+    a.items = items;
+    a.nfrag = nfrag;
+    a.t_off = static_cast<uint32_t>(iz->img.t_off);
+    hipLaunchKernelGGL(frame_verify_kernel, dim3(static_cast<unsigned>((items + 127) / 128)), dim3(128),
+                       0, static_cast<hipStream_t>(stream), a, iz->d, il->d, crc, blocksize, d_status);
+    HIP_TRY(hipGetLastError());
+    if (tmp) HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int ecamd_crc32(int legacy, const void* d_base, int64_t stripe_stride, int64_t frag_stride,
+                int nfrag, int64_t len, int nstripes, uint32_t* d_crc, void* stream)
+{
+    int dev = 0;
+    int rc = dev_ensure(&dev);
+    if (rc) return rc;
+    if (!d_base || !d_crc || nfrag < 1 || len < 0 || nstripes < 0)
+        return dev_fail(ECAMD_EINVAL, "bad crc32 arguments");
+    if (!a16(d_base) || stripe_stride % 16 || frag_stride % 16)
+        return dev_fail(ECAMD_EINVAL, "crc32: base and strides must be 16-byte aligned");
+    HeaderArgs none{};
+    return run_crc(dev, legacy != 0, true, static_cast<const uint8_t*>(d_base), stripe_stride,
+                   frag_stride, 0, nfrag, len, nstripes, d_crc, none, stream);
+}
+
+}  // extern "C"

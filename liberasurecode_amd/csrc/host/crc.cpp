@@ -1,0 +1,75 @@
+// crc.cpp -- checksum machines and device table images (see crc.hpp).
+#include "crc.hpp"
+
+#include <cstring>
+
+namespace ecamd {
+
+CrcMachine::CrcMachine(bool legacy_variant) : legacy(legacy_variant)
+{
+    // The reflected CRC-32 byte table (polynomial 0xEDB88320) shared by both variants.
+    for (uint32_t n = 0; n < 256; n++) {
+        uint32_t c = n;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        t[n] = c;
+    }
+}
+
+Mat32 mat_mul(const Mat32& a, const Mat32& b)
+{
+    Mat32 r;
+    for (int i = 0; i < 32; i++) r.col[i] = a.apply(b.col[i]);
+    return r;
+}
+
+Mat32 zero_shift(const CrcMachine& m, uint64_t nbytes)
+{
+    Mat32 step, acc;
+    for (int b = 0; b < 32; b++) {
+        step.col[b] = m.step(1u << b, 0);
+        acc.col[b] = 1u << b;
+    }
+    while (nbytes) {
+        if (nbytes & 1u) acc = mat_mul(step, acc);
+        step = mat_mul(step, step);
+        nbytes >>= 1;
+    }
+    return acc;
+}
+
+void field_tables(const Mat32& M, int B, uint32_t* out)
+{
+    const int E = 1 << B;
+    for (int f = 0; f < 32 / B; f++)
+        for (int v = 0; v < E; v++) out[f * E + v] = M.apply(static_cast<uint32_t>(v) << (f * B));
+}
+
+CrcImage build_crc_image(const CrcMachine& m, int B, int J)
+{
+    CrcImage img;
+    img.B = B;
+    img.J = J;
+    const int E = 1 << B, NF = 32 / B;
+    const size_t piece = static_cast<size_t>(4 * NF) * E, fields = static_cast<size_t>(NF) * E;
+    img.lds_words = piece + fields * 7;
+    img.span_off = img.lds_words;
+    img.t_off = img.span_off + 4 * 256;
+    img.words.assign(img.t_off + 256, 0);
+    uint32_t* w = img.words.data();
+    // piece tables: word w of the 16-byte piece = v << (f * B), the rest zero; r0 by running it.
+    for (int word = 0; word < 4; word++)
+        for (int f = 0; f < NF; f++)
+            for (int v = 0; v < E; v++) {
+                uint8_t bytes[16] = {0};
+                const uint32_t x = static_cast<uint32_t>(v) << (f * B);
+                for (int q = 0; q < 4; q++) bytes[4 * word + q] = static_cast<uint8_t>(x >> (8 * q));
+                w[(word * NF + f) * E + v] = m.run(0, bytes, 16);
+            }
+    field_tables(zero_shift(m, 64 * 16), B, w + piece);
+    for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), B, w + piece + fields * (1 + t));
+    field_tables(zero_shift(m, static_cast<uint64_t>(J) * 1024), 8, w + img.span_off);
+    std::memcpy(w + img.t_off, m.t, sizeof(m.t));
+    return img;
+}
+
+}  // namespace ecamd

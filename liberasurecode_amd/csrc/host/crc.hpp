@@ -1,0 +1,76 @@
+// crc.hpp -- the fragment checksums of the reference as GF(2)-linear state machines, and the
+// table images the device CRC kernels (hip/ecamd_frame.hip) consume.
+//
+// Two machines, both "state' = T[(state ^ byte) & 0xff] ^ shift(state)", init ~0, final ~:
+//   * zlib crc32 (system zlib 1.2.11; called at src/erasurecode_postprocessing.c:66-67 and
+//     src/erasurecode_helpers.c:485), shift(s) = s >> 8;
+//   * liberasurecode_crc32_alt, the legacy checksum (src/utils/chksum/crc32.c:79-91), whose shift
+//     sign-extends bit 31 into the top byte.
+// Both are linear in (state, message), so with r0(M) = the state after M from state 0:
+//   r0(X || Y) = A^|Y| r0(X) ^ r0(Y),   crc(M) = ~(A^|M| ~0 ^ r0(M)),
+// where A is the machine's zero-byte step.  Every table below is built by running the machine
+// itself, so the device path follows whichever variant is selected without special cases.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace ecamd {
+
+struct CrcMachine {
+    bool legacy;
+    uint32_t t[256];
+    explicit CrcMachine(bool legacy_variant);
+    uint32_t step(uint32_t s, uint8_t b) const
+    {
+        uint32_t sh = s >> 8;
+        if (legacy && (s & 0x80000000u)) sh |= 0xff000000u;
+        return t[(s ^ b) & 0xffu] ^ sh;
+    }
+    uint32_t run(uint32_t s, const uint8_t* p, size_t n) const
+    {
+        while (n--) s = step(s, *p++);
+        return s;
+    }
+    uint32_t crc(const void* p, size_t n) const
+    {
+        return ~run(~0u, static_cast<const uint8_t*>(p), n);
+    }
+};
+
+// 32 x 32 matrix over GF(2), stored by columns: M(x) = XOR of col[b] for the set bits b of x.
+struct Mat32 {
+    uint32_t col[32];
+    uint32_t apply(uint32_t x) const
+    {
+        uint32_t r = 0;
+        for (int b = 0; b < 32; b++)
+            if (x >> b & 1u) r ^= col[b];
+        return r;
+    }
+};
+Mat32 mat_mul(const Mat32& a, const Mat32& b);  // a after b
+Mat32 zero_shift(const CrcMachine& m, uint64_t nbytes);  // A^nbytes
+
+// Field tables of a linear map for B-bit index fields: out[f * 2^B + v] = M(v << (f * B)),
+// f = 0 .. 32/B - 1.
+void field_tables(const Mat32& M, int B, uint32_t* out);
+
+// Image of one device CRC configuration (layout documented in hip/ecamd_frame.hip):
+//   [ piece tables: 128/B tables, r0 of a 16-byte piece holding v in field f of word w ]
+//   [ gap tables  : A^(64 lanes * 16 B) as 32/B field tables                          ]
+//   [ level tables: A^(16 * 2^t), t = 0..5, for the in-wave butterfly                    ]
+//   [ span tables : A^(J * 1024) as 4 byte tables (finalize kernel)                      ]
+//   [ T           : the machine's byte table (finalize: tail bytes and header checksum)  ]
+struct CrcImage {
+    int B = 8;
+    int J = 16;
+    std::vector<uint32_t> words;
+    size_t lds_words = 0;  // prefix staged into LDS by the partial kernel
+    size_t span_off = 0;
+    size_t t_off = 0;
+};
+CrcImage build_crc_image(const CrcMachine& m, int B, int J);
+
+}  // namespace ecamd

@@ -18,10 +18,9 @@
  *   Gauss-Jordan inversion over GF(2^16) ............. liberasurecode_rs_vand.c:293-334
  *   region xor / multiply / dot product .............. liberasurecode_rs_vand.c:336-397
  *   encode / decode / reconstruct .................... liberasurecode_rs_vand.c:399-558
- *   flat-XOR HD codes (bitmaps, encode, decode, reconstruct, fragments_needed)
- *                                   .................. src/builtin/xor_codes/xor_code.c:36-395,
- *                                                      src/builtin/xor_codes/xor_hd_code.c:30-708,
- *                                                      include/xor_codes/xor_hd_code_defs.h:29-173
+ *   fragment checksums: zlib crc32 (zlib 1.2.11, as called at src/erasurecode_postprocessing.c:
+ *   66-67) and the legacy liberasurecode_crc32_alt .... src/utils/chksum/crc32.c:79-91
+ * The flat-XOR HD codes are restated buffer-level in oracle/xor_oracle.py.
  *
  * One deliberate definition: for an odd blocksize the reference multiplies the trailing
  * byte through a signed `char` (liberasurecode_rs_vand.c:367-370), which indexes its log
@@ -353,4 +352,45 @@ void orc_splitmix_fill(uint64_t seed, uint8_t *out, int64_t nbytes)
                 out[o] = (uint8_t)(z >> (8 * b));
         }
     }
+}
+
+/* ------------------------------------------------------- checksums ---- */
+
+static uint32_t orc_crc_tab[256];
+
+static void orc_crc_init(void)
+{
+    if (orc_crc_tab[1])
+        return;
+    for (uint32_t n = 0; n < 256; n++) {
+        uint32_t c = n;
+        for (int b = 0; b < 8; b++)
+            c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        orc_crc_tab[n] = c;
+    }
+}
+
+/* zlib crc32(crc, buf, n): reflected CRC-32, polynomial 0xEDB88320, pre/post inversion. */
+uint32_t orc_crc32(uint32_t crc, const uint8_t *buf, int64_t n)
+{
+    orc_crc_init();
+    crc = ~crc;
+    while (n--)
+        crc = orc_crc_tab[(crc ^ *buf++) & 0xffu] ^ (crc >> 8);
+    return ~crc;
+}
+
+/* liberasurecode_crc32_alt: the same table, but the 8-bit shift of the (signed) state keeps
+ * bit 31 in the top byte (src/utils/chksum/crc32.c:86-88). */
+uint32_t orc_crc32_alt(uint32_t crc, const uint8_t *buf, int64_t n)
+{
+    orc_crc_init();
+    crc = ~crc;
+    while (n--) {
+        uint32_t sh = crc >> 8;
+        if (crc & 0x80000000u)
+            sh |= 0xff000000u;
+        crc = orc_crc_tab[(crc ^ *buf++) & 0xffu] ^ sh;
+    }
+    return ~crc;
 }

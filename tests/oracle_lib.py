@@ -64,3 +64,14 @@ def reconstruct(k, m, frags, missing, dest):
     G = ints(generator(k, m))
     return lib().orc_rs_reconstruct(G, ptr_array(frags[:k]), ptr_array(frags[k:]), k, m,
                                      ints(list(missing) + [-1]), dest, bs)
+
+
+def crc32(data, legacy=False) -> int:
+    """zlib crc32 / liberasurecode_crc32_alt of a bytes-like or uint8 array (oracle restatement)."""
+    L = lib()
+    fn = L.orc_crc32_alt if legacy else L.orc_crc32
+    fn.restype = C.c_uint32
+    fn.argtypes = [C.c_uint32, C.c_void_p, C.c_int64]
+    buf = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8)
+                               if not isinstance(data, np.ndarray) else data)
+    return fn(0, buf.ctypes.data, buf.size)

@@ -1,0 +1,284 @@
+"""GPU parity of the device-resident framed path (include/ecamd.h "on-device framing"):
+zlib / legacy CRC32 on the device against the oracle, and whole fragments (80-byte header +
+payload) against the framing restatement of tests/ec_api.py (pinned to the reference's
+known-answer headers, test/liberasurecode_test.c:2239-2315) with parity from the oracles."""
+import os
+import sys
+import zlib
+
+import numpy as np
+import pytest
+
+import ec_api
+import oracle_lib as O
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import xor_oracle as XO  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def F():
+    import torch  # noqa: F401  (one HIP runtime per process: torch's)
+    from liberasurecode_amd import _lib, frame
+    assert _lib.dev().ecamd_init() == 0
+    return frame
+
+
+@pytest.fixture(params=[8, 4], ids=["byte_tables", "nibble_tables"])
+def bits(request):
+    from liberasurecode_amd import _lib
+    _lib.check(_lib.dev().ecamd_tune(b"crc_bits", request.param), "tune")
+    yield request.param
+    _lib.dev().ecamd_tune(b"crc_bits", 8)
+
+
+CRC_LENGTHS = [0, 1, 15, 16, 17, 100, 1023, 1024, 1025, 4096, 16383, 16384, 16400, 65536 + 13,
+               (1 << 20), (1 << 20) + 7, 3 * (1 << 20) + 1]
+
+
+def test_crc32_lengths(F, bits):
+    from liberasurecode_amd.device import DeviceBuffer
+    rng = np.random.default_rng(bits)
+    for n in CRC_LENGTHS:
+        nbuf = 5
+        stride = max((n + 15) // 16 * 16, 16)
+        host = rng.integers(0, 256, nbuf * stride, dtype=np.uint8)
+        d = DeviceBuffer(host.size)
+        d.upload(host)
+        got = F.crc32(d, nbuf, n, stride)
+        want = [zlib.crc32(host[i * stride:i * stride + n].tobytes()) for i in range(nbuf)]
+        assert got.tolist() == want, n
+        if n <= (1 << 20):
+            got = F.crc32(d, nbuf, n, stride, legacy=True)
+            want = [O.crc32(host[i * stride:i * stride + n], legacy=True) for i in range(nbuf)]
+            assert got.tolist() == want, ("legacy", n)
+
+
+def test_crc32_edge_patterns(F):
+    from liberasurecode_amd.device import DeviceBuffer
+    n = 70000
+    for fill in (0x00, 0xFF, 0x80):
+        host = np.full(n, fill, dtype=np.uint8)
+        d = DeviceBuffer(n + 16)
+        d.upload(host)
+        assert F.crc32(d, 1, n, (n + 15) // 16 * 16)[0] == zlib.crc32(host.tobytes())
+        assert F.crc32(d, 1, n, (n + 15) // 16 * 16, legacy=True)[0] == O.crc32(host, legacy=True)
+
+
+def expected_stripe(backend, k, m, hd, obj: bytes, ct, legacy=False):
+    """The fragments liberasurecode_encode returns for obj (restated)."""
+    a = k * (4 if backend == ec_api.EC_BACKEND_FLAT_XOR_HD else 2)
+    bs = (len(obj) + a - 1) // a * a // k
+    data = np.zeros((k, bs), dtype=np.uint8)
+    flat = np.frombuffer(obj, dtype=np.uint8)
+    data.reshape(-1)[:len(flat)] = flat
+    if backend == ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND:
+        parity = O.encode(k, m, data)
+    else:
+        parity = XO.encode_bytes(k, m, hd, data)
+    frags = []
+    for i, payload in enumerate(list(data) + list(parity)):
+        p = payload.tobytes()
+        if ct == ec_api.CHKSUM_CRC32 and legacy:
+            hdr = ec_api.expected_header(i, bs, len(obj), backend, ct, b"", with_crc=False,
+                                         legacy=True)
+            hdr = _with_crc(hdr, O.crc32(p, legacy=True), legacy=True)
+        else:
+            hdr = ec_api.expected_header(i, bs, len(obj), backend, ct, p, legacy=legacy)
+        frags.append(hdr + p)
+    return frags
+
+
+def _with_crc(hdr, crc, legacy):
+    import struct
+    meta = bytearray(hdr[:59])
+    meta[21:25] = struct.pack("<I", crc)
+    mcrc = O.crc32(bytes(meta), legacy=True) if legacy else zlib.crc32(bytes(meta))
+    return bytes(meta) + hdr[59:67] + struct.pack("<I", mcrc) + hdr[71:]
+
+
+CODES = [("rs", 4, 2, 0), ("rs", 10, 4, 0), ("rs", 20, 8, 0), ("rs", 1, 1, 0),
+         ("xor", 3, 3, 3), ("xor", 10, 6, 4), ("xor", 10, 5, 3)]
+SIZES = [1, 1000, 12345, 65536 * 4, 1048576 + 4]
+
+
+def _backend(name):
+    return (ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND if name == "rs"
+            else ec_api.EC_BACKEND_FLAT_XOR_HD)
+
+
+def _objects(S, size, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(S)]
+
+
+def _upload_objects(objs, stride):
+    from liberasurecode_amd.device import DeviceBuffer
+    host = np.zeros((len(objs), stride), dtype=np.uint8)
+    for s, o in enumerate(objs):
+        host[s, :len(o)] = np.frombuffer(o, dtype=np.uint8)
+    d = DeviceBuffer(max(host.size, 16))
+    d.upload(host.reshape(-1))
+    return d
+
+
+@pytest.mark.parametrize("code", CODES, ids=[f"{c[0]}_{c[1]}_{c[2]}" for c in CODES])
+@pytest.mark.parametrize("ct", [ec_api.CHKSUM_CRC32, ec_api.CHKSUM_NONE])
+def test_frame_encode_bytes(F, code, ct):
+    name, k, m, hd = code
+    be = _backend(name)
+    for size in SIZES:
+        if k == 20 and size > 65536 * 4:
+            continue
+        S = 3
+        objs = _objects(S, size, size + k)
+        fb = F.FrameBatch(be, k, m, size, S, hd=hd or 3, checksum=ct)
+        d_obj = _upload_objects(objs, fb.obj_stride)
+        fb.encode(d_obj)
+        got = fb.fragments()
+        for s in range(S):
+            want = expected_stripe(be, k, m, hd, objs[s], ct)
+            for i in range(k + m):
+                assert got[s, i].tobytes() == want[i], (size, s, i)
+
+
+def test_frame_encode_legacy_crc(F, monkeypatch):
+    monkeypatch.setenv("LIBERASURECODE_WRITE_LEGACY_CRC", "1")
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    for size in (999, 300000):
+        objs = _objects(2, size, 77)
+        fb = F.FrameBatch(be, 4, 2, size, 2)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        got = fb.fragments()
+        for s in range(2):
+            want = expected_stripe(be, 4, 2, 0, objs[s], ec_api.CHKSUM_CRC32, legacy=True)
+            for i in range(6):
+                assert got[s, i].tobytes() == want[i], (size, s, i)
+
+
+def test_frame_md5_type_stored_not_computed(F):
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    objs = _objects(1, 5000, 5)
+    fb = F.FrameBatch(be, 4, 2, 5000, 1, checksum=ec_api.CHKSUM_MD5)
+    fb.encode(_upload_objects(objs, fb.obj_stride))
+    got = fb.fragments()
+    want = expected_stripe(be, 4, 2, 0, objs[0], ec_api.CHKSUM_MD5)
+    assert all(got[0, i].tobytes() == want[i] for i in range(6))
+
+
+DECODE = [("rs", 10, 4, 0, [0, 1, 2, 3]), ("rs", 10, 4, 0, [0, 5, 10, 13]),
+          ("rs", 20, 8, 0, [0, 2, 4, 6, 20, 22, 24, 26]), ("rs", 4, 2, 0, [4, 5]),
+          ("xor", 10, 6, 4, [0, 1, 2]), ("xor", 3, 3, 3, [1, 4]), ("xor", 10, 5, 3, [9, 12])]
+
+
+@pytest.mark.parametrize("case", DECODE, ids=[f"{c[0]}_{c[1]}_{c[2]}_{len(c[4])}" for c in DECODE])
+def test_frame_decode_roundtrip(F, case):
+    from liberasurecode_amd.device import DeviceBuffer
+    name, k, m, hd, missing = case
+    be = _backend(name)
+    for size in (777, 1048576 * 2 + 6):
+        S = 2
+        objs = _objects(S, size, 3 + size)
+        fb = F.FrameBatch(be, k, m, size, S, hd=hd or 3)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        frags = fb.fragments()
+        for i in missing:
+            frags[:, i, :] = 0xA5  # lost: garbage in the slot
+        fb.upload_fragments(frags)
+        out = DeviceBuffer(fb.obj_stride * S)
+        fb.decode(missing, out)
+        host = out.download(fb.obj_stride * S).reshape(S, fb.obj_stride)
+        for s in range(S):
+            assert host[s, :size].tobytes() == objs[s], (size, s)
+
+
+RECON = [("rs", 10, 4, 0, [3, 11], 3), ("rs", 10, 4, 0, [3, 11], 11), ("rs", 20, 8, 0,
+         list(range(8)), 5), ("xor", 10, 6, 4, [2, 12, 5], 12), ("xor", 3, 3, 3, [0, 3], 0)]
+
+
+@pytest.mark.parametrize("case", RECON, ids=[f"{c[0]}_{c[1]}_{c[2]}_d{c[5]}" for c in RECON])
+def test_frame_reconstruct_byte_equal(F, case):
+    """liberasurecode_test.c:1331: a reconstructed fragment equals the original, header
+    included."""
+    name, k, m, hd, missing, dest = case
+    be = _backend(name)
+    size = 1048576 + 12
+    S = 2
+    objs = _objects(S, size, 11)
+    fb = F.FrameBatch(be, k, m, size, S, hd=hd or 3)
+    fb.encode(_upload_objects(objs, fb.obj_stride))
+    orig = fb.fragments()
+    frags = orig.copy()
+    for i in missing:
+        frags[:, i, :] = 0x5A
+    fb.upload_fragments(frags)
+    fb.reconstruct(missing, dest)
+    got = fb.fragments()
+    assert np.array_equal(got[:, dest], orig[:, dest])
+
+
+def test_frame_verify(F):
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    size = 10 * 1048576
+    S = 2
+    objs = _objects(S, size, 21)
+    fb = F.FrameBatch(be, 10, 4, size, S)
+    fb.encode(_upload_objects(objs, fb.obj_stride))
+    st, crc = fb.verify()
+    assert not st.any()
+    frags = fb.fragments()
+    for s in range(S):
+        for i in range(14):
+            assert crc[s, i] == zlib.crc32(frags[s, i, 80:].tobytes())
+    frags[0, 3, 80 + 123456] ^= 1      # payload bit flip
+    frags[1, 7, 4] ^= 1                # header: size field (metadata checksum breaks too)
+    frags[1, 9, 60] ^= 1               # magic
+    frags[0, 12, 0] = 11               # idx (metadata checksum breaks too)
+    fb.upload_fragments(frags)
+    st, _ = fb.verify()
+    assert st[0, 3] == 16
+    assert st[1, 7] & 8 and st[1, 7] & 2
+    assert st[1, 9] & 1
+    assert st[0, 12] & 4 and st[0, 12] & 2
+    mask = np.ones_like(st, dtype=bool)
+    for s, i in [(0, 3), (1, 7), (1, 9), (0, 12)]:
+        mask[s, i] = False
+    assert not st[mask].any()
+
+
+def test_frame_large_c3_roundtrip(F):
+    """BASELINE C3 shape: 10 MiB objects, RS(10,4), CRC32; decode with 4 data fragments lost."""
+    from liberasurecode_amd.device import DeviceBuffer
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    size, S = 10 * 1048576, 8
+    objs = _objects(S, size, 99)
+    fb = F.FrameBatch(be, 10, 4, size, S)
+    fb.encode(_upload_objects(objs, fb.obj_stride))
+    frags = fb.fragments()
+    for s in (0, S - 1):
+        want = expected_stripe(be, 10, 4, 0, objs[s], ec_api.CHKSUM_CRC32)
+        assert all(frags[s, i].tobytes() == want[i] for i in range(14))
+    frags[:, :4] = 0
+    fb.upload_fragments(frags)
+    out = DeviceBuffer(fb.obj_stride * S)
+    fb.decode([0, 1, 2, 3], out)
+    host = out.download(fb.obj_stride * S).reshape(S, fb.obj_stride)
+    assert all(host[s, :size].tobytes() == objs[s] for s in range(S))
+
+
+def test_frame_errors(F):
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    d = _lib.dev()
+    buf = DeviceBuffer(1 << 16)
+    # unsupported backend, bad xor code, too many missing, bad stride
+    assert d.ecamd_frame_encode(1, 4, 2, 0, 2, buf.ptr, 4096, 4000, buf.ptr, 6 * 2048, 2048, 1,
+                                None) < 0
+    assert d.ecamd_frame_encode(3, 4, 3, 3, 2, buf.ptr, 4096, 4000, buf.ptr, 7 * 2048, 2048, 1,
+                                None) < 0
+    assert d.ecamd_frame_encode(6, 4, 2, 0, 2, buf.ptr, 4096, 4000, buf.ptr, 6 * 1072, 1072, 1,
+                                None) < 0  # frag_stride < 80 + 1000 rounded
+    assert d.ecamd_frame_decode(6, 4, 2, 0, _lib.ints([0, 1, 2, -1]), buf.ptr, 6 * 2048, 2048, 1,
+                                buf.ptr, 4096, 4000, None) < 0

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Device-resident framed path timings at the C3 shape (10 MiB objects, RS(10,4), CRC32):
+CRC32 kernel alone (byte vs nibble tables), and whole framed encode / decode per stripe batch.
+Prints one JSON line per measurement."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+
+from liberasurecode_amd import _lib, frame  # noqa: E402
+from liberasurecode_amd import device as D  # noqa: E402
+
+
+def timed(fn, stream, reps):
+    a, b = D.Event(), D.Event()
+    fn()
+    stream.synchronize()
+    a.record(stream)
+    for _ in range(reps):
+        fn()
+    b.record(stream)
+    return a.elapsed_ms(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stripes", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    S, k, m, size = args.stripes, 10, 4, 10 * 1048576
+    d = _lib.dev()
+    st = D.Stream()
+    fb = frame.FrameBatch(frame.RS_VAND, k, m, size, S)
+    obj = D.DeviceBuffer(fb.obj_stride * S)
+    lay = D.Layout(obj, 1, size, S, fb.obj_stride, fb.obj_stride)
+    lay.fill_splitmix(stream=st)
+    crc = D.DeviceBuffer(4 * S * (k + m))
+    payload_bytes = S * (k + m) * fb.blocksize
+    for bits in (8, 4):
+        for wgs in (0, 2, 4):
+            d.ecamd_tune(b"crc_bits", bits)
+            d.ecamd_tune(b"crc_wgs", wgs)
+            ms = timed(lambda: _lib.check(d.ecamd_crc32(0, fb.buf.ptr + 80, fb.stripe_stride,
+                                                         fb.frag_stride, k + m, fb.blocksize, S,
+                                                         crc.ptr, st.handle), "crc"), st, args.reps)
+            print(json.dumps({"op": "crc32", "bits": bits, "crc_wgs": wgs, "ms": round(ms, 3),
+                              "GBps": round(payload_bytes / ms / 1e6, 1)}), flush=True)
+    d.ecamd_tune(b"crc_bits", 8)
+    d.ecamd_tune(b"crc_wgs", 0)
+    obj_bytes = S * size
+    for ct in (frame.CHKSUM_NONE, frame.CHKSUM_CRC32):
+        fb.checksum = ct
+        ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
+        print(json.dumps({"op": "frame_encode", "checksum": ct, "ms": round(ms, 3),
+                          "GiBps_object": round(obj_bytes / (ms / 1e3) / 2**30, 1),
+                          "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms / 1e6, 1)}),
+              flush=True)
+    out = D.DeviceBuffer(fb.obj_stride * S)
+    ms = timed(lambda: fb.decode([0, 1, 2, 3], out, stream=st), st, args.reps)
+    print(json.dumps({"op": "frame_decode_4data", "ms": round(ms, 3),
+                      "GiBps_object": round(obj_bytes / (ms / 1e3) / 2**30, 1)}), flush=True)
+    ms = timed(lambda: fb.verify(stream=st), st, args.reps)
+    print(json.dumps({"op": "frame_verify", "ms": round(ms, 3),
+                      "GBps": round(payload_bytes / ms / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
