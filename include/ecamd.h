@@ -146,7 +146,7 @@ int ecamd_malloc(void **d_ptr, int64_t bytes);
 int ecamd_free(void *d_ptr);
 int ecamd_memcpy_h2d(void *d_dst, const void *h_src, int64_t bytes);
 int ecamd_memcpy_d2h(void *h_dst, const void *d_src, int64_t bytes);
-int ecamd_memset(void *d_ptr, int value, int64_t bytes);
+int ecamd_memset(void *d_ptr, int value, int64_t bytes); /* synchronous: complete on return */
 /* kind: 0 host->device, 1 device->host, 2 device->device; asynchronous on stream */
 int ecamd_memcpy_async(void *dst, const void *src, int64_t bytes, int kind, void *stream);
 int ecamd_host_alloc(void **h_ptr, int64_t bytes); /* pinned host memory */

@@ -73,7 +73,7 @@ int ensure_device(int* dev_out)
     }
     if (!di.lds_attr_set) {
         // Allow the full 160 KiB of gfx950 LDS as dynamic shared memory.
-#define K_(W, P, N) reinterpret_cast<const void*>(&gf16_apply_kernel<W, P, N>)
+#define K_(W, P, N) reinterpret_cast<const void*>(&gf16_apply_kernel<W, P, N, false>)
         const void* ks[] = {K_(2, false, false), K_(4, false, false), K_(8, false, false),
                             K_(2, true, false),  K_(4, true, false),  K_(8, true, false),
                             K_(2, false, true),  K_(4, false, true),  K_(8, false, true),
@@ -107,6 +107,7 @@ struct Tuning {
     int nt = 1;          // 1: non-temporal global loads/stores in the gf16 kernel (+7% on MI355X)
     int exp_ch = 0;      // sweeps: experimental W=4 kernel with 1 or 2 chunks per lane
     int ablate = 0;      // sweeps: experimental kernel without LDS lookups (wrong results)
+    int nib = 0;         // gf16 kernel: 1 = nibble tables (4 conflict-free lookups per word)
     int crc_bits = 8;    // CRC32 kernel: 8 (byte tables) or 4 (conflict-free nibble tables)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
 };
@@ -141,8 +142,10 @@ int dev_tune(const char* key)
 struct ecamd_map {
     struct Pass {
         int row0, width, col0, ncols;
-        size_t offset;  // into d_tables
+        size_t offset;  // into d_tables: byte-split image
         size_t bytes;
+        size_t nib_offset;  // nibble image (build_nibble_tables)
+        size_t nib_bytes;
     };
     int device = 0;
     int R = 0, K = 0;
@@ -189,11 +192,13 @@ struct Geometry {
     uint32_t ntiles;
 };
 
-int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chunks = 1)
+int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chunks = 1,
+             int max_threads = 1024)
 {
     int wgs = lds ? static_cast<int>(std::min<size_t>(8, std::max<size_t>(1, kLdsBytes / lds))) : 8;
     int threads = lds ? std::min(1024, std::max(256, (1024 / wgs) / 64 * 64)) : 256;
     if (lds && g_tune.threads > 0) threads = g_tune.threads;
+    threads = std::min(threads, max_threads);
     if (lds && g_tune.wgs_per_cu > 0) wgs = std::min<int>(g_tune.wgs_per_cu, std::max<size_t>(1, kLdsBytes / lds));
     int64_t span = static_cast<int64_t>(threads) * 16 * chunks;
     int64_t tps = (bs + span - 1) / span;
@@ -239,14 +244,34 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             HIP_TRY(hipGetLastError());
             continue;
         }
+        if (g_tune.nib) {
+            a.tables = map->d_tables + p.nib_offset;
+            rc = geometry(map->device, p.nib_bytes, bs, nstripes, g);
+            if (rc) return rc;
+            if (g.threads > 512) {  // the nibble kernels are built for <= 512 threads
+                rc = geometry(map->device, p.nib_bytes, bs, nstripes, g, 1, 512);
+                if (rc) return rc;
+            }
+            a.ntiles = g.ntiles;
+            a.tiles_per_stripe = g.tiles_per_stripe;
+            grid = dim3(g.grid);
+            block = dim3(g.threads);
+            switch (p.width) {
+            case 2: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, true, true>), grid, block, g.lds, st, a); break;
+            case 4: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, true, true>), grid, block, g.lds, st, a); break;
+            default: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, true, true>), grid, block, g.lds, st, a); break;
+            }
+            HIP_TRY(hipGetLastError());
+            continue;
+        }
         const bool nt = g_tune.nt != 0;
         switch (p.width * 2 + (nt ? 1 : 0)) {
-        case 4: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, false>), grid, block, g.lds, st, a); break;
-        case 5: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, true>), grid, block, g.lds, st, a); break;
-        case 8: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, false>), grid, block, g.lds, st, a); break;
-        case 9: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, true>), grid, block, g.lds, st, a); break;
-        case 16: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, false>), grid, block, g.lds, st, a); break;
-        default: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, true>), grid, block, g.lds, st, a); break;
+        case 4: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, false, false>), grid, block, g.lds, st, a); break;
+        case 5: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, true, false>), grid, block, g.lds, st, a); break;
+        case 8: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, false, false>), grid, block, g.lds, st, a); break;
+        case 9: hipLaunchKernelGGL((gf16_apply_kernel<4, PTRS, true, false>), grid, block, g.lds, st, a); break;
+        case 16: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, false, false>), grid, block, g.lds, st, a); break;
+        default: hipLaunchKernelGGL((gf16_apply_kernel<8, PTRS, true, false>), grid, block, g.lds, st, a); break;
         }
         HIP_TRY(hipGetLastError());
     }
@@ -383,6 +408,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.exp_ch = (value == 1 || value == 2) ? value : 0;
     } else if (k == "ablate") {
         g_tune.ablate = value != 0;
+    } else if (k == "nib") {
+        g_tune.nib = value != 0;
     } else if (k == "crc_bits") {
         g_tune.crc_bits = value == 4 ? 4 : 8;
     } else if (k == "crc_wgs") {
@@ -412,10 +439,17 @@ int ecamd_map_create(const int* coeff, int R, int K, ecamd_map** out)
     for (int& v : c) v &= 0xffff;
     auto passes = plan_passes(R, K);
     size_t total = passes.back().offset + passes.back().bytes;
+    for (auto& p : passes) {
+        p.nib_offset = total;
+        p.nib_bytes = static_cast<size_t>(p.ncols) * 64 * 2 * p.width;
+        total += p.nib_bytes;
+    }
     std::vector<uint8_t> img(total);
     for (const auto& p : passes) {
         auto t = build_split_tables(c, R, K, p.row0, p.width, p.col0, p.ncols);
         std::memcpy(img.data() + p.offset, t.data(), t.size());
+        auto n = build_nibble_tables(c, R, K, p.row0, p.width, p.col0, p.ncols);
+        std::memcpy(img.data() + p.nib_offset, n.data(), n.size());
     }
     auto* map = new ecamd_map();
     map->device = dev;
@@ -637,7 +671,10 @@ int ecamd_memcpy_d2h(void* h_dst, const void* d_src, int64_t bytes)
 
 int ecamd_memset(void* d_ptr, int value, int64_t bytes)
 {
+    // Complete on return (hipMemset alone may still be running when the host moves on, and
+    // streams made by ecamd_stream_create do not order against the null stream).
     HIP_TRY(hipMemset(d_ptr, value, static_cast<size_t>(bytes)));
+    HIP_TRY(hipDeviceSynchronize());
     return 0;
 }
 

@@ -131,7 +131,28 @@ __device__ __forceinline__ void mac_chunk(const uint8_t* tl, uint4 x, uint32_t (
     }
 }
 
-template <int W, bool PTRS, bool NT, bool TAIL>
+// Nibble tables (host/tables.hpp build_nibble_tables): four conflict-free lookups per word.
+template <int W>
+__device__ __forceinline__ void mac_chunk_nib(const uint8_t* t, uint4 x, uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const uint32_t v = xs[w >> 1] >> ((w & 1) * 16);
+#pragma unroll
+        for (int q = 0; q < 4; q += 2) {
+            uint32_t e0[D], e1[D];
+            lds_entry<D>(t + (q * 16 + ((v >> (4 * q)) & 0xfu)) * EB, e0);
+            lds_entry<D>(t + ((q + 1) * 16 + ((v >> (4 * q + 4)) & 0xfu)) * EB, e1);
+#pragma unroll
+            for (int d = 0; d < D; d++) acc[w][d] ^= e0[d] ^ e1[d];
+        }
+    }
+}
+
+template <int W, bool PTRS, bool NT, bool NIB, bool TAIL>
 __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* lds, uint32_t s,
                                            int64_t off, int rem)
 {
@@ -157,7 +178,12 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
             nxt[i] = (j0 + 4 + i < K) ? fetch(j0 + 4 + i) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < 4; i++)
-            if (j0 + i < K) mac_chunk<W>(lds + static_cast<size_t>(j0 + i) * 512 * EB, cur[i], acc);
+            if (j0 + i < K) {
+                if constexpr (NIB)
+                    mac_chunk_nib<W>(lds + static_cast<size_t>(j0 + i) * 64 * EB, cur[i], acc);
+                else
+                    mac_chunk<W>(lds + static_cast<size_t>(j0 + i) * 512 * EB, cur[i], acc);
+            }
 #pragma unroll
         for (int i = 0; i < 4; i++) cur[i] = nxt[i];
     }
@@ -189,12 +215,12 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
 
 }  // namespace
 
-template <int W, bool PTRS, bool NT>
-__global__ void __launch_bounds__(1024) gf16_apply_kernel(const ApplyArgs a)
+template <int W, bool PTRS, bool NT, bool NIB>
+__global__ void __launch_bounds__(NIB ? 512 : 1024) gf16_apply_kernel(const ApplyArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int EB = 2 * W;
-    const int tbytes = a.ncols * 512 * EB;
+    const int tbytes = a.ncols * (NIB ? 64 : 512) * EB;
     for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
         *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
     __syncthreads();
@@ -207,17 +233,19 @@ __global__ void __launch_bounds__(1024) gf16_apply_kernel(const ApplyArgs a)
         const int64_t rem = a.bs - off;
         if (rem <= 0) continue;
         if (rem >= 16)
-            apply_tile<W, PTRS, NT, false>(a, lds, s, off, 16);
+            apply_tile<W, PTRS, NT, NIB, false>(a, lds, s, off, 16);
         else
-            apply_tile<W, PTRS, NT, true>(a, lds, s, off, static_cast<int>(rem));
+            apply_tile<W, PTRS, NT, NIB, true>(a, lds, s, off, static_cast<int>(rem));
     }
 }
 
-#define ECAMD_INST(W, P, N) template __global__ void gf16_apply_kernel<W, P, N>(const ApplyArgs);
-ECAMD_INST(2, false, false) ECAMD_INST(4, false, false) ECAMD_INST(8, false, false)
-ECAMD_INST(2, true, false) ECAMD_INST(4, true, false) ECAMD_INST(8, true, false)
-ECAMD_INST(2, false, true) ECAMD_INST(4, false, true) ECAMD_INST(8, false, true)
-ECAMD_INST(2, true, true) ECAMD_INST(4, true, true) ECAMD_INST(8, true, true)
+#define ECAMD_INST(W, P, N, B) \
+    template __global__ void gf16_apply_kernel<W, P, N, B>(const ApplyArgs);
+#define ECAMD_INST2(P, N, B) ECAMD_INST(2, P, N, B) ECAMD_INST(4, P, N, B) ECAMD_INST(8, P, N, B)
+ECAMD_INST2(false, false, false) ECAMD_INST2(true, false, false)
+ECAMD_INST2(false, true, false) ECAMD_INST2(true, true, false)
+ECAMD_INST2(false, true, true) ECAMD_INST2(true, true, true)
+#undef ECAMD_INST2
 #undef ECAMD_INST
 
 // ---------------------------------------------------------------- flat XOR ----

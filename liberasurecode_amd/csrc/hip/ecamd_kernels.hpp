@@ -39,7 +39,7 @@ struct FillArgs {
     uint64_t seed_base;
 };
 
-template <int W, bool PTRS, bool NT>
+template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);

@@ -21,3 +21,15 @@ std::vector<uint8_t> build_split_tables(const std::vector<int>& coeff, int R, in
                                         int width, int col0, int ncols);
 
 }  // namespace ecamd
+
+namespace ecamd {
+
+// Nibble form of the same map: c*x = XOR_q c*(((x >> 4q) & 15) << 4q), q = 0..3, so per input
+//   T_q[n] = pack_r( A[r][j] * (n << 4q) )    n = 0..15
+// Layout: input-major, [T_0(16) | T_1(16) | T_2(16) | T_3(16)] per input.  A 16-entry table of
+// W*2-byte entries spans 16 distinct LDS bank slots (W = 8: exactly one 256-byte bank row), so
+// the lookups of a wave never conflict -- four lookups per word instead of two conflicted ones.
+std::vector<uint8_t> build_nibble_tables(const std::vector<int>& coeff, int R, int K, int row0,
+                                         int width, int col0, int ncols);
+
+}  // namespace ecamd
