@@ -75,6 +75,13 @@ int ecamd_rs_encode(int k, int m, void *base, int64_t stripe_stride, int64_t fra
 int ecamd_rs_decode(int k, int m, const int *missing, int rebuild_parity, void *base,
                     int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
                     void *stream);
+/* Heterogeneous batch decode: stripe s has its own -1 terminated erasure list at
+ * missing + s*missing_stride (at most missing_stride entries).  Stripes are grouped by erasure
+ * set; each group is one launch over a device pointer table, so a batch of stripes that lost
+ * different fragments still costs one launch per distinct pattern, not per stripe. */
+int ecamd_rs_decode_multi(int k, int m, const int *missing, int missing_stride,
+                          int rebuild_parity, void *base, int64_t stripe_stride,
+                          int64_t frag_stride, int64_t blocksize, int nstripes, void *stream);
 /* Reconstruct one destination, as liberasurecode_rs_vand_reconstruct does. */
 int ecamd_rs_reconstruct(int k, int m, const int *missing, int dest, void *base,
                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,

@@ -82,6 +82,9 @@ def dev():
                [C.c_int, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
         _proto(d, "ecamd_rs_decode", C.c_int,
                [C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
+        _proto(d, "ecamd_rs_decode_multi", C.c_int,
+               [C.c_int, C.c_int, IP, C.c_int, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64,
+                C.c_int, VP])
         _proto(d, "ecamd_rs_reconstruct", C.c_int,
                [C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
         _proto(d, "ecamd_fill_splitmix", C.c_int,

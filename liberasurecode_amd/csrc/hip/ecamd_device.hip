@@ -78,6 +78,9 @@ int ensure_device(int* dev_out)
                             K_(2, true, false),  K_(4, true, false),  K_(8, true, false),
                             K_(2, false, true),  K_(4, false, true),  K_(8, false, true),
                             K_(2, true, true),   K_(4, true, true),   K_(8, true, true),
+                            reinterpret_cast<const void*>(&gf16_copy_apply_kernel<2>),
+                            reinterpret_cast<const void*>(&gf16_copy_apply_kernel<4>),
+                            reinterpret_cast<const void*>(&gf16_copy_apply_kernel<8>),
                             reinterpret_cast<const void*>(&gf16_apply_exp_kernel<1, false>),
                             reinterpret_cast<const void*>(&gf16_apply_exp_kernel<1, true>),
                             reinterpret_cast<const void*>(&gf16_apply_exp_kernel<2, false>),
@@ -110,6 +113,7 @@ struct Tuning {
     int nib = 0;         // gf16 kernel: 1 = nibble tables (4 conflict-free lookups per word)
     int crc_bits = 8;    // CRC32 kernel: 8 (byte tables) or 4 (conflict-free nibble tables)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
+    int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
 };
 Tuning g_tune;
 
@@ -134,6 +138,7 @@ int dev_tune(const char* key)
     const std::string k(key);
     if (k == "crc_bits") return g_tune.crc_bits;
     if (k == "crc_wgs") return g_tune.crc_wgs;
+    if (k == "frame_unfused") return g_tune.frame_unfused;
     return 0;
 }
 
@@ -388,6 +393,65 @@ int rs_run(const RsEntry& e, void* base, int64_t stripe_stride, int64_t frag_str
 
 }  // namespace
 
+namespace ecamd {
+
+int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                   int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                   void* stream)
+{
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
+    if (rc) return rc;
+    if (!e->map || nstripes <= 0 || bs <= 0) return 0;
+    if (!aligned16(obj) || !aligned16(payload0) || obj_stride % 16 || stripe_stride % 16 ||
+        frag_stride % 16 || bs % 16)
+        return fail(ECAMD_EINVAL, "copy-through encode needs 16-byte aligned objects and payloads");
+    const ecamd_map* map = e->map.get();
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    for (const auto& p : map->passes) {
+        ApplyArgs a{};
+        a.tables = map->d_tables + p.offset;
+        a.in_base = static_cast<const uint8_t*>(obj);
+        a.in_stride = obj_stride;
+        a.out_base = static_cast<uint8_t*>(payload0);
+        a.out_stride = stripe_stride;
+        a.copy_base = static_cast<uint8_t*>(payload0);
+        a.copy_stride = stripe_stride;
+        a.bs = bs;
+        a.ncols = p.ncols;
+        a.nrows = std::min(p.width, map->R - p.row0);
+        a.accumulate = p.col0 > 0;
+        for (int j = 0; j < p.ncols; j++) {
+            a.in_off[j] = static_cast<int64_t>(e->inputs[p.col0 + j]) * bs;
+            a.copy_off[j] = static_cast<int64_t>(e->inputs[p.col0 + j]) * frag_stride;
+        }
+        for (int r = 0; r < a.nrows; r++) a.out_off[r] = e->outputs[p.row0 + r] * frag_stride;
+        Geometry g;
+        rc = geometry(map->device, p.bytes, bs, nstripes, g);
+        if (rc) return rc;
+        a.ntiles = g.ntiles;
+        a.tiles_per_stripe = g.tiles_per_stripe;
+        dim3 grid(g.grid), block(g.threads);
+        if (p.row0 == 0) {  // the first row group copies the data through
+            switch (p.width) {
+            case 2: hipLaunchKernelGGL((gf16_copy_apply_kernel<2>), grid, block, g.lds, st, a); break;
+            case 4: hipLaunchKernelGGL((gf16_copy_apply_kernel<4>), grid, block, g.lds, st, a); break;
+            default: hipLaunchKernelGGL((gf16_copy_apply_kernel<8>), grid, block, g.lds, st, a); break;
+            }
+        } else {
+            switch (p.width) {
+            case 2: hipLaunchKernelGGL((gf16_apply_kernel<2, false, true, false>), grid, block, g.lds, st, a); break;
+            case 4: hipLaunchKernelGGL((gf16_apply_kernel<4, false, true, false>), grid, block, g.lds, st, a); break;
+            default: hipLaunchKernelGGL((gf16_apply_kernel<8, false, true, false>), grid, block, g.lds, st, a); break;
+            }
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+}  // namespace ecamd
+
 extern "C" {
 
 int ecamd_init(void) { return ensure_device(nullptr); }
@@ -414,6 +478,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_bits = value == 4 ? 4 : 8;
     } else if (k == "crc_wgs") {
         g_tune.crc_wgs = std::max(0, std::min(value, 4));
+    } else if (k == "frame_unfused") {
+        g_tune.frame_unfused = value != 0;
     } else {
         return fail(ECAMD_EINVAL, "unknown tuning key %s", key);
     }
@@ -577,6 +643,84 @@ int ecamd_rs_decode(int k, int m, const int* missing, int rebuild_parity, void* 
     int rc = rs_entry(1, k, m, missing, rebuild_parity ? 1 : 0, -1, e);
     if (rc) return rc;
     return rs_run(*e, base, stripe_stride, frag_stride, blocksize, nstripes, stream);
+}
+
+int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
+                          int rebuild_parity, void* base, int64_t stripe_stride,
+                          int64_t frag_stride, int64_t blocksize, int nstripes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!missing || missing_stride < 1 || k <= 0 || m < 0 || k + m > 256)
+        return fail(ECAMD_EINVAL, "bad decode_multi arguments");
+    if (nstripes <= 0 || blocksize <= 0) return 0;
+    if (!aligned16(base) || stripe_stride % 16 || frag_stride % 16)
+        return fail(ECAMD_EINVAL, "fragment addresses must be 16-byte aligned");
+    // Group stripes by erasure set (decode depends on the set, not the order of the list).
+    std::map<std::vector<int>, std::vector<int>> groups;
+    for (int s = 0; s < nstripes; s++) {
+        const int* row = missing + static_cast<int64_t>(s) * missing_stride;
+        std::vector<int> pat;
+        for (int i = 0; i < missing_stride && row[i] >= 0; i++) {
+            if (row[i] >= k + m) return fail(ECAMD_EINVAL, "stripe %d: missing index %d", s, row[i]);
+            pat.push_back(row[i]);
+        }
+        std::sort(pat.begin(), pat.end());
+        pat.erase(std::unique(pat.begin(), pat.end()), pat.end());
+        if (static_cast<int>(pat.size()) > m)
+            return fail(ECAMD_EINVAL, "stripe %d: %zu fragments missing > m=%d", s, pat.size(), m);
+        groups[pat].push_back(s);
+    }
+    // One pointer table row (k+m fragment addresses) per stripe, laid out group by group.
+    const int row = k + m;
+    std::vector<uint8_t*> table;
+    table.reserve(static_cast<size_t>(nstripes) * row);
+    for (const auto& g : groups)
+        for (int s : g.second)
+            for (int f = 0; f < row; f++)
+                table.push_back(static_cast<uint8_t*>(base) + s * stripe_stride + f * frag_stride);
+    static std::mutex mu;
+    static std::map<std::pair<int, void*>, std::pair<void*, size_t>> scratch;  // dev, stream
+    std::lock_guard<std::mutex> lk(mu);
+    auto& sc = scratch[{dev, stream}];
+    const size_t bytes = table.size() * sizeof(uint8_t*);
+    // The previous call on this stream may still read the table: drain the stream first.
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    if (sc.second < bytes) {
+        if (sc.first) HIP_TRY(hipFree(sc.first));
+        sc.first = nullptr;
+        HIP_TRY(hipMalloc(&sc.first, bytes));
+        sc.second = bytes;
+    }
+    HIP_TRY(hipMemcpy(sc.first, table.data(), bytes, hipMemcpyHostToDevice));
+    auto* d_table = static_cast<uint8_t**>(sc.first);
+    size_t at = 0;
+    for (const auto& g : groups) {
+        const int G = static_cast<int>(g.second.size());
+        uint8_t** t = d_table + at;
+        at += static_cast<size_t>(G) * row;
+        if (g.first.empty()) continue;
+        std::vector<int> list(g.first);
+        list.push_back(-1);
+        std::shared_ptr<RsEntry> e;
+        rc = rs_entry(1, k, m, list.data(), rebuild_parity ? 1 : 0, -1, e);
+        if (rc) return rc;
+        if (e->outputs.empty()) continue;
+        if (e->inputs.empty()) {
+            for (int s : g.second)
+                for (int o : e->outputs)
+                    HIP_TRY(hipMemsetAsync(static_cast<uint8_t*>(base) + s * stripe_stride +
+                                               o * frag_stride, 0, blocksize,
+                                           static_cast<hipStream_t>(stream)));
+            continue;
+        }
+        rc = ecamd_map_apply_ptrs(e->map.get(), reinterpret_cast<const void* const*>(t), row,
+                                  e->inputs.data(), reinterpret_cast<void* const*>(t), row,
+                                  e->outputs.data(), blocksize, G, stream);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 int ecamd_rs_reconstruct(int k, int m, const int* missing, int dest, void* base,

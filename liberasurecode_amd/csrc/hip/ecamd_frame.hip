@@ -34,14 +34,55 @@ __device__ __forceinline__ u32x4 nt_load16(const uint8_t* p)
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
+// 4 * byte K of v in one VALU op (v_lshlrev_b32 with an SDWA byte-select source).
+template <int K>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t v)
+{
+    uint32_t r;
+    if constexpr (K == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+            : "=v"(r) : "v"(v));
+    else if constexpr (K == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+            : "=v"(r) : "v"(v));
+    else if constexpr (K == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+            : "=v"(r) : "v"(v));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+            : "=v"(r) : "v"(v));
+    return r;
+}
+
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 template <int B>
 __device__ __forceinline__ uint32_t lmap(const uint32_t* tab, uint32_t x)
 {
     constexpr int E = 1 << B;
-    constexpr uint32_t M = E - 1;
     uint32_t r = 0;
-#pragma unroll
-    for (int f = 0; f < 32 / B; ++f) r ^= tab[f * E + ((x >> (f * B)) & M)];
+    if constexpr (B == 4) {
+        // Spread the nibbles into bytes once (3 ops for 8 fields); every lookup address is then
+        // one SDWA byte-select shift (the compiler re-fuses a plain shift+mask, hence the asm).
+        const uint32_t lo = x & 0x0f0f0f0fu, hi = (x >> 4) & 0x0f0f0f0fu;
+        const char* t = reinterpret_cast<const char*>(tab);
+        auto at = [&](int f, uint32_t off) {
+            return *reinterpret_cast<const uint32_t*>(t + f * E * 4 + off);
+        };
+        const uint32_t a = xor3(at(0, byte_x4<0>(lo)), at(1, byte_x4<0>(hi)), at(2, byte_x4<1>(lo)));
+        const uint32_t b = xor3(at(3, byte_x4<1>(hi)), at(4, byte_x4<2>(lo)), at(5, byte_x4<2>(hi)));
+        r = xor3(a, b, at(6, byte_x4<3>(lo)) ^ at(7, byte_x4<3>(hi)));
+    } else {
+        static_assert(B == 8, "byte or nibble tables");
+        r = xor3(tab[x & 0xffu], tab[E + ((x >> 8) & 0xffu)], tab[2 * E + ((x >> 16) & 0xffu)]) ^
+            tab[3 * E + (x >> 24)];
+    }
     return r;
 }
 
@@ -49,7 +90,7 @@ template <int B>
 __device__ __forceinline__ uint32_t piece_r0(const uint32_t* tab, u32x4 v)
 {
     constexpr int S = (32 / B) << B;  // words of one data word's tables
-    return lmap<B>(tab, v.x) ^ lmap<B>(tab + S, v.y) ^ lmap<B>(tab + 2 * S, v.z) ^
+    return xor3(lmap<B>(tab, v.x), lmap<B>(tab + S, v.y), lmap<B>(tab + 2 * S, v.z)) ^
            lmap<B>(tab + 3 * S, v.w);
 }
 
@@ -90,15 +131,22 @@ __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const
         const uint8_t* p = item_ptr(a, item) + a.payload_off;
         const int64_t start = a.body - static_cast<int64_t>(a.nspans - q) * span + lane * 16;
         uint32_t st = 0;
-        for (int j = 0; j < a.J; j += 4) {
-            u32x4 v[4];
+        // Two groups of 4 pieces in flight: group g+1 is loading while group g is looked up.
+        auto load4 = [&](int j, u32x4 (&v)[4]) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int64_t off = start + static_cast<int64_t>(j + u) * 1024;
                 v[u] = off >= 0 ? nt_load16(p + off) : u32x4{0, 0, 0, 0};
             }
+        };
+        u32x4 cur[4], nxt[4];
+        load4(0, cur);
+        for (int j = 0; j < a.J; j += 4) {
+            if (j + 4 < a.J) load4(j + 4, nxt);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) st = lmap<B>(gap, st) ^ piece_r0<B>(tab, v[u]);
+            for (int u = 0; u < 4; ++u) st = lmap<B>(gap, st) ^ piece_r0<B>(tab, cur[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
         }
         // Lane l's state sits (63 - l) pieces before the span end: fold pairs, quads, ...
 #pragma unroll

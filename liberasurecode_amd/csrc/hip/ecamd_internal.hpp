@@ -1,5 +1,6 @@
 // ecamd_internal.hpp -- helpers ecamd_device.hip shares with the other launch files.
 #pragma once
+#include <stdint.h>
 
 namespace ecamd {
 
@@ -7,5 +8,12 @@ int dev_ensure(int* dev_out);                       // 0, or ECAMD_ENODEV / ECAM
 int dev_cu_count(int dev);
 int dev_fail(int code, const char* fmt, ...);       // sets ecamd_last_error(), returns code
 int dev_tune(const char* key);                      // current value of an ecamd_tune() knob
+
+// rs_vand encode whose k data inputs are read from objects (input j of stripe s at
+// obj + s*obj_stride + j*bs) and copied into payload j while the parity is computed
+// (payload f of stripe s at payload0 + s*stripe_stride + f*frag_stride).  16-byte alignment.
+int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                   int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                   void* stream);
 
 }  // namespace ecamd

@@ -152,7 +152,7 @@ __device__ __forceinline__ void mac_chunk_nib(const uint8_t* t, uint4 x, uint32_
     }
 }
 
-template <int W, bool PTRS, bool NT, bool NIB, bool TAIL>
+template <int W, bool PTRS, bool NT, bool NIB, bool COPY, bool TAIL>
 __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* lds, uint32_t s,
                                            int64_t off, int rem)
 {
@@ -179,6 +179,14 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
 #pragma unroll
         for (int i = 0; i < 4; i++)
             if (j0 + i < K) {
+                if constexpr (COPY) {  // copy-through: the input also lands in its own slot
+                    uint8_t* c = a.copy_base + static_cast<int64_t>(s) * a.copy_stride +
+                                 a.copy_off[j0 + i] + off;
+                    if (TAIL)
+                        store_tail(c, cur[i], rem);
+                    else
+                        stream_store16<NT>(c, cur[i]);
+                }
                 if constexpr (NIB)
                     mac_chunk_nib<W>(lds + static_cast<size_t>(j0 + i) * 64 * EB, cur[i], acc);
                 else
@@ -215,8 +223,8 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
 
 }  // namespace
 
-template <int W, bool PTRS, bool NT, bool NIB>
-__global__ void __launch_bounds__(NIB ? 512 : 1024) gf16_apply_kernel(const ApplyArgs a)
+template <int W, bool PTRS, bool NT, bool NIB, bool COPY>
+__device__ __forceinline__ void gf16_apply_body(const ApplyArgs& a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int EB = 2 * W;
@@ -233,11 +241,28 @@ __global__ void __launch_bounds__(NIB ? 512 : 1024) gf16_apply_kernel(const Appl
         const int64_t rem = a.bs - off;
         if (rem <= 0) continue;
         if (rem >= 16)
-            apply_tile<W, PTRS, NT, NIB, false>(a, lds, s, off, 16);
+            apply_tile<W, PTRS, NT, NIB, COPY, false>(a, lds, s, off, 16);
         else
-            apply_tile<W, PTRS, NT, NIB, true>(a, lds, s, off, static_cast<int>(rem));
+            apply_tile<W, PTRS, NT, NIB, COPY, true>(a, lds, s, off, static_cast<int>(rem));
     }
 }
+
+template <int W, bool PTRS, bool NT, bool NIB>
+__global__ void __launch_bounds__(NIB ? 512 : 1024) gf16_apply_kernel(const ApplyArgs a)
+{
+    gf16_apply_body<W, PTRS, NT, NIB, false>(a);
+}
+
+// Framed encode (hip/ecamd_frame_api.hip): the k data inputs are read straight from the object
+// and copied into their fragment payloads by the same launch that computes the parity.
+template <int W>
+__global__ void __launch_bounds__(1024) gf16_copy_apply_kernel(const ApplyArgs a)
+{
+    gf16_apply_body<W, false, true, false, true>(a);
+}
+template __global__ void gf16_copy_apply_kernel<2>(const ApplyArgs);
+template __global__ void gf16_copy_apply_kernel<4>(const ApplyArgs);
+template __global__ void gf16_copy_apply_kernel<8>(const ApplyArgs);
 
 #define ECAMD_INST(W, P, N, B) \
     template __global__ void gf16_apply_kernel<W, P, N, B>(const ApplyArgs);

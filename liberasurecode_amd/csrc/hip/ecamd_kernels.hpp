@@ -26,6 +26,9 @@ struct ApplyArgs {
     uint32_t masks[kMaxRows];         // xor kernel: input selection per output
     int64_t in_off[kMaxCols];         // byte offset (strided) / column (table) of input j
     int64_t out_off[kMaxRows];
+    uint8_t* copy_base;               // gf16_copy_apply_kernel: input j is also stored at
+    int64_t copy_stride;              //   copy_base + s*copy_stride + copy_off[j]
+    int64_t copy_off[kMaxCols];
 };
 
 struct FillArgs {
@@ -41,6 +44,8 @@ struct FillArgs {
 
 template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
+template <int W>
+__global__ void gf16_copy_apply_kernel(const ApplyArgs a);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>

@@ -129,6 +129,18 @@ def rs_decode(k, m, missing, lay: Layout, rebuild_parity=True, stream=None):
                                 _s(stream)), "rs_decode")
 
 
+def rs_decode_multi(k, m, missing_per_stripe, lay: Layout, rebuild_parity=True, stream=None):
+    """One erasure list per stripe; stripes are grouped by pattern on the host."""
+    width = m + 1
+    flat = []
+    for pat in missing_per_stripe:
+        row = list(pat)[:m] + [-1] * (width - min(len(pat), m))
+        flat += row
+    check(dev().ecamd_rs_decode_multi(k, m, ints(flat), width, int(rebuild_parity), lay.buf.ptr,
+                                      lay.stripe_stride, lay.frag_stride, lay.blocksize,
+                                      lay.nstripes, _s(stream)), "rs_decode_multi")
+
+
 def rs_reconstruct(k, m, missing, dest, lay: Layout, stream=None):
     check(dev().ecamd_rs_reconstruct(k, m, ints(list(missing) + [-1]), dest, lay.buf.ptr,
                                      lay.stripe_stride, lay.frag_stride, lay.blocksize,

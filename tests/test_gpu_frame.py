@@ -282,3 +282,24 @@ def test_frame_errors(F):
                                 None) < 0  # frag_stride < 80 + 1000 rounded
     assert d.ecamd_frame_decode(6, 4, 2, 0, _lib.ints([0, 1, 2, -1]), buf.ptr, 6 * 2048, 2048, 1,
                                 buf.ptr, 4096, 4000, None) < 0
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (20, 8), (10, 12), (4, 2)])
+def test_frame_encode_copy_through_matches_split(F, k, m):
+    """Objects that fill the k payloads exactly take the copy-through launch (data read from the
+    object and written to the payloads while the parity is computed); its fragments equal the
+    split-then-encode path's and the restated reference framing."""
+    from liberasurecode_amd import _lib
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    size = k * 65536
+    objs = _objects(3, size, k * 31 + m)
+    out = []
+    for unfused in (0, 1):
+        _lib.check(_lib.dev().ecamd_tune(b"frame_unfused", unfused), "tune")
+        fb = F.FrameBatch(be, k, m, size, 3)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        out.append(fb.fragments())
+    _lib.dev().ecamd_tune(b"frame_unfused", 0)
+    assert np.array_equal(out[0], out[1])
+    want = expected_stripe(be, k, m, 0, objs[2], ec_api.CHKSUM_CRC32)
+    assert all(out[0][2, i].tobytes() == want[i] for i in range(k + m))

@@ -137,6 +137,34 @@ def test_roundtrip_encode_erase_decode(k, m, bs, S, missing):
         assert (lay.download_stripes()[:, d] == ref[:, d]).all()
 
 
+@pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 64), (4, 2, 4096, 200), (20, 8, 8192, 40)])
+def test_decode_multi_heterogeneous(k, m, bs, S):
+    """Every stripe lost its own set of fragments (including none, all-parity and
+    m-missing cases); one call rebuilds them all, each equal to the oracle's decode of that
+    stripe on the same (inconsistent, garbage-filled) buffers."""
+    rng = np.random.default_rng(k * 100 + S)
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix(nfrags=k, stripe0=9)
+    D.rs_encode(k, m, lay)
+    host = lay.download_stripes()
+    pats = []
+    for s in range(S):
+        n = int(rng.integers(0, m + 1))
+        pat = sorted(rng.choice(k + m, n, replace=False).tolist())
+        if s % 7 == 0:
+            pat = list(range(k, k + m))  # parity only
+        rng.shuffle(pat)
+        pats.append(pat)
+        host[s, pat] = rng.integers(0, 256, (len(pat), bs), dtype=np.uint8)
+    lay.upload_stripes(host)
+    D.rs_decode_multi(k, m, pats, lay)
+    got = lay.download_stripes()
+    for s in range(S):
+        frags = [host[s, f].copy() for f in range(k + m)]
+        assert orc.decode(k, m, frags, pats[s]) == 0
+        assert all((got[s, f] == frags[f]).all() for f in range(k + m)), (s, pats[s])
+
+
 @pytest.mark.parametrize("bs", [1, 2, 3, 15, 16, 17, 31, 33, 255, 1000, 4097])
 @pytest.mark.parametrize("R,K", [(1, 3), (2, 5), (3, 4), (4, 10), (6, 7), (8, 20), (9, 25), (5, 45)])
 def test_map_tails_and_shapes(bs, R, K):

@@ -39,6 +39,10 @@ def main():
     lay = D.Layout(obj, 1, size, S, fb.obj_stride, fb.obj_stride)
     lay.fill_splitmix(stream=st)
     crc = D.DeviceBuffer(4 * S * (k + m))
+    # Random payload bytes: the byte-table CRC lookups conflict in LDS on random data only
+    # (all-zero payloads broadcast one entry and would overstate its speed).
+    _lib.check(d.ecamd_fill_splitmix(fb.buf.ptr + 80, fb.stripe_stride, fb.frag_stride, k + m,
+                                     fb.blocksize, S, 0, 0x5EED, st.handle), "fill")
     payload_bytes = S * (k + m) * fb.blocksize
     for bits in (8, 4):
         for wgs in (0, 2, 4):
@@ -52,13 +56,16 @@ def main():
     d.ecamd_tune(b"crc_bits", 8)
     d.ecamd_tune(b"crc_wgs", 0)
     obj_bytes = S * size
-    for ct in (frame.CHKSUM_NONE, frame.CHKSUM_CRC32):
+    for unfused, ct in ((0, frame.CHKSUM_NONE), (0, frame.CHKSUM_CRC32), (1, frame.CHKSUM_NONE),
+                        (1, frame.CHKSUM_CRC32)):
         fb.checksum = ct
+        d.ecamd_tune(b"frame_unfused", unfused)
         ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
-        print(json.dumps({"op": "frame_encode", "checksum": ct, "ms": round(ms, 3),
+        print(json.dumps({"op": "frame_encode", "unfused": unfused, "checksum": ct, "ms": round(ms, 3),
                           "GiBps_object": round(obj_bytes / (ms / 1e3) / 2**30, 1),
                           "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms / 1e6, 1)}),
               flush=True)
+    d.ecamd_tune(b"frame_unfused", 0)
     out = D.DeviceBuffer(fb.obj_stride * S)
     ms = timed(lambda: fb.decode([0, 1, 2, 3], out, stream=st), st, args.reps)
     print(json.dumps({"op": "frame_decode_4data", "ms": round(ms, 3),
