@@ -97,6 +97,14 @@ int ecamd_host_map_apply(const int *coeff, int R, int K, const void *const *in, 
 int ecamd_host_xor_apply(const uint64_t *sources, int R, int nbuf, const void *const *bufs,
                          void *const *out, int64_t blocksize);
 
+/* Per-call checksum handoff (used by liberasurecode.so.1 around encode / reconstruct): while armed
+ * on the calling thread, the two calls above also compute the CRC32 (zlib, or the legacy
+ * liberasurecode_crc32_alt when legacy != 0) of every input and output fragment on the GPU while
+ * the bytes are resident; lookup returns 0 and the CRC for a (pointer, length) seen since arm. */
+int ecamd_percall_crc_arm(int legacy);
+int ecamd_percall_crc_lookup(const void *ptr, int64_t len, uint32_t *crc);
+void ecamd_percall_crc_disarm(void);
+
 /* ---- on-device framing: the wire format of liberasurecode_encode, in HBM ----
  * backend 6 = liberasurecode_rs_vand, 3 = flat_xor_hd (hd used only there); checksum is the
  * ec_checksum_type_t of the instance (1 none, 2 CRC32; anything else is stored, not computed, as the
@@ -115,7 +123,8 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
                        int64_t obj_stride, uint64_t obj_size, void *d_frags, int64_t stripe_stride,
                        int64_t frag_stride, int nstripes, void *stream);
 /* liberasurecode_decode (src/erasurecode.c:523-734) with fragments already in their index slots:
- * rebuild the missing (-1 terminated) data payloads in place, then write the objects. */
+ * write the objects, rebuilding the missing (-1 terminated) data.  Surviving fragments are not
+ * modified; the slots of missing ones may be overwritten (with their rebuilt payload). */
 int ecamd_frame_decode(int backend, int k, int m, int hd, const int *missing, void *d_frags,
                        int64_t stripe_stride, int64_t frag_stride, int nstripes, void *d_obj,
                        int64_t obj_stride, uint64_t obj_size, void *stream);

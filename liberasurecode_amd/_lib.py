@@ -104,6 +104,10 @@ def dev():
                [C.c_int, C.c_int64, C.c_int, VP, C.c_int64, C.c_int64, C.c_int, VP, VP, VP])
         _proto(d, "ecamd_crc32", C.c_int,
                [C.c_int, VP, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int, VP, VP])
+        _proto(d, "ecamd_host_map_apply", C.c_int, [IP, C.c_int, C.c_int, VP, VP, C.c_int64])
+        _proto(d, "ecamd_percall_crc_arm", C.c_int, [C.c_int])
+        _proto(d, "ecamd_percall_crc_lookup", C.c_int, [VP, C.c_int64, C.POINTER(C.c_uint32)])
+        _proto(d, "ecamd_percall_crc_disarm", None, [])
         _proto(d, "ecamd_debug_stream_copy", C.c_int, [VP, VP, C.c_int64, VP])
         _proto(d, "ecamd_malloc", C.c_int, [C.POINTER(VP), C.c_int64])
         _proto(d, "ecamd_free", C.c_int, [VP])

@@ -347,12 +347,69 @@ int aligned_size(ec_backend* be, int data_len)
     return ((data_len + a - 1) / a) * a;
 }
 
+// GPU checksum handoff (include/ecamd.h ecamd_percall_crc_*): found in the dependency chain of
+// this repo's codec libraries; with a foreign codec library it is absent and zlib runs here.
+struct CrcHooks {
+    int (*arm)(int);
+    int (*lookup)(const void*, int64_t, uint32_t*);
+    void (*disarm)(void);
+};
+thread_local const CrcHooks* t_hooks = nullptr;
+
+const CrcHooks* crc_hooks(ec_backend* be)
+{
+    static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    static std::vector<std::pair<void*, CrcHooks>> cache;
+    void* so = be->desc.backend_sohandle;
+    if (!so) return nullptr;
+    pthread_mutex_lock(&mu);
+    const CrcHooks* found = nullptr;
+    for (auto& e : cache)
+        if (e.first == so) found = &e.second;
+    if (!found) {
+        CrcHooks h;
+        h.arm = reinterpret_cast<int (*)(int)>(dlsym(so, "ecamd_percall_crc_arm"));
+        h.lookup = reinterpret_cast<int (*)(const void*, int64_t, uint32_t*)>(
+            dlsym(so, "ecamd_percall_crc_lookup"));
+        h.disarm = reinterpret_cast<void (*)(void)>(dlsym(so, "ecamd_percall_crc_disarm"));
+        cache.emplace_back(so, h);
+        found = &cache.back().second;
+    }
+    const CrcHooks* r = (found->arm && found->lookup && found->disarm) ? found : nullptr;
+    pthread_mutex_unlock(&mu);
+    return r;
+}
+
+// Armed for one encode / reconstruct call when the instance stores CRC32 checksums: the codec
+// call then checksums the fragments on the GPU while they are resident.
+struct CrcArm {
+    const CrcHooks* h = nullptr;
+    CrcArm(ec_backend* be, bool want)
+    {
+        if (want && (h = crc_hooks(be)) != nullptr) {
+            h->arm(env_legacy_crc() ? 1 : 0);
+            t_hooks = h;
+        }
+    }
+    ~CrcArm()
+    {
+        if (h) {
+            h->disarm();
+            t_hooks = nullptr;
+        }
+    }
+};
+
 void write_checksum(char* f, ec_checksum_type_t ct, int bs)
 {
     fragment_header_t* h = hdr(f);
     h->meta.chksum_type = static_cast<uint8_t>(ct);
     h->meta.chksum_mismatch = 0;
-    if (ct == CHKSUM_CRC32)
+    if (ct != CHKSUM_CRC32) return;
+    uint32_t c = 0;
+    if (t_hooks && t_hooks->lookup(payload(f), bs, &c) == 0)
+        h->meta.chksum[0] = c;
+    else
         h->meta.chksum[0] = env_legacy_crc()
                                 ? static_cast<uint32_t>(liberasurecode_crc32_alt(0, payload(f), bs))
                                 : zcrc(payload(f), static_cast<size_t>(bs));
@@ -710,6 +767,7 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
                     parity[i - k] = f;
                 }
             }
+            CrcArm arm(be, be->args.uargs.ct == CHKSUM_CRC32);  // through the stamping below
             if (ret == 0) {
                 std::vector<char*> dp(k), pp(m);
                 for (int i = 0; i < k; i++) dp[i] = payload(data[i]);
@@ -857,6 +915,7 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
     int orig = 0, bs = 0;
     ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
                          fragment_len, owned);
+    CrcArm arm(be, be->args.uargs.ct == CHKSUM_CRC32);  // through the stamping below
     if (ret == 0) {
         std::vector<char*> dp(k), pp(m);
         for (int i = 0; i < k; i++) dp[i] = payload(data[i]);

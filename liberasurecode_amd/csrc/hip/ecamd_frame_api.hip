@@ -353,6 +353,13 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     if (nmiss > m) return dev_fail(ECAMD_EINVAL, "%d fragments missing, at most m = %d", nmiss, m);
     auto* frags = static_cast<uint8_t*>(d_frags);
     uint8_t* p0 = frags + kHeaderBytes;
+    if (data_missing && backend == kBackendRs && d_obj && a16(d_obj) && obj_stride % 16 == 0 &&
+        bs % 16 == 0 && static_cast<int64_t>(obj_size) == k * bs && dev_tune("frame_unfused") == 0) {
+        // One launch: the lost data are computed straight into the objects and the surviving data
+        // payloads are copied there as they stream through (no separate join pass).
+        return rs_decode_join(k, m, missing, p0, stripe_stride, frag_stride, d_obj, obj_stride, bs,
+                              nstripes, stream);
+    }
     if (data_missing) {  // the systematic fast path (src/erasurecode.c:597-607) skips this
         if (backend == kBackendRs)
             rc = ecamd_rs_decode(k, m, missing, 0, p0, stripe_stride, frag_stride, bs, nstripes, stream);

@@ -16,4 +16,11 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
                    void* stream);
 
+// rs_vand decode straight into objects: the missing data fragments (at least one, -1 terminated
+// `missing`) are computed into their object positions (j*bs) and the available data inputs are
+// copied there by the same launch (fragments_to_string without a separate join pass).
+int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
+                   int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
+                   void* stream);
+
 }  // namespace ecamd

@@ -180,12 +180,14 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
         for (int i = 0; i < 4; i++)
             if (j0 + i < K) {
                 if constexpr (COPY) {  // copy-through: the input also lands in its own slot
-                    uint8_t* c = a.copy_base + static_cast<int64_t>(s) * a.copy_stride +
-                                 a.copy_off[j0 + i] + off;
-                    if (TAIL)
-                        store_tail(c, cur[i], rem);
-                    else
-                        stream_store16<NT>(c, cur[i]);
+                    if (a.copy_off[j0 + i] >= 0) {  // wave-uniform
+                        uint8_t* c = a.copy_base + static_cast<int64_t>(s) * a.copy_stride +
+                                     a.copy_off[j0 + i] + off;
+                        if (TAIL)
+                            store_tail(c, cur[i], rem);
+                        else
+                            stream_store16<NT>(c, cur[i]);
+                    }
                 }
                 if constexpr (NIB)
                     mac_chunk_nib<W>(lds + static_cast<size_t>(j0 + i) * 64 * EB, cur[i], acc);

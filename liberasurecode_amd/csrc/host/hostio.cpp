@@ -15,9 +15,44 @@
 #include <mutex>
 #include <vector>
 
+#include "crc.hpp"
 #include "ecamd.h"
 
 namespace {
+
+// Per-call checksum handoff (ecamd_percall_crc_*): while armed on a thread, the chunked
+// pipeline also checksums every fragment slab on the GPU and records (pointer, length, crc).
+struct CrcRecord {
+    bool armed = false;
+    bool legacy = false;
+    struct Entry {
+        const void* ptr;
+        int64_t len;
+        uint32_t crc;
+    };
+    std::vector<Entry> entries;
+};
+thread_local CrcRecord t_crc;
+
+// zlib crc32_combine: crc(A || B) = A^|B| crc(A) ^ crc(B) for both checksum machines.
+uint32_t crc_combine(bool legacy, uint32_t a, uint32_t b, int64_t len_b)
+{
+    static std::mutex mu;
+    static std::map<std::pair<bool, int64_t>, ecamd::Mat32> cache;
+    ecamd::Mat32 m;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find({legacy, len_b});
+        if (it == cache.end()) {
+            if (cache.size() > 256) cache.clear();
+            it = cache.emplace(std::make_pair(legacy, len_b),
+                               ecamd::zero_shift(ecamd::CrcMachine(legacy),
+                                                 static_cast<uint64_t>(len_b))).first;
+        }
+        m = it->second;
+    }
+    return m.apply(a) ^ b;
+}
 
 constexpr int64_t kChunkTarget = 8 << 20;  // bytes of all fragments per chunk (both directions)
 
@@ -130,8 +165,11 @@ int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t b
     const int64_t padded = (bs + 15) / 16 * 16;
     chunk = std::min(chunk, padded);
     int rc = 0;
-    Staging* st = acquire(chunk * nfr, &rc);
+    const bool want_crc = t_crc.armed && nfr <= 64;
+    Staging* st = acquire(chunk * nfr + 256, &rc);  // last 256 B of each slab: chunk CRCs
     if (!st) return rc;
+    const int64_t crc_off = st->cap - 256;
+    std::vector<uint32_t> crc(want_crc ? nfr : 0, 0u);
     const int64_t nchunks = (bs + chunk - 1) / chunk;
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
     auto drain = [&](int s) -> int {
@@ -142,6 +180,10 @@ int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t b
         const int64_t n = std::min(chunk, bs - off);
         for (int o = 0; o < R; o++)
             std::memcpy(out[o] + off, st->slot[s].h_pin + (K + o) * chunk, static_cast<size_t>(n));
+        if (want_crc) {  // chunks drain in order, so the running CRCs extend by this chunk
+            const auto* cc = reinterpret_cast<const uint32_t*>(st->slot[s].h_pin + crc_off);
+            for (int f = 0; f < nfr; f++) crc[f] = crc_combine(t_crc.legacy, crc[f], cc[f], n);
+        }
         pending[s] = -1;
         return 0;
     };
@@ -153,12 +195,21 @@ int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t b
         const int64_t n = std::min(chunk, bs - off);
         for (int j = 0; j < K; j++)
             std::memcpy(sl.h_pin + j * chunk, in[j] + off, static_cast<size_t>(n));
-        for (int j = 0; j < K && rc == 0; j++)
-            rc = ecamd_memcpy_async(sl.d_buf + j * chunk, sl.h_pin + j * chunk, n, 0, sl.stream);
+        // One DMA each way per chunk (the slabs are [K inputs | R outputs] x chunk, contiguous):
+        // for small fragments the per-call cost is API latency, not bytes.  A short last chunk
+        // also moves the stale tail of each slot, which the kernel and the unpack never read.
+        rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
         if (rc == 0) rc = launch(ctx, sl.d_buf, chunk, n, sl.stream);
-        for (int o = 0; o < R && rc == 0; o++)
-            rc = ecamd_memcpy_async(sl.h_pin + (K + o) * chunk, sl.d_buf + (K + o) * chunk, n, 1,
-                                    sl.stream);
+        if (rc == 0)
+            rc = ecamd_memcpy_async(sl.h_pin + K * chunk, sl.d_buf + K * chunk,
+                                    (R - 1) * chunk + n, 1, sl.stream);
+        if (rc == 0 && want_crc) {
+            auto* d_crc = reinterpret_cast<uint32_t*>(sl.d_buf + crc_off);
+            rc = ecamd_crc32(t_crc.legacy ? 1 : 0, sl.d_buf, 0, chunk, static_cast<int>(nfr), n,
+                             1, d_crc, sl.stream);
+            if (rc == 0)
+                rc = ecamd_memcpy_async(sl.h_pin + crc_off, d_crc, nfr * 4, 1, sl.stream);
+        }
         pending[s] = c;
     }
     for (int s = 0; s < 2; s++) {
@@ -166,6 +217,10 @@ int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t b
         if (rc == 0) rc = r;
     }
     release(st);
+    if (rc == 0 && want_crc) {  // outputs after inputs: a lookup takes the latest entry
+        for (int j = 0; j < K; j++) t_crc.entries.push_back({in[j], bs, crc[j]});
+        for (int o = 0; o < R; o++) t_crc.entries.push_back({out[o], bs, crc[K + o]});
+    }
     return rc;
 }
 
@@ -250,6 +305,30 @@ int ecamd_host_xor_apply(const uint64_t* sources, int R, int nbuf, const void* c
     // after the whole chunk's inputs were packed, so every output sees the ORIGINAL inputs.
     return run_chunked(ctx.K, R, in.data(), reinterpret_cast<char* const*>(out), blocksize, &ctx,
                        launch_xor);
+}
+
+int ecamd_percall_crc_arm(int legacy)
+{
+    t_crc.armed = true;
+    t_crc.legacy = legacy != 0;
+    t_crc.entries.clear();
+    return 0;
+}
+
+int ecamd_percall_crc_lookup(const void* ptr, int64_t len, uint32_t* crc)
+{
+    for (auto it = t_crc.entries.rbegin(); it != t_crc.entries.rend(); ++it)
+        if (it->ptr == ptr && it->len == len) {
+            *crc = it->crc;
+            return 0;
+        }
+    return -1;
+}
+
+void ecamd_percall_crc_disarm(void)
+{
+    t_crc.armed = false;
+    t_crc.entries.clear();
 }
 
 }  // extern "C"

@@ -31,7 +31,7 @@ def bits(request):
     from liberasurecode_amd import _lib
     _lib.check(_lib.dev().ecamd_tune(b"crc_bits", request.param), "tune")
     yield request.param
-    _lib.dev().ecamd_tune(b"crc_bits", 8)
+    _lib.dev().ecamd_tune(b"crc_bits", 0)
 
 
 CRC_LENGTHS = [0, 1, 15, 16, 17, 100, 1023, 1024, 1025, 4096, 16383, 16384, 16400, 65536 + 13,
@@ -303,3 +303,61 @@ def test_frame_encode_copy_through_matches_split(F, k, m):
     assert np.array_equal(out[0], out[1])
     want = expected_stripe(be, k, m, 0, objs[2], ec_api.CHKSUM_CRC32)
     assert all(out[0][2, i].tobytes() == want[i] for i in range(k + m))
+
+
+@pytest.mark.parametrize("k,m,missing", [(10, 4, [0, 1, 2, 3]), (10, 4, [0, 5, 10, 13]),
+                                         (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]), (10, 12, [1, 2, 3, 4, 5, 6, 7, 8, 9]),
+                                         (4, 2, [3])])
+def test_frame_decode_join_matches_split(F, k, m, missing):
+    """Objects that fill the payloads exactly decode in one launch (lost data computed into the
+    object, surviving data copied through); same objects as decode-then-join."""
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    size, S = k * 65536, 3
+    objs = _objects(S, size, 17 * k + m)
+    for unfused in (0, 1):
+        _lib.check(_lib.dev().ecamd_tune(b"frame_unfused", unfused), "tune")
+        fb = F.FrameBatch(be, k, m, size, S)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        frags = fb.fragments()
+        frags[:, missing] = 0x3C
+        fb.upload_fragments(frags)
+        out = DeviceBuffer(fb.obj_stride * S)
+        fb.decode(missing, out)
+        host = out.download(fb.obj_stride * S).reshape(S, fb.obj_stride)
+        assert all(host[s, :size].tobytes() == objs[s] for s in range(S)), unfused
+        survivors = [i for i in range(k + m) if i not in missing]
+        assert np.array_equal(fb.fragments()[:, survivors], frags[:, survivors])
+    _lib.dev().ecamd_tune(b"frame_unfused", 0)
+
+
+@pytest.mark.parametrize("bs", [1000, 65536, (1 << 20) + 6, 3 * (1 << 20)])
+@pytest.mark.parametrize("legacy", [0, 1])
+def test_percall_crc_handoff(F, bs, legacy):
+    """ecamd_percall_crc_*: while armed, the per-call host path checksums every input and output
+    fragment on the GPU (chunk CRCs combined on the host); each equals zlib / the legacy CRC of
+    the final bytes.  This is what liberasurecode.so.1 stamps into the headers."""
+    import ctypes as C
+    from liberasurecode_amd import _lib
+    d = _lib.dev()
+    k, m = 10, 4
+    rng = np.random.default_rng(bs + legacy)
+    data = [rng.integers(0, 256, bs, dtype=np.uint8) for _ in range(k)]
+    parity = [np.zeros(bs, dtype=np.uint8) for _ in range(m)]
+    G = O.generator(k, m)
+    rows = G[k * k:]
+    inp = (C.c_void_p * k)(*[x.ctypes.data for x in data])
+    out = (C.c_void_p * m)(*[x.ctypes.data for x in parity])
+    d.ecamd_percall_crc_arm(legacy)
+    try:
+        assert d.ecamd_host_map_apply(_lib.ints(rows), m, k, inp, out, bs) == 0
+        for buf in data + parity:
+            c = C.c_uint32()
+            assert d.ecamd_percall_crc_lookup(buf.ctypes.data, bs, C.byref(c)) == 0
+            assert c.value == O.crc32(buf, legacy=bool(legacy))
+        c = C.c_uint32()
+        assert d.ecamd_percall_crc_lookup(data[0].ctypes.data, bs + 1, C.byref(c)) != 0
+    finally:
+        d.ecamd_percall_crc_disarm()
+    assert np.array_equal(np.stack(parity), O.encode(k, m, np.stack(data)))

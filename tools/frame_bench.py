@@ -53,7 +53,7 @@ def main():
                                                          crc.ptr, st.handle), "crc"), st, args.reps)
             print(json.dumps({"op": "crc32", "bits": bits, "crc_wgs": wgs, "ms": round(ms, 3),
                               "GBps": round(payload_bytes / ms / 1e6, 1)}), flush=True)
-    d.ecamd_tune(b"crc_bits", 8)
+    d.ecamd_tune(b"crc_bits", 0)
     d.ecamd_tune(b"crc_wgs", 0)
     obj_bytes = S * size
     for unfused, ct in ((0, frame.CHKSUM_NONE), (0, frame.CHKSUM_CRC32), (1, frame.CHKSUM_NONE),

@@ -27,13 +27,15 @@ def counters(path):
 def main(cfg, rnd="r01"):
     g = os.path.join(ROOT, "gpurun_out")
     out = {"config": cfg, "round": rnd, "kernels": {}}
-    stats = os.path.join(g, f"prof_trace_{cfg}", "run_kernel_stats.csv")
+    # cfg "frame": tools/gpu_prof_frame.sh (framing / CRC kernels), dirs gpurun_out/fprof_<tag>
+    d_of = (lambda tag: f"fprof_{tag}") if cfg == "frame" else (lambda tag: f"prof_{tag}_{cfg}")
+    stats = os.path.join(g, d_of("trace"), "run_kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
         out["kernels"][r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                      "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
                                      "pct": float(r["Percentage"])}
     for tag in ("fetch", "write", "lds"):
-        p = os.path.join(g, f"prof_{tag}_{cfg}", "run_counter_collection.csv")
+        p = os.path.join(g, d_of(tag), "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
         for (kern, cname), vals in counters(p).items():
