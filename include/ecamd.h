@@ -82,6 +82,13 @@ int ecamd_rs_decode(int k, int m, const int *missing, int rebuild_parity, void *
 int ecamd_rs_decode_multi(int k, int m, const int *missing, int missing_stride,
                           int rebuild_parity, void *base, int64_t stripe_stride,
                           int64_t frag_stride, int64_t blocksize, int nstripes, void *stream);
+/* Fragment placement across GPUs: fragment f of every stripe (frag_len bytes at
+ * d_src + s*stripe_stride + f*frag_stride on the current device) goes to d_dst[f] +
+ * s*dst_stride[f] on device dst_dev[f]: one strided DMA per fragment, over xGMI when dst_dev[f]
+ * is a peer (peer access is enabled on first use).  Asynchronous on `stream`. */
+int ecamd_scatter_fragments(const void *d_src, int64_t stripe_stride, int64_t frag_stride,
+                            int64_t frag_len, int nfrags, int nstripes, const int *dst_dev,
+                            void *const *d_dst, const int64_t *dst_stride, void *stream);
 /* Reconstruct one destination, as liberasurecode_rs_vand_reconstruct does. */
 int ecamd_rs_reconstruct(int k, int m, const int *missing, int dest, void *base,
                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,

@@ -68,6 +68,16 @@ int ecamd_xor_fragments_needed(int k, int m, int hd, const unsigned int *parity_
                                const unsigned int *data_bms, const int *to_reconstruct,
                                const int *to_exclude, int *needed);
 
+/* Batched planning: liberasurecode_fragments_needed for nstripes stripes at once.
+ * Stripe s: to_reconstruct at recon + s*list_stride, to_exclude at excl + s*list_stride (each
+ * -1 terminated within list_stride entries); its needed list (-1 terminated, padded with -1) at
+ * needed + s*(k+m+1) and its return code at rcs[s].  backend 6 (rs_vand): the first k indices
+ * neither missing nor excluded (src/backends/rs_vand/liberasurecode_rs_vand.c:119-145), rc -1 if
+ * fewer remain; backend 3 (flat_xor_hd): xor_hd_fragments_needed.  Returns -1 on bad arguments. */
+int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int *recon,
+                                 const int *excl, int list_stride, int nstripes, int *needed,
+                                 int *rcs);
+
 #ifdef __cplusplus
 }
 #endif

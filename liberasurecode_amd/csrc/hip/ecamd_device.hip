@@ -775,6 +775,48 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
     return 0;
 }
 
+int ecamd_scatter_fragments(const void* d_src, int64_t stripe_stride, int64_t frag_stride,
+                            int64_t frag_len, int nfrags, int nstripes, const int* dst_dev,
+                            void* const* d_dst, const int64_t* dst_stride, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!d_src || !dst_dev || !d_dst || !dst_stride || nfrags < 0 || nstripes < 0 || frag_len < 0)
+        return fail(ECAMD_EINVAL, "bad scatter arguments");
+    if (nfrags == 0 || nstripes == 0 || frag_len == 0) return 0;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    static std::mutex mu;
+    static std::vector<std::pair<int, int>> enabled;  // (from, to) peer links already opened
+    for (int f = 0; f < nfrags; f++) {
+        const int to = dst_dev[f];
+        if (to < 0 || to >= ndev) return fail(ECAMD_EINVAL, "fragment %d: bad device %d", f, to);
+        if (!d_dst[f] || dst_stride[f] < frag_len)
+            return fail(ECAMD_EINVAL, "fragment %d: bad destination / stride", f);
+        if (to != dev) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (std::find(enabled.begin(), enabled.end(), std::make_pair(dev, to)) == enabled.end()) {
+                int can = 0;
+                HIP_TRY(hipDeviceCanAccessPeer(&can, dev, to));
+                if (!can) return fail(ECAMD_EINVAL, "no peer path from device %d to %d", dev, to);
+                hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    return fail(ECAMD_EHIP, "hipDeviceEnablePeerAccess(%d): %s", to, hipGetErrorString(e));
+                (void)hipGetLastError();
+                enabled.emplace_back(dev, to);
+            }
+        }
+        // One strided copy per fragment: nstripes rows of frag_len bytes (xGMI DMA when to != dev).
+        HIP_TRY(hipMemcpy2DAsync(d_dst[f], static_cast<size_t>(dst_stride[f]),
+                                 static_cast<const uint8_t*>(d_src) + f * frag_stride,
+                                 static_cast<size_t>(stripe_stride), static_cast<size_t>(frag_len),
+                                 static_cast<size_t>(nstripes), hipMemcpyDefault,
+                                 static_cast<hipStream_t>(stream)));
+    }
+    return 0;
+}
+
 int ecamd_rs_reconstruct(int k, int m, const int* missing, int dest, void* base,
                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
                          int nstripes, void* stream)

@@ -135,4 +135,52 @@ int ecamd_xor_fragments_needed(int k, int m, int hd, const unsigned int* parity_
     return rc;
 }
 
+int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int* recon,
+                                 const int* excl, int list_stride, int nstripes, int* needed,
+                                 int* rcs)
+{
+    if (!recon || !excl || !needed || !rcs || list_stride < 1 || nstripes < 0 || k < 1 || m < 0 ||
+        k + m > 64)
+        return -1;
+    unsigned pb[64], db[64];
+    if (backend == 3 && ecamd_xor_code_tables(k, m, hd, pb, db) != 0) return -1;
+    if (backend != 3 && backend != 6) return -1;
+    const int row = k + m + 1;
+    for (int s = 0; s < nstripes; s++) {
+        const int* r = recon + static_cast<int64_t>(s) * list_stride;
+        const int* x = excl + static_cast<int64_t>(s) * list_stride;
+        int* out = needed + static_cast<int64_t>(s) * row;
+        std::vector<int> rl, xl;
+        for (int i = 0; i < list_stride && r[i] >= 0; i++) rl.push_back(r[i]);
+        for (int i = 0; i < list_stride && x[i] >= 0; i++) xl.push_back(x[i]);
+        rl.push_back(-1);
+        xl.push_back(-1);
+        if (backend == 3) {
+            // xor_hd_fragments_needed (xor_hd_code.c:209-412), exactly as the shim calls it
+            std::vector<int> tmp(row, -1);
+            rcs[s] = ecamd_xor_fragments_needed(k, m, hd, pb, db, rl.data(), xl.data(), tmp.data());
+            std::memcpy(out, tmp.data(), sizeof(int) * row);
+            if (rcs[s] >= 0) {
+                int n = 0;
+                while (n < row && tmp[n] >= 0) n++;
+                for (int i = n; i < row; i++) out[i] = -1;
+            }
+        } else {
+            // rs_vand shim (src/backends/rs_vand/liberasurecode_rs_vand.c:119-145): the first k
+            // indices neither missing nor excluded.
+            std::vector<bool> gone(k + m, false);
+            for (int v : xl)
+                if (v >= 0 && v < k + m) gone[v] = true;
+            for (int v : rl)
+                if (v >= 0 && v < k + m) gone[v] = true;
+            int j = 0;
+            for (int i = 0; i < k + m && j < k; i++)
+                if (!gone[i]) out[j++] = i;
+            for (int i = j; i < row; i++) out[i] = -1;
+            rcs[s] = j == k ? 0 : -1;
+        }
+    }
+    return 0;
+}
+
 }  // extern "C"

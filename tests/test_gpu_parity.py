@@ -283,3 +283,26 @@ def test_reference_unit_test_runs_on_our_codec():
     assert os.path.join("liberasurecode_amd", "lib", "liberasurecode_rs_vand.so.1") in probe
     r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_scatter_fragments_single_device():
+    """ecamd_scatter_fragments with every destination on this device (the one-GPU box): each
+    fragment column lands, stripe by stripe, at its own strided destination."""
+    k, m, bs, S = 10, 4, 4096 + 80, 6
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix()
+    src = lay.download_stripes()
+    dsts = [D.DeviceBuffer(S * (bs + 32 * f + 16)) for f in range(k + m)]
+    strides = [bs + 32 * f + 16 for f in range(k + m)]
+    d = _lib.dev()
+    f = d.ecamd_scatter_fragments
+    f.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_void_p,
+                  C.c_void_p, C.c_void_p, C.c_void_p]
+    assert f(lay.buf.ptr, lay.stripe_stride, lay.frag_stride, bs, k + m, S, _lib.ints([0] * (k + m)),
+             (C.c_void_p * (k + m))(*[b.ptr for b in dsts]), _lib.i64s(strides), None) == 0
+    D.synchronize()
+    for i in range(k + m):
+        got = dsts[i].download(S * strides[i]).reshape(S, strides[i])[:, :bs]
+        assert (got == src[:, i]).all(), i
+    assert f(lay.buf.ptr, lay.stripe_stride, lay.frag_stride, bs, 1, S, _lib.ints([7]),
+             (C.c_void_p * 1)(dsts[0].ptr), _lib.i64s([strides[0]]), None) != 0
