@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "ecamd_frame.hpp"
+#include "ecamd_isa.hpp"
 
 namespace ecamd {
 
@@ -34,32 +35,11 @@ __device__ __forceinline__ u32x4 nt_load16(const uint8_t* p)
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
-// 4 * byte K of v in one VALU op (v_lshlrev_b32 with an SDWA byte-select source).
+// 4 * byte K of v in one VALU op (ecamd_isa.hpp).
 template <int K>
 __device__ __forceinline__ uint32_t byte_x4(uint32_t v)
 {
-    uint32_t r;
-    if constexpr (K == 0)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
-            : "=v"(r) : "v"(v));
-    else if constexpr (K == 1)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
-            : "=v"(r) : "v"(v));
-    else if constexpr (K == 2)
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
-            : "=v"(r) : "v"(v));
-    else
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
-            : "=v"(r) : "v"(v));
-    return r;
-}
-
-// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
-{
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
+    return byte_shl<K, 2>(v);
 }
 
 template <int B>

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ecamd_isa.hpp"
 #include "ecamd_kernels.hpp"
 
 namespace ecamd {
@@ -127,28 +128,39 @@ __device__ __forceinline__ void mac_chunk(const uint8_t* tl, uint4 x, uint32_t (
         lds_entry<D>(tl + (v & 0xffu) * EB, e0);
         lds_entry<D>(th + ((v >> 8) & 0xffu) * EB, e1);
 #pragma unroll
-        for (int d = 0; d < D; d++) acc[w][d] ^= e0[d] ^ e1[d];
+        for (int d = 0; d < D; d++) acc[w][d] = xor3(acc[w][d], e0[d], e1[d]);
     }
 }
 
-// Nibble tables (host/tables.hpp build_nibble_tables): four conflict-free lookups per word.
-template <int W>
-__device__ __forceinline__ void mac_chunk_nib(const uint8_t* t, uint4 x, uint32_t (&acc)[8][W / 2])
+constexpr int log2i(int v) { return v <= 1 ? 0 : 1 + log2i(v / 2); }
+
+// Nibble tables (host/tables.hpp build_nibble_tables): four conflict-free lookups per word.  The
+// nibbles of a data dword are spread into bytes once; each table offset is then one SDWA shift.
+template <int W, int H>
+__device__ __forceinline__ void mac_word_nib(const uint8_t* t, uint32_t lo, uint32_t hi,
+                                             uint32_t (&acc)[W / 2])
 {
     constexpr int D = W / 2;
     constexpr int EB = 2 * W;
+    constexpr int S = log2i(EB);
+    uint32_t e0[D], e1[D], e2[D], e3[D];
+    lds_entry<D>(t + 0 * 16 * EB + byte_shl<2 * H, S>(lo), e0);      // bits 0-3 of the word
+    lds_entry<D>(t + 1 * 16 * EB + byte_shl<2 * H, S>(hi), e1);      // bits 4-7
+    lds_entry<D>(t + 2 * 16 * EB + byte_shl<2 * H + 1, S>(lo), e2);  // bits 8-11
+    lds_entry<D>(t + 3 * 16 * EB + byte_shl<2 * H + 1, S>(hi), e3);  // bits 12-15
+#pragma unroll
+    for (int d = 0; d < D; d++) acc[d] = xor3(xor3(acc[d], e0[d], e1[d]), e2[d], e3[d]);
+}
+
+template <int W>
+__device__ __forceinline__ void mac_chunk_nib(const uint8_t* t, uint4 x, uint32_t (&acc)[8][W / 2])
+{
     const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-    for (int w = 0; w < 8; w++) {
-        const uint32_t v = xs[w >> 1] >> ((w & 1) * 16);
-#pragma unroll
-        for (int q = 0; q < 4; q += 2) {
-            uint32_t e0[D], e1[D];
-            lds_entry<D>(t + (q * 16 + ((v >> (4 * q)) & 0xfu)) * EB, e0);
-            lds_entry<D>(t + ((q + 1) * 16 + ((v >> (4 * q + 4)) & 0xfu)) * EB, e1);
-#pragma unroll
-            for (int d = 0; d < D; d++) acc[w][d] ^= e0[d] ^ e1[d];
-        }
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = xs[i] & 0x0f0f0f0fu, hi = (xs[i] >> 4) & 0x0f0f0f0fu;
+        mac_word_nib<W, 0>(t, lo, hi, acc[2 * i]);
+        mac_word_nib<W, 1>(t, lo, hi, acc[2 * i + 1]);
     }
 }
 
