@@ -115,6 +115,7 @@ struct Tuning {
                          // random payloads: 4.77 vs 4.25 TB/s) or 8 (byte tables)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
+    int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
 };
 Tuning g_tune;
 
@@ -140,6 +141,7 @@ int dev_tune(const char* key)
     if (k == "crc_bits") return g_tune.crc_bits;
     if (k == "crc_wgs") return g_tune.crc_wgs;
     if (k == "frame_unfused") return g_tune.frame_unfused;
+    if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     return 0;
 }
 
@@ -530,6 +532,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_bits = value == 8 ? 8 : 4;  // 0 restores the default (4)
     } else if (k == "crc_wgs") {
         g_tune.crc_wgs = std::max(0, std::min(value, 4));
+    } else if (k == "crc_gap_bits") {
+        g_tune.crc_gap_bits = value == 4 ? 4 : 8;  // 0 restores the default (8)
     } else if (k == "frame_unfused") {
         g_tune.frame_unfused = value != 0;
     } else {

@@ -90,12 +90,12 @@ __device__ __forceinline__ const uint8_t* item_ptr(const CrcArgs& a, int64_t ite
 
 }  // namespace
 
-template <int B>
+template <int B, int G>
 __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
                                                           uint32_t* __restrict__ partial)
 {
     constexpr int E = 1 << B, NF = 32 / B;
-    constexpr int PIECE = 4 * NF * E, FIELDS = NF * E, WORDS = PIECE + 7 * FIELDS;
+    constexpr int PIECE = 4 * NF * E, FIELDS = (32 / G) << G, WORDS = PIECE + 7 * FIELDS;
     __shared__ uint32_t tab[WORDS];
     for (int i = threadIdx.x; i < WORDS; i += blockDim.x) tab[i] = img[i];
     __syncthreads();
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const
         for (int j = 0; j < a.J; j += 4) {
             if (j + 4 < a.J) load4(j + 4, nxt);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) st = lmap<B>(gap, st) ^ piece_r0<B>(tab, cur[u]);
+            for (int u = 0; u < 4; ++u) st = lmap<G>(gap, st) ^ piece_r0<B>(tab, cur[u]);
 #pragma unroll
             for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
         }
@@ -132,16 +132,18 @@ __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const
 #pragma unroll
         for (int t = 0; t < 6; ++t) {
             const uint32_t right = __shfl_down(st, 1 << t, 64);
-            st = lmap<B>(tab + PIECE + FIELDS * (1 + t), st) ^ right;
+            st = lmap<G>(tab + PIECE + FIELDS * (1 + t), st) ^ right;
         }
         if (lane == 0) partial[ws] = st;
     }
 }
 
-template __global__ void crc_partial_kernel<8>(const CrcArgs, const uint32_t* __restrict__,
-                                               uint32_t* __restrict__);
-template __global__ void crc_partial_kernel<4>(const CrcArgs, const uint32_t* __restrict__,
-                                               uint32_t* __restrict__);
+template __global__ void crc_partial_kernel<8, 8>(const CrcArgs, const uint32_t* __restrict__,
+                                                  uint32_t* __restrict__);
+template __global__ void crc_partial_kernel<4, 4>(const CrcArgs, const uint32_t* __restrict__,
+                                                  uint32_t* __restrict__);
+template __global__ void crc_partial_kernel<4, 8>(const CrcArgs, const uint32_t* __restrict__,
+                                                  uint32_t* __restrict__);
 
 namespace {
 

@@ -47,17 +47,17 @@ struct DevImage {
 };
 
 std::mutex g_mu;
-std::map<std::tuple<int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J
+std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J, G
 std::map<std::pair<int, void*>, std::pair<uint32_t*, size_t>> g_scratch;     // dev, stream
 
-int image(int dev, bool legacy, int B, int J, const DevImage** out)
+int image(int dev, bool legacy, int B, int J, int G, const DevImage** out)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_tuple(dev, legacy ? 1 : 0, B, J);
+    auto key = std::make_tuple(dev, legacy ? 1 : 0, B, J, G);
     auto it = g_images.find(key);
     if (it == g_images.end()) {
         auto di = std::make_unique<DevImage>();
-        di->img = build_crc_image(CrcMachine(legacy), B, J);
+        di->img = build_crc_image(CrcMachine(legacy), B, J, G);
         const size_t bytes = di->img.words.size() * sizeof(uint32_t);
         HIP_TRY(hipMalloc(&di->d, bytes));
         HIP_TRY(hipMemcpy(di->d, di->img.words.data(), bytes, hipMemcpyHostToDevice));
@@ -144,10 +144,11 @@ int run_crc(int dev, bool legacy, bool with_crc, const uint8_t* base, int64_t ss
     const int64_t items = static_cast<int64_t>(nfrag) * nstripes;
     if (items == 0) return 0;
     const int B = dev_tune("crc_bits") == 4 ? 4 : 8;
+    const int G = B == 8 ? 8 : (dev_tune("crc_gap_bits") == 4 ? 4 : 8);
     const int64_t body = len & ~int64_t(15);
     int J = static_cast<int>(std::min<int64_t>(16, std::max<int64_t>(4, ((body / 1024 + 3) / 4) * 4)));
     const DevImage* di = nullptr;
-    int rc = image(dev, legacy, B, J, &di);
+    int rc = image(dev, legacy, B, J, G, &di);
     if (rc) return rc;
     CrcArgs a{};
     a.base = base;
@@ -179,12 +180,13 @@ int run_crc(int dev, bool legacy, bool with_crc, const uint8_t* base, int64_t ss
         const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(
                                                       static_cast<int64_t>(dev_cu_count(dev)) * wpc,
                                                       (waves + 7) / 8));
+        const dim3 gd(static_cast<unsigned>(grid)), bd(512);
         if (B == 8)
-            hipLaunchKernelGGL(crc_partial_kernel<8>, dim3(static_cast<unsigned>(grid)), dim3(512), 0,
-                               st, a, di->d, partial);
+            hipLaunchKernelGGL((crc_partial_kernel<8, 8>), gd, bd, 0, st, a, di->d, partial);
+        else if (G == 8)
+            hipLaunchKernelGGL((crc_partial_kernel<4, 8>), gd, bd, 0, st, a, di->d, partial);
         else
-            hipLaunchKernelGGL(crc_partial_kernel<4>, dim3(static_cast<unsigned>(grid)), dim3(512), 0,
-                               st, a, di->d, partial);
+            hipLaunchKernelGGL((crc_partial_kernel<4, 4>), gd, bd, 0, st, a, di->d, partial);
         HIP_TRY(hipGetLastError());
     }
     if (with_crc || h.write) {
@@ -436,7 +438,7 @@ int ecamd_frame_verify(int nfrag, int64_t blocksize, int legacy, const void* d_f
                  blocksize, nstripes, crc, none, stream);
     if (rc) return rc;
     const DevImage *iz = nullptr, *il = nullptr;
-    if ((rc = image(dev, false, 8, 4, &iz)) || (rc = image(dev, true, 8, 4, &il))) return rc;
+    if ((rc = image(dev, false, 8, 4, 8, &iz)) || (rc = image(dev, true, 8, 4, 8, &il))) return rc;
     CrcArgs a{};
     a.base = frags;
     a.stripe_stride = stripe_stride;

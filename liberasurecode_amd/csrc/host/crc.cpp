@@ -44,13 +44,15 @@ void field_tables(const Mat32& M, int B, uint32_t* out)
         for (int v = 0; v < E; v++) out[f * E + v] = M.apply(static_cast<uint32_t>(v) << (f * B));
 }
 
-CrcImage build_crc_image(const CrcMachine& m, int B, int J)
+CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G)
 {
     CrcImage img;
     img.B = B;
+    img.G = G;
     img.J = J;
     const int E = 1 << B, NF = 32 / B;
-    const size_t piece = static_cast<size_t>(4 * NF) * E, fields = static_cast<size_t>(NF) * E;
+    const size_t piece = static_cast<size_t>(4 * NF) * E;
+    const size_t fields = static_cast<size_t>(32 / G) << G;  // one gap / level map
     img.lds_words = piece + fields * 7;
     img.span_off = img.lds_words;
     img.t_off = img.span_off + 4 * 256;
@@ -65,8 +67,8 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J)
                 for (int q = 0; q < 4; q++) bytes[4 * word + q] = static_cast<uint8_t>(x >> (8 * q));
                 w[(word * NF + f) * E + v] = m.run(0, bytes, 16);
             }
-    field_tables(zero_shift(m, 64 * 16), B, w + piece);
-    for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), B, w + piece + fields * (1 + t));
+    field_tables(zero_shift(m, 64 * 16), G, w + piece);
+    for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), G, w + piece + fields * (1 + t));
     field_tables(zero_shift(m, static_cast<uint64_t>(J) * 1024), 8, w + img.span_off);
     std::memcpy(w + img.t_off, m.t, sizeof(m.t));
     return img;

@@ -59,18 +59,19 @@ void field_tables(const Mat32& M, int B, uint32_t* out);
 
 // Image of one device CRC configuration (layout documented in hip/ecamd_frame.hip):
 //   [ piece tables: 128/B tables, r0 of a 16-byte piece holding v in field f of word w ]
-//   [ gap tables  : A^(64 lanes * 16 B) as 32/B field tables                          ]
-//   [ level tables: A^(16 * 2^t), t = 0..5, for the in-wave butterfly                    ]
+//   [ gap tables  : A^(64 lanes * 16 B) as 32/G field tables                          ]
+//   [ level tables: A^(16 * 2^t), t = 0..5, for the in-wave butterfly (G-bit fields)     ]
 //   [ span tables : A^(J * 1024) as 4 byte tables (finalize kernel)                      ]
 //   [ T           : the machine's byte table (finalize: tail bytes and header checksum)  ]
 struct CrcImage {
     int B = 8;
+    int G = 8;
     int J = 16;
     std::vector<uint32_t> words;
     size_t lds_words = 0;  // prefix staged into LDS by the partial kernel
     size_t span_off = 0;
     size_t t_off = 0;
 };
-CrcImage build_crc_image(const CrcMachine& m, int B, int J);
+CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G);
 
 }  // namespace ecamd
