@@ -223,7 +223,8 @@ def main():
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
-    kernel = f"gf16_apply_kernel<{width}, false, true, false>"  # <W, PTRS, NT, NIB>
+    # <W outputs per pass, KG groups of 4 inputs, CH chunks per lane, PF prefetch>
+    kernel = f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false>"
     traffic, traffic_src = pmc_traffic(args.config, kernel)
     if traffic is not None and S != CONFIGS[args.config][3]:
         traffic = int(traffic * S / CONFIGS[args.config][3])  # profile ran at the default S

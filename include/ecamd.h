@@ -163,6 +163,13 @@ int ecamd_debug_stream_copy(void *d_dst, const void *d_src, int64_t bytes, void 
  * flight, grid = CUs x wgs_per_cu workgroups of 256 lanes (bandwidth ceilings for DESIGN.md). */
 int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void *d_dst, const void *d_src,
                          int64_t bytes, void *stream);
+/* Codec-shaped streaming probe: K fragment reads and R fragment writes per tile over nstripes
+ * stripes of (K+R) fragments of blocksize bytes at d_base (stripe stride (K+R)*blocksize), the tile
+ * order of gf16_apply_kernel, no table work.  lp / sp: buffer-load / store cache policy (gfx950
+ * cpol: 1 sc0, 2 nt, 16 sc1; pairs listed in ECAMD_MIX_POLICIES), ch: 16-B chunks per lane (1, 2).
+ * blocksize must be a multiple of threads*16*ch; stripe stride < 2 GiB. */
+int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d_base,
+                          int64_t blocksize, int K, int R, int nstripes, void *stream);
 
 /* ---- device memory helpers for C / ctypes callers ---- */
 int ecamd_malloc(void **d_ptr, int64_t bytes);

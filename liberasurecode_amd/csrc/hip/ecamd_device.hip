@@ -88,6 +88,15 @@ int ensure_device(int* dev_out)
 #undef K_
         for (const void* k : ks)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+#define K_(W, KG, CH, PF) reinterpret_cast<const void*>(&gf16_stream_kernel<W, KG, CH, PF>)
+#define KG_(W, CH, PF) K_(W, 1, CH, PF), K_(W, 2, CH, PF), K_(W, 3, CH, PF), K_(W, 4, CH, PF), K_(W, 5, CH, PF)
+        const void* sk[] = {KG_(2, 1, true),  KG_(4, 1, true),  KG_(8, 1, true), KG_(2, 1, false),
+                            KG_(4, 1, false), KG_(8, 1, false), KG_(2, 2, true), KG_(4, 2, true),
+                            KG_(2, 2, false), KG_(4, 2, false)};
+#undef KG_
+#undef K_
+        for (const void* k : sk)
+            HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         di.lds_attr_set = true;
     }
     if (dev_out) *dev_out = dev;
@@ -116,6 +125,10 @@ struct Tuning {
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
+    int stream = 1;         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
+    int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
+    int stream_pf = 0;      //   next group's loads issued before the lookups (1) or after (0);
+                            //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
 };
 Tuning g_tune;
 
@@ -201,9 +214,9 @@ struct Geometry {
 };
 
 int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chunks = 1,
-             int max_threads = 1024)
+             int max_threads = 1024, int max_wgs = 8)
 {
-    int wgs = lds ? static_cast<int>(std::min<size_t>(8, std::max<size_t>(1, kLdsBytes / lds))) : 8;
+    int wgs = lds ? static_cast<int>(std::min<size_t>(max_wgs, std::max<size_t>(1, kLdsBytes / lds))) : 8;
     int threads = lds ? std::min(1024, std::max(256, (1024 / wgs) / 64 * 64)) : 256;
     if (lds && g_tune.threads > 0) threads = g_tune.threads;
     threads = std::min(threads, max_threads);
@@ -219,6 +232,63 @@ int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chu
     int64_t grid = std::min<int64_t>(nt, static_cast<int64_t>(cu_count(dev)) * wgs);
     g.grid = static_cast<int>(std::max<int64_t>(grid, 1));
     return 0;
+}
+
+// gf16_stream_kernel addresses a stripe's fragments as 32-bit offsets from one buffer resource:
+// usable when every offset is non-negative and the furthest byte stays below 2^31.
+bool stream_offsets(ApplyArgs& a, int64_t bs)
+{
+    int64_t in_max = 0, out_max = 0;
+    for (int j = 0; j < a.ncols; j++) {
+        if (a.in_off[j] < 0) return false;
+        in_max = std::max(in_max, a.in_off[j] + bs);
+    }
+    for (int r = 0; r < a.nrows; r++) {
+        if (a.out_off[r] < 0) return false;
+        out_max = std::max(out_max, a.out_off[r] + bs);
+    }
+    const int64_t lim = int64_t(1) << 31;
+    if (in_max >= lim || out_max >= lim) return false;
+    for (int j = 0; j < a.ncols; j++) a.in_off32[j] = static_cast<int32_t>(a.in_off[j]);
+    for (int r = 0; r < a.nrows; r++) a.out_off32[r] = static_cast<int32_t>(a.out_off[r]);
+    a.in_records = static_cast<uint32_t>(in_max);
+    a.out_records = static_cast<uint32_t>(out_max);
+    return true;
+}
+
+template <int W, int CH, bool PF>
+int launch_stream_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st)
+{
+    const int kg = (a.ncols + 3) / 4;
+    switch (kg) {
+    case 1: hipLaunchKernelGGL((gf16_stream_kernel<W, 1, CH, PF>), grid, block, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((gf16_stream_kernel<W, 2, CH, PF>), grid, block, lds, st, a); break;
+    case 3: hipLaunchKernelGGL((gf16_stream_kernel<W, 3, CH, PF>), grid, block, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((gf16_stream_kernel<W, 4, CH, PF>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((gf16_stream_kernel<W, 5, CH, PF>), grid, block, lds, st, a); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, dim3 grid, dim3 block, size_t lds,
+                  hipStream_t st)
+{
+    if (ch == 2 && width <= 4) {
+        if (pf)
+            return width == 2 ? launch_stream_w<2, 2, true>(a, grid, block, lds, st)
+                              : launch_stream_w<4, 2, true>(a, grid, block, lds, st);
+        return width == 2 ? launch_stream_w<2, 2, false>(a, grid, block, lds, st)
+                          : launch_stream_w<4, 2, false>(a, grid, block, lds, st);
+    }
+    if (pf) {
+        if (width == 2) return launch_stream_w<2, 1, true>(a, grid, block, lds, st);
+        if (width == 4) return launch_stream_w<4, 1, true>(a, grid, block, lds, st);
+        return launch_stream_w<8, 1, true>(a, grid, block, lds, st);
+    }
+    if (width == 2) return launch_stream_w<2, 1, false>(a, grid, block, lds, st);
+    if (width == 4) return launch_stream_w<4, 1, false>(a, grid, block, lds, st);
+    return launch_stream_w<8, 1, false>(a, grid, block, lds, st);
 }
 
 template <bool PTRS>
@@ -273,6 +343,18 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             continue;
         }
         const bool nt = g_tune.nt != 0;
+        if (!PTRS && nt && g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs)) {
+            const int ch = p.width <= 4 ? g_tune.stream_ch : 1;
+            // 16 waves per CU (4 x 256 threads, or fewer, larger workgroups when the tables
+            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5
+            rc = geometry(map->device, p.bytes, bs, nstripes, g, ch, 1024, 4);
+            if (rc) return rc;
+            a.ntiles = g.ntiles;
+            a.tiles_per_stripe = g.tiles_per_stripe;
+            rc = launch_stream(a, p.width, ch, g_tune.stream_pf != 0, dim3(g.grid), dim3(g.threads), g.lds, st);
+            if (rc) return rc;
+            continue;
+        }
         switch (p.width * 2 + (nt ? 1 : 0)) {
         case 4: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, false, false>), grid, block, g.lds, st, a); break;
         case 5: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, true, false>), grid, block, g.lds, st, a); break;
@@ -536,6 +618,12 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_gap_bits = value == 4 ? 4 : 8;  // 0 restores the default (8)
     } else if (k == "frame_unfused") {
         g_tune.frame_unfused = value != 0;
+    } else if (k == "stream") {
+        g_tune.stream = value != 0;
+    } else if (k == "stream_ch") {
+        g_tune.stream_ch = value == 2 ? 2 : 1;
+    } else if (k == "stream_pf") {
+        g_tune.stream_pf = value != 0;
     } else {
         return fail(ECAMD_EINVAL, "unknown tuning key %s", key);
     }
@@ -881,6 +969,40 @@ int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void* dst, const 
     case 4: hipLaunchKernelGGL(bw_probe_kernel<4>, grid, block, 0, st, d, s, bytes, kind, sink); break;
     default: hipLaunchKernelGGL(bw_probe_kernel<8>, grid, block, 0, st, d, s, bytes, kind, sink); break;
     }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void* base,
+                          int64_t bs, int K, int R, int nstripes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (ch != 1 && ch != 2) return fail(ECAMD_EINVAL, "mix probe: ch must be 1 or 2");
+    if (threads < 64 || threads > 1024 || threads % 64) return fail(ECAMD_EINVAL, "mix probe: threads");
+    const int64_t span = static_cast<int64_t>(threads) * 16 * ch;
+    const int64_t sstride = bs * (K + R);
+    if (K < 1 || R < 0 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
+        return fail(ECAMD_EINVAL, "mix probe: bad shape");
+    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0};
+    a.tiles_per_stripe = static_cast<uint32_t>(bs / span);
+    a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
+    const int grid = static_cast<int>(std::min<int64_t>(a.ntiles,
+                                                        static_cast<int64_t>(cu_count(dev)) * std::max(1, wgs_per_cu)));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    bool launched = false;
+#define ECAMD_MIX(LP, SP)                                                                         \
+    if (!launched && lp == LP && sp == SP) {                                                      \
+        if (ch == 1)                                                                              \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 1>), dim3(grid), dim3(threads), 0, st, a); \
+        else                                                                                      \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 2>), dim3(grid), dim3(threads), 0, st, a); \
+        launched = true;                                                                          \
+    }
+    ECAMD_MIX_POLICIES(ECAMD_MIX)
+#undef ECAMD_MIX
+    if (!launched) return fail(ECAMD_EINVAL, "mix probe: policy pair (%d, %d) not instantiated", lp, sp);
     HIP_TRY(hipGetLastError());
     return 0;
 }

@@ -278,6 +278,175 @@ template __global__ void gf16_copy_apply_kernel<2>(const ApplyArgs);
 template __global__ void gf16_copy_apply_kernel<4>(const ApplyArgs);
 template __global__ void gf16_copy_apply_kernel<8>(const ApplyArgs);
 
+// ------------------------------------------------------------ streaming form ----
+// gf16_stream_kernel<W, KG, CH, PF>: the strided gf16 apply for up to 4*KG inputs, written so the
+// HBM stream never stalls behind the table work:
+//   * buffer loads/stores on one resource per stripe (32-bit offsets, no 64-bit address math);
+//     the loads of a group of 4 inputs are unconditional -- an input index past ncols gets an
+//     out-of-range offset, which the buffer unit answers with zeros and no memory traffic -- so
+//     the code is straight-line and the next group's loads stay in flight (counted vmcnt) while
+//     the current group's lookups run;
+//   * inputs fully unrolled: each input's table base is a compile-time LDS offset and each
+//     table index one SDWA byte-select shift (byte_shl), i.e. one VALU op per lookup;
+//   * CH 16-byte chunks per lane per fragment (blockDim*16 bytes apart): CH*1 KiB per wave per
+//     fragment in one tile;
+//   * PF: the next group's loads issued before (true) or after (false) this group's lookups.
+// Partial tiles at the end of a fragment go through apply_tile's byte-exact tail code.
+namespace {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <int W, int J>
+__device__ __forceinline__ void mac_chunk_imm(const uint8_t* lds, v4u x, uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    constexpr int S = log2i(EB);
+    constexpr int TL = J * 512 * EB;
+    constexpr int TH = TL + 256 * EB;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const uint32_t v = x[w >> 1];
+        uint32_t e0[D], e1[D];
+        if (w & 1) {
+            lds_entry<D>(lds + TL + byte_shl<2, S>(v), e0);
+            lds_entry<D>(lds + TH + byte_shl<3, S>(v), e1);
+        } else {
+            lds_entry<D>(lds + TL + byte_shl<0, S>(v), e0);
+            lds_entry<D>(lds + TH + byte_shl<1, S>(v), e1);
+        }
+#pragma unroll
+        for (int d = 0; d < D; d++) acc[w][d] = xor3(acc[w][d], e0[d], e1[d]);
+    }
+}
+
+template <int W, int CH, int J>
+__device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds, const v4u (&x)[CH],
+                                          uint32_t (&acc)[CH][8][W / 2])
+{
+    if (J < a.ncols) {  // wave-uniform
+#pragma unroll
+        for (int c = 0; c < CH; c++) mac_chunk_imm<W, J>(lds, x[c], acc[c]);
+    }
+}
+
+template <int W, int CH, int G, int KG>
+__device__ __forceinline__ void load_group(const ApplyArgs& a, __amdgpu_buffer_rsrc_t rin, int off,
+                                           int cstride, v4u (&x)[4][CH])
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int j = 4 * G + i;
+        const int base = (j < a.ncols) ? a.in_off32[j] + off : static_cast<int>(0x80000000u);
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+            x[i][c] = __builtin_amdgcn_raw_buffer_load_b128(rin, base + c * cstride, 0, 2);
+    }
+}
+
+// Group G's lookups; with PF the loads of group G+1 are issued before them (in flight during the
+// lookups), without PF after them (each wave: load, wait, look up -- latency hidden by occupancy).
+template <int W, int CH, int G, int KG, bool PF>
+__device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* lds,
+                                             __amdgpu_buffer_rsrc_t rin, int off, int cstride,
+                                             v4u (&cur)[4][CH], uint32_t (&acc)[CH][8][W / 2])
+{
+    v4u nxt[4][CH];
+    if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG>(a, rin, off, cstride, nxt);
+    input_mac<W, CH, 4 * G + 0>(a, lds, cur[0], acc);
+    input_mac<W, CH, 4 * G + 1>(a, lds, cur[1], acc);
+    input_mac<W, CH, 4 * G + 2>(a, lds, cur[2], acc);
+    input_mac<W, CH, 4 * G + 3>(a, lds, cur[3], acc);
+    if constexpr (G + 1 < KG) {
+        if constexpr (!PF) load_group<W, CH, G + 1, KG>(a, rin, off, cstride, nxt);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
+        stream_group<W, CH, G + 1, KG, PF>(a, lds, rin, off, cstride, cur, acc);
+    }
+}
+
+}  // namespace
+
+template <int W, int KG, int CH, bool PF>
+__global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    const int tbytes = a.ncols * 512 * EB;
+    for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
+        *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
+    __syncthreads();
+
+    const int cstride = static_cast<int>(blockDim.x) * 16;
+    const int64_t span = static_cast<int64_t>(cstride) * CH;
+    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
+        if (toff + span > a.bs) {  // last, partial tile of each fragment
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                const int64_t o = toff + c * cstride + static_cast<int64_t>(threadIdx.x) * 16;
+                const int64_t rem = a.bs - o;
+                if (rem >= 16)
+                    apply_tile<W, false, true, false, false, false>(a, lds, s, o, 16);
+                else if (rem > 0)
+                    apply_tile<W, false, true, false, false, true>(a, lds, s, o, static_cast<int>(rem));
+            }
+            continue;
+        }
+        const int off = static_cast<int>(toff) + static_cast<int>(threadIdx.x) * 16;
+        const auto rin = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(a.in_base) + static_cast<int64_t>(s) * a.in_stride, 0,
+            static_cast<int>(a.in_records), 0x00020000);
+        const auto rout = __builtin_amdgcn_make_buffer_rsrc(
+            a.out_base + static_cast<int64_t>(s) * a.out_stride, 0, static_cast<int>(a.out_records),
+            0x00020000);
+
+        uint32_t acc[CH][8][D];
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+#pragma unroll
+            for (int w = 0; w < 8; w++)
+#pragma unroll
+                for (int d = 0; d < D; d++) acc[c][w][d] = 0u;
+        v4u cur[4][CH];
+        load_group<W, CH, 0, KG>(a, rin, off, cstride, cur);
+        stream_group<W, CH, 0, KG, PF>(a, lds, rin, off, cstride, cur, acc);
+
+#pragma unroll
+        for (int r = 0; r < W; r++) {
+            if (r >= a.nrows) break;
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                v4u v;
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const uint32_t A = acc[c][2 * d][r >> 1], B = acc[c][2 * d + 1][r >> 1];
+                    v[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+                }
+                const int o = a.out_off32[r] + off + c * cstride;
+                if (a.accumulate) v ^= __builtin_amdgcn_raw_buffer_load_b128(rout, o, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, rout, o, 0, 2);  // nt
+            }
+        }
+    }
+}
+
+#define ECAMD_STREAM_INST(W, KG, CH, PF) \
+    template __global__ void gf16_stream_kernel<W, KG, CH, PF>(const ApplyArgs);
+#define ECAMD_STREAM_KG(W, CH, PF)                                                                  \
+    ECAMD_STREAM_INST(W, 1, CH, PF) ECAMD_STREAM_INST(W, 2, CH, PF) ECAMD_STREAM_INST(W, 3, CH, PF) \
+    ECAMD_STREAM_INST(W, 4, CH, PF) ECAMD_STREAM_INST(W, 5, CH, PF)
+ECAMD_STREAM_KG(2, 1, true) ECAMD_STREAM_KG(4, 1, true) ECAMD_STREAM_KG(8, 1, true)
+ECAMD_STREAM_KG(2, 1, false) ECAMD_STREAM_KG(4, 1, false) ECAMD_STREAM_KG(8, 1, false)
+ECAMD_STREAM_KG(2, 2, true) ECAMD_STREAM_KG(4, 2, true)
+ECAMD_STREAM_KG(2, 2, false) ECAMD_STREAM_KG(4, 2, false)
+#undef ECAMD_STREAM_KG
+#undef ECAMD_STREAM_INST
+
 #define ECAMD_INST(W, P, N, B) \
     template __global__ void gf16_apply_kernel<W, P, N, B>(const ApplyArgs);
 #define ECAMD_INST2(P, N, B) ECAMD_INST(2, P, N, B) ECAMD_INST(4, P, N, B) ECAMD_INST(8, P, N, B)

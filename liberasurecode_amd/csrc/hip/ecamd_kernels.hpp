@@ -29,7 +29,14 @@ struct ApplyArgs {
     uint8_t* copy_base;               // gf16_copy_apply_kernel: input j is also stored at
     int64_t copy_stride;              //   copy_base + s*copy_stride + copy_off[j]
     int64_t copy_off[kMaxCols];
+    uint32_t in_records;              // gf16_stream_kernel: bytes addressable from one stripe's
+    uint32_t out_records;             //   in_base / out_base (buffer-resource range, < 2^31)
+    int32_t in_off32[kMaxCols];       // in_off / out_off as 32-bit buffer offsets
+    int32_t out_off32[kMaxRows];
 };
+
+// gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).
+constexpr int kStreamGroups = 5;
 
 struct FillArgs {
     uint8_t* base;
@@ -46,11 +53,31 @@ template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
 template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);
+template <int W, int KG, int CH, bool PF>
+__global__ void gf16_stream_kernel(const ApplyArgs a);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);
 __global__ void splitmix_fill_kernel(FillArgs f);
+struct MixArgs {
+    uint8_t* base;
+    int64_t stripe_stride;
+    int frag_stride;
+    int K, R;
+    uint32_t ntiles;
+    uint32_t tiles_per_stripe;
+};
+
+// (load policy, store policy) pairs instantiated for mix_probe_kernel; gfx950 cpol bits
+// 1 = sc0, 2 = nt, 16 = sc1.
+#define ECAMD_MIX_POLICIES(X) \
+    X(0, 0) X(0, 2) X(0, 16) X(0, 18) X(0, 1) \
+    X(2, 0) X(2, 2) X(2, 16) X(2, 18) X(2, 1) \
+    X(1, 0) X(1, 2) X(16, 2) X(18, 2) X(3, 2) X(18, 18)
+template <int LP, int SP, int CH>
+__global__ void mix_probe_kernel(MixArgs a);
+
 template <int U>
 __global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int kind,
                                 uint32_t* sink);

@@ -186,4 +186,64 @@ template __global__ void bw_probe_kernel<1>(uint8_t*, const uint8_t*, int64_t, i
 template __global__ void bw_probe_kernel<4>(uint8_t*, const uint8_t*, int64_t, int, uint32_t*);
 template __global__ void bw_probe_kernel<8>(uint8_t*, const uint8_t*, int64_t, int, uint32_t*);
 
+// Codec-shaped streaming probe (sweeps only): the access pattern of gf16_apply_kernel on the
+// strided [S][K+R][bs] layout -- K fragment reads, R fragment writes per tile, the same tile order
+// and prefetch depth -- with no LDS work, and the cache policy of the buffer loads (LP) and stores
+// (SP) as the aux immediate (gfx950 cpol: 1 = sc0, 2 = nt, 16 = sc1).  CH chunks of 16 B per lane
+// per fragment, the chunks of one lane blockDim*16 bytes apart.
+template <int LP, int SP, int CH>
+__global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
+{
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const int cstride = static_cast<int>(blockDim.x) * 16;
+    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int off = static_cast<int>(t - s * a.tiles_per_stripe) * cstride * CH +
+                        static_cast<int>(threadIdx.x) * 16;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            a.base + static_cast<int64_t>(s) * a.stripe_stride, 0,
+            static_cast<int>(a.stripe_stride), 0x00020000);
+        v4 acc[CH];
+#pragma unroll
+        for (int c = 0; c < CH; c++) acc[c] = v4{0u, 0u, 0u, 0u};
+        v4 cur[4][CH], nxt[4][CH];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                cur[i][c] = (i < a.K) ? __builtin_amdgcn_raw_buffer_load_b128(
+                                            rsrc, i * a.frag_stride + off + c * cstride, 0, LP)
+                                      : v4{0u, 0u, 0u, 0u};
+        for (int j0 = 0; j0 < a.K; j0 += 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < CH; c++)
+                    nxt[i][c] = (j0 + 4 + i < a.K)
+                                    ? __builtin_amdgcn_raw_buffer_load_b128(
+                                          rsrc, (j0 + 4 + i) * a.frag_stride + off + c * cstride, 0, LP)
+                                    : v4{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < CH; c++) {
+                    acc[c] ^= cur[i][c];
+                    cur[i][c] = nxt[i][c];
+                }
+        }
+        for (int r = 0; r < a.R; r++)
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                __builtin_amdgcn_raw_buffer_store_b128(acc[c] + static_cast<unsigned>(r), rsrc,
+                                                       (a.K + r) * a.frag_stride + off + c * cstride,
+                                                       0, SP);
+    }
+}
+
+#define ECAMD_MIX(LP, SP) \
+    template __global__ void mix_probe_kernel<LP, SP, 1>(MixArgs); \
+    template __global__ void mix_probe_kernel<LP, SP, 2>(MixArgs);
+ECAMD_MIX_POLICIES(ECAMD_MIX)
+#undef ECAMD_MIX
+
 }  // namespace ecamd
