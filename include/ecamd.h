@@ -170,6 +170,11 @@ int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void *d_dst, cons
  * blocksize must be a multiple of threads*16*ch; stripe stride < 2 GiB. */
 int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d_base,
                           int64_t blocksize, int K, int R, int nstripes, void *stream);
+/* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup) and the
+ * chunk layout (wave_contig 1: a wave's ch chunks are 1 KiB apart, contiguous) as parameters. */
+int ecamd_debug_mix_probe2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
+                           int wave_contig, void *d_base, int64_t blocksize, int K, int R,
+                           int nstripes, void *stream);
 
 /* ---- device memory helpers for C / ctypes callers ---- */
 int ecamd_malloc(void **d_ptr, int64_t bytes);

@@ -88,11 +88,14 @@ int ensure_device(int* dev_out)
 #undef K_
         for (const void* k : ks)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
-#define K_(W, KG, CH, PF) reinterpret_cast<const void*>(&gf16_stream_kernel<W, KG, CH, PF>)
-#define KG_(W, CH, PF) K_(W, 1, CH, PF), K_(W, 2, CH, PF), K_(W, 3, CH, PF), K_(W, 4, CH, PF), K_(W, 5, CH, PF)
-        const void* sk[] = {KG_(2, 1, true),  KG_(4, 1, true),  KG_(8, 1, true), KG_(2, 1, false),
-                            KG_(4, 1, false), KG_(8, 1, false), KG_(2, 2, true), KG_(4, 2, true),
-                            KG_(2, 2, false), KG_(4, 2, false)};
+#define K_(W, KG, CH, PF, N) reinterpret_cast<const void*>(&gf16_stream_kernel<W, KG, CH, PF, N>)
+#define KG_(W, CH, PF, N) K_(W, 1, CH, PF, N), K_(W, 2, CH, PF, N), K_(W, 3, CH, PF, N), \
+                          K_(W, 4, CH, PF, N), K_(W, 5, CH, PF, N)
+        const void* sk[] = {KG_(2, 1, true, false),  KG_(4, 1, true, false),  KG_(8, 1, true, false),
+                            KG_(2, 1, false, false), KG_(4, 1, false, false), KG_(8, 1, false, false),
+                            KG_(2, 2, true, false),  KG_(4, 2, true, false),  KG_(2, 2, false, false),
+                            KG_(4, 2, false, false), KG_(2, 1, false, true),  KG_(4, 1, false, true),
+                            KG_(8, 1, false, true)};
 #undef KG_
 #undef K_
         for (const void* k : sk)
@@ -127,6 +130,8 @@ struct Tuning {
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     int stream = 1;         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
+    int stream_order = 0;   //   tile order: 0 grid-stride, 1 contiguous range per workgroup
+    int stream_nib = 0;     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     int stream_pf = 0;      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
 };
@@ -256,24 +261,29 @@ bool stream_offsets(ApplyArgs& a, int64_t bs)
     return true;
 }
 
-template <int W, int CH, bool PF>
+template <int W, int CH, bool PF, bool NIB = false>
 int launch_stream_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st)
 {
     const int kg = (a.ncols + 3) / 4;
     switch (kg) {
-    case 1: hipLaunchKernelGGL((gf16_stream_kernel<W, 1, CH, PF>), grid, block, lds, st, a); break;
-    case 2: hipLaunchKernelGGL((gf16_stream_kernel<W, 2, CH, PF>), grid, block, lds, st, a); break;
-    case 3: hipLaunchKernelGGL((gf16_stream_kernel<W, 3, CH, PF>), grid, block, lds, st, a); break;
-    case 4: hipLaunchKernelGGL((gf16_stream_kernel<W, 4, CH, PF>), grid, block, lds, st, a); break;
-    default: hipLaunchKernelGGL((gf16_stream_kernel<W, 5, CH, PF>), grid, block, lds, st, a); break;
+    case 1: hipLaunchKernelGGL((gf16_stream_kernel<W, 1, CH, PF, NIB>), grid, block, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((gf16_stream_kernel<W, 2, CH, PF, NIB>), grid, block, lds, st, a); break;
+    case 3: hipLaunchKernelGGL((gf16_stream_kernel<W, 3, CH, PF, NIB>), grid, block, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((gf16_stream_kernel<W, 4, CH, PF, NIB>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((gf16_stream_kernel<W, 5, CH, PF, NIB>), grid, block, lds, st, a); break;
     }
     HIP_TRY(hipGetLastError());
     return 0;
 }
 
-int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, dim3 grid, dim3 block, size_t lds,
-                  hipStream_t st)
+int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3 grid, dim3 block,
+                  size_t lds, hipStream_t st)
 {
+    if (nib) {  // a.tables is the nibble image
+        if (width == 2) return launch_stream_w<2, 1, false, true>(a, grid, block, lds, st);
+        if (width == 4) return launch_stream_w<4, 1, false, true>(a, grid, block, lds, st);
+        return launch_stream_w<8, 1, false, true>(a, grid, block, lds, st);
+    }
     if (ch == 2 && width <= 4) {
         if (pf)
             return width == 2 ? launch_stream_w<2, 2, true>(a, grid, block, lds, st)
@@ -322,6 +332,24 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             HIP_TRY(hipGetLastError());
             continue;
         }
+        if (!PTRS && g_tune.nt && !exp && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
+            stream_offsets(a, bs)) {
+            const bool nib = g_tune.stream_nib == 1 || (g_tune.stream_nib == 2 && p.width == 8) ||
+                             (g_tune.nib != 0);
+            const int ch = (p.width <= 4 && !nib) ? g_tune.stream_ch : 1;
+            if (nib) a.tables = map->d_tables + p.nib_offset;
+            // 16 waves per CU (4 x 256 threads, or fewer, larger workgroups when the tables
+            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5
+            rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4);
+            if (rc) return rc;
+            a.ntiles = g.ntiles;
+            a.tiles_per_stripe = g.tiles_per_stripe;
+            a.tile_order = g_tune.stream_order;
+            rc = launch_stream(a, p.width, ch, g_tune.stream_pf != 0, nib, dim3(g.grid),
+                               dim3(g.threads), g.lds, st);
+            if (rc) return rc;
+            continue;
+        }
         if (g_tune.nib) {
             a.tables = map->d_tables + p.nib_offset;
             rc = geometry(map->device, p.nib_bytes, bs, nstripes, g);
@@ -343,18 +371,6 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             continue;
         }
         const bool nt = g_tune.nt != 0;
-        if (!PTRS && nt && g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs)) {
-            const int ch = p.width <= 4 ? g_tune.stream_ch : 1;
-            // 16 waves per CU (4 x 256 threads, or fewer, larger workgroups when the tables
-            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5
-            rc = geometry(map->device, p.bytes, bs, nstripes, g, ch, 1024, 4);
-            if (rc) return rc;
-            a.ntiles = g.ntiles;
-            a.tiles_per_stripe = g.tiles_per_stripe;
-            rc = launch_stream(a, p.width, ch, g_tune.stream_pf != 0, dim3(g.grid), dim3(g.threads), g.lds, st);
-            if (rc) return rc;
-            continue;
-        }
         switch (p.width * 2 + (nt ? 1 : 0)) {
         case 4: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, false, false>), grid, block, g.lds, st, a); break;
         case 5: hipLaunchKernelGGL((gf16_apply_kernel<2, PTRS, true, false>), grid, block, g.lds, st, a); break;
@@ -622,6 +638,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream = value != 0;
     } else if (k == "stream_ch") {
         g_tune.stream_ch = value == 2 ? 2 : 1;
+    } else if (k == "stream_order") {
+        g_tune.stream_order = value != 0;
+    } else if (k == "stream_nib") {
+        g_tune.stream_nib = std::max(0, std::min(value, 2));
     } else if (k == "stream_pf") {
         g_tune.stream_pf = value != 0;
     } else {
@@ -976,6 +996,13 @@ int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void* dst, const 
 int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void* base,
                           int64_t bs, int K, int R, int nstripes, void* stream)
 {
+    return ecamd_debug_mix_probe2(lp, sp, ch, threads, wgs_per_cu, 0, 0, base, bs, K, R, nstripes, stream);
+}
+
+int ecamd_debug_mix_probe2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
+                           int wave_contig, void* base, int64_t bs, int K, int R, int nstripes,
+                           void* stream)
+{
     int dev = 0;
     int rc = ensure_device(&dev);
     if (rc) return rc;
@@ -985,7 +1012,8 @@ int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, v
     const int64_t sstride = bs * (K + R);
     if (K < 1 || R < 0 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
         return fail(ECAMD_EINVAL, "mix probe: bad shape");
-    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0};
+    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0, order != 0,
+              wave_contig != 0};
     a.tiles_per_stripe = static_cast<uint32_t>(bs / span);
     a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     const int grid = static_cast<int>(std::min<int64_t>(a.ntiles,

@@ -320,13 +320,50 @@ __device__ __forceinline__ void mac_chunk_imm(const uint8_t* lds, v4u x, uint32_
     }
 }
 
-template <int W, int CH, int J>
+// Nibble tables (host/tables.cpp build_nibble_tables: per input 4 tables of 16 entries, table q
+// for bits 4q..4q+3 of the word).  A 16-entry table of EB-byte entries spans 16*EB <= 256 bytes,
+// one LDS bank row, so no lookup ever conflicts -- at twice the lookups of the byte tables.  The
+// nibbles of a data dword are moved to scaled-index position once (L: low nibbles, H: high
+// nibbles, each times EB), each lookup address is then one byte extract, the table base a
+// compile-time offset.
+template <int W, int J>
+__device__ __forceinline__ void mac_chunk_nib_imm(const uint8_t* lds, v4u x, uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    constexpr int S = log2i(EB);
+    constexpr uint32_t M = 0x0f0f0f0fu << S;
+    constexpr int T = J * 64 * EB;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t L = (x[i] << S) & M;
+        const uint32_t H = (S >= 4 ? (x[i] << (S - 4)) : (x[i] >> (4 - S))) & M;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {  // word 2i+h = bytes 2h (bits 0-7), 2h+1 (bits 8-15)
+            uint32_t e0[D], e1[D], e2[D], e3[D];
+            lds_entry<D>(lds + T + 0 * 16 * EB + ((L >> (16 * h)) & 0xffu), e0);
+            lds_entry<D>(lds + T + 1 * 16 * EB + ((H >> (16 * h)) & 0xffu), e1);
+            lds_entry<D>(lds + T + 2 * 16 * EB + ((L >> (16 * h + 8)) & 0xffu), e2);
+            lds_entry<D>(lds + T + 3 * 16 * EB + ((H >> (16 * h + 8)) & 0xffu), e3);
+#pragma unroll
+            for (int d = 0; d < D; d++)
+                acc[2 * i + h][d] = xor3(xor3(acc[2 * i + h][d], e0[d], e1[d]), e2[d], e3[d]);
+        }
+    }
+}
+
+template <int W, int CH, int J, bool NIB>
 __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds, const v4u (&x)[CH],
                                           uint32_t (&acc)[CH][8][W / 2])
 {
     if (J < a.ncols) {  // wave-uniform
 #pragma unroll
-        for (int c = 0; c < CH; c++) mac_chunk_imm<W, J>(lds, x[c], acc[c]);
+        for (int c = 0; c < CH; c++) {
+            if constexpr (NIB)
+                mac_chunk_nib_imm<W, J>(lds, x[c], acc[c]);
+            else
+                mac_chunk_imm<W, J>(lds, x[c], acc[c]);
+        }
     }
 }
 
@@ -346,43 +383,49 @@ __device__ __forceinline__ void load_group(const ApplyArgs& a, __amdgpu_buffer_r
 
 // Group G's lookups; with PF the loads of group G+1 are issued before them (in flight during the
 // lookups), without PF after them (each wave: load, wait, look up -- latency hidden by occupancy).
-template <int W, int CH, int G, int KG, bool PF>
+template <int W, int CH, int G, int KG, bool PF, bool NIB>
 __device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* lds,
                                              __amdgpu_buffer_rsrc_t rin, int off, int cstride,
                                              v4u (&cur)[4][CH], uint32_t (&acc)[CH][8][W / 2])
 {
     v4u nxt[4][CH];
     if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG>(a, rin, off, cstride, nxt);
-    input_mac<W, CH, 4 * G + 0>(a, lds, cur[0], acc);
-    input_mac<W, CH, 4 * G + 1>(a, lds, cur[1], acc);
-    input_mac<W, CH, 4 * G + 2>(a, lds, cur[2], acc);
-    input_mac<W, CH, 4 * G + 3>(a, lds, cur[3], acc);
+    input_mac<W, CH, 4 * G + 0, NIB>(a, lds, cur[0], acc);
+    input_mac<W, CH, 4 * G + 1, NIB>(a, lds, cur[1], acc);
+    input_mac<W, CH, 4 * G + 2, NIB>(a, lds, cur[2], acc);
+    input_mac<W, CH, 4 * G + 3, NIB>(a, lds, cur[3], acc);
     if constexpr (G + 1 < KG) {
         if constexpr (!PF) load_group<W, CH, G + 1, KG>(a, rin, off, cstride, nxt);
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
-        stream_group<W, CH, G + 1, KG, PF>(a, lds, rin, off, cstride, cur, acc);
+        stream_group<W, CH, G + 1, KG, PF, NIB>(a, lds, rin, off, cstride, cur, acc);
     }
 }
 
 }  // namespace
 
-template <int W, int KG, int CH, bool PF>
+template <int W, int KG, int CH, bool PF, bool NIB>
 __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int D = W / 2;
     constexpr int EB = 2 * W;
-    const int tbytes = a.ncols * 512 * EB;
+    const int tbytes = a.ncols * (NIB ? 64 : 512) * EB;
     for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
         *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
     __syncthreads();
 
     const int cstride = static_cast<int>(blockDim.x) * 16;
     const int64_t span = static_cast<int64_t>(cstride) * CH;
-    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    // tile_order 1: each workgroup walks its own contiguous range of tiles (a long sequential
+    // run through each fragment); 0: tiles strided over the grid.
+    const uint32_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+    const uint32_t t0 = a.tile_order ? blockIdx.x * per : blockIdx.x;
+    const uint32_t t1 = a.tile_order ? min(a.ntiles, t0 + per) : a.ntiles;
+    const uint32_t dt = a.tile_order ? 1u : gridDim.x;
+    for (uint32_t t = t0; t < t1; t += dt) {
         const uint32_t s = t / a.tiles_per_stripe;
         const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
         if (toff + span > a.bs) {  // last, partial tile of each fragment
@@ -391,9 +434,9 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
                 const int64_t o = toff + c * cstride + static_cast<int64_t>(threadIdx.x) * 16;
                 const int64_t rem = a.bs - o;
                 if (rem >= 16)
-                    apply_tile<W, false, true, false, false, false>(a, lds, s, o, 16);
+                    apply_tile<W, false, true, NIB, false, false>(a, lds, s, o, 16);
                 else if (rem > 0)
-                    apply_tile<W, false, true, false, false, true>(a, lds, s, o, static_cast<int>(rem));
+                    apply_tile<W, false, true, NIB, false, true>(a, lds, s, o, static_cast<int>(rem));
             }
             continue;
         }
@@ -414,7 +457,7 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
                 for (int d = 0; d < D; d++) acc[c][w][d] = 0u;
         v4u cur[4][CH];
         load_group<W, CH, 0, KG>(a, rin, off, cstride, cur);
-        stream_group<W, CH, 0, KG, PF>(a, lds, rin, off, cstride, cur, acc);
+        stream_group<W, CH, 0, KG, PF, NIB>(a, lds, rin, off, cstride, cur, acc);
 
 #pragma unroll
         for (int r = 0; r < W; r++) {
@@ -435,15 +478,17 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
     }
 }
 
-#define ECAMD_STREAM_INST(W, KG, CH, PF) \
-    template __global__ void gf16_stream_kernel<W, KG, CH, PF>(const ApplyArgs);
-#define ECAMD_STREAM_KG(W, CH, PF)                                                                  \
-    ECAMD_STREAM_INST(W, 1, CH, PF) ECAMD_STREAM_INST(W, 2, CH, PF) ECAMD_STREAM_INST(W, 3, CH, PF) \
-    ECAMD_STREAM_INST(W, 4, CH, PF) ECAMD_STREAM_INST(W, 5, CH, PF)
-ECAMD_STREAM_KG(2, 1, true) ECAMD_STREAM_KG(4, 1, true) ECAMD_STREAM_KG(8, 1, true)
-ECAMD_STREAM_KG(2, 1, false) ECAMD_STREAM_KG(4, 1, false) ECAMD_STREAM_KG(8, 1, false)
-ECAMD_STREAM_KG(2, 2, true) ECAMD_STREAM_KG(4, 2, true)
-ECAMD_STREAM_KG(2, 2, false) ECAMD_STREAM_KG(4, 2, false)
+#define ECAMD_STREAM_INST(W, KG, CH, PF, NIB) \
+    template __global__ void gf16_stream_kernel<W, KG, CH, PF, NIB>(const ApplyArgs);
+#define ECAMD_STREAM_KG(W, CH, PF, NIB)                                                   \
+    ECAMD_STREAM_INST(W, 1, CH, PF, NIB) ECAMD_STREAM_INST(W, 2, CH, PF, NIB)             \
+    ECAMD_STREAM_INST(W, 3, CH, PF, NIB) ECAMD_STREAM_INST(W, 4, CH, PF, NIB)             \
+    ECAMD_STREAM_INST(W, 5, CH, PF, NIB)
+ECAMD_STREAM_KG(2, 1, true, false) ECAMD_STREAM_KG(4, 1, true, false) ECAMD_STREAM_KG(8, 1, true, false)
+ECAMD_STREAM_KG(2, 1, false, false) ECAMD_STREAM_KG(4, 1, false, false) ECAMD_STREAM_KG(8, 1, false, false)
+ECAMD_STREAM_KG(2, 2, true, false) ECAMD_STREAM_KG(4, 2, true, false)
+ECAMD_STREAM_KG(2, 2, false, false) ECAMD_STREAM_KG(4, 2, false, false)
+ECAMD_STREAM_KG(2, 1, false, true) ECAMD_STREAM_KG(4, 1, false, true) ECAMD_STREAM_KG(8, 1, false, true)
 #undef ECAMD_STREAM_KG
 #undef ECAMD_STREAM_INST
 

@@ -33,6 +33,7 @@ struct ApplyArgs {
     uint32_t out_records;             //   in_base / out_base (buffer-resource range, < 2^31)
     int32_t in_off32[kMaxCols];       // in_off / out_off as 32-bit buffer offsets
     int32_t out_off32[kMaxRows];
+    int tile_order;                   // gf16_stream_kernel: 1 = contiguous tile range per workgroup
 };
 
 // gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).
@@ -53,7 +54,7 @@ template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
 template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);
-template <int W, int KG, int CH, bool PF>
+template <int W, int KG, int CH, bool PF, bool NIB>
 __global__ void gf16_stream_kernel(const ApplyArgs a);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
@@ -67,6 +68,8 @@ struct MixArgs {
     int K, R;
     uint32_t ntiles;
     uint32_t tiles_per_stripe;
+    int order;        // 0: grid-stride tile order, 1: contiguous tile range per workgroup
+    int wave_contig;  // 1: a wave's CH chunks are contiguous (1 KiB apart)
 };
 
 // (load policy, store policy) pairs instantiated for mix_probe_kernel; gfx950 cpol bits

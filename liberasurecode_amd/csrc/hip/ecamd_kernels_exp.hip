@@ -195,11 +195,21 @@ template <int LP, int SP, int CH>
 __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
 {
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
-    const int cstride = static_cast<int>(blockDim.x) * 16;
-    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    // wave_contig: each wave covers CH KiB of a fragment contiguously (chunks 1 KiB apart);
+    // otherwise the chunks of a lane are blockDim*16 bytes apart.  order 1: every workgroup
+    // walks a contiguous range of tiles instead of striding over the grid.
+    const int cstride = a.wave_contig ? 1024 : static_cast<int>(blockDim.x) * 16;
+    const int lane_off = a.wave_contig
+                             ? static_cast<int>(threadIdx.x / 64) * 1024 * CH + static_cast<int>(threadIdx.x % 64) * 16
+                             : static_cast<int>(threadIdx.x) * 16;
+    const uint32_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+    const uint32_t t0 = a.order ? blockIdx.x * per : blockIdx.x;
+    const uint32_t t1 = a.order ? min(a.ntiles, t0 + per) : a.ntiles;
+    const uint32_t dt = a.order ? 1u : gridDim.x;
+    for (uint32_t t = t0; t < t1; t += dt) {
         const uint32_t s = t / a.tiles_per_stripe;
-        const int off = static_cast<int>(t - s * a.tiles_per_stripe) * cstride * CH +
-                        static_cast<int>(threadIdx.x) * 16;
+        const int off = static_cast<int>(t - s * a.tiles_per_stripe) * static_cast<int>(blockDim.x) * 16 * CH +
+                        lane_off;
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
             a.base + static_cast<int64_t>(s) * a.stripe_stride, 0,
             static_cast<int>(a.stripe_stride), 0x00020000);

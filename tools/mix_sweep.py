@@ -31,13 +31,15 @@ def main():
     ap.add_argument("--S", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--geoms", default="256x4,512x2,1024x1")
+    ap.add_argument("--policies", default="")
+    ap.add_argument("--layouts", default="0x0", help="order x wave_contig pairs")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "mix_sweep.jsonl"))
     args = ap.parse_args()
     k, m, F, S = args.k, args.m, args.F, args.S
     C = _lib.C
     d = _lib.dev()
-    d.ecamd_debug_mix_probe.argtypes = [C.c_int] * 5 + [_lib.VP, C.c_int64, C.c_int, C.c_int,
-                                                         C.c_int, _lib.VP]
+    d.ecamd_debug_mix_probe2.argtypes = [C.c_int] * 7 + [_lib.VP, C.c_int64, C.c_int, C.c_int,
+                                                          C.c_int, _lib.VP]
     lay = D.Layout.alloc(k + m, F, S)
     st = D.Stream()
     lay.fill_splitmix(nfrags=k, stream=st)
@@ -45,13 +47,18 @@ def main():
 
     variants = {}
     geoms = [tuple(int(x) for x in g.split("x")) for g in args.geoms.split(",")]
-    for lp, sp in POLICIES:
+    pols = POLICIES if not args.policies else [tuple(int(x) for x in p.split("/"))
+                                               for p in args.policies.split(",")]
+    lays = [tuple(int(x) for x in p.split("x")) for p in args.layouts.split(",")]
+    for lp, sp in pols:
         for ch in (1, 2):
             for threads, wgs in geoms:
-                def fn(lp=lp, sp=sp, ch=ch, threads=threads, wgs=wgs):
-                    _lib.check(d.ecamd_debug_mix_probe(lp, sp, ch, threads, wgs, lay.buf.ptr, F, k, m,
-                                                       S, st.handle), "mix probe")
-                variants[f"mix_l{lp}_s{sp}_ch{ch}_t{threads}_w{wgs}"] = fn
+                for order, wc in lays:
+                    def fn(lp=lp, sp=sp, ch=ch, threads=threads, wgs=wgs, order=order, wc=wc):
+                        _lib.check(d.ecamd_debug_mix_probe2(lp, sp, ch, threads, wgs, order, wc,
+                                                            lay.buf.ptr, F, k, m, S, st.handle),
+                                   "mix probe")
+                    variants[f"mix_l{lp}_s{sp}_ch{ch}_t{threads}_w{wgs}_o{order}_wc{wc}"] = fn
 
     def enc():
         D.rs_encode(k, m, lay, stream=st)

@@ -21,14 +21,14 @@ CFGS = {"c3": (10, 4, 1 << 20, 256, [0, 1, 2, 3]),
         "c5": (20, 8, 4 << 20, 32, list(range(8)))}
 
 
-VARIANTS = [(0, 1, 0), (1, 1, 0), (1, 2, 0), (1, 1, 1)]
+VARIANTS = [(0, 1, 0, 0, 0), (1, 1, 0, 0, 0), (1, 1, 0, 0, 1), (1, 2, 0, 0, 1)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", default="c3,c5,c2")
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--geoms", default="0x0,256x4,512x2,1024x1")
+    ap.add_argument("--geoms", default="0x0,512x2")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stream_sweep.jsonl"))
     args = ap.parse_args()
     d = _lib.dev()
@@ -41,8 +41,10 @@ def main():
         lay.fill_splitmix(nfrags=k, stream=st)
         algo = S * (k + m) * F
 
-        def setk(stream, ch, pf, threads, wgs):
+        def setk(stream, ch, pf, nib, order, threads, wgs):
+            d.ecamd_tune(b"stream_order", order)
             d.ecamd_tune(b"stream", stream)
+            d.ecamd_tune(b"stream_nib", nib)
             d.ecamd_tune(b"stream_ch", ch)
             d.ecamd_tune(b"stream_pf", pf)
             d.ecamd_tune(b"threads", threads)
@@ -50,12 +52,12 @@ def main():
 
         variants = {}
         for (threads, wgs) in geoms:
-            for (stream, ch, pf) in VARIANTS:
+            for (stream, ch, pf, nib, order) in VARIANTS:
                 if stream == 0 and (threads, wgs) != (0, 0):
                     continue
-                tag = f"{cfg}_{'old' if not stream else f'st_ch{ch}_pf{pf}'}_t{threads}_w{wgs}"
+                tag = f"{cfg}_{'old' if not stream else f'st_ch{ch}_pf{pf}_nib{nib}_o{order}'}_t{threads}_w{wgs}"
                 for op in ("enc", "dec"):
-                    def fn(op=op, a=(stream, ch, pf, threads, wgs)):
+                    def fn(op=op, a=(stream, ch, pf, nib, order, threads, wgs)):
                         setk(*a)
                         if op == "enc":
                             D.rs_encode(k, m, lay, stream=st)
@@ -63,7 +65,7 @@ def main():
                             D.rs_decode(k, m, miss, lay, stream=st)
                     variants[f"{op}_{tag}"] = fn
         # correctness: every variant reproduces the old kernel's encode and decode output
-        setk(0, 1, 0, 0, 0)
+        setk(0, 1, 0, 0, 0, 0, 0)
         D.rs_encode(k, m, lay, stream=st)
         st.synchronize()
         ref = lay.buf.download(lay.stripe_stride * min(S, 4))
@@ -72,7 +74,7 @@ def main():
             lay.buf.zero()
             lay.fill_splitmix(nfrags=k, stream=st)
             if name.startswith("dec"):
-                setk(0, 1, 0, 0, 0)
+                setk(0, 1, 0, 0, 0, 0, 0)
                 D.rs_encode(k, m, lay, stream=st)
             fn()
             st.synchronize()
@@ -99,7 +101,7 @@ def main():
             out.write(json.dumps(r) + "\n")
             print(json.dumps(r), flush=True)
         lay.buf.free()
-        setk(1, 1, 0, 0, 0)
+        setk(1, 1, 0, 0, 0, 0, 0)
 
 
 if __name__ == "__main__":
