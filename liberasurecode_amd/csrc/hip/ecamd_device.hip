@@ -130,6 +130,8 @@ struct Tuning {
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     int stream = 1;         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
+    int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
+                            // measured best, tools/xor_sweep.py)
     int stream_order = 0;   //   tile order: 0 grid-stride, 1 contiguous range per workgroup
     int stream_nib = 0;     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     int stream_pf = 0;      //   next group's loads issued before the lookups (1) or after (0);
@@ -258,6 +260,22 @@ bool stream_offsets(ApplyArgs& a, int64_t bs)
     for (int r = 0; r < a.nrows; r++) a.out_off32[r] = static_cast<int32_t>(a.out_off[r]);
     a.in_records = static_cast<uint32_t>(in_max);
     a.out_records = static_cast<uint32_t>(out_max);
+    return true;
+}
+
+// Copy-through offsets for gf16_stream_kernel (framed encode / decode-join): every non-skipped
+// copy destination must be addressable as a 32-bit offset from the stripe's copy_base.
+bool stream_copy_offsets(ApplyArgs& a, int64_t bs)
+{
+    int64_t mx = 0;
+    for (int j = 0; j < a.ncols; j++) {
+        if (a.copy_off[j] < 0) continue;
+        mx = std::max(mx, a.copy_off[j] + bs);
+    }
+    if (mx >= (int64_t(1) << 31)) return false;
+    for (int j = 0; j < a.ncols; j++)
+        a.copy_off32[j] = a.copy_off[j] < 0 ? -1 : static_cast<int32_t>(a.copy_off[j]);
+    a.copy_records = static_cast<uint32_t>(std::max<int64_t>(mx, 16));
     return true;
 }
 
@@ -407,8 +425,22 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             if (rc) return rc;
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
-            hipLaunchKernelGGL((xor_apply_kernel<8, PTRS>), dim3(g.grid), dim3(g.threads), 0, st,
-                               a);
+            if (!PTRS && g_tune.stream && stream_offsets(a, bs)) {
+                // geometry: 256 threads, xor_wgs (default 4) workgroups per CU
+                const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : 2;
+                g.grid = static_cast<int>(std::min<int64_t>(g.ntiles, static_cast<int64_t>(cu_count(dev)) * wgs));
+                const dim3 grid(std::max(g.grid, 1)), block(g.threads);
+                switch ((a.ncols + 3) / 4) {
+                case 1: hipLaunchKernelGGL((xor_stream_kernel<1>), grid, block, 0, st, a); break;
+                case 2: hipLaunchKernelGGL((xor_stream_kernel<2>), grid, block, 0, st, a); break;
+                case 3: hipLaunchKernelGGL((xor_stream_kernel<3>), grid, block, 0, st, a); break;
+                case 4: hipLaunchKernelGGL((xor_stream_kernel<4>), grid, block, 0, st, a); break;
+                default: hipLaunchKernelGGL((xor_stream_kernel<8>), grid, block, 0, st, a); break;
+                }
+            } else {
+                hipLaunchKernelGGL((xor_apply_kernel<8, PTRS>), dim3(g.grid), dim3(g.threads), 0, st,
+                                   a);
+            }
             HIP_TRY(hipGetLastError());
         }
     }
@@ -527,7 +559,20 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         }
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
         Geometry g;
-        int rc = geometry(map->device, p.bytes, bs, nstripes, g);
+        int rc;
+        if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs) &&
+            (p.row0 != 0 || stream_copy_offsets(a, bs))) {
+            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4);
+            if (rc) return rc;
+            a.ntiles = g.ntiles;
+            a.tiles_per_stripe = g.tiles_per_stripe;
+            a.tile_order = g_tune.stream_order;
+            rc = launch_stream(a, p.width, 1, g_tune.stream_pf != 0, false, dim3(g.grid),
+                               dim3(g.threads), g.lds, st);
+            if (rc) return rc;
+            continue;
+        }
+        rc = geometry(map->device, p.bytes, bs, nstripes, g);
         if (rc) return rc;
         a.ntiles = g.ntiles;
         a.tiles_per_stripe = g.tiles_per_stripe;
@@ -638,6 +683,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream = value != 0;
     } else if (k == "stream_ch") {
         g_tune.stream_ch = value == 2 ? 2 : 1;
+    } else if (k == "xor_wgs") {
+        g_tune.xor_wgs = std::max(0, std::min(value, 8));
     } else if (k == "stream_order") {
         g_tune.stream_order = value != 0;
     } else if (k == "stream_nib") {

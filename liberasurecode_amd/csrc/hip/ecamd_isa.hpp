@@ -14,6 +14,14 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
+// a ^ (b & c) in one VALU op (v_bitop3_b32, truth table 0x78): masked accumulate.
+__device__ __forceinline__ uint32_t xor_and(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+
 // (byte K of v) << S in one VALU op: v_lshlrev_b32 with an SDWA byte-select source.  Given a
 // shift-and-mask instead, the compiler re-fuses it into two ops.
 template <int K, int S>

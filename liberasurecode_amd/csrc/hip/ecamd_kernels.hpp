@@ -33,6 +33,8 @@ struct ApplyArgs {
     uint32_t out_records;             //   in_base / out_base (buffer-resource range, < 2^31)
     int32_t in_off32[kMaxCols];       // in_off / out_off as 32-bit buffer offsets
     int32_t out_off32[kMaxRows];
+    uint32_t copy_records;            // gf16_stream_kernel copy-through: 0 = off; else range of
+    int32_t copy_off32[kMaxCols];     //   copy_base per stripe and 32-bit copy_off (< 0: skip)
     int tile_order;                   // gf16_stream_kernel: 1 = contiguous tile range per workgroup
 };
 
@@ -60,6 +62,8 @@ template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);
+template <int KG>
+__global__ void xor_stream_kernel(const ApplyArgs a);
 __global__ void splitmix_fill_kernel(FillArgs f);
 struct MixArgs {
     uint8_t* base;

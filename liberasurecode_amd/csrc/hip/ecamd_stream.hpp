@@ -1,0 +1,242 @@
+// ecamd_stream.hpp -- gf16_stream_kernel, the strided GF(2^16) apply used for every strided launch
+// that fits it (definition; instantiated per output width in ecamd_stream_w{2,4,8}.hip so the
+// variants compile in parallel).
+#pragma once
+#include "ecamd_apply.hpp"
+
+namespace ecamd {
+
+// ------------------------------------------------------------ streaming form ----
+// gf16_stream_kernel<W, KG, CH, PF>: the strided gf16 apply for up to 4*KG inputs, written so the
+// HBM stream never stalls behind the table work:
+//   * buffer loads/stores on one resource per stripe (32-bit offsets, no 64-bit address math);
+//     the loads of a group of 4 inputs are unconditional -- an input index past ncols gets an
+//     out-of-range offset, which the buffer unit answers with zeros and no memory traffic -- so
+//     the code is straight-line and the next group's loads stay in flight (counted vmcnt) while
+//     the current group's lookups run;
+//   * inputs fully unrolled: each input's table base is a compile-time LDS offset and each
+//     table index one SDWA byte-select shift (byte_shl), i.e. one VALU op per lookup;
+//   * CH 16-byte chunks per lane per fragment (blockDim*16 bytes apart): CH*1 KiB per wave per
+//     fragment in one tile;
+//   * PF: the next group's loads issued before (true) or after (false) this group's lookups.
+// Partial tiles at the end of a fragment go through apply_tile's byte-exact tail code.
+namespace {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <int W, int J>
+__device__ __forceinline__ void mac_chunk_imm(const uint8_t* lds, v4u x, uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    constexpr int S = log2i(EB);
+    constexpr int TL = J * 512 * EB;
+    constexpr int TH = TL + 256 * EB;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const uint32_t v = x[w >> 1];
+        uint32_t e0[D], e1[D];
+        if (w & 1) {
+            lds_entry<D>(lds + TL + byte_shl<2, S>(v), e0);
+            lds_entry<D>(lds + TH + byte_shl<3, S>(v), e1);
+        } else {
+            lds_entry<D>(lds + TL + byte_shl<0, S>(v), e0);
+            lds_entry<D>(lds + TH + byte_shl<1, S>(v), e1);
+        }
+#pragma unroll
+        for (int d = 0; d < D; d++) acc[w][d] = xor3(acc[w][d], e0[d], e1[d]);
+    }
+}
+
+// Nibble tables (host/tables.cpp build_nibble_tables: per input 4 tables of 16 entries, table q
+// for bits 4q..4q+3 of the word).  A 16-entry table of EB-byte entries spans 16*EB <= 256 bytes,
+// one LDS bank row, so no lookup ever conflicts -- at twice the lookups of the byte tables.  The
+// nibbles of a data dword are moved to scaled-index position once (L: low nibbles, H: high
+// nibbles, each times EB), each lookup address is then one byte extract, the table base a
+// compile-time offset.
+template <int W, int J>
+__device__ __forceinline__ void mac_chunk_nib_imm(const uint8_t* lds, v4u x, uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    constexpr int S = log2i(EB);
+    constexpr uint32_t M = 0x0f0f0f0fu << S;
+    constexpr int T = J * 64 * EB;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t L = (x[i] << S) & M;
+        const uint32_t H = (S >= 4 ? (x[i] << (S - 4)) : (x[i] >> (4 - S))) & M;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {  // word 2i+h = bytes 2h (bits 0-7), 2h+1 (bits 8-15)
+            uint32_t e0[D], e1[D], e2[D], e3[D];
+            lds_entry<D>(lds + T + 0 * 16 * EB + ((L >> (16 * h)) & 0xffu), e0);
+            lds_entry<D>(lds + T + 1 * 16 * EB + ((H >> (16 * h)) & 0xffu), e1);
+            lds_entry<D>(lds + T + 2 * 16 * EB + ((L >> (16 * h + 8)) & 0xffu), e2);
+            lds_entry<D>(lds + T + 3 * 16 * EB + ((H >> (16 * h + 8)) & 0xffu), e3);
+#pragma unroll
+            for (int d = 0; d < D; d++)
+                acc[2 * i + h][d] = xor3(xor3(acc[2 * i + h][d], e0[d], e1[d]), e2[d], e3[d]);
+        }
+    }
+}
+
+// Per-tile addressing shared by the helpers below: the input and copy-through resources of the
+// stripe, this lane's byte offset in a fragment and the distance between its chunks.
+struct StreamTile {
+    __amdgpu_buffer_rsrc_t rin;
+    __amdgpu_buffer_rsrc_t rcopy;
+    int off;
+    int cstride;
+};
+
+template <int W, int CH, int J, bool NIB>
+__device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds, const StreamTile& t,
+                                          const v4u (&x)[CH], uint32_t (&acc)[CH][8][W / 2])
+{
+    if (J < a.ncols) {  // wave-uniform
+        if (a.copy_records && a.copy_off32[J] >= 0) {  // copy-through: input J also lands in its slot
+#pragma unroll
+            for (int c = 0; c < CH; c++)
+                __builtin_amdgcn_raw_buffer_store_b128(x[c], t.rcopy, a.copy_off32[J] + t.off + c * t.cstride,
+                                                       0, 2);
+        }
+#pragma unroll
+        for (int c = 0; c < CH; c++) {
+            if constexpr (NIB)
+                mac_chunk_nib_imm<W, J>(lds, x[c], acc[c]);
+            else
+                mac_chunk_imm<W, J>(lds, x[c], acc[c]);
+        }
+    }
+}
+
+template <int W, int CH, int G, int KG>
+__device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile& t, v4u (&x)[4][CH])
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int j = 4 * G + i;
+        const int base = (j < a.ncols) ? a.in_off32[j] + t.off : static_cast<int>(0x80000000u);
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+            x[i][c] = __builtin_amdgcn_raw_buffer_load_b128(t.rin, base + c * t.cstride, 0, 2);
+    }
+}
+
+// Group G's lookups; with PF the loads of group G+1 are issued before them (in flight during the
+// lookups), without PF after them (each wave: load, wait, look up -- latency hidden by occupancy).
+template <int W, int CH, int G, int KG, bool PF, bool NIB>
+__device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* lds, const StreamTile& t,
+                                             v4u (&cur)[4][CH], uint32_t (&acc)[CH][8][W / 2])
+{
+    v4u nxt[4][CH];
+    if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG>(a, t, nxt);
+    input_mac<W, CH, 4 * G + 0, NIB>(a, lds, t, cur[0], acc);
+    input_mac<W, CH, 4 * G + 1, NIB>(a, lds, t, cur[1], acc);
+    input_mac<W, CH, 4 * G + 2, NIB>(a, lds, t, cur[2], acc);
+    input_mac<W, CH, 4 * G + 3, NIB>(a, lds, t, cur[3], acc);
+    if constexpr (G + 1 < KG) {
+        if constexpr (!PF) load_group<W, CH, G + 1, KG>(a, t, nxt);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
+        stream_group<W, CH, G + 1, KG, PF, NIB>(a, lds, t, cur, acc);
+    }
+}
+
+}  // namespace
+
+template <int W, int KG, int CH, bool PF, bool NIB>
+__global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    const int tbytes = a.ncols * (NIB ? 64 : 512) * EB;
+    for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
+        *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
+    __syncthreads();
+
+    const int cstride = static_cast<int>(blockDim.x) * 16;
+    const int64_t span = static_cast<int64_t>(cstride) * CH;
+    // tile_order 1: each workgroup walks its own contiguous range of tiles (a long sequential
+    // run through each fragment); 0: tiles strided over the grid.
+    const uint32_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+    const uint32_t t0 = a.tile_order ? blockIdx.x * per : blockIdx.x;
+    const uint32_t t1 = a.tile_order ? min(a.ntiles, t0 + per) : a.ntiles;
+    const uint32_t dt = a.tile_order ? 1u : gridDim.x;
+    for (uint32_t t = t0; t < t1; t += dt) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
+        if (toff + span > a.bs) {  // last, partial tile of each fragment
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                const int64_t o = toff + c * cstride + static_cast<int64_t>(threadIdx.x) * 16;
+                const int64_t rem = a.bs - o;
+                if (a.copy_records) {  // copy-through launches (framed encode / decode-join)
+                    if (rem >= 16)
+                        apply_tile<W, false, true, NIB, true, false>(a, lds, s, o, 16);
+                    else if (rem > 0)
+                        apply_tile<W, false, true, NIB, true, true>(a, lds, s, o, static_cast<int>(rem));
+                } else if (rem >= 16) {
+                    apply_tile<W, false, true, NIB, false, false>(a, lds, s, o, 16);
+                } else if (rem > 0) {
+                    apply_tile<W, false, true, NIB, false, true>(a, lds, s, o, static_cast<int>(rem));
+                }
+            }
+            continue;
+        }
+        const int off = static_cast<int>(toff) + static_cast<int>(threadIdx.x) * 16;
+        StreamTile tile;
+        tile.rin = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(a.in_base) + static_cast<int64_t>(s) * a.in_stride, 0,
+            static_cast<int>(a.in_records), 0x00020000);
+        tile.rcopy = __builtin_amdgcn_make_buffer_rsrc(
+            a.copy_base + static_cast<int64_t>(s) * a.copy_stride, 0, static_cast<int>(a.copy_records),
+            0x00020000);
+        tile.off = off;
+        tile.cstride = cstride;
+        const auto rout = __builtin_amdgcn_make_buffer_rsrc(
+            a.out_base + static_cast<int64_t>(s) * a.out_stride, 0, static_cast<int>(a.out_records),
+            0x00020000);
+
+        uint32_t acc[CH][8][D];
+#pragma unroll
+        for (int c = 0; c < CH; c++)
+#pragma unroll
+            for (int w = 0; w < 8; w++)
+#pragma unroll
+                for (int d = 0; d < D; d++) acc[c][w][d] = 0u;
+        v4u cur[4][CH];
+        load_group<W, CH, 0, KG>(a, tile, cur);
+        stream_group<W, CH, 0, KG, PF, NIB>(a, lds, tile, cur, acc);
+
+#pragma unroll
+        for (int r = 0; r < W; r++) {
+            if (r >= a.nrows) break;
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                v4u v;
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const uint32_t A = acc[c][2 * d][r >> 1], B = acc[c][2 * d + 1][r >> 1];
+                    v[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+                }
+                const int o = a.out_off32[r] + off + c * cstride;
+                if (a.accumulate) v ^= __builtin_amdgcn_raw_buffer_load_b128(rout, o, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(v, rout, o, 0, 2);  // nt
+            }
+        }
+    }
+}
+
+
+}  // namespace ecamd
+
+#define ECAMD_STREAM_INST(W, KG, CH, PF, NIB) \
+    template __global__ void ecamd::gf16_stream_kernel<W, KG, CH, PF, NIB>(const ecamd::ApplyArgs);
+#define ECAMD_STREAM_KG(W, CH, PF, NIB)                                                   \
+    ECAMD_STREAM_INST(W, 1, CH, PF, NIB) ECAMD_STREAM_INST(W, 2, CH, PF, NIB)             \
+    ECAMD_STREAM_INST(W, 3, CH, PF, NIB) ECAMD_STREAM_INST(W, 4, CH, PF, NIB)             \
+    ECAMD_STREAM_INST(W, 5, CH, PF, NIB)

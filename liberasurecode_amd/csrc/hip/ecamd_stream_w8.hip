@@ -1,0 +1,6 @@
+// ecamd_stream_w8.hip -- gf16_stream_kernel instantiations for 8-output passes.
+#include "ecamd_stream.hpp"
+
+ECAMD_STREAM_KG(8, 1, false, false)
+ECAMD_STREAM_KG(8, 1, true, false)
+ECAMD_STREAM_KG(8, 1, false, true)
