@@ -426,7 +426,7 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
             if (!PTRS && g_tune.stream && stream_offsets(a, bs)) {
-                // geometry: 256 threads, xor_wgs (default 4) workgroups per CU
+                // geometry: 256 threads, xor_wgs (default 2) workgroups per CU
                 const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : 2;
                 g.grid = static_cast<int>(std::min<int64_t>(g.ntiles, static_cast<int64_t>(cu_count(dev)) * wgs));
                 const dim3 grid(std::max(g.grid, 1)), block(g.threads);
