@@ -306,3 +306,54 @@ def test_scatter_fragments_single_device():
         assert (got == src[:, i]).all(), i
     assert f(lay.buf.ptr, lay.stripe_stride, lay.frag_stride, bs, 1, S, _lib.ints([7]),
              (C.c_void_p * 1)(dsts[0].ptr), _lib.i64s([strides[0]]), None) != 0
+
+
+# ------------------------------------------- stream kernels vs the first-version kernels ----
+
+@pytest.fixture
+def tune():
+    d = _lib.dev()
+    yield d.ecamd_tune
+    for key, val in ((b"stream", 1), (b"stream_ch", 1), (b"stream_pf", 0), (b"stream_nib", 0),
+                     (b"stream_order", 0), (b"xor_wgs", 0)):
+        d.ecamd_tune(key, val)
+
+
+@pytest.mark.parametrize("R,K", [(1, 1), (2, 4), (2, 5), (4, 10), (4, 13), (7, 16), (8, 20), (3, 21)])
+@pytest.mark.parametrize("variant", [(b"stream", 0), (b"stream", 1), (b"stream_pf", 1),
+                                     (b"stream_nib", 1), (b"stream_ch", 2), (b"stream_order", 1)])
+def test_stream_kernel_variants(tune, R, K, variant):
+    """Every gf16 kernel variant (the stream kernel and its tuning knobs, the first-version kernel,
+    K = 21 falling back to it) against the numpy GF(2^16) reference on full 4 KiB tiles plus a
+    ragged tail, 3 stripes."""
+    tune(*variant)
+    bs = 3 * 4096 + 48
+    rng = np.random.default_rng(R * 100 + K)
+    coeff = rng.integers(0, 65536, size=(R, K))
+    frags = rng.integers(0, 256, size=(3, K + R, bs), dtype=np.uint8)
+    lay = _upload(frags)
+    D.GF16Map(coeff).apply(lay, list(range(K)), list(range(K, K + R)))
+    out = lay.download_stripes()
+    for s in range(3):
+        want = gfnp.apply_map(coeff, [frags[s, j] for j in range(K)])
+        for r in range(R):
+            assert (out[s, K + r] == want[r]).all(), (s, r)
+
+
+@pytest.mark.parametrize("K", [1, 3, 4, 7, 12, 17, 32])
+@pytest.mark.parametrize("stream", [0, 1])
+def test_xor_stream_kernel(tune, K, stream):
+    tune(b"stream", stream)
+    R, S, bs = 5, 3, 2 * 4096 + 1040
+    rng = np.random.default_rng(K)
+    frags = rng.integers(0, 256, size=(S, K + R, bs), dtype=np.uint8)
+    masks = [int(x) for x in rng.integers(0, 1 << K, size=R)]
+    lay = _upload(frags)
+    D.xor_apply(masks, lay, list(range(K)), list(range(K, K + R)))
+    out = lay.download_stripes()
+    for r, mk in enumerate(masks):
+        want = np.zeros((S, bs), dtype=np.uint8)
+        for j in range(K):
+            if mk >> j & 1:
+                want ^= frags[:, j]
+        assert (out[:, K + r] == want).all(), r
