@@ -98,6 +98,15 @@ int ensure_device(int* dev_out)
                             KG_(8, 1, false, true)};
 #undef KG_
 #undef K_
+#define KP_(W) reinterpret_cast<const void*>(&gf16_ptrs_stream_kernel<W, 1>),                 \
+               reinterpret_cast<const void*>(&gf16_ptrs_stream_kernel<W, 2>),                 \
+               reinterpret_cast<const void*>(&gf16_ptrs_stream_kernel<W, 3>),                 \
+               reinterpret_cast<const void*>(&gf16_ptrs_stream_kernel<W, 4>),                 \
+               reinterpret_cast<const void*>(&gf16_ptrs_stream_kernel<W, 5>)
+        const void* pk[] = {KP_(2), KP_(4), KP_(8)};
+#undef KP_
+        for (const void* k : pk)
+            HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         for (const void* k : sk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         di.lds_attr_set = true;
@@ -319,6 +328,27 @@ int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3
     return launch_stream_w<8, 1, false>(a, grid, block, lds, st);
 }
 
+template <int W>
+int launch_ptrs_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st)
+{
+    switch ((a.ncols + 3) / 4) {
+    case 1: hipLaunchKernelGGL((gf16_ptrs_stream_kernel<W, 1>), grid, block, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((gf16_ptrs_stream_kernel<W, 2>), grid, block, lds, st, a); break;
+    case 3: hipLaunchKernelGGL((gf16_ptrs_stream_kernel<W, 3>), grid, block, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((gf16_ptrs_stream_kernel<W, 4>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((gf16_ptrs_stream_kernel<W, 5>), grid, block, lds, st, a); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, size_t lds, hipStream_t st)
+{
+    if (width == 2) return launch_ptrs_w<2>(a, grid, block, lds, st);
+    if (width == 4) return launch_ptrs_w<4>(a, grid, block, lds, st);
+    return launch_ptrs_w<8>(a, grid, block, lds, st);
+}
+
 template <bool PTRS>
 int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off,
                 const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st)
@@ -365,6 +395,16 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             a.tile_order = g_tune.stream_order;
             rc = launch_stream(a, p.width, ch, g_tune.stream_pf != 0, nib, dim3(g.grid),
                                dim3(g.threads), g.lds, st);
+            if (rc) return rc;
+            continue;
+        }
+        if (PTRS && g_tune.nt && !exp && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
+            bs < (int64_t(1) << 31)) {
+            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4);
+            if (rc) return rc;
+            a.ntiles = g.ntiles;
+            a.tiles_per_stripe = g.tiles_per_stripe;
+            rc = launch_ptrs_stream(a, p.width, dim3(g.grid), dim3(g.threads), g.lds, st);
             if (rc) return rc;
             continue;
         }

@@ -58,6 +58,8 @@ template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);
 template <int W, int KG, int CH, bool PF, bool NIB>
 __global__ void gf16_stream_kernel(const ApplyArgs a);
+template <int W, int KG>
+__global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>

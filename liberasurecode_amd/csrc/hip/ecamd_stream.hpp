@@ -232,10 +232,98 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
 }
 
 
+// One group of 4 inputs of gf16_ptrs_stream_kernel: a buffer resource per fragment, loads
+// unconditional (out-of-range offset past ncols), lookups at compile-time table offsets.
+template <int W, int G, int KG>
+__device__ __forceinline__ void ptrs_group(const ApplyArgs& a, const uint8_t* lds,
+                                           const uint8_t* const (&ptr)[4 * KG], int off,
+                                           uint32_t (&acc)[8][W / 2])
+{
+    v4u x[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int j = 4 * G + i;
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ptr[j]), 0,
+                                                         static_cast<int>(a.bs), 0x00020000);
+        x[i] = __builtin_amdgcn_raw_buffer_load_b128(r, j < a.ncols ? off : static_cast<int>(0x80000000u), 0, 2);
+    }
+    if (4 * G + 0 < a.ncols) mac_chunk_imm<W, 4 * G + 0>(lds, x[0], acc);
+    if (4 * G + 1 < a.ncols) mac_chunk_imm<W, 4 * G + 1>(lds, x[1], acc);
+    if (4 * G + 2 < a.ncols) mac_chunk_imm<W, 4 * G + 2>(lds, x[2], acc);
+    if (4 * G + 3 < a.ncols) mac_chunk_imm<W, 4 * G + 3>(lds, x[3], acc);
+    if constexpr (G + 1 < KG) ptrs_group<W, G + 1, KG>(a, lds, ptr, off, acc);
+}
+
+// gf16_ptrs_stream_kernel<W, KG>: the pointer-table form (ecamd_map_apply_ptrs, heterogeneous
+// decode batches): input j of stripe s is the fragment at in_ptrs[s*in_stride + in_off[j]], so
+// every fragment gets its own buffer resource (base from a scalar load of the table, range = the
+// fragment) and the same unconditional, unrolled loads / compile-time table offsets as above.
+template <int W, int KG>
+__global__ void __launch_bounds__(1024) gf16_ptrs_stream_kernel(const ApplyArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    const int tbytes = a.ncols * 512 * EB;
+    for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
+        *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
+    __syncthreads();
+
+    const int span = static_cast<int>(blockDim.x) * 16;
+    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+        const uint32_t s = t / a.tiles_per_stripe;
+        const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
+        const int64_t o64 = toff + static_cast<int64_t>(threadIdx.x) * 16;
+        if (toff + span > a.bs) {  // last, partial tile of each fragment
+            const int64_t rem = a.bs - o64;
+            if (rem >= 16)
+                apply_tile<W, true, true, false, false, false>(a, lds, s, o64, 16);
+            else if (rem > 0)
+                apply_tile<W, true, true, false, false, true>(a, lds, s, o64, static_cast<int>(rem));
+            continue;
+        }
+        const int off = static_cast<int>(o64);
+        // every fragment pointer of the stripe up front: one burst of scalar loads, one wait
+        const uint8_t* const* inp = a.in_ptrs + static_cast<int64_t>(s) * a.in_stride;
+        uint8_t* const* outp = a.out_ptrs + static_cast<int64_t>(s) * a.out_stride;
+        const uint8_t* ptr[4 * KG];
+#pragma unroll
+        for (int j = 0; j < 4 * KG; j++) ptr[j] = inp[a.in_off[j < a.ncols ? j : 0]];
+        uint8_t* optr[W];
+#pragma unroll
+        for (int r = 0; r < W; r++) optr[r] = outp[a.out_off[r < a.nrows ? r : 0]];
+        uint32_t acc[8][D];
+#pragma unroll
+        for (int w = 0; w < 8; w++)
+#pragma unroll
+            for (int d = 0; d < D; d++) acc[w][d] = 0u;
+        ptrs_group<W, 0, KG>(a, lds, ptr, off, acc);
+#pragma unroll
+        for (int r = 0; r < W; r++) {
+            if (r >= a.nrows) break;
+            v4u v;
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const uint32_t A = acc[2 * d][r >> 1], B = acc[2 * d + 1][r >> 1];
+                v[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+            }
+            const auto ro = __builtin_amdgcn_make_buffer_rsrc(optr[r], 0, static_cast<int>(a.bs), 0x00020000);
+            if (a.accumulate) v ^= __builtin_amdgcn_raw_buffer_load_b128(ro, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, off, 0, 2);  // nt
+        }
+    }
+}
+
 }  // namespace ecamd
 
 #define ECAMD_STREAM_INST(W, KG, CH, PF, NIB) \
     template __global__ void ecamd::gf16_stream_kernel<W, KG, CH, PF, NIB>(const ecamd::ApplyArgs);
+#define ECAMD_PTRS_KG(W)                                                                  \
+    template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 1>(const ecamd::ApplyArgs);      \
+    template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 2>(const ecamd::ApplyArgs);      \
+    template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 3>(const ecamd::ApplyArgs);      \
+    template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 4>(const ecamd::ApplyArgs);      \
+    template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 5>(const ecamd::ApplyArgs);
 #define ECAMD_STREAM_KG(W, CH, PF, NIB)                                                   \
     ECAMD_STREAM_INST(W, 1, CH, PF, NIB) ECAMD_STREAM_INST(W, 2, CH, PF, NIB)             \
     ECAMD_STREAM_INST(W, 3, CH, PF, NIB) ECAMD_STREAM_INST(W, 4, CH, PF, NIB)             \

@@ -184,8 +184,9 @@ def test_map_tails_and_shapes(bs, R, K):
         assert (out[1, K + r] == want[r]).all()
 
 
-def test_map_apply_pointer_tables():
-    k, m, bs, S = 10, 4, 8192, 5
+@pytest.mark.parametrize("bs", [8192, 3 * 4096 + 40])
+def test_map_apply_pointer_tables(bs):
+    k, m, S = 10, 4, 5
     lay = D.Layout.alloc(k + m, bs, S)
     lay.fill_splitmix(nfrags=k)
     G = np.array(orc.generator(k, m)).reshape(k + m, k)
@@ -338,6 +339,28 @@ def test_stream_kernel_variants(tune, R, K, variant):
         want = gfnp.apply_map(coeff, [frags[s, j] for j in range(K)])
         for r in range(R):
             assert (out[s, K + r] == want[r]).all(), (s, r)
+
+
+@pytest.mark.parametrize("stream", [0, 1])
+@pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 24), (20, 8, 8192 + 2, 10)])
+def test_decode_multi_pointer_kernels(tune, stream, k, m, bs, S):
+    """Heterogeneous batch decode (pointer-table launches) on both the stream and the
+    first-version pointer kernels, checked against the oracle on garbage-filled buffers."""
+    tune(b"stream", stream)
+    rng = np.random.default_rng(k * 7 + stream)
+    host = rng.integers(0, 256, size=(S, k + m, bs), dtype=np.uint8)
+    for s in range(S):
+        host[s, k:] = orc.encode(k, m, host[s, :k])
+    pats = [sorted(rng.choice(k + m, size=int(rng.integers(1, m + 1)), replace=False).tolist())
+            for _ in range(S)]
+    dirty = host.copy()
+    for s in range(S):
+        for f in pats[s]:
+            dirty[s, f] = rng.integers(0, 256, size=bs, dtype=np.uint8)
+    lay = _upload(dirty)
+    D.rs_decode_multi(k, m, pats, lay)
+    got = lay.download_stripes()
+    assert (got == host).all()
 
 
 @pytest.mark.parametrize("K", [1, 3, 4, 7, 12, 17, 32])
