@@ -380,3 +380,29 @@ def test_xor_stream_kernel(tune, K, stream):
             if mk >> j & 1:
                 want ^= frags[:, j]
         assert (out[:, K + r] == want).all(), r
+
+
+def test_fragment_major_layout_beyond_2gib():
+    """Fragment-major layout [k+m][S][bs] whose fragment offsets pass 2 GiB: the stream kernel's
+    32-bit buffer offsets do not reach, so the launch falls back to the 64-bit-address kernel.
+    Encode and a decode of the data stripes, checked against the oracle at both ends."""
+    k, m, bs = 4, 2, 4096
+    S = (1 << 31) // bs + 8  # frag_stride = S*bs > 2 GiB
+    buf = D.DeviceBuffer((k + m) * S * bs)
+    lay = D.Layout(buf, k + m, bs, S, frag_stride=S * bs, stripe_stride=bs)
+    lay.fill_splitmix(nfrags=k)
+    D.rs_encode(k, m, lay)
+    D.synchronize()
+
+    def stripe(s):
+        return np.stack([buf.download(bs, f * S * bs + s * bs) for f in range(k + m)])
+
+    for s in (0, S - 1):
+        got = stripe(s)
+        assert (got[:k] == stripe_fragments(s, k, bs)).all()
+        assert (got[k:] == orc.encode(k, m, got[:k])).all(), s
+    want = stripe(S - 1)
+    D.rs_decode(k, m, [0, 3], lay)
+    D.synchronize()
+    assert (stripe(S - 1) == want).all()
+    buf.free()
