@@ -141,7 +141,7 @@ struct Tuning {
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
                             // measured best, tools/xor_sweep.py)
-    int stream_order = 0;   //   tile order: 0 grid-stride, 1 contiguous range per workgroup
+    int stream_order = 0;   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     int stream_nib = 0;     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     int stream_pf = 0;      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
@@ -726,7 +726,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "xor_wgs") {
         g_tune.xor_wgs = std::max(0, std::min(value, 8));
     } else if (k == "stream_order") {
-        g_tune.stream_order = value != 0;
+        g_tune.stream_order = std::max(0, std::min(value, 3));
     } else if (k == "stream_nib") {
         g_tune.stream_nib = std::max(0, std::min(value, 2));
     } else if (k == "stream_pf") {

@@ -160,12 +160,17 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
 
     const int cstride = static_cast<int>(blockDim.x) * 16;
     const int64_t span = static_cast<int64_t>(cstride) * CH;
-    // tile_order 1: each workgroup walks its own contiguous range of tiles (a long sequential
-    // run through each fragment); 0: tiles strided over the grid.
+    // tile_order bit 0: each workgroup walks its own contiguous range of tiles (a long sequential
+    // run through each fragment), else tiles strided over the grid; bit 1: XCD-grouped block ids
+    // (workgroups are dispatched round-robin over the 8 XCDs, so block b runs on XCD b % 8; the
+    // remap gives each XCD a contiguous 1/8 of the logical blocks).
+    uint32_t bid = blockIdx.x;
+    if ((a.tile_order & 2) && gridDim.x % 8 == 0) bid = (bid % 8) * (gridDim.x / 8) + bid / 8;
+    const bool ranged = a.tile_order & 1;
     const uint32_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
-    const uint32_t t0 = a.tile_order ? blockIdx.x * per : blockIdx.x;
-    const uint32_t t1 = a.tile_order ? min(a.ntiles, t0 + per) : a.ntiles;
-    const uint32_t dt = a.tile_order ? 1u : gridDim.x;
+    const uint32_t t0 = ranged ? bid * per : bid;
+    const uint32_t t1 = ranged ? min(a.ntiles, t0 + per) : a.ntiles;
+    const uint32_t dt = ranged ? 1u : gridDim.x;
     for (uint32_t t = t0; t < t1; t += dt) {
         const uint32_t s = t / a.tiles_per_stripe;
         const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;

@@ -21,14 +21,14 @@ CFGS = {"c3": (10, 4, 1 << 20, 256, [0, 1, 2, 3]),
         "c5": (20, 8, 4 << 20, 32, list(range(8)))}
 
 
-VARIANTS = [(0, 1, 0, 0, 0), (1, 1, 0, 0, 0), (1, 2, 0, 0, 0)]
+VARIANTS = [(0, 1, 0, 0, 0), (1, 1, 0, 0, 0), (1, 1, 0, 0, 1), (1, 1, 0, 0, 2), (1, 1, 0, 0, 3)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cfg", default="c3,c5,c2")
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--geoms", default="0x0,256x2,256x3,512x1")
+    ap.add_argument("--geoms", default="0x0")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stream_sweep.jsonl"))
     args = ap.parse_args()
     d = _lib.dev()
