@@ -132,11 +132,13 @@ struct Tuning {
     int exp_ch = 0;      // sweeps: experimental W=4 kernel with 1 or 2 chunks per lane
     int ablate = 0;      // sweeps: experimental kernel without LDS lookups (wrong results)
     int nib = 0;         // gf16 kernel: 1 = nibble tables (4 conflict-free lookups per word)
-    int crc_bits = 4;    // CRC32 kernel: 4 (conflict-free nibble tables, measured faster on
-                         // random payloads: 4.77 vs 4.25 TB/s) or 8 (byte tables)
+    int crc_bits = 5;    // CRC32 kernel piece tables: 4 nibble, 8 byte, 5..7 byte tables for the first
+                         // bits-4 dwords of a piece (5 measured best with crc_pos, tools/frame_bench.py)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
+    int crc_span_kib = 128; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
+    int crc_pos = 1;        // CRC32 kernel: position-specific piece tables (one gap step per 4 pieces)
     int stream = 1;         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
@@ -171,6 +173,8 @@ int dev_tune(const char* key)
     if (k == "crc_wgs") return g_tune.crc_wgs;
     if (k == "frame_unfused") return g_tune.frame_unfused;
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
+    if (k == "crc_pos") return g_tune.crc_pos;
+    if (k == "crc_span_kib") return g_tune.crc_span_kib;
     return 0;
 }
 
@@ -712,11 +716,16 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "nib") {
         g_tune.nib = value != 0;
     } else if (k == "crc_bits") {
-        g_tune.crc_bits = value == 8 ? 8 : 4;  // 0 restores the default (4)
+        // 4 nibble tables, 8 byte tables, 5..7 byte tables for the first bits-4 dwords of a piece
+        g_tune.crc_bits = (value >= 4 && value <= 8) ? value : 5;  // 0 restores the default (5)
     } else if (k == "crc_wgs") {
         g_tune.crc_wgs = std::max(0, std::min(value, 4));
     } else if (k == "crc_gap_bits") {
         g_tune.crc_gap_bits = value == 4 ? 4 : 8;  // 0 restores the default (8)
+    } else if (k == "crc_span_kib") {
+        g_tune.crc_span_kib = (value >= 4 && value <= 256) ? value / 4 * 4 : 128;  // 0: default
+    } else if (k == "crc_pos") {
+        g_tune.crc_pos = value;  // 0 off, anything else on
     } else if (k == "frame_unfused") {
         g_tune.frame_unfused = value != 0;
     } else if (k == "stream") {

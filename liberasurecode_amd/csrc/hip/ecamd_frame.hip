@@ -16,10 +16,13 @@
 //   crc_finalize_kernel    one thread per payload: Horner over its spans with A^(J KiB), the last
 //     len % 16 bytes through the byte table, crc = ~(A^len ~0 ^ r0), and -- when asked -- the
 //     whole 80-byte header with its metadata checksum.
-// B = 8 (byte tables, 20 KiB + 24 KiB) or B = 4 (nibble tables: 16 entries span 16 distinct LDS
-// banks, so lookups never conflict, at twice the lookups).
+// Piece tables per dword: byte tables (4 KiB, random lookups conflict in the LDS banks) or nibble
+// tables (16 entries span 16 distinct banks, so lookups never conflict, at twice the lookups and
+// VALU work); crc_partial_kernel<MB, G> takes byte tables for the first MB dwords of a piece.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 #include "ecamd_frame.hpp"
 #include "ecamd_isa.hpp"
@@ -46,32 +49,40 @@ template <int B>
 __device__ __forceinline__ uint32_t lmap(const uint32_t* tab, uint32_t x)
 {
     constexpr int E = 1 << B;
-    uint32_t r = 0;
+    const char* t = reinterpret_cast<const char*>(tab);
+    auto at = [&](int f, uint32_t off) { return *reinterpret_cast<const uint32_t*>(t + f * E * 4 + off); };
     if constexpr (B == 4) {
         // Spread the nibbles into bytes once (3 ops for 8 fields); every lookup address is then
         // one SDWA byte-select shift (the compiler re-fuses a plain shift+mask, hence the asm).
         const uint32_t lo = x & 0x0f0f0f0fu, hi = (x >> 4) & 0x0f0f0f0fu;
-        const char* t = reinterpret_cast<const char*>(tab);
-        auto at = [&](int f, uint32_t off) {
-            return *reinterpret_cast<const uint32_t*>(t + f * E * 4 + off);
-        };
         const uint32_t a = xor3(at(0, byte_x4<0>(lo)), at(1, byte_x4<0>(hi)), at(2, byte_x4<1>(lo)));
         const uint32_t b = xor3(at(3, byte_x4<1>(hi)), at(4, byte_x4<2>(lo)), at(5, byte_x4<2>(hi)));
-        r = xor3(a, b, at(6, byte_x4<3>(lo)) ^ at(7, byte_x4<3>(hi)));
+        return xor3(a, b, at(6, byte_x4<3>(lo)) ^ at(7, byte_x4<3>(hi)));
     } else {
         static_assert(B == 8, "byte or nibble tables");
-        r = xor3(tab[x & 0xffu], tab[E + ((x >> 8) & 0xffu)], tab[2 * E + ((x >> 16) & 0xffu)]) ^
-            tab[3 * E + (x >> 24)];
+        return xor3(at(0, byte_x4<0>(x)), at(1, byte_x4<1>(x)), at(2, byte_x4<2>(x))) ^ at(3, byte_x4<3>(x));
     }
-    return r;
 }
 
-template <int B>
+// Piece tables of dword w: byte tables (4 x 256 words) for the first MB dwords, nibble tables
+// (8 x 16 words) for the rest -- MB trades LDS bank conflicts (byte tables) against VALU work
+// (nibble tables: twice the lookups, conflict-free).
+constexpr int piece_off(int MB, int w) { return (w < MB ? w : MB) * 1024 + (w < MB ? 0 : w - MB) * 128; }
+constexpr int piece_words(int MB) { return piece_off(MB, 4); }
+
+template <int MB>
 __device__ __forceinline__ uint32_t piece_r0(const uint32_t* tab, u32x4 v)
 {
-    constexpr int S = (32 / B) << B;  // words of one data word's tables
-    return xor3(lmap<B>(tab, v.x), lmap<B>(tab + S, v.y), lmap<B>(tab + 2 * S, v.z)) ^
-           lmap<B>(tab + 3 * S, v.w);
+    auto map = [&](auto W, uint32_t x) {
+        constexpr int w = decltype(W)::value;
+        if constexpr (w < MB)
+            return lmap<8>(tab + piece_off(MB, w), x);
+        else
+            return lmap<4>(tab + piece_off(MB, w), x);
+    };
+    return xor3(map(std::integral_constant<int, 0>{}, v.x), map(std::integral_constant<int, 1>{}, v.y),
+                map(std::integral_constant<int, 2>{}, v.z)) ^
+           map(std::integral_constant<int, 3>{}, v.w);
 }
 
 __device__ __forceinline__ uint32_t byte_step(const uint32_t* T, uint32_t s, uint32_t b, int legacy)
@@ -90,12 +101,15 @@ __device__ __forceinline__ const uint8_t* item_ptr(const CrcArgs& a, int64_t ite
 
 }  // namespace
 
-template <int B, int G>
+template <int MB, int G, bool POS>
 __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
                                                           uint32_t* __restrict__ partial)
 {
-    constexpr int E = 1 << B, NF = 32 / B;
-    constexpr int PIECE = 4 * NF * E, FIELDS = (32 / G) << G, WORDS = PIECE + 7 * FIELDS;
+    // POS: position tables -- piece u of a group of 4 has its own tables with the shift to the
+    // group's last piece (A^(1024*(3-u))) folded in, so the lane state takes one A^4096 step per
+    // 4 pieces instead of four A^1024 steps (a quarter of the serial lookup chain).
+    constexpr int PW = piece_words(MB), PIECE = POS ? 4 * PW : PW;
+    constexpr int FIELDS = (32 / G) << G, WORDS = PIECE + 7 * FIELDS;
     __shared__ uint32_t tab[WORDS];
     for (int i = threadIdx.x; i < WORDS; i += blockDim.x) tab[i] = img[i];
     __syncthreads();
@@ -111,20 +125,33 @@ __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const
         const uint8_t* p = item_ptr(a, item) + a.payload_off;
         const int64_t start = a.body - static_cast<int64_t>(a.nspans - q) * span + lane * 16;
         uint32_t st = 0;
-        // Two groups of 4 pieces in flight: group g+1 is loading while group g is looked up.
+        // Two groups of 4 pieces in flight: group g+1 is loading while group g is looked up.  The
+        // loads are unconditional buffer loads: a piece before the payload (the first span's
+        // leading zeros) or past the span gets an out-of-range offset, which reads zeros with no
+        // memory traffic, so the compiler can count the loads in flight (vmcnt(N), not vmcnt(0)).
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0,
+                                                          static_cast<int>(a.body), 0x00020000);
         auto load4 = [&](int j, u32x4 (&v)[4]) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int64_t off = start + static_cast<int64_t>(j + u) * 1024;
-                v[u] = off >= 0 ? nt_load16(p + off) : u32x4{0, 0, 0, 0};
+                const bool live = j + u < a.J && off >= 0;
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, live ? static_cast<int>(off)
+                                                                      : static_cast<int>(0x80000000u),
+                                                             0, 2);
             }
         };
         u32x4 cur[4], nxt[4];
         load4(0, cur);
         for (int j = 0; j < a.J; j += 4) {
-            if (j + 4 < a.J) load4(j + 4, nxt);
+            load4(j + 4, nxt);
+            if constexpr (POS) {
+                st = xor3(lmap<G>(gap, st), piece_r0<MB>(tab, cur[0]), piece_r0<MB>(tab + PW, cur[1])) ^
+                     piece_r0<MB>(tab + 2 * PW, cur[2]) ^ piece_r0<MB>(tab + 3 * PW, cur[3]);
+            } else {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) st = lmap<G>(gap, st) ^ piece_r0<B>(tab, cur[u]);
+                for (int u = 0; u < 4; ++u) st = lmap<G>(gap, st) ^ piece_r0<MB>(tab, cur[u]);
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
         }
@@ -138,12 +165,14 @@ __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const
     }
 }
 
-template __global__ void crc_partial_kernel<8, 8>(const CrcArgs, const uint32_t* __restrict__,
-                                                  uint32_t* __restrict__);
-template __global__ void crc_partial_kernel<4, 4>(const CrcArgs, const uint32_t* __restrict__,
-                                                  uint32_t* __restrict__);
-template __global__ void crc_partial_kernel<4, 8>(const CrcArgs, const uint32_t* __restrict__,
-                                                  uint32_t* __restrict__);
+#define ECAMD_CRC_INST(MB, G, POS) \
+    template __global__ void crc_partial_kernel<MB, G, POS>(const CrcArgs, const uint32_t* __restrict__, \
+                                                            uint32_t* __restrict__);
+ECAMD_CRC_INST(4, 8, false) ECAMD_CRC_INST(0, 8, false) ECAMD_CRC_INST(0, 4, false)
+ECAMD_CRC_INST(1, 8, false) ECAMD_CRC_INST(2, 8, false) ECAMD_CRC_INST(3, 8, false)
+ECAMD_CRC_INST(4, 8, true) ECAMD_CRC_INST(0, 8, true) ECAMD_CRC_INST(1, 8, true)
+ECAMD_CRC_INST(2, 8, true) ECAMD_CRC_INST(3, 8, true)
+#undef ECAMD_CRC_INST
 
 namespace {
 

@@ -66,7 +66,7 @@ struct JoinArgs {
     int aligned;
 };
 
-template <int B, int G>
+template <int MB, int G, bool POS>
 __global__ void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
                                    uint32_t* __restrict__ partial);
 __global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict__ img,

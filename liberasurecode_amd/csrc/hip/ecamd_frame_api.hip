@@ -47,17 +47,17 @@ struct DevImage {
 };
 
 std::mutex g_mu;
-std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J, G
+std::map<std::tuple<int, int, int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J, G, pos
 std::map<std::pair<int, void*>, std::pair<uint32_t*, size_t>> g_scratch;     // dev, stream
 
-int image(int dev, bool legacy, int B, int J, int G, const DevImage** out)
+int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** out)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_tuple(dev, legacy ? 1 : 0, B, J, G);
+    auto key = std::make_tuple(dev, legacy ? 1 : 0, B, J, G, pos ? 1 : 0);
     auto it = g_images.find(key);
     if (it == g_images.end()) {
         auto di = std::make_unique<DevImage>();
-        di->img = build_crc_image(CrcMachine(legacy), B, J, G);
+        di->img = build_crc_image(CrcMachine(legacy), B, J, G, pos);
         const size_t bytes = di->img.words.size() * sizeof(uint32_t);
         HIP_TRY(hipMalloc(&di->d, bytes));
         HIP_TRY(hipMemcpy(di->d, di->img.words.data(), bytes, hipMemcpyHostToDevice));
@@ -143,12 +143,14 @@ int run_crc(int dev, bool legacy, bool with_crc, const uint8_t* base, int64_t ss
 {
     const int64_t items = static_cast<int64_t>(nfrag) * nstripes;
     if (items == 0) return 0;
-    const int B = dev_tune("crc_bits") == 4 ? 4 : 8;
-    const int G = B == 8 ? 8 : (dev_tune("crc_gap_bits") == 4 ? 4 : 8);
+    const int B = dev_tune("crc_bits");  // 4 .. 8 (host/crc.cpp build_crc_image)
+    const int G = B != 4 ? 8 : (dev_tune("crc_gap_bits") == 4 ? 4 : 8);
+    const bool pos = dev_tune("crc_pos") != 0 && G == 8;
     const int64_t body = len & ~int64_t(15);
-    int J = static_cast<int>(std::min<int64_t>(16, std::max<int64_t>(4, ((body / 1024 + 3) / 4) * 4)));
+    const int jmax = dev_tune("crc_span_kib") > 0 ? dev_tune("crc_span_kib") : 16;  // KiB per span
+    int J = static_cast<int>(std::min<int64_t>(jmax, std::max<int64_t>(4, ((body / 1024 + 3) / 4) * 4)));
     const DevImage* di = nullptr;
-    int rc = image(dev, legacy, B, J, G, &di);
+    int rc = image(dev, legacy, B, J, G, pos, &di);
     if (rc) return rc;
     CrcArgs a{};
     a.base = base;
@@ -181,12 +183,31 @@ int run_crc(int dev, bool legacy, bool with_crc, const uint8_t* base, int64_t ss
                                                       static_cast<int64_t>(dev_cu_count(dev)) * wpc,
                                                       (waves + 7) / 8));
         const dim3 gd(static_cast<unsigned>(grid)), bd(512);
-        if (B == 8)
-            hipLaunchKernelGGL((crc_partial_kernel<8, 8>), gd, bd, 0, st, a, di->d, partial);
-        else if (G == 8)
-            hipLaunchKernelGGL((crc_partial_kernel<4, 8>), gd, bd, 0, st, a, di->d, partial);
-        else
-            hipLaunchKernelGGL((crc_partial_kernel<4, 4>), gd, bd, 0, st, a, di->d, partial);
+        // template: number of byte-table dwords per piece, gap field bits, position tables
+#define ECAMD_CRC_LAUNCH(MB, GG, P) \
+    hipLaunchKernelGGL((crc_partial_kernel<MB, GG, P>), gd, bd, 0, st, a, di->d, partial)
+        if (pos) {
+            switch (B) {
+            case 8: ECAMD_CRC_LAUNCH(4, 8, true); break;
+            case 7: ECAMD_CRC_LAUNCH(3, 8, true); break;
+            case 6: ECAMD_CRC_LAUNCH(2, 8, true); break;
+            case 5: ECAMD_CRC_LAUNCH(1, 8, true); break;
+            default: ECAMD_CRC_LAUNCH(0, 8, true); break;
+            }
+        } else {
+            switch (B) {
+            case 8: ECAMD_CRC_LAUNCH(4, 8, false); break;
+            case 7: ECAMD_CRC_LAUNCH(3, 8, false); break;
+            case 6: ECAMD_CRC_LAUNCH(2, 8, false); break;
+            case 5: ECAMD_CRC_LAUNCH(1, 8, false); break;
+            default:
+                if (G == 8)
+                    ECAMD_CRC_LAUNCH(0, 8, false);
+                else
+                    ECAMD_CRC_LAUNCH(0, 4, false);
+            }
+        }
+#undef ECAMD_CRC_LAUNCH
         HIP_TRY(hipGetLastError());
     }
     if (with_crc || h.write) {
@@ -438,7 +459,7 @@ int ecamd_frame_verify(int nfrag, int64_t blocksize, int legacy, const void* d_f
                  blocksize, nstripes, crc, none, stream);
     if (rc) return rc;
     const DevImage *iz = nullptr, *il = nullptr;
-    if ((rc = image(dev, false, 8, 4, 8, &iz)) || (rc = image(dev, true, 8, 4, 8, &il))) return rc;
+    if ((rc = image(dev, false, 8, 4, 8, false, &iz)) || (rc = image(dev, true, 8, 4, 8, false, &il))) return rc;
     CrcArgs a{};
     a.base = frags;
     a.stripe_stride = stripe_stride;

@@ -44,30 +44,42 @@ void field_tables(const Mat32& M, int B, uint32_t* out)
         for (int v = 0; v < E; v++) out[f * E + v] = M.apply(static_cast<uint32_t>(v) << (f * B));
 }
 
-CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G)
+CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
 {
     CrcImage img;
     img.B = B;
     img.G = G;
     img.J = J;
-    const int E = 1 << B, NF = 32 / B;
-    const size_t piece = static_cast<size_t>(4 * NF) * E;
+    // B = 8: byte tables for all 4 dwords of a piece; 4: nibble tables; 5..7: byte tables for the
+    // first B - 4 dwords, nibble tables for the rest (crc_partial_kernel<MB = B-4 or 4 or 0, G>).
+    const int mb = B == 8 ? 4 : B - 4;
+    size_t pw = 0;
+    for (int word = 0; word < 4; word++) pw += word < mb ? 4 * 256 : 8 * 16;
+    const size_t piece = pos ? 4 * pw : pw;
     const size_t fields = static_cast<size_t>(32 / G) << G;  // one gap / level map
     img.lds_words = piece + fields * 7;
     img.span_off = img.lds_words;
     img.t_off = img.span_off + 4 * 256;
     img.words.assign(img.t_off + 256, 0);
     uint32_t* w = img.words.data();
-    // piece tables: word w of the 16-byte piece = v << (f * B), the rest zero; r0 by running it.
-    for (int word = 0; word < 4; word++)
-        for (int f = 0; f < NF; f++)
-            for (int v = 0; v < E; v++) {
-                uint8_t bytes[16] = {0};
-                const uint32_t x = static_cast<uint32_t>(v) << (f * B);
-                for (int q = 0; q < 4; q++) bytes[4 * word + q] = static_cast<uint8_t>(x >> (8 * q));
-                w[(word * NF + f) * E + v] = m.run(0, bytes, 16);
-            }
-    field_tables(zero_shift(m, 64 * 16), G, w + piece);
+    // piece tables: word w of the 16-byte piece = v << (f * b), the rest zero; r0 by running it
+    // (then shifted to the group's last piece for position set u when pos).
+    for (int u = 0; u < (pos ? 4 : 1); u++) {
+        const Mat32 sh = zero_shift(m, pos ? 1024ull * (3 - u) : 0);
+        size_t off = u * pw;
+        for (int word = 0; word < 4; word++) {
+            const int b = word < mb ? 8 : 4, E = 1 << b, NF = 32 / b;
+            for (int f = 0; f < NF; f++)
+                for (int v = 0; v < E; v++) {
+                    uint8_t bytes[16] = {0};
+                    const uint32_t x = static_cast<uint32_t>(v) << (f * b);
+                    for (int q = 0; q < 4; q++) bytes[4 * word + q] = static_cast<uint8_t>(x >> (8 * q));
+                    w[off + static_cast<size_t>(f) * E + v] = sh.apply(m.run(0, bytes, 16));
+                }
+            off += static_cast<size_t>(NF) * E;
+        }
+    }
+    field_tables(zero_shift(m, pos ? 4 * 1024 : 64 * 16), G, w + piece);
     for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), G, w + piece + fields * (1 + t));
     field_tables(zero_shift(m, static_cast<uint64_t>(J) * 1024), 8, w + img.span_off);
     std::memcpy(w + img.t_off, m.t, sizeof(m.t));

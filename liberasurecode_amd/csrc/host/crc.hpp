@@ -58,8 +58,9 @@ Mat32 zero_shift(const CrcMachine& m, uint64_t nbytes);  // A^nbytes
 void field_tables(const Mat32& M, int B, uint32_t* out);
 
 // Image of one device CRC configuration (layout documented in hip/ecamd_frame.hip):
-//   [ piece tables: 128/B tables, r0 of a 16-byte piece holding v in field f of word w ]
-//   [ gap tables  : A^(64 lanes * 16 B) as 32/G field tables                          ]
+//   [ piece tables: 128/B tables, r0 of a 16-byte piece holding v in field f of word w
+//                   (x4 position sets when pos)                                        ]
+//   [ gap tables  : A^(64 lanes * 16 B) (A^4096 when pos) as 32/G field tables         ]
 //   [ level tables: A^(16 * 2^t), t = 0..5, for the in-wave butterfly (G-bit fields)     ]
 //   [ span tables : A^(J * 1024) as 4 byte tables (finalize kernel)                      ]
 //   [ T           : the machine's byte table (finalize: tail bytes and header checksum)  ]
@@ -72,6 +73,8 @@ struct CrcImage {
     size_t span_off = 0;
     size_t t_off = 0;
 };
-CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G);
+// pos: four position-specific piece-table sets (piece u of a group of 4 pre-shifted by
+// A^(1024*(3-u))) and an A^4096 gap map instead of one set and A^1024.
+CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos = false);
 
 }  // namespace ecamd

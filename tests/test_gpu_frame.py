@@ -26,12 +26,20 @@ def F():
     return frame
 
 
-@pytest.fixture(params=[8, 4], ids=["byte_tables", "nibble_tables"])
+@pytest.fixture(params=[(8, 0, 0), (7, 0, 0), (6, 0, 0), (5, 0, 0), (4, 0, 0), (8, 1, 0), (6, 1, 0),
+                        (4, 1, 0), (5, 1, 32), (5, 1, 64), (4, 0, 8)],
+                ids=["byte_tables", "mixed3", "mixed2", "mixed1", "nibble_tables", "byte_pos",
+                     "mixed2_pos", "nibble_pos", "mixed1_pos_span32", "mixed1_pos_span64",
+                     "nibble_span8"])
 def bits(request):
     from liberasurecode_amd import _lib
-    _lib.check(_lib.dev().ecamd_tune(b"crc_bits", request.param), "tune")
-    yield request.param
-    _lib.dev().ecamd_tune(b"crc_bits", 0)
+    d = _lib.dev()
+    _lib.check(d.ecamd_tune(b"crc_bits", request.param[0]), "tune")
+    _lib.check(d.ecamd_tune(b"crc_pos", request.param[1]), "tune")
+    _lib.check(d.ecamd_tune(b"crc_span_kib", request.param[2]), "tune")
+    yield request.param[0] * 100 + request.param[1] * 10 + request.param[2]
+    for key, default in ((b"crc_bits", 0), (b"crc_pos", 1), (b"crc_span_kib", 0)):
+        d.ecamd_tune(key, default)
 
 
 CRC_LENGTHS = [0, 1, 15, 16, 17, 100, 1023, 1024, 1025, 4096, 16383, 16384, 16400, 65536 + 13,

@@ -44,19 +44,23 @@ def main():
     _lib.check(d.ecamd_fill_splitmix(fb.buf.ptr + 80, fb.stripe_stride, fb.frag_stride, k + m,
                                      fb.blocksize, S, 0, 0x5EED, st.handle), "fill")
     payload_bytes = S * (k + m) * fb.blocksize
-    for bits, gap in ((8, 8), (4, 4), (4, 8)):
-        for wgs in (0, 2, 4):
+    for bits, gap, pos, span in ((4, 8, 0, 16), (5, 8, 1, 64), (5, 8, 1, 128), (4, 8, 1, 64),
+                                 (7, 8, 1, 64)):
+        for wgs in (0, 4):
+            d.ecamd_tune(b"crc_span_kib", span)
+            d.ecamd_tune(b"crc_pos", pos)
             d.ecamd_tune(b"crc_bits", bits)
             d.ecamd_tune(b"crc_gap_bits", gap)
             d.ecamd_tune(b"crc_wgs", wgs)
             ms = timed(lambda: _lib.check(d.ecamd_crc32(0, fb.buf.ptr + 80, fb.stripe_stride,
                                                          fb.frag_stride, k + m, fb.blocksize, S,
                                                          crc.ptr, st.handle), "crc"), st, args.reps)
-            print(json.dumps({"op": "crc32", "bits": bits, "gap_bits": gap, "crc_wgs": wgs,
+            print(json.dumps({"op": "crc32", "bits": bits, "gap_bits": gap, "pos": pos, "span_kib": span, "crc_wgs": wgs,
                               "ms": round(ms, 3), "GBps": round(payload_bytes / ms / 1e6, 1)}),
                   flush=True)
-    for key in (b"crc_bits", b"crc_gap_bits", b"crc_wgs"):
-        d.ecamd_tune(key, 0)
+    for key, default in ((b"crc_bits", 0), (b"crc_gap_bits", 0), (b"crc_wgs", 0), (b"crc_pos", 1),
+                         (b"crc_span_kib", 0)):
+        d.ecamd_tune(key, default)
     obj_bytes = S * size
     for unfused, ct in ((0, frame.CHKSUM_NONE), (0, frame.CHKSUM_CRC32), (1, frame.CHKSUM_NONE),
                         (1, frame.CHKSUM_CRC32)):
