@@ -29,7 +29,8 @@ import torch  # noqa: E402  (before libecamd: one HIP runtime per process)
 from liberasurecode_amd import device as D  # noqa: E402
 from liberasurecode_amd.shard import Coordinator, stripe_range  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
 
 CONFIGS = {
@@ -231,6 +232,19 @@ def main():
 
     copy_gbs = measured_copy_peak(stream)
 
+    # The survey's second decode pattern per config, outside the timed steps:
+    # erasures mixing data and parity (fewer full dot products than all-data erasures).
+    mixed = MIXED_PATTERNS.get(args.config)
+    mixed_gibs = None
+    if mixed is not None:
+        a, b = D.Event(), D.Event()
+        D.rs_decode(k, m, mixed, lay, stream=stream)
+        a.record(stream)
+        for _ in range(5):
+            D.rs_decode(k, m, mixed, lay, stream=stream)
+        b.record(stream)
+        mixed_gibs = round(obj_bytes / GIB / (a.elapsed_ms(b) / 5 / 1e3), 3)
+
     if rank == 0:
         out = {
             "metric": "device-resident encode+decode GiB/s (RS k=10 m=4, 1 MiB frags), 1/2/4/8 GPU"
@@ -251,6 +265,8 @@ def main():
                        "parallelism": f"stripe-sharded x{world} (no data-path collective)"},
             "encode_gibs_per_gpu": round(obj_bytes / GIB / (sum(enc_ms) / len(enc_ms) / 1e3), 3),
             "decode_gibs_per_gpu": round(obj_bytes / GIB / (sum(dec_ms) / len(dec_ms) / 1e3), 3),
+            "decode_mixed_pattern": mixed,
+            "decode_mixed_gibs_per_gpu": mixed_gibs,
             "roofline": {"bound": "hbm", "kernel": kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
