@@ -11,7 +11,7 @@ Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent,
 its own S stripes (weak scaling) and there is no data-path collective -- the process group is used
 for the start barrier and the max-over-ranks of the elapsed time only.
 
-Extra fields: "roofline" (gf16_apply_kernel, HIP-event timed per launch on the launch stream; peak =
+Extra fields: "roofline" (gf16_stream_kernel, HIP-event timed per launch on the launch stream; peak =
 8 TB/s spec, plus a copy peak measured live) and "cpu_baseline" (the reference codec compiled from
 its sources -- or the oracle restatement when that build is absent -- on the host cores; rank 0).
 """
@@ -29,8 +29,9 @@ import torch  # noqa: E402  (before libecamd: one HIP runtime per process)
 from liberasurecode_amd import device as D  # noqa: E402
 from liberasurecode_amd.shard import Coordinator, stripe_range  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0
-MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+# second decode pattern per config, data and parity mixed
+MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}
 GIB = float(1 << 30)
 
 CONFIGS = {
@@ -224,8 +225,8 @@ def main():
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
-    # <W outputs per pass, KG groups of 4 inputs, CH chunks per lane, PF prefetch>
-    kernel = f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false>"
+    # <W outputs per pass, KG groups of 4 inputs, CH chunks per lane, PF prefetch, NIB nibble tables>
+    kernel = f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>"
     traffic, traffic_src = pmc_traffic(args.config, kernel)
     if traffic is not None and S != CONFIGS[args.config][3]:
         traffic = int(traffic * S / CONFIGS[args.config][3])  # profile ran at the default S
