@@ -475,8 +475,11 @@ int assemble(int k, char** frags, int n, char** out, uint64_t* out_len)
 }
 
 // prepare_fragments_for_decode (erasurecode_preprocessing.c:117-217)
+// realign = false keeps unaligned caller fragments in place: this repo's codec stages every
+// fragment through its own pinned slabs, so 16-byte alignment buys nothing there, and
+// liberasurecode_rs_vand writes only the missing slots (which are always fresh buffers).
 int prepare_decode(int k, int m, char** data, char** parity, const int* missing, int* orig,
-                   int* bs, uint64_t frag_len, std::vector<char*>& owned)
+                   int* bs, uint64_t frag_len, std::vector<char*>& owned, bool realign = true)
 {
     bool gone[EC_MAX_FRAGMENTS] = {};
     for (int i = 0; missing[i] >= 0; i++) gone[missing[i]] = true;
@@ -486,7 +489,7 @@ int prepare_decode(int k, int m, char** data, char** parity, const int* missing,
             slot = new_fragment(static_cast<int>(frag_len - kHdr));
             if (!slot) return -ENOMEM;
             owned.push_back(slot);
-        } else if (reinterpret_cast<uintptr_t>(slot) & 15u) {
+        } else if (realign && (reinterpret_cast<uintptr_t>(slot) & 15u)) {
             char* t = new_fragment(static_cast<int>(frag_len - kHdr));
             if (!t) return -ENOMEM;
             std::memcpy(t, slot, frag_len);
@@ -849,9 +852,10 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
     int ret = get_fragment_partition(k, m, available_fragments, num_fragments, data.data(),
                                      parity.data(), missing.data());
     int orig = 0, bs = 0;
+    const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && crc_hooks(be));
     if (ret == 0)
         ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
-                             fragment_len, owned);
+                             fragment_len, owned, realign);
     if (ret == 0) {
         std::vector<char*> dp(k), pp(m);
         for (int i = 0; i < k; i++) dp[i] = payload(data[i]);
@@ -913,8 +917,9 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
         if (ret < 0) return ret;
     }
     int orig = 0, bs = 0;
+    const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && crc_hooks(be));
     ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
-                         fragment_len, owned);
+                         fragment_len, owned, realign);
     CrcArm arm(be, be->args.uargs.ct == CHKSUM_CRC32);  // through the stamping below
     if (ret == 0) {
         std::vector<char*> dp(k), pp(m);
