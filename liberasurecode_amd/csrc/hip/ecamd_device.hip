@@ -18,6 +18,7 @@
 #include "ecamd.h"
 #include "ecamd_internal.hpp"
 #include "ecamd_kernels.hpp"
+#include "ecamd_frame.hpp"
 
 using namespace ecamd;
 
@@ -107,6 +108,15 @@ int ensure_device(int* dev_out)
 #undef KP_
         for (const void* k : pk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+#define KF_(W) reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 1>),                   \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 2>),                   \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 3>),                   \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4>),                   \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5>)
+        const void* fk[] = {KF_(2), KF_(4), KF_(8)};
+#undef KF_
+        for (const void* k : fk)
+            HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         for (const void* k : sk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         di.lds_attr_set = true;
@@ -135,6 +145,7 @@ struct Tuning {
     int crc_bits = 5;    // CRC32 kernel piece tables: 4 nibble, 8 byte, 5..7 byte tables for the first
                          // bits-4 dwords of a piece (5 measured best with crc_pos, tools/frame_bench.py)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
+    int frame_crc_fused = 1;  // framed encode with CRC32: codec + checksums in one launch
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     int crc_span_kib = 128; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
@@ -175,6 +186,7 @@ int dev_tune(const char* key)
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     if (k == "crc_pos") return g_tune.crc_pos;
     if (k == "crc_span_kib") return g_tune.crc_span_kib;
+    if (k == "frame_crc_fused") return g_tune.frame_crc_fused;
     return 0;
 }
 
@@ -669,6 +681,77 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
                           stripe_stride, out_off, p0, stripe_stride, copy_off, bs, nstripes, stream);
 }
 
+// rs_encode_copy with the payload CRC32 folded in (gf16_frame_crc_kernel): r0 of range r of
+// payload f of stripe s lands in d_partial[(s*(k+m) + f)*q + r].  Returns ECAMD_EINVAL without
+// launching when the shape does not fit the fused kernel (the caller then runs the split path).
+int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                       int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream)
+{
+    constexpr int kThreads = 512;
+    constexpr int64_t kTile = kThreads * 16;
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
+    if (rc) return rc;
+    if (!e->map || nstripes <= 0 || bs <= 0 || bs % kTile || q <= 0 || (bs / kTile) % q)
+        return ECAMD_EINVAL;
+    const ecamd_map* map = e->map.get();
+    if (map->passes.size() != 1 || !copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
+        return ECAMD_EINVAL;
+    for (int j = 0; j < k; j++)
+        if (e->inputs[j] != j) return ECAMD_EINVAL;
+    for (int r = 0; r < m; r++)
+        if (e->outputs[r] != k + r) return ECAMD_EINVAL;
+    const auto& p = map->passes[0];
+    ApplyArgs a{};
+    a.tables = map->d_tables + p.offset;
+    a.in_base = static_cast<const uint8_t*>(obj);
+    a.in_stride = obj_stride;
+    a.out_base = static_cast<uint8_t*>(payload0);
+    a.out_stride = stripe_stride;
+    a.copy_base = static_cast<uint8_t*>(payload0);
+    a.copy_stride = stripe_stride;
+    a.bs = bs;
+    a.ncols = k;
+    a.nrows = m;
+    for (int j = 0; j < k; j++) {
+        a.in_off[j] = j * bs;
+        a.copy_off[j] = j * frag_stride;
+    }
+    for (int r = 0; r < m; r++) a.out_off[r] = (k + r) * frag_stride;
+    if (k > 4 * kStreamGroups || !stream_offsets(a, bs) || !stream_copy_offsets(a, bs)) return ECAMD_EINVAL;
+    const int kg = (k + 3) / 4;
+    const int ns = 4 * kg + p.width;
+    const size_t lds = p.bytes + (static_cast<size_t>(crc_fused_words()) + 8 * ns) * 4;
+    if (lds > static_cast<size_t>(kLdsBytes)) return ECAMD_EINVAL;
+    a.tiles_per_stripe = static_cast<uint32_t>(bs / kTile);
+    a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
+    FusedCrcArgs c{d_img, d_partial, q, static_cast<int>(bs / kTile) / q, k + m};
+    const int64_t units = static_cast<int64_t>(nstripes) * q;
+    const int wgs = std::max<int>(1, std::min<int>(2, kLdsBytes / static_cast<int>(lds)));
+    const dim3 grid(static_cast<unsigned>(std::min<int64_t>(units, static_cast<int64_t>(cu_count(map->device)) * wgs)));
+    const dim3 block(kThreads);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+#define ECAMD_FUSED(W)                                                                                      \
+    switch (kg) {                                                                                           \
+    case 1: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 1>), grid, block, lds, st, a, c); break;            \
+    case 2: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 2>), grid, block, lds, st, a, c); break;            \
+    case 3: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 3>), grid, block, lds, st, a, c); break;            \
+    case 4: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 4>), grid, block, lds, st, a, c); break;            \
+    default: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 5>), grid, block, lds, st, a, c); break;           \
+    }
+    if (p.width == 2) {
+        ECAMD_FUSED(2)
+    } else if (p.width == 4) {
+        ECAMD_FUSED(4)
+    } else {
+        ECAMD_FUSED(8)
+    }
+#undef ECAMD_FUSED
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
                    int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
                    void* stream)
@@ -726,6 +809,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_span_kib = (value >= 4 && value <= 256) ? value / 4 * 4 : 128;  // 0: default
     } else if (k == "crc_pos") {
         g_tune.crc_pos = value;  // 0 off, anything else on
+    } else if (k == "frame_crc_fused") {
+        g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_unfused") {
         g_tune.frame_unfused = value != 0;
     } else if (k == "stream") {

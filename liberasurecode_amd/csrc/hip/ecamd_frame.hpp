@@ -66,6 +66,16 @@ struct JoinArgs {
     int aligned;
 };
 
+// gf16_frame_crc_kernel (ecamd_frame_fused.hip): partial[(s*nfrag + f)*q + r] = r0 of range r
+// (q ranges of `per` tiles per fragment) of fragment f of stripe s.
+struct FusedCrcArgs {
+    const uint32_t* img;  // [piece tables, MB = 1 | A^tile | A^(16*2^t), t < 6 | A^1024], G = 4 maps
+    uint32_t* partial;
+    int q;
+    int per;
+    int nfrag;
+};
+
 template <int MB, int G, bool POS>
 __global__ void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
                                    uint32_t* __restrict__ partial);

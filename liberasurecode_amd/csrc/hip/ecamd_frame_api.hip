@@ -283,6 +283,72 @@ int xor_plan_apply(const Code& c, int op, const int* missing, int arg, uint8_t* 
                                    in_off.data(), payload0, ss, out_off.data(), bs, nstripes, stream);
 }
 
+// ---- fused CHKSUM_CRC32 framed encode (hip/ecamd_frame_fused.hip) ----
+
+std::map<std::pair<int, int>, uint32_t*> g_fused_images;  // (dev, legacy) -> device image
+
+int fused_image(int dev, bool legacy, const uint32_t** out)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_pair(dev, legacy ? 1 : 0);
+    auto it = g_fused_images.find(key);
+    if (it == g_fused_images.end()) {
+        const std::vector<uint32_t> w = build_fused_crc_image(CrcMachine(legacy), 8192);
+        uint32_t* d = nullptr;
+        HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(d, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        it = g_fused_images.emplace(key, d).first;
+    }
+    *out = it->second;
+    return 0;
+}
+
+// The object-filling rs_vand encode with CRC32 checksums as ONE codec launch that also folds the
+// payload checksums (q ranges per payload), then crc_finalize_kernel over the ranges and the
+// headers.  ECAMD_EINVAL (nothing launched) when the shape does not fit: the caller runs the
+// copy-through encode + separate CRC pass instead.
+int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64_t obj_stride,
+                     uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs,
+                     int nstripes, void* stream)
+{
+    if (dev_tune("frame_crc_fused") == 0 || bs % 8192 || nstripes <= 0) return ECAMD_EINVAL;
+    const int64_t tiles = bs / 8192;
+    int q = 1;  // ranges per payload: enough work units to fill the chip, each a long sequential run
+    while (tiles % (2 * q) == 0 && static_cast<int64_t>(nstripes) * q < 4ll * dev_cu_count(dev)) q *= 2;
+    const int nf = c.k + c.m;
+    uint32_t* partial = nullptr;
+    int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * q, &partial);
+    if (rc) return rc;
+    const uint32_t* img = nullptr;
+    if ((rc = fused_image(dev, legacy, &img))) return rc;
+    rc = rs_encode_copy_crc(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                            partial, q, stream);
+    if (rc) return rc;
+    const int J = static_cast<int>(bs / q / 1024);  // KiB per range
+    const DevImage* di = nullptr;
+    if ((rc = image(dev, legacy, 5, J, 8, false, &di))) return rc;
+    CrcArgs a{};
+    a.base = frags;
+    a.stripe_stride = ss;
+    a.frag_stride = fs;
+    a.payload_off = kHeaderBytes;
+    a.len = bs;
+    a.body = bs;
+    a.items = static_cast<int64_t>(nstripes) * nf;
+    a.nfrag = nf;
+    a.nspans = q;
+    a.J = J;
+    a.legacy = legacy ? 1 : 0;
+    a.c0 = zero_shift(CrcMachine(legacy), static_cast<uint64_t>(bs)).apply(~0u);
+    a.span_off = static_cast<uint32_t>(di->img.span_off);
+    a.t_off = static_cast<uint32_t>(di->img.t_off);
+    hipLaunchKernelGGL(crc_finalize_kernel, dim3(static_cast<unsigned>((a.items + 127) / 128)), dim3(128), 0,
+                       static_cast<hipStream_t>(stream), a, di->d, partial, nullptr,
+                       header_args(c, kChksumCrc32, bs, obj_size, 0));
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -322,7 +388,13 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
         dev_tune("frame_unfused") == 0) {
         // The object fills the k payloads exactly (no padding): one launch reads it, copies the
         // data into the payloads and writes the parity (10 MiB read + 14 MiB written per C3
-        // stripe instead of a separate split pass).
+        // stripe instead of a separate split pass) -- with CRC32 checksums, the same launch also
+        // folds the payload checksums (no re-read of the 14 MiB).
+        if (checksum == kChksumCrc32) {
+            rc = encode_crc_fused(dev, c, legacy_crc(), d_obj, obj_stride, obj_size, frags, stripe_stride,
+                                  frag_stride, bs, nstripes, stream);
+            if (rc != ECAMD_EINVAL) return rc;
+        }
         rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes,
                             stream);
         if (rc) return rc;

@@ -23,4 +23,13 @@ int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64
                    int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
                    void* stream);
 
+// rs_encode_copy with the payload CRC32s folded into the same launch (ecamd_frame_fused.hip):
+// d_img = build_fused_crc_image(machine, 8192) in device memory; r0 of range r (q ranges of
+// bs/q bytes) of payload f of stripe s -> d_partial[(s*(k+m) + f)*q + r].  ECAMD_EINVAL, with
+// nothing launched, when the shape does not fit (bs % 8192, q must divide bs/8192, one map pass).
+int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                       int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream);
+constexpr int crc_fused_words() { return 4 * 256 + 3 * 8 * 16 + 8 * 128; }  // fused image words
+
 }  // namespace ecamd

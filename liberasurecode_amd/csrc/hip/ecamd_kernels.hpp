@@ -60,6 +60,9 @@ template <int W, int KG, int CH, bool PF, bool NIB>
 __global__ void gf16_stream_kernel(const ApplyArgs a);
 template <int W, int KG>
 __global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
+struct FusedCrcArgs;
+template <int W, int KG>
+__global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>

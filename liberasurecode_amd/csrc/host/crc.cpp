@@ -1,6 +1,9 @@
 // crc.cpp -- checksum machines and device table images (see crc.hpp).
 #include "crc.hpp"
 
+#include <algorithm>
+#include <cstddef>
+
 #include <cstring>
 
 namespace ecamd {
@@ -84,6 +87,18 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
     field_tables(zero_shift(m, static_cast<uint64_t>(J) * 1024), 8, w + img.span_off);
     std::memcpy(w + img.t_off, m.t, sizeof(m.t));
     return img;
+}
+
+std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes)
+{
+    const CrcImage pieces = build_crc_image(m, 5, 4, 4, false);  // MB = 1 piece tables first
+    size_t pw = 4 * 256 + 3 * 8 * 16;
+    std::vector<uint32_t> w(pw + 8 * 128, 0);
+    std::copy(pieces.words.begin(), pieces.words.begin() + static_cast<std::ptrdiff_t>(pw), w.begin());
+    field_tables(zero_shift(m, tile_bytes), 4, w.data() + pw);
+    for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), 4, w.data() + pw + 128 * (1 + t));
+    field_tables(zero_shift(m, 1024), 4, w.data() + pw + 128 * 7);
+    return w;
 }
 
 }  // namespace ecamd
