@@ -146,6 +146,8 @@ struct Tuning {
                          // bits-4 dwords of a piece (5 measured best with crc_pos, tools/frame_bench.py)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
     int frame_crc_fused = 1;  // framed encode with CRC32: codec + checksums in one launch
+    int frame_crc_wgs = 0;    //   512-thread workgroups per CU (0 = 2)
+    int frame_crc_units = 0;  //   work units (stripe ranges) per CU to aim for (0 = 4)
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     int crc_span_kib = 128; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
@@ -187,6 +189,8 @@ int dev_tune(const char* key)
     if (k == "crc_pos") return g_tune.crc_pos;
     if (k == "crc_span_kib") return g_tune.crc_span_kib;
     if (k == "frame_crc_fused") return g_tune.frame_crc_fused;
+    if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
+    if (k == "frame_crc_units") return g_tune.frame_crc_units;
     return 0;
 }
 
@@ -728,7 +732,8 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     FusedCrcArgs c{d_img, d_partial, q, static_cast<int>(bs / kTile) / q, k + m};
     const int64_t units = static_cast<int64_t>(nstripes) * q;
-    const int wgs = std::max<int>(1, std::min<int>(2, kLdsBytes / static_cast<int>(lds)));
+    const int want = dev_tune("frame_crc_wgs") > 0 ? dev_tune("frame_crc_wgs") : 2;
+    const int wgs = std::max<int>(1, std::min<int>(want, kLdsBytes / static_cast<int>(lds)));
     const dim3 grid(static_cast<unsigned>(std::min<int64_t>(units, static_cast<int64_t>(cu_count(map->device)) * wgs)));
     const dim3 block(kThreads);
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -809,6 +814,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_span_kib = (value >= 4 && value <= 256) ? value / 4 * 4 : 128;  // 0: default
     } else if (k == "crc_pos") {
         g_tune.crc_pos = value;  // 0 off, anything else on
+    } else if (k == "frame_crc_wgs") {
+        g_tune.frame_crc_wgs = std::max(0, std::min(value, 4));
+    } else if (k == "frame_crc_units") {
+        g_tune.frame_crc_units = std::max(0, std::min(value, 64));
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_unfused") {

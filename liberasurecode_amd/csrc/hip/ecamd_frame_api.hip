@@ -314,7 +314,8 @@ int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64
     if (dev_tune("frame_crc_fused") == 0 || bs % 8192 || nstripes <= 0) return ECAMD_EINVAL;
     const int64_t tiles = bs / 8192;
     int q = 1;  // ranges per payload: enough work units to fill the chip, each a long sequential run
-    while (tiles % (2 * q) == 0 && static_cast<int64_t>(nstripes) * q < 4ll * dev_cu_count(dev)) q *= 2;
+    const int64_t per_cu = dev_tune("frame_crc_units") > 0 ? dev_tune("frame_crc_units") : 4;
+    while (tiles % (2 * q) == 0 && static_cast<int64_t>(nstripes) * q < per_cu * dev_cu_count(dev)) q *= 2;
     const int nf = c.k + c.m;
     uint32_t* partial = nullptr;
     int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * q, &partial);

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--fused-sweep", action="store_true")
     args = ap.parse_args()
     S, k, m, size = args.stripes, 10, 4, 10 * 1048576
     d = _lib.dev()
@@ -72,6 +73,17 @@ def main():
                           "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms / 1e6, 1)}),
               flush=True)
     d.ecamd_tune(b"frame_unfused", 0)
+    if args.fused_sweep:  # fused CRC encode geometry: workgroups per CU x work units per CU
+        fb.checksum = frame.CHKSUM_CRC32
+        for wgs in (1, 2, 3):
+            for units in (2, 4, 8, 16):
+                d.ecamd_tune(b"frame_crc_wgs", wgs)
+                d.ecamd_tune(b"frame_crc_units", units)
+                ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
+                print(json.dumps({"op": "frame_encode_fused_crc", "wgs": wgs, "units_per_cu": units,
+                                  "ms": round(ms, 3)}), flush=True)
+        d.ecamd_tune(b"frame_crc_wgs", 0)
+        d.ecamd_tune(b"frame_crc_units", 0)
     out = D.DeviceBuffer(fb.obj_stride * S)
     ms = timed(lambda: fb.decode([0, 1, 2, 3], out, stream=st), st, args.reps)
     print(json.dumps({"op": "frame_decode_4data", "ms": round(ms, 3),
