@@ -62,10 +62,19 @@ void* aligned_zero(size_t n)
     return p;
 }
 
-// header + payload, zeroed, magic set (alloc_fragment_buffer, :124-138)
-char* new_fragment(int payload)
+// header + payload, zeroed, magic set (alloc_fragment_buffer, :124-138).  zero_payload = false
+// zeroes the header only: for buffers whose payload the codec overwrites in full.
+char* new_fragment(int payload, bool zero_payload = true)
 {
-    char* f = static_cast<char*>(aligned_zero(static_cast<size_t>(payload) + kHdr));
+    const size_t n = static_cast<size_t>(payload) + kHdr;
+    char* f = nullptr;
+    if (zero_payload) {
+        f = static_cast<char*>(aligned_zero(n));
+    } else if (posix_memalign(reinterpret_cast<void**>(&f), 16, n) == 0) {
+        std::memset(f, 0, kHdr);
+    } else {
+        f = nullptr;
+    }
     if (f) hdr(f)->magic = LIBERASURECODE_FRAG_HEADER_MAGIC;
     return f;
 }
@@ -486,7 +495,9 @@ int prepare_decode(int k, int m, char** data, char** parity, const int* missing,
     int o = -1, p = -1;
     auto fix = [&](char*& slot, int idx) -> int {
         if (!slot) {
-            slot = new_fragment(static_cast<int>(frag_len - kHdr));
+            // this repo's RS codec (realign == false) writes every missing slot it is asked
+            // for in full and never reads the others, so they need no zeroing pass
+            slot = new_fragment(static_cast<int>(frag_len - kHdr), realign);
             if (!slot) return -ENOMEM;
             owned.push_back(slot);
         } else if (realign && (reinterpret_cast<uintptr_t>(slot) & 15u)) {
