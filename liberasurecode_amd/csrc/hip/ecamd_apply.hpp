@@ -161,6 +161,11 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
 
     auto fetch = [&](int j) -> uint4 {
         const uint8_t* p = in_frag<PTRS>(a, s, j) + off;
+        if (a.limited) {  // padded objects: bytes past in_len32[j] read as zeros
+            const int64_t lim = a.in_len32[j] - off < rem ? a.in_len32[j] - off : rem;
+            if (lim >= 16) return stream_load16<NT>(p);
+            return lim > 0 ? load_tail(p, static_cast<int>(lim)) : make_uint4(0, 0, 0, 0);
+        }
         return TAIL ? load_tail(p, rem) : stream_load16<NT>(p);
     };
     uint4 cur[4], nxt[4];

@@ -146,6 +146,7 @@ struct Tuning {
                          // bits-4 dwords of a piece (5 measured best with crc_pos, tools/frame_bench.py)
     int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
     int frame_crc_fused = 1;  // framed encode with CRC32: codec + checksums in one launch
+    int frame_copy_padded = 1;  // framed encode: copy-through also for objects shorter than k*bs
     int frame_crc_wgs = 0;    //   512-thread workgroups per CU (0 = 2)
     int frame_crc_units = 0;  //   work units (stripe ranges) per CU to aim for (0 = 4)
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
@@ -189,6 +190,7 @@ int dev_tune(const char* key)
     if (k == "crc_pos") return g_tune.crc_pos;
     if (k == "crc_span_kib") return g_tune.crc_span_kib;
     if (k == "frame_crc_fused") return g_tune.frame_crc_fused;
+    if (k == "frame_copy_padded") return g_tune.frame_copy_padded;
     if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
     return 0;
@@ -596,7 +598,8 @@ namespace {
 int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
                    const std::vector<int64_t>& in_off, uint8_t* out_base, int64_t out_stride,
                    const std::vector<int64_t>& out_off, uint8_t* copy_base, int64_t copy_stride,
-                   const std::vector<int64_t>& copy_off, int64_t bs, int nstripes, void* stream)
+                   const std::vector<int64_t>& copy_off, int64_t bs, int nstripes, void* stream,
+                   const std::vector<int64_t>* in_len = nullptr)
 {
     const ecamd_map* map = e.map.get();
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -616,7 +619,11 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         for (int j = 0; j < p.ncols; j++) {
             a.in_off[j] = in_off[p.col0 + j];
             a.copy_off[j] = copy_off[p.col0 + j];
+            a.in_len32[j] = static_cast<int32_t>(in_len ? (*in_len)[p.col0 + j] : bs);
+            if (a.in_len32[j] < bs) a.limited = 1;
         }
+        a.min_len = bs;
+        for (int j = 0; j < p.ncols; j++) a.min_len = std::min<int64_t>(a.min_len, a.in_len32[j]);
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
         Geometry g;
         int rc;
@@ -662,27 +669,40 @@ bool copy_aligned(const void* obj, const void* payload0, int64_t obj_stride, int
            stripe_stride % 16 == 0 && frag_stride % 16 == 0 && bs % 16 == 0;
 }
 
+// Copy-through encode from objects whose k chunks of bs bytes start at unaligned object offsets
+// (j*bs, bs even but not a multiple of 16) and may end early (objects shorter than k*bs): the
+// payload side stays 16-byte aligned, the object side is read with unaligned 16-byte loads.
+bool copy_aligned_payloads(const void* obj, const void* payload0, int64_t obj_stride,
+                           int64_t stripe_stride, int64_t frag_stride, int64_t bs)
+{
+    return aligned16(obj) && aligned16(payload0) && obj_stride % 16 == 0 && stripe_stride % 16 == 0 &&
+           frag_stride % 16 == 0 && bs % 2 == 0;
+}
+
 }  // namespace
 
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                   void* stream)
+                   void* stream, int64_t obj_size)
 {
     std::shared_ptr<RsEntry> e;
     int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
     if (rc) return rc;
     if (!e->map || nstripes <= 0 || bs <= 0) return 0;
-    if (!copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
+    if (obj_size < 0) obj_size = k * bs;
+    if (obj_size > k * bs || !copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
         return fail(ECAMD_EINVAL, "copy-through encode needs 16-byte aligned objects and payloads");
-    std::vector<int64_t> in_off, out_off, copy_off;
+    std::vector<int64_t> in_off, out_off, copy_off, in_len;
     for (int i : e->inputs) {
         in_off.push_back(static_cast<int64_t>(i) * bs);
         copy_off.push_back(static_cast<int64_t>(i) * frag_stride);
+        in_len.push_back(std::max<int64_t>(0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(i) * bs)));
     }
     for (int o : e->outputs) out_off.push_back(static_cast<int64_t>(o) * frag_stride);
     auto* p0 = static_cast<uint8_t*>(payload0);
     return map_apply_copy(*e, static_cast<const uint8_t*>(obj), obj_stride, in_off, p0,
-                          stripe_stride, out_off, p0, stripe_stride, copy_off, bs, nstripes, stream);
+                          stripe_stride, out_off, p0, stripe_stride, copy_off, bs, nstripes, stream,
+                          &in_len);
 }
 
 // rs_encode_copy with the payload CRC32 folded in (gf16_frame_crc_kernel): r0 of range r of
@@ -818,6 +838,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_wgs = std::max(0, std::min(value, 4));
     } else if (k == "frame_crc_units") {
         g_tune.frame_crc_units = std::max(0, std::min(value, 64));
+    } else if (k == "frame_copy_padded") {
+        g_tune.frame_copy_padded = value;  // 0 off, anything else on
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_unfused") {

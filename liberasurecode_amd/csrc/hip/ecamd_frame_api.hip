@@ -403,6 +403,18 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
                        frag_stride, kHeaderBytes, k + m, bs, nstripes, nullptr,
                        header_args(c, checksum, bs, obj_size, 0), stream);
     }
+    if (backend == kBackendRs && a16(d_obj) && obj_stride % 16 == 0 && dev_tune("frame_unfused") == 0 &&
+        dev_tune("frame_copy_padded") != 0) {
+        // Objects that do not fill the payloads exactly (any size: Swift's 1 MiB segments give
+        // bs = 104858): the same copy-through launch reads each chunk j*bs of the object with
+        // unaligned loads and reads zeros past the object's end, so no split pass either.
+        rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes,
+                            stream, static_cast<int64_t>(obj_size));
+        if (rc) return rc;
+        return run_crc(dev, legacy_crc(), checksum == kChksumCrc32, frags, stripe_stride,
+                       frag_stride, kHeaderBytes, k + m, bs, nstripes, nullptr,
+                       header_args(c, checksum, bs, obj_size, 0), stream);
+    }
     SplitArgs sa{static_cast<const uint8_t*>(d_obj), obj_stride, static_cast<int64_t>(obj_size),
                  frags, stripe_stride, frag_stride, bs, k, nstripes, aligned ? 1 : 0};
     hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),

@@ -85,8 +85,8 @@ __device__ __forceinline__ void mac_chunk_nib_imm(const uint8_t* lds, v4u x, uin
 struct StreamTile {
     __amdgpu_buffer_rsrc_t rin;
     __amdgpu_buffer_rsrc_t rcopy;
-    int off;
-    int cstride;
+    int off;      // this lane's byte offset in a fragment
+    int cstride;  // bytes between a lane's chunks
 };
 
 template <int W, int CH, int J, bool NIB>
@@ -174,7 +174,10 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
     for (uint32_t t = t0; t < t1; t += dt) {
         const uint32_t s = t / a.tiles_per_stripe;
         const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
-        if (toff + span > a.bs) {  // last, partial tile of each fragment
+        // last, partial tile of each fragment -- and, for objects shorter than the k payloads
+        // (ApplyArgs::limited), every tile reaching past the shortest input's end: the byte-exact
+        // per-chunk path reads zeros there
+        if (toff + span > a.bs || (a.limited && toff + span > a.min_len)) {
 #pragma unroll
             for (int c = 0; c < CH; c++) {
                 const int64_t o = toff + c * cstride + static_cast<int64_t>(threadIdx.x) * 16;
@@ -279,7 +282,10 @@ __global__ void __launch_bounds__(1024) gf16_ptrs_stream_kernel(const ApplyArgs 
         const uint32_t s = t / a.tiles_per_stripe;
         const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
         const int64_t o64 = toff + static_cast<int64_t>(threadIdx.x) * 16;
-        if (toff + span > a.bs) {  // last, partial tile of each fragment
+        // last, partial tile of each fragment -- and, for objects shorter than the k payloads
+        // (ApplyArgs::limited), every tile reaching past the shortest input's end: the byte-exact
+        // per-chunk path reads zeros there
+        if (toff + span > a.bs || (a.limited && toff + span > a.min_len)) {
             const int64_t rem = a.bs - o64;
             if (rem >= 16)
                 apply_tile<W, true, true, false, false, false>(a, lds, s, o64, 16);

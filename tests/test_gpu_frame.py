@@ -398,3 +398,27 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, monkeypatc
     if bs <= (1 << 16):
         want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
         assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
+
+
+@pytest.mark.parametrize("k,m,size", [(10, 4, 1 << 20), (10, 4, (1 << 20) + 7), (10, 4, 3 * 104858 + 5),
+                                      (4, 2, 1), (4, 2, 100), (6, 3, 6 * 4096 - 2), (8, 4, 777777),
+                                      (20, 8, 4096 * 20 + 40), (12, 6, 65536 * 12 - 24)])
+@pytest.mark.parametrize("ct", [1, 2])
+def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
+    """Objects that do not fill the k payloads (any size; Swift's 1 MiB segments at k=10 give
+    bs = 104858): the copy-through launch reads the object's chunks at unaligned offsets and zeros
+    past its end.  Fragments equal the split-then-encode path's and the restated framing."""
+    from liberasurecode_amd import _lib
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    S = 3
+    objs = _objects(S, size, k * 13 + m + size)
+    out = []
+    for padded in (1, 0):
+        _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
+        fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        out.append(fb.fragments())
+    _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
+    assert np.array_equal(out[0], out[1])
+    want = expected_stripe(be, k, m, 0, objs[1], ct)
+    assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))

@@ -84,6 +84,23 @@ def main():
                                   "ms": round(ms, 3)}), flush=True)
         d.ecamd_tune(b"frame_crc_wgs", 0)
         d.ecamd_tune(b"frame_crc_units", 0)
+    # objects that do not fill the payloads: Swift's default 1 MiB EC segments (bs = 104858) and a
+    # C3 object 6 bytes short -- copy-through with zero padding vs split + encode
+    for size2, S2, tag in (((1 << 20), 2560, "swift_1MiB_segment"), (k * (1 << 20) - 6, S, "c3_minus_6B")):
+        fb2 = frame.FrameBatch(6, k, m, size2, S2)
+        obj2 = D.DeviceBuffer(fb2.obj_stride * S2)
+        _lib.check(d.ecamd_fill_splitmix(obj2.ptr, fb2.obj_stride, 0, 1, size2, S2, 0, 0xB0B, st.handle), "fill")
+        for padded, ct in ((1, frame.CHKSUM_NONE), (0, frame.CHKSUM_NONE), (1, frame.CHKSUM_CRC32),
+                           (0, frame.CHKSUM_CRC32)):
+            fb2.checksum = ct
+            d.ecamd_tune(b"frame_copy_padded", padded)
+            ms = timed(lambda: fb2.encode(obj2, stream=st), st, args.reps)
+            print(json.dumps({"op": "frame_encode_" + tag, "copy_padded": padded, "checksum": ct,
+                              "ms": round(ms, 3), "GiBps_object": round(S2 * size2 / (ms / 1e3) / 2**30, 1)}),
+                  flush=True)
+        d.ecamd_tune(b"frame_copy_padded", 1)
+        obj2.free()
+        fb2.buf.free()
     out = D.DeviceBuffer(fb.obj_stride * S)
     ms = timed(lambda: fb.decode([0, 1, 2, 3], out, stream=st), st, args.reps)
     print(json.dumps({"op": "frame_decode_4data", "ms": round(ms, 3),
