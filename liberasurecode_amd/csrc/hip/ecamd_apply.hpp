@@ -38,9 +38,11 @@ __device__ __forceinline__ void stream_store16(uint8_t* p, uint4 v)
     }
 }
 
-// Partial 16-byte chunk at the end of a fragment: bytes [0, rem) of p, zero filled.
+// Partial 16-byte chunk at the end of a fragment: bytes [0, rem) of p, zero filled (rem >= 16:
+// one 16-byte load).
 __device__ __forceinline__ uint4 load_tail(const uint8_t* p, int rem)
 {
+    if (rem >= 16) return *reinterpret_cast<const uint4*>(p);
     uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < 16; i++) {
@@ -52,6 +54,10 @@ __device__ __forceinline__ uint4 load_tail(const uint8_t* p, int rem)
 
 __device__ __forceinline__ void store_tail(uint8_t* p, uint4 v, int rem)
 {
+    if (rem >= 16) {
+        *reinterpret_cast<uint4*>(p) = v;
+        return;
+    }
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 16; i++)
@@ -182,10 +188,12 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
                     if (a.copy_off[j0 + i] >= 0) {  // wave-uniform
                         uint8_t* c = a.copy_base + static_cast<int64_t>(s) * a.copy_stride +
                                      a.copy_off[j0 + i] + off;
-                        if (TAIL)
-                            store_tail(c, cur[i], rem);
-                        else
+                        const int64_t lim = a.limited && a.copy_len32[j0 + i] - off < rem
+                                                ? a.copy_len32[j0 + i] - off : rem;
+                        if (lim >= 16 && !TAIL)
                             stream_store16<NT>(c, cur[i]);
+                        else if (lim > 0)
+                            store_tail(c, cur[i], static_cast<int>(lim < 16 ? lim : 16));
                     }
                 }
                 if constexpr (NIB)
@@ -208,15 +216,18 @@ __device__ __forceinline__ void apply_tile(const ApplyArgs& a, const uint8_t* ld
         }
         uint4 v = make_uint4(o[0], o[1], o[2], o[3]);
         uint8_t* q = out_frag<PTRS>(a, s, r) + off;
+        // limited outputs (decode straight into objects shorter than k*bs): nothing past out_len32
+        const int64_t lim = a.limited && a.out_len32[r] - off < rem ? a.out_len32[r] - off : rem;
+        if (lim <= 0) continue;
         if (a.accumulate) {
-            uint4 prev = TAIL ? load_tail(q, rem) : load16(q);
+            uint4 prev = (TAIL || lim < 16) ? load_tail(q, static_cast<int>(lim < 16 ? lim : 16)) : load16(q);
             v.x ^= prev.x;
             v.y ^= prev.y;
             v.z ^= prev.z;
             v.w ^= prev.w;
         }
-        if (TAIL)
-            store_tail(q, v, rem);
+        if (TAIL || lim < 16)
+            store_tail(q, v, static_cast<int>(lim < 16 ? lim : 16));
         else
             stream_store16<NT>(q, v);
     }

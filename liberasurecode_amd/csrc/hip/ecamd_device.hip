@@ -599,7 +599,9 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
                    const std::vector<int64_t>& in_off, uint8_t* out_base, int64_t out_stride,
                    const std::vector<int64_t>& out_off, uint8_t* copy_base, int64_t copy_stride,
                    const std::vector<int64_t>& copy_off, int64_t bs, int nstripes, void* stream,
-                   const std::vector<int64_t>* in_len = nullptr)
+                   const std::vector<int64_t>* in_len = nullptr,
+                   const std::vector<int64_t>* out_len = nullptr,
+                   const std::vector<int64_t>* copy_len = nullptr)
 {
     const ecamd_map* map = e.map.get();
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -620,10 +622,17 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
             a.in_off[j] = in_off[p.col0 + j];
             a.copy_off[j] = copy_off[p.col0 + j];
             a.in_len32[j] = static_cast<int32_t>(in_len ? (*in_len)[p.col0 + j] : bs);
-            if (a.in_len32[j] < bs) a.limited = 1;
+            a.copy_len32[j] = static_cast<int32_t>(copy_len ? (*copy_len)[p.col0 + j] : bs);
         }
+        for (int r = 0; r < a.nrows; r++)
+            a.out_len32[r] = static_cast<int32_t>(out_len ? (*out_len)[p.row0 + r] : bs);
         a.min_len = bs;
-        for (int j = 0; j < p.ncols; j++) a.min_len = std::min<int64_t>(a.min_len, a.in_len32[j]);
+        for (int j = 0; j < p.ncols; j++) {
+            a.min_len = std::min<int64_t>(a.min_len, a.in_len32[j]);
+            if (a.copy_off[j] >= 0) a.min_len = std::min<int64_t>(a.min_len, a.copy_len32[j]);
+        }
+        for (int r = 0; r < a.nrows; r++) a.min_len = std::min<int64_t>(a.min_len, a.out_len32[r]);
+        a.limited = a.min_len < bs ? 1 : 0;
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
         Geometry g;
         int rc;
@@ -779,24 +788,34 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
 
 int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
                    int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
-                   void* stream)
+                   void* stream, int64_t obj_size)
 {
     std::shared_ptr<RsEntry> e;
     int rc = rs_entry(1, k, m, missing, 0, -1, e);
     if (rc) return rc;
     if (!e->map || nstripes <= 0 || bs <= 0)
         return fail(ECAMD_EINVAL, "decode-join needs at least one missing data fragment");
-    if (!copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
+    if (obj_size < 0) obj_size = k * bs;
+    if (obj_size > k * bs || !copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
         return fail(ECAMD_EINVAL, "decode-join needs 16-byte aligned objects and payloads");
-    std::vector<int64_t> in_off, out_off, copy_off;
+    // object chunk j = [j*bs, j*bs + len_j): shorter (or empty) past the object's end
+    auto chunk = [&](int j) {
+        return std::max<int64_t>(0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(j) * bs));
+    };
+    std::vector<int64_t> in_off, out_off, copy_off, out_len, copy_len;
     for (int i : e->inputs) {
         in_off.push_back(static_cast<int64_t>(i) * frag_stride);
         copy_off.push_back(i < k ? static_cast<int64_t>(i) * bs : -1);  // parity is not copied
+        copy_len.push_back(i < k ? chunk(i) : bs);
     }
-    for (int o : e->outputs) out_off.push_back(static_cast<int64_t>(o) * bs);
+    for (int o : e->outputs) {
+        out_off.push_back(static_cast<int64_t>(o) * bs);
+        out_len.push_back(chunk(o));
+    }
     auto* ob = static_cast<uint8_t*>(obj);
     return map_apply_copy(*e, static_cast<const uint8_t*>(payload0), stripe_stride, in_off, ob,
-                          obj_stride, out_off, ob, obj_stride, copy_off, bs, nstripes, stream);
+                          obj_stride, out_off, ob, obj_stride, copy_off, bs, nstripes, stream, nullptr,
+                          &out_len, &copy_len);
 }
 
 }  // namespace ecamd

@@ -462,11 +462,13 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     auto* frags = static_cast<uint8_t*>(d_frags);
     uint8_t* p0 = frags + kHeaderBytes;
     if (data_missing && backend == kBackendRs && d_obj && a16(d_obj) && obj_stride % 16 == 0 &&
-        bs % 16 == 0 && static_cast<int64_t>(obj_size) == k * bs && dev_tune("frame_unfused") == 0) {
+        dev_tune("frame_unfused") == 0 &&
+        (static_cast<int64_t>(obj_size) == k * bs || dev_tune("frame_copy_padded") != 0)) {
         // One launch: the lost data are computed straight into the objects and the surviving data
-        // payloads are copied there as they stream through (no separate join pass).
+        // payloads are copied there as they stream through (no separate join pass); objects of
+        // any size (unaligned chunk offsets j*bs, nothing written past an object's end).
         return rs_decode_join(k, m, missing, p0, stripe_stride, frag_stride, d_obj, obj_stride, bs,
-                              nstripes, stream);
+                              nstripes, stream, static_cast<int64_t>(obj_size));
     }
     if (data_missing) {  // the systematic fast path (src/erasurecode.c:597-607) skips this
         if (backend == kBackendRs)

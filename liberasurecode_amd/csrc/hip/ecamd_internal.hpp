@@ -21,9 +21,10 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
 // rs_vand decode straight into objects: the missing data fragments (at least one, -1 terminated
 // `missing`) are computed into their object positions (j*bs) and the available data inputs are
 // copied there by the same launch (fragments_to_string without a separate join pass).
+// Objects of obj_size bytes (< 0: k*bs): nothing is written past an object's end.
 int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
                    int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
-                   void* stream);
+                   void* stream, int64_t obj_size = -1);
 
 // rs_encode_copy with the payload CRC32s folded into the same launch (ecamd_frame_fused.hip):
 // d_img = build_fused_crc_image(machine, 8192) in device memory; r0 of range r (q ranges of

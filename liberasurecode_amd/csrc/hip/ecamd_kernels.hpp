@@ -34,9 +34,10 @@ struct ApplyArgs {
     int32_t in_off32[kMaxCols];       // in_off / out_off as 32-bit buffer offsets
     int32_t out_off32[kMaxRows];
     int limited;                      // 1: input j holds only in_len32[j] valid bytes (the rest
-    int32_t in_len32[kMaxCols];       //   of its blocksize reads as zeros): objects shorter than
-    int64_t min_len;                  //   the k payloads (prepare_fragments_for_encode padding);
-                                      //   min_len = the smallest in_len32
+    int32_t in_len32[kMaxCols];       //   of its blocksize reads as zeros), output r / copy j take
+    int32_t out_len32[kMaxRows];      //   only out_len32[r] / copy_len32[j] bytes: objects shorter
+    int32_t copy_len32[kMaxCols];     //   than the k payloads (encode padding, decode into objects);
+    int64_t min_len;                  //   min_len = the smallest of them (tiles past it go byte-exact)
     uint32_t copy_records;            // gf16_stream_kernel copy-through: 0 = off; else range of
     int32_t copy_off32[kMaxCols];     //   copy_base per stripe and 32-bit copy_off (< 0: skip)
     int tile_order;                   // gf16_stream_kernel: 1 = contiguous tile range per workgroup

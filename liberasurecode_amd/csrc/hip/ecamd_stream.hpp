@@ -182,15 +182,13 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
             for (int c = 0; c < CH; c++) {
                 const int64_t o = toff + c * cstride + static_cast<int64_t>(threadIdx.x) * 16;
                 const int64_t rem = a.bs - o;
-                if (a.copy_records) {  // copy-through launches (framed encode / decode-join)
-                    if (rem >= 16)
-                        apply_tile<W, false, true, NIB, true, false>(a, lds, s, o, 16);
-                    else if (rem > 0)
-                        apply_tile<W, false, true, NIB, true, true>(a, lds, s, o, static_cast<int>(rem));
-                } else if (rem >= 16) {
-                    apply_tile<W, false, true, NIB, false, false>(a, lds, s, o, 16);
-                } else if (rem > 0) {
-                    apply_tile<W, false, true, NIB, false, true>(a, lds, s, o, static_cast<int>(rem));
+                // byte-exact chunk path (load_tail / store_tail take whole chunks in one access)
+                const int rc = static_cast<int>(rem < 16 ? rem : 16);
+                if (rem <= 0) {
+                } else if (a.copy_records) {  // copy-through launches (framed encode / decode-join)
+                    apply_tile<W, false, true, NIB, true, true>(a, lds, s, o, rc);
+                } else {
+                    apply_tile<W, false, true, NIB, false, true>(a, lds, s, o, rc);
                 }
             }
             continue;

@@ -422,3 +422,32 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
     assert np.array_equal(out[0], out[1])
     want = expected_stripe(be, k, m, 0, objs[1], ct)
     assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
+
+
+@pytest.mark.parametrize("k,m,size,missing", [(10, 4, 1 << 20, [0, 1, 2, 3]), (10, 4, (1 << 20) + 7, [9, 3, 11]),
+                                              (4, 2, 100, [3]), (4, 2, 5, [0, 1]), (6, 3, 6 * 4096 - 2, [5, 6]),
+                                              (8, 4, 777777, [7, 0, 8, 9]), (12, 6, 65536 * 12 - 24, [11, 10, 1])])
+def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
+    """Decode straight into objects that do not fill the payloads: unaligned object chunks, nothing
+    written past an object's end (guard bytes between objects stay intact)."""
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    S = 3
+    objs = _objects(S, size, k * 17 + m + size)
+    fb = F.FrameBatch(be, k, m, size, S)
+    fb.encode(_upload_objects(objs, fb.obj_stride))
+    stride = (size + 16 + 15) // 16 * 16  # 16+ guard bytes after every object
+    got = []
+    for padded in (1, 0):
+        _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
+        host = np.full(S * stride, 0xA5, dtype=np.uint8)
+        d = DeviceBuffer(host.size)
+        d.upload(host)
+        fb.decode(missing, d, obj_stride=stride)
+        got.append(d.download().reshape(S, stride))
+    _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
+    assert np.array_equal(got[0], got[1])
+    for s in range(S):
+        assert got[0][s, :size].tobytes() == objs[s]
+        assert (got[0][s, size:] == 0xA5).all()

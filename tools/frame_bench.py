@@ -98,7 +98,14 @@ def main():
             print(json.dumps({"op": "frame_encode_" + tag, "copy_padded": padded, "checksum": ct,
                               "ms": round(ms, 3), "GiBps_object": round(S2 * size2 / (ms / 1e3) / 2**30, 1)}),
                   flush=True)
+        out2 = D.DeviceBuffer(fb2.obj_stride * S2)
+        for padded in (1, 0):
+            d.ecamd_tune(b"frame_copy_padded", padded)
+            ms = timed(lambda: fb2.decode([0, 1, 2, 3], out2, stream=st), st, args.reps)
+            print(json.dumps({"op": "frame_decode_4data_" + tag, "copy_padded": padded, "ms": round(ms, 3),
+                              "GiBps_object": round(S2 * size2 / (ms / 1e3) / 2**30, 1)}), flush=True)
         d.ecamd_tune(b"frame_copy_padded", 1)
+        out2.free()
         obj2.free()
         fb2.buf.free()
     out = D.DeviceBuffer(fb.obj_stride * S)
