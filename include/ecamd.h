@@ -170,6 +170,10 @@ int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void *d_dst, cons
  * blocksize must be a multiple of threads*16*ch; stripe stride < 2 GiB. */
 int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d_base,
                           int64_t blocksize, int K, int R, int nstripes, void *stream);
+/* Lookup-engine probe: random 16-byte lookups into four 4 KiB tables (d_table, 16 KiB) from LDS
+ * (mode 0), from global memory through the vector L1 (1) or half each (2); grid = CUs x wgs_per_cu
+ * workgroups of 256 lanes, iters x 4 lookups per lane. */
+int ecamd_debug_lookup_probe(int mode, int wgs_per_cu, int iters, const void *d_table, void *stream);
 /* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup) and the
  * chunk layout (wave_contig 1: a wave's ch chunks are 1 KiB apart, contiguous) as parameters. */
 int ecamd_debug_mix_probe2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,

@@ -113,7 +113,12 @@ int ensure_device(int* dev_out)
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 3>),                   \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4>),                   \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5>)
-        const void* fk[] = {KF_(2), KF_(4), KF_(8)};
+        const void* fk[] = {KF_(2), KF_(4), KF_(8),
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<1>),
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<4>),
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>)};
 #undef KF_
         for (const void* k : fk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
@@ -157,6 +162,7 @@ struct Tuning {
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
                             // measured best, tools/xor_sweep.py)
+    int stream_hybrid = 1;  //   8-output passes: one input in 4 looks its hi table up via L1
     int stream_order = 0;   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     int stream_nib = 0;     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     int stream_pf = 0;      //   next group's loads issued before the lookups (1) or after (0);
@@ -328,6 +334,17 @@ int launch_stream_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipSt
 int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3 grid, dim3 block,
                   size_t lds, hipStream_t st)
 {
+    if (width == 8 && !nib && g_tune.stream_hybrid) {  // LDS + L1 lookups (gf16_hybrid_kernel)
+        switch ((a.ncols + 3) / 4) {
+        case 1: hipLaunchKernelGGL((gf16_hybrid_kernel<1>), grid, block, lds, st, a); break;
+        case 2: hipLaunchKernelGGL((gf16_hybrid_kernel<2>), grid, block, lds, st, a); break;
+        case 3: hipLaunchKernelGGL((gf16_hybrid_kernel<3>), grid, block, lds, st, a); break;
+        case 4: hipLaunchKernelGGL((gf16_hybrid_kernel<4>), grid, block, lds, st, a); break;
+        default: hipLaunchKernelGGL((gf16_hybrid_kernel<5>), grid, block, lds, st, a); break;
+        }
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (nib) {  // a.tables is the nibble image
         if (width == 2) return launch_stream_w<2, 1, false, true>(a, grid, block, lds, st);
         if (width == 4) return launch_stream_w<4, 1, false, true>(a, grid, block, lds, st);
@@ -869,6 +886,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_ch = value == 2 ? 2 : 1;
     } else if (k == "xor_wgs") {
         g_tune.xor_wgs = std::max(0, std::min(value, 8));
+    } else if (k == "stream_hybrid") {
+        g_tune.stream_hybrid = value;
     } else if (k == "stream_order") {
         g_tune.stream_order = std::max(0, std::min(value, 3));
     } else if (k == "stream_nib") {
@@ -1219,6 +1238,25 @@ int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void* dst, const 
     case 1: hipLaunchKernelGGL(bw_probe_kernel<1>, grid, block, 0, st, d, s, bytes, kind, sink); break;
     case 4: hipLaunchKernelGGL(bw_probe_kernel<4>, grid, block, 0, st, d, s, bytes, kind, sink); break;
     default: hipLaunchKernelGGL(bw_probe_kernel<8>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_debug_lookup_probe(int mode, int wgs_per_cu, int iters, const void* d_table, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    static uint32_t* sink = nullptr;
+    if (!sink) HIP_TRY(hipMalloc(&sink, 64));
+    const dim3 grid(cu_count(dev) * std::max(1, wgs_per_cu)), block(256);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const auto* t = static_cast<const uint4*>(d_table);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(lookup_probe_kernel<0>, grid, block, 0, st, t, iters, sink); break;
+    case 1: hipLaunchKernelGGL(lookup_probe_kernel<1>, grid, block, 0, st, t, iters, sink); break;
+    default: hipLaunchKernelGGL(lookup_probe_kernel<2>, grid, block, 0, st, t, iters, sink); break;
     }
     HIP_TRY(hipGetLastError());
     return 0;

@@ -65,6 +65,8 @@ template <int W, int KG, int CH, bool PF, bool NIB>
 __global__ void gf16_stream_kernel(const ApplyArgs a);
 template <int W, int KG>
 __global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
+template <int KG>
+__global__ void gf16_hybrid_kernel(const ApplyArgs a);
 struct FusedCrcArgs;
 template <int W, int KG>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);
@@ -94,6 +96,9 @@ struct MixArgs {
     X(1, 0) X(1, 2) X(16, 2) X(18, 2) X(3, 2) X(18, 18)
 template <int LP, int SP, int CH>
 __global__ void mix_probe_kernel(MixArgs a);
+
+template <int MODE>
+__global__ void lookup_probe_kernel(const uint4* __restrict__ table, int iters, uint32_t* sink);
 
 template <int U>
 __global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int kind,

@@ -257,3 +257,44 @@ ECAMD_MIX_POLICIES(ECAMD_MIX)
 #undef ECAMD_MIX
 
 }  // namespace ecamd
+
+namespace ecamd {
+
+// Table-lookup engine probe (sweeps only): random 16-byte lookups into 4 KiB tables, from LDS
+// (MODE 0), from global memory through the CU's vector L1 (MODE 1), or half and half (MODE 2),
+// 4 lookups per xorshift step.  Prices the L1 as a second lookup engine beside the LDS.
+template <int MODE>
+__global__ void __launch_bounds__(256) lookup_probe_kernel(const uint4* __restrict__ table, int iters,
+                                                           uint32_t* sink)
+{
+    __shared__ uint4 tab[1024];  // 4 tables x 256 entries x 16 B
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = table[i];
+    __syncthreads();
+    uint32_t x = 0x9e3779b9u ^ (blockIdx.x * 1024 + threadIdx.x) * 0x85ebca6bu;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int it = 0; it < iters; it++) {
+        x ^= x << 13;
+        x ^= x >> 17;
+        x ^= x << 5;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t idx = b * 256 + ((x >> (8 * b)) & 0xffu);
+            uint4 e;
+            if (MODE == 0 || (MODE == 2 && (b & 1)))
+                e = tab[idx];
+            else
+                e = table[idx];
+            acc.x ^= e.x;
+            acc.y ^= e.y;
+            acc.z ^= e.z;
+            acc.w ^= e.w;
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = acc.x;
+}
+
+template __global__ void lookup_probe_kernel<0>(const uint4*, int, uint32_t*);
+template __global__ void lookup_probe_kernel<1>(const uint4*, int, uint32_t*);
+template __global__ void lookup_probe_kernel<2>(const uint4*, int, uint32_t*);
+
+}  // namespace ecamd

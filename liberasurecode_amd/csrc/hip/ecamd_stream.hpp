@@ -89,7 +89,64 @@ struct StreamTile {
     int cstride;  // bytes between a lane's chunks
 };
 
-template <int W, int CH, int J, bool NIB>
+// Hybrid lookups (TM >= 2, 8-output passes): some table lookups of each group of 4 inputs are
+// read through the vector L1 (plain global loads of the same image) instead of the LDS, so the
+// two lookup engines work side by side -- random 16-byte lookups run ~5.4 per clock per CU from
+// LDS and ~2 from L1 (tools/lookup_probe.py).  The L1 lookups are all issued at the start of the
+// group and consumed after the other inputs' LDS lookups, so their latency overlaps LDS work.
+// hyb_fetch: words 0..N-1 of input J's lo (HI = 0) or hi (HI = 1) byte table.
+template <int W, int J, int HI, int N>
+__device__ __forceinline__ void hyb_fetch(const uint8_t* gtab, v4u x, uint32_t (&e)[N][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int S = log2i(2 * W);
+    constexpr int T = J * 512 * 2 * W + HI * 256 * 2 * W;
+#pragma unroll
+    for (int w = 0; w < N; w++) {
+        const uint32_t v = x[w >> 1];
+        if (w & 1)
+            lds_entry<D>(gtab + T + byte_shl<2 + HI, S>(v), e[w]);
+        else
+            lds_entry<D>(gtab + T + byte_shl<0 + HI, S>(v), e[w]);
+    }
+}
+
+// mac_chunk_imm with the first NL lo and NH hi lookups taken from registers (hyb_fetch).
+template <int W, int J, int NL, int NH>
+__device__ __forceinline__ void mac_chunk_mixed(const uint8_t* lds, v4u x, const uint32_t (&el)[NL ? NL : 1][W / 2],
+                                                const uint32_t (&eh)[NH ? NH : 1][W / 2],
+                                                uint32_t (&acc)[8][W / 2])
+{
+    constexpr int D = W / 2;
+    constexpr int S = log2i(2 * W);
+    constexpr int TL = J * 512 * 2 * W;
+    constexpr int TH = TL + 256 * 2 * W;
+#pragma unroll
+    for (int w = 0; w < 8; w++) {
+        const uint32_t v = x[w >> 1];
+        uint32_t e0[D], e1[D];
+        if (w < NL) {
+#pragma unroll
+            for (int d = 0; d < D; d++) e0[d] = el[w < NL ? w : 0][d];
+        } else if (w & 1) {
+            lds_entry<D>(lds + TL + byte_shl<2, S>(v), e0);
+        } else {
+            lds_entry<D>(lds + TL + byte_shl<0, S>(v), e0);
+        }
+        if (w < NH) {
+#pragma unroll
+            for (int d = 0; d < D; d++) e1[d] = eh[w < NH ? w : 0][d];
+        } else if (w & 1) {
+            lds_entry<D>(lds + TH + byte_shl<3, S>(v), e1);
+        } else {
+            lds_entry<D>(lds + TH + byte_shl<1, S>(v), e1);
+        }
+#pragma unroll
+        for (int d = 0; d < D; d++) acc[w][d] = xor3(acc[w][d], e0[d], e1[d]);
+    }
+}
+
+template <int W, int CH, int J, int TM>
 __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds, const StreamTile& t,
                                           const v4u (&x)[CH], uint32_t (&acc)[CH][8][W / 2])
 {
@@ -102,7 +159,7 @@ __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds
         }
 #pragma unroll
         for (int c = 0; c < CH; c++) {
-            if constexpr (NIB)
+            if constexpr (TM == 1)
                 mac_chunk_nib_imm<W, J>(lds, x[c], acc[c]);
             else
                 mac_chunk_imm<W, J>(lds, x[c], acc[c]);
@@ -125,30 +182,47 @@ __device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile&
 
 // Group G's lookups; with PF the loads of group G+1 are issued before them (in flight during the
 // lookups), without PF after them (each wave: load, wait, look up -- latency hidden by occupancy).
-template <int W, int CH, int G, int KG, bool PF, bool NIB>
+template <int W, int CH, int G, int KG, bool PF, int TM>
 __device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* lds, const StreamTile& t,
                                              v4u (&cur)[4][CH], uint32_t (&acc)[CH][8][W / 2])
 {
     v4u nxt[4][CH];
     if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG>(a, t, nxt);
-    input_mac<W, CH, 4 * G + 0, NIB>(a, lds, t, cur[0], acc);
-    input_mac<W, CH, 4 * G + 1, NIB>(a, lds, t, cur[1], acc);
-    input_mac<W, CH, 4 * G + 2, NIB>(a, lds, t, cur[2], acc);
-    input_mac<W, CH, 4 * G + 3, NIB>(a, lds, t, cur[3], acc);
+    if constexpr (TM == 2 && CH == 1) {
+        // input 0's hi table via L1 (12.5% of the lookups; taking 3/16 -- input 2's hi for words
+        // 0..3, or input 0's lo for words 0..3 -- measured 12% slower than none: a 40 KiB table
+        // footprint no longer fits the 32 KiB L1)
+        uint32_t eh0[8][W / 2], dummy[1][W / 2];
+        const bool live0 = 4 * G < a.ncols;
+        if (live0) {
+            hyb_fetch<W, 4 * G, 1, 8>(a.tables, cur[0][0], eh0);
+            if (a.copy_records && a.copy_off32[4 * G] >= 0)
+                __builtin_amdgcn_raw_buffer_store_b128(cur[0][0], t.rcopy, a.copy_off32[4 * G] + t.off, 0, 2);
+        }
+        input_mac<W, CH, 4 * G + 1, 0>(a, lds, t, cur[1], acc);
+        input_mac<W, CH, 4 * G + 2, 0>(a, lds, t, cur[2], acc);
+        input_mac<W, CH, 4 * G + 3, 0>(a, lds, t, cur[3], acc);
+        if (live0) mac_chunk_mixed<W, 4 * G, 0, 8>(lds, cur[0][0], dummy, eh0, acc[0]);
+    } else {
+        input_mac<W, CH, 4 * G + 0, TM>(a, lds, t, cur[0], acc);
+        input_mac<W, CH, 4 * G + 1, TM>(a, lds, t, cur[1], acc);
+        input_mac<W, CH, 4 * G + 2, TM>(a, lds, t, cur[2], acc);
+        input_mac<W, CH, 4 * G + 3, TM>(a, lds, t, cur[3], acc);
+    }
     if constexpr (G + 1 < KG) {
         if constexpr (!PF) load_group<W, CH, G + 1, KG>(a, t, nxt);
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
-        stream_group<W, CH, G + 1, KG, PF, NIB>(a, lds, t, cur, acc);
+        stream_group<W, CH, G + 1, KG, PF, TM>(a, lds, t, cur, acc);
     }
 }
 
 }  // namespace
 
-template <int W, int KG, int CH, bool PF, bool NIB>
-__global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
+template <int W, int KG, int CH, bool PF, bool NIB, int TM>
+__device__ __forceinline__ void gf16_stream_body(const ApplyArgs& a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int D = W / 2;
@@ -216,7 +290,7 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
                 for (int d = 0; d < D; d++) acc[c][w][d] = 0u;
         v4u cur[4][CH];
         load_group<W, CH, 0, KG>(a, tile, cur);
-        stream_group<W, CH, 0, KG, PF, NIB>(a, lds, tile, cur, acc);
+        stream_group<W, CH, 0, KG, PF, TM>(a, lds, tile, cur, acc);
 
 #pragma unroll
         for (int r = 0; r < W; r++) {
@@ -237,6 +311,19 @@ __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
     }
 }
 
+
+template <int W, int KG, int CH, bool PF, bool NIB>
+__global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
+{
+    gf16_stream_body<W, KG, CH, PF, NIB, NIB ? 1 : 0>(a);
+}
+
+// 8-output passes with the hybrid LDS + L1 lookups (TM = 2), e.g. C5's 20 -> 8.
+template <int KG>
+__global__ void __launch_bounds__(1024) gf16_hybrid_kernel(const ApplyArgs a)
+{
+    gf16_stream_body<8, KG, 1, false, false, 2>(a);
+}
 
 // One group of 4 inputs of gf16_ptrs_stream_kernel: a buffer resource per fragment, loads
 // unconditional (out-of-range offset past ncols), lookups at compile-time table offsets.
@@ -327,6 +414,12 @@ __global__ void __launch_bounds__(1024) gf16_ptrs_stream_kernel(const ApplyArgs 
 
 #define ECAMD_STREAM_INST(W, KG, CH, PF, NIB) \
     template __global__ void ecamd::gf16_stream_kernel<W, KG, CH, PF, NIB>(const ecamd::ApplyArgs);
+#define ECAMD_HYBRID_KG \
+    template __global__ void ecamd::gf16_hybrid_kernel<1>(const ecamd::ApplyArgs); \
+    template __global__ void ecamd::gf16_hybrid_kernel<2>(const ecamd::ApplyArgs); \
+    template __global__ void ecamd::gf16_hybrid_kernel<3>(const ecamd::ApplyArgs); \
+    template __global__ void ecamd::gf16_hybrid_kernel<4>(const ecamd::ApplyArgs); \
+    template __global__ void ecamd::gf16_hybrid_kernel<5>(const ecamd::ApplyArgs);
 #define ECAMD_PTRS_KG(W)                                                                  \
     template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 1>(const ecamd::ApplyArgs);      \
     template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 2>(const ecamd::ApplyArgs);      \

@@ -5,3 +5,4 @@ ECAMD_STREAM_KG(8, 1, false, false)
 ECAMD_STREAM_KG(8, 1, true, false)
 ECAMD_STREAM_KG(8, 1, false, true)
 ECAMD_PTRS_KG(8)
+ECAMD_HYBRID_KG

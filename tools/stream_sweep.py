@@ -21,7 +21,8 @@ CFGS = {"c3": (10, 4, 1 << 20, 256, [0, 1, 2, 3]),
         "c5": (20, 8, 4 << 20, 32, list(range(8)))}
 
 
-VARIANTS = [(0, 1, 0, 0, 0), (1, 1, 0, 0, 0), (1, 1, 0, 0, 1), (1, 1, 0, 0, 2), (1, 1, 0, 0, 3)]
+# (stream, ch, pf, nib, order, hybrid)
+VARIANTS = [(0, 1, 0, 0, 0, 0), (1, 1, 0, 0, 0, 0), (1, 1, 0, 0, 0, 1), (1, 1, 0, 0, 1, 1)]
 
 
 def main():
@@ -41,8 +42,9 @@ def main():
         lay.fill_splitmix(nfrags=k, stream=st)
         algo = S * (k + m) * F
 
-        def setk(stream, ch, pf, nib, order, threads, wgs):
+        def setk(stream, ch, pf, nib, order, hyb, threads, wgs):
             d.ecamd_tune(b"stream_order", order)
+            d.ecamd_tune(b"stream_hybrid", hyb)
             d.ecamd_tune(b"stream", stream)
             d.ecamd_tune(b"stream_nib", nib)
             d.ecamd_tune(b"stream_ch", ch)
@@ -52,12 +54,12 @@ def main():
 
         variants = {}
         for (threads, wgs) in geoms:
-            for (stream, ch, pf, nib, order) in VARIANTS:
+            for (stream, ch, pf, nib, order, hyb) in VARIANTS:
                 if stream == 0 and (threads, wgs) != (0, 0):
                     continue
-                tag = f"{cfg}_{'old' if not stream else f'st_ch{ch}_pf{pf}_nib{nib}_o{order}'}_t{threads}_w{wgs}"
+                tag = f"{cfg}_{'old' if not stream else f'st_ch{ch}_pf{pf}_nib{nib}_o{order}_h{hyb}'}_t{threads}_w{wgs}"
                 for op in ("enc", "dec"):
-                    def fn(op=op, a=(stream, ch, pf, nib, order, threads, wgs)):
+                    def fn(op=op, a=(stream, ch, pf, nib, order, hyb, threads, wgs)):
                         setk(*a)
                         if op == "enc":
                             D.rs_encode(k, m, lay, stream=st)
@@ -65,7 +67,7 @@ def main():
                             D.rs_decode(k, m, miss, lay, stream=st)
                     variants[f"{op}_{tag}"] = fn
         # correctness: every variant reproduces the old kernel's encode and decode output
-        setk(0, 1, 0, 0, 0, 0, 0)
+        setk(0, 1, 0, 0, 0, 0, 0, 0)
         D.rs_encode(k, m, lay, stream=st)
         st.synchronize()
         ref = lay.buf.download(lay.stripe_stride * min(S, 4))
@@ -74,7 +76,7 @@ def main():
             lay.buf.zero()
             lay.fill_splitmix(nfrags=k, stream=st)
             if name.startswith("dec"):
-                setk(0, 1, 0, 0, 0, 0, 0)
+                setk(0, 1, 0, 0, 0, 0, 0, 0)
                 D.rs_encode(k, m, lay, stream=st)
             fn()
             st.synchronize()
@@ -101,7 +103,7 @@ def main():
             out.write(json.dumps(r) + "\n")
             print(json.dumps(r), flush=True)
         lay.buf.free()
-        setk(1, 1, 0, 0, 0, 0, 0)
+        setk(1, 1, 0, 0, 0, 1, 0, 0)
 
 
 if __name__ == "__main__":
