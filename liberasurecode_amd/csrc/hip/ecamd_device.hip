@@ -1256,7 +1256,10 @@ int ecamd_debug_lookup_probe(int mode, int wgs_per_cu, int iters, const void* d_
     switch (mode) {
     case 0: hipLaunchKernelGGL(lookup_probe_kernel<0>, grid, block, 0, st, t, iters, sink); break;
     case 1: hipLaunchKernelGGL(lookup_probe_kernel<1>, grid, block, 0, st, t, iters, sink); break;
-    default: hipLaunchKernelGGL(lookup_probe_kernel<2>, grid, block, 0, st, t, iters, sink); break;
+    case 2: hipLaunchKernelGGL(lookup_probe_kernel<2>, grid, block, 0, st, t, iters, sink); break;
+    case 3: hipLaunchKernelGGL(lookup_probe_kernel<3>, grid, block, 0, st, t, iters, sink); break;
+    case 4: hipLaunchKernelGGL(lookup_probe_kernel<4>, grid, block, 0, st, t, iters, sink); break;
+    default: hipLaunchKernelGGL(lookup_probe_kernel<5>, grid, block, 0, st, t, iters, sink); break;
     }
     HIP_TRY(hipGetLastError());
     return 0;

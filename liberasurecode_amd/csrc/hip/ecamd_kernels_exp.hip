@@ -262,7 +262,9 @@ namespace ecamd {
 
 // Table-lookup engine probe (sweeps only): random 16-byte lookups into 4 KiB tables, from LDS
 // (MODE 0), from global memory through the CU's vector L1 (MODE 1), or half and half (MODE 2),
-// 4 lookups per xorshift step.  Prices the L1 as a second lookup engine beside the LDS.
+// 4 lookups per xorshift step; MODE 3 / 4: 16-entry (256 B, nibble-sized) tables from L1 / LDS;
+// MODE 5: LDS byte tables and L1 16-entry tables half and half.  Prices the L1 as a second
+// lookup engine beside the LDS.
 template <int MODE>
 __global__ void __launch_bounds__(256) lookup_probe_kernel(const uint4* __restrict__ table, int iters,
                                                            uint32_t* sink)
@@ -278,9 +280,10 @@ __global__ void __launch_bounds__(256) lookup_probe_kernel(const uint4* __restri
         x ^= x << 5;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
-            const uint32_t idx = b * 256 + ((x >> (8 * b)) & 0xffu);
+            const bool nib = MODE == 3 || MODE == 4 || (MODE == 5 && !(b & 1));
+            const uint32_t idx = nib ? b * 256 + ((x >> (8 * b)) & 0xfu) : b * 256 + ((x >> (8 * b)) & 0xffu);
             uint4 e;
-            if (MODE == 0 || (MODE == 2 && (b & 1)))
+            if (MODE == 0 || MODE == 4 || ((MODE == 2 || MODE == 5) && (b & 1)))
                 e = tab[idx];
             else
                 e = table[idx];
@@ -296,5 +299,8 @@ __global__ void __launch_bounds__(256) lookup_probe_kernel(const uint4* __restri
 template __global__ void lookup_probe_kernel<0>(const uint4*, int, uint32_t*);
 template __global__ void lookup_probe_kernel<1>(const uint4*, int, uint32_t*);
 template __global__ void lookup_probe_kernel<2>(const uint4*, int, uint32_t*);
+template __global__ void lookup_probe_kernel<3>(const uint4*, int, uint32_t*);
+template __global__ void lookup_probe_kernel<4>(const uint4*, int, uint32_t*);
+template __global__ void lookup_probe_kernel<5>(const uint4*, int, uint32_t*);
 
 }  // namespace ecamd

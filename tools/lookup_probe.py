@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Lookup engines on one MI355X (development tool): random 16-byte table lookups per clock per CU
-from LDS, from global memory through the vector L1, and half each (ecamd_debug_lookup_probe)."""
+from LDS, from global memory through the vector L1, and half each; 16-entry (nibble-sized) tables from each
+(ecamd_debug_lookup_probe)."""
 import ctypes as C
 import json
 import os
@@ -24,7 +25,8 @@ def main():
     iters = 4096
     a, b = D.Event(), D.Event()
     cus = 256
-    for mode in (0, 1, 2):
+    names = ["lds", "l1", "half", "l1_16ent", "lds_16ent", "lds_byte+l1_16ent"]
+    for mode in range(6):
         for wgs in (2, 4, 8):
             ts = []
             for _ in range(5):
@@ -36,7 +38,7 @@ def main():
             ms = statistics.median(ts)
             lookups = cus * wgs * 256 * iters * 4
             per_clk_cu = lookups / (ms * 1e-3) / 2.4e9 / cus
-            print(json.dumps({"mode": ["lds", "l1", "half"][mode], "wgs_per_cu": wgs, "ms": round(ms, 3),
+            print(json.dumps({"mode": names[mode], "wgs_per_cu": wgs, "ms": round(ms, 3),
                               "lookups_per_clk_per_cu": round(per_clk_cu, 2),
                               "bytes_per_clk_per_cu": round(per_clk_cu * 16, 1)}), flush=True)
 
