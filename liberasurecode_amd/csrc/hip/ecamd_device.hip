@@ -162,6 +162,7 @@ struct Tuning {
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
                             // measured best, tools/xor_sweep.py)
+    int multi_list = 1;     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     int stream_hybrid = 1;  //   8-output passes: one input in 4 looks its hi table up via L1
     int stream_order = 0;   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     int stream_nib = 0;     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
@@ -437,6 +438,8 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             if (rc) return rc;
             continue;
         }
+        if (a.stripe_list)  // only the stream kernel reads a stripe list
+            return fail(ECAMD_EINVAL, "stripe list on a non-stream launch");
         if (PTRS && g_tune.nt && !exp && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
             bs < (int64_t(1) << 31)) {
             rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4);
@@ -886,6 +889,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_ch = value == 2 ? 2 : 1;
     } else if (k == "xor_wgs") {
         g_tune.xor_wgs = std::max(0, std::min(value, 8));
+    } else if (k == "multi_list") {
+        g_tune.multi_list = value;
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
     } else if (k == "stream_order") {
@@ -1086,40 +1091,75 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
             return fail(ECAMD_EINVAL, "stripe %d: %zu fragments missing > m=%d", s, pat.size(), m);
         groups[pat].push_back(s);
     }
-    // One pointer table row (k+m fragment addresses) per stripe, laid out group by group.
+    // The stream kernel walks each group's stripes of the strided layout through a stripe list
+    // (one scalar load per tile); otherwise -- first-version kernels, k > 20 inputs, stripes
+    // wider than 2 GiB -- one pointer table row (k+m fragment addresses) per stripe. Both are
+    // laid out group by group.
     const int row = k + m;
+    const bool use_list = g_tune.multi_list && g_tune.stream && g_tune.nt && g_tune.exp_ch <= 0 &&
+                          k <= 4 * kStreamGroups &&
+                          (row - 1) * frag_stride + blocksize < (int64_t(1) << 31);
     std::vector<uint8_t*> table;
-    table.reserve(static_cast<size_t>(nstripes) * row);
-    for (const auto& g : groups)
-        for (int s : g.second)
-            for (int f = 0; f < row; f++)
-                table.push_back(static_cast<uint8_t*>(base) + s * stripe_stride + f * frag_stride);
-    static std::mutex mu;
-    static std::map<std::pair<int, void*>, std::pair<void*, size_t>> scratch;  // dev, stream
-    std::lock_guard<std::mutex> lk(mu);
-    auto& sc = scratch[{dev, stream}];
-    const size_t bytes = table.size() * sizeof(uint8_t*);
-    // The previous call on this stream may still read the table: drain the stream first.
-    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-    if (sc.second < bytes) {
-        if (sc.first) HIP_TRY(hipFree(sc.first));
-        sc.first = nullptr;
-        HIP_TRY(hipMalloc(&sc.first, bytes));
-        sc.second = bytes;
+    std::vector<int32_t> list;
+    if (use_list) {
+        list.reserve(nstripes);
+        for (const auto& g : groups) list.insert(list.end(), g.second.begin(), g.second.end());
+    } else {
+        table.reserve(static_cast<size_t>(nstripes) * row);
+        for (const auto& g : groups)
+            for (int s : g.second)
+                for (int f = 0; f < row; f++)
+                    table.push_back(static_cast<uint8_t*>(base) + s * stripe_stride + f * frag_stride);
     }
-    HIP_TRY(hipMemcpy(sc.first, table.data(), bytes, hipMemcpyHostToDevice));
-    auto* d_table = static_cast<uint8_t**>(sc.first);
+    // The table goes up asynchronously on the caller's stream, ahead of the launches that read it,
+    // from one of kSlots (pinned host, device) buffer pairs per (device, stream): a slot is reused
+    // only after the event recorded behind its last launches has fired, so back-to-back calls do
+    // not drain the stream (the GPU stays busy while the host plans the next call).
+    struct Slot {
+        void* host = nullptr;
+        void* dev = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+    };
+    constexpr int kSlots = 4;
+    struct Ring {
+        Slot slot[kSlots];
+        int next = 0;
+    };
+    static std::mutex mu;
+    static std::map<std::pair<int, void*>, Ring> rings;  // (device, stream)
+    std::lock_guard<std::mutex> lk(mu);
+    Ring& ring = rings[{dev, stream}];
+    Slot& sc = ring.slot[ring.next];
+    ring.next = (ring.next + 1) % kSlots;
+    const size_t bytes = use_list ? list.size() * sizeof(int32_t) : table.size() * sizeof(uint8_t*);
+    if (sc.done) HIP_TRY(hipEventSynchronize(sc.done));
+    else HIP_TRY(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
+    if (sc.cap < bytes) {
+        if (sc.host) HIP_TRY(hipHostFree(sc.host));
+        if (sc.dev) HIP_TRY(hipFree(sc.dev));
+        sc.host = sc.dev = nullptr;
+        sc.cap = 0;
+        HIP_TRY(hipHostMalloc(&sc.host, bytes, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&sc.dev, bytes));
+        sc.cap = bytes;
+    }
+    std::memcpy(sc.host, use_list ? static_cast<const void*>(list.data()) : table.data(), bytes);
+    HIP_TRY(hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
+    auto* d_table = static_cast<uint8_t**>(sc.dev);
+    auto* d_list = static_cast<const int32_t*>(sc.dev);
     size_t at = 0;
     for (const auto& g : groups) {
         const int G = static_cast<int>(g.second.size());
-        uint8_t** t = d_table + at;
-        at += static_cast<size_t>(G) * row;
+        uint8_t** t = d_table + at * row;
+        const int32_t* sl = d_list + at;
+        at += static_cast<size_t>(G);
         if (g.first.empty()) continue;
         std::vector<int> list(g.first);
         list.push_back(-1);
         std::shared_ptr<RsEntry> e;
         rc = rs_entry(1, k, m, list.data(), rebuild_parity ? 1 : 0, -1, e);
-        if (rc) return rc;
+        if (rc) break;
         if (e->outputs.empty()) continue;
         if (e->inputs.empty()) {
             for (int s : g.second)
@@ -1129,12 +1169,26 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
                                            static_cast<hipStream_t>(stream)));
             continue;
         }
-        rc = ecamd_map_apply_ptrs(e->map.get(), reinterpret_cast<const void* const*>(t), row,
-                                  e->inputs.data(), reinterpret_cast<void* const*>(t), row,
-                                  e->outputs.data(), blocksize, G, stream);
-        if (rc) return rc;
+        if (use_list) {
+            std::vector<int64_t> in_off, out_off;
+            for (int i : e->inputs) in_off.push_back(i * frag_stride);
+            for (int o : e->outputs) out_off.push_back(o * frag_stride);
+            ApplyArgs a{};
+            a.in_base = static_cast<const uint8_t*>(base);
+            a.out_base = static_cast<uint8_t*>(base);
+            a.in_stride = a.out_stride = stripe_stride;
+            a.stripe_list = sl;
+            rc = launch_gf16<false>(e->map.get(), a, in_off.data(), out_off.data(), blocksize, G,
+                                    static_cast<hipStream_t>(stream));
+        } else {
+            rc = ecamd_map_apply_ptrs(e->map.get(), reinterpret_cast<const void* const*>(t), row,
+                                      e->inputs.data(), reinterpret_cast<void* const*>(t), row,
+                                      e->outputs.data(), blocksize, G, stream);
+        }
+        if (rc) break;
     }
-    return 0;
+    HIP_TRY(hipEventRecord(sc.done, static_cast<hipStream_t>(stream)));
+    return rc;
 }
 
 int ecamd_scatter_fragments(const void* d_src, int64_t stripe_stride, int64_t frag_stride,

@@ -246,8 +246,9 @@ __device__ __forceinline__ void gf16_stream_body(const ApplyArgs& a)
     const uint32_t t1 = ranged ? min(a.ntiles, t0 + per) : a.ntiles;
     const uint32_t dt = ranged ? 1u : gridDim.x;
     for (uint32_t t = t0; t < t1; t += dt) {
-        const uint32_t s = t / a.tiles_per_stripe;
-        const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span;
+        const uint32_t sl = t / a.tiles_per_stripe;
+        const int64_t toff = static_cast<int64_t>(t - sl * a.tiles_per_stripe) * span;
+        const uint32_t s = a.stripe_list ? static_cast<uint32_t>(a.stripe_list[sl]) : sl;
         // last, partial tile of each fragment -- and, for objects shorter than the k payloads
         // (ApplyArgs::limited), every tile reaching past the shortest input's end: the byte-exact
         // per-chunk path reads zeros there

@@ -316,7 +316,7 @@ def tune():
     d = _lib.dev()
     yield d.ecamd_tune
     for key, val in ((b"stream", 1), (b"stream_ch", 1), (b"stream_pf", 0), (b"stream_nib", 0),
-                     (b"stream_order", 0), (b"stream_hybrid", 1), (b"xor_wgs", 0)):
+                     (b"stream_order", 0), (b"stream_hybrid", 1), (b"multi_list", 1), (b"xor_wgs", 0)):
         d.ecamd_tune(key, val)
 
 
@@ -342,12 +342,14 @@ def test_stream_kernel_variants(tune, R, K, variant):
             assert (out[s, K + r] == want[r]).all(), (s, r)
 
 
-@pytest.mark.parametrize("stream", [0, 1])
+@pytest.mark.parametrize("stream,multi_list", [(0, 0), (1, 0), (1, 1)])
 @pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 24), (20, 8, 8192 + 2, 10)])
-def test_decode_multi_pointer_kernels(tune, stream, k, m, bs, S):
-    """Heterogeneous batch decode (pointer-table launches) on both the stream and the
-    first-version pointer kernels, checked against the oracle on garbage-filled buffers."""
+def test_decode_multi_pointer_kernels(tune, stream, multi_list, k, m, bs, S):
+    """Heterogeneous batch decode on the stripe-list stream launches, the pointer-table stream
+    kernel and the first-version pointer kernel, checked against the oracle on garbage-filled
+    buffers."""
     tune(b"stream", stream)
+    tune(b"multi_list", multi_list)
     rng = np.random.default_rng(k * 7 + stream)
     host = rng.integers(0, 256, size=(S, k + m, bs), dtype=np.uint8)
     for s in range(S):

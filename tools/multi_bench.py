@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Heterogeneous batch decode (ecamd_rs_decode_multi: one pointer-table launch per distinct erasure
-pattern) at the C3 shape, stream kernel vs first version (development tool)."""
+"""Heterogeneous batch decode (ecamd_rs_decode_multi: one launch per distinct erasure pattern) at
+the C3 shape: stripe-list stream launches, pointer-table stream kernel, first-version pointer kernel,
+and a single-pattern strided decode for reference (development tool)."""
 import json
 import os
 import statistics
@@ -21,27 +22,39 @@ def main():
     st = D.Stream()
     lay.fill_splitmix(nfrags=k, stream=st)
     D.rs_encode(k, m, lay, stream=st)
-    pats = [[0, 1, 2, 3], [4, 5, 6, 7], [0, 5, 10, 13], [2, 3, 8, 9]]
-    per = [pats[s % len(pats)] for s in range(S)]
     algo = S * (k + m) * F
     a, b = D.Event(), D.Event()
-    res = {}
-    for stream in (1, 0, 1, 0):
-        d.ecamd_tune(b"stream", stream)
+    allpats = [[0, 1, 2, 3], [4, 5, 6, 7], [0, 5, 10, 13], [2, 3, 8, 9]]
+
+    def timed(fn):
         ts = []
-        for _ in range(5):
-            D.rs_decode_multi(k, m, per, lay, stream=st)
+        for _ in range(7):
+            fn()
             a.record(st)
             for _ in range(3):
-                D.rs_decode_multi(k, m, per, lay, stream=st)
+                fn()
             b.record(st)
             ts.append(a.elapsed_ms(b) / 3)
-        res.setdefault(stream, []).append(statistics.median(ts))
-    d.ecamd_tune(b"stream", 1)
-    for stream, ts in res.items():
-        ms = min(ts)
-        print(json.dumps({"decode_multi": "stream" if stream else "first_version", "patterns": len(pats),
-                          "ms": round(ms, 4), "GBps": round(algo / ms / 1e6, 1)}))
+        return statistics.median(ts)
+
+    for npat in (1, 2, 4):
+        pats = allpats[:npat]
+        per = [pats[s % len(pats)] for s in range(S)]
+        res = {}
+        names = {(1, 1): "stripe_list", (1, 0): "ptrs_stream", (0, 0): "first_version"}
+        for _ in range(2):
+            for key in names:
+                d.ecamd_tune(b"stream", key[0])
+                d.ecamd_tune(b"multi_list", key[1])
+                res.setdefault(key, []).append(timed(lambda: D.rs_decode_multi(k, m, per, lay, stream=st)))
+        d.ecamd_tune(b"stream", 1)
+        d.ecamd_tune(b"multi_list", 1)
+        for key, ts in res.items():
+            ms = min(ts)
+            print(json.dumps({"decode_multi": names[key], "patterns": npat,
+                              "ms": round(ms, 4), "GBps": round(algo / ms / 1e6, 1)}), flush=True)
+    ms = timed(lambda: D.rs_decode(k, m, allpats[0], lay, stream=st))
+    print(json.dumps({"decode_strided": allpats[0], "ms": round(ms, 4), "GBps": round(algo / ms / 1e6, 1)}))
 
 
 if __name__ == "__main__":
