@@ -219,14 +219,16 @@ def main():
     dec_ms = [b.elapsed_ms(c) for _, b, c in ev]
     obj_bytes = S * k * F  # object bytes per stripe batch per GPU
     value = 2 * obj_bytes * args.steps * world / GIB / elapsed
-    # dominant kernel: gf16_apply_kernel<4> (encode: 10 in, 4 out; decode: 10 in, 4 out)
+    # dominant kernel: the stream kernel (C3 encode and decode: 10 in, 4 out per launch)
     launch_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
     # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
-    # <W outputs per pass, KG groups of 4 inputs, CH chunks per lane, PF prefetch, NIB nibble tables>
-    kernel = f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>"
+    # <W outputs per pass, KG groups of 4 inputs, CH chunks per lane, PF prefetch, NIB nibble tables>;
+    # 8-output passes run its hybrid LDS + L1 lookup form <KG>
+    kernel = (f"gf16_hybrid_kernel<{(k + 3) // 4}>" if width == 8 else
+              f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>")
     traffic, traffic_src = pmc_traffic(args.config, kernel)
     if traffic is not None and S != CONFIGS[args.config][3]:
         traffic = int(traffic * S / CONFIGS[args.config][3])  # profile ran at the default S
