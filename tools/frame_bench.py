@@ -31,29 +31,32 @@ def main():
     ap.add_argument("--stripes", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fused-sweep", action="store_true")
+    ap.add_argument("--align", type=int, default=128, help="payload alignment of the fragment batch")
+    ap.add_argument("--no-crc-sweep", action="store_true")
     args = ap.parse_args()
     S, k, m, size = args.stripes, 10, 4, 10 * 1048576
     d = _lib.dev()
     st = D.Stream()
-    fb = frame.FrameBatch(frame.RS_VAND, k, m, size, S)
+    fb = frame.FrameBatch(frame.RS_VAND, k, m, size, S, align=args.align)
+    print(json.dumps({"align": args.align, "frag_stride": fb.frag_stride, "head": fb.head}), flush=True)
     obj = D.DeviceBuffer(fb.obj_stride * S)
     lay = D.Layout(obj, 1, size, S, fb.obj_stride, fb.obj_stride)
     lay.fill_splitmix(stream=st)
     crc = D.DeviceBuffer(4 * S * (k + m))
     # Random payload bytes: the byte-table CRC lookups conflict in LDS on random data only
     # (all-zero payloads broadcast one entry and would overstate its speed).
-    _lib.check(d.ecamd_fill_splitmix(fb.buf.ptr + 80, fb.stripe_stride, fb.frag_stride, k + m,
+    _lib.check(d.ecamd_fill_splitmix(fb.base + 80, fb.stripe_stride, fb.frag_stride, k + m,
                                      fb.blocksize, S, 0, 0x5EED, st.handle), "fill")
     payload_bytes = S * (k + m) * fb.blocksize
-    for bits, gap, pos, span in ((4, 8, 0, 16), (5, 8, 1, 64), (5, 8, 1, 128), (4, 8, 1, 64),
-                                 (7, 8, 1, 64)):
+    for bits, gap, pos, span in (() if args.no_crc_sweep else
+                                 ((4, 8, 0, 16), (5, 8, 1, 64), (5, 8, 1, 128), (4, 8, 1, 64), (7, 8, 1, 64))):
         for wgs in (0, 4):
             d.ecamd_tune(b"crc_span_kib", span)
             d.ecamd_tune(b"crc_pos", pos)
             d.ecamd_tune(b"crc_bits", bits)
             d.ecamd_tune(b"crc_gap_bits", gap)
             d.ecamd_tune(b"crc_wgs", wgs)
-            ms = timed(lambda: _lib.check(d.ecamd_crc32(0, fb.buf.ptr + 80, fb.stripe_stride,
+            ms = timed(lambda: _lib.check(d.ecamd_crc32(0, fb.base + 80, fb.stripe_stride,
                                                          fb.frag_stride, k + m, fb.blocksize, S,
                                                          crc.ptr, st.handle), "crc"), st, args.reps)
             print(json.dumps({"op": "crc32", "bits": bits, "gap_bits": gap, "pos": pos, "span_kib": span, "crc_wgs": wgs,
@@ -87,7 +90,7 @@ def main():
     # objects that do not fill the payloads: Swift's default 1 MiB EC segments (bs = 104858) and a
     # C3 object 6 bytes short -- copy-through with zero padding vs split + encode
     for size2, S2, tag in (((1 << 20), 2560, "swift_1MiB_segment"), (k * (1 << 20) - 6, S, "c3_minus_6B")):
-        fb2 = frame.FrameBatch(6, k, m, size2, S2)
+        fb2 = frame.FrameBatch(6, k, m, size2, S2, align=args.align)
         obj2 = D.DeviceBuffer(fb2.obj_stride * S2)
         _lib.check(d.ecamd_fill_splitmix(obj2.ptr, fb2.obj_stride, 0, 1, size2, S2, 0, 0xB0B, st.handle), "fill")
         for padded, ct in ((1, frame.CHKSUM_NONE), (0, frame.CHKSUM_NONE), (1, frame.CHKSUM_CRC32),

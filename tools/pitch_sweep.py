@@ -20,20 +20,29 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pads", default="0,256,1024,4096,65536,4352")
     ap.add_argument("--spads", default="0")
+    ap.add_argument("--offs", default="0", help="base offsets (e.g. 80: payloads behind 80-byte headers)")
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--cfg", default="10,4,1048576,256")
     args = ap.parse_args()
     k, m, F, S = (int(x) for x in args.cfg.split(","))
     st = D.Stream()
     lays = {}
+    class Shifted:  # a view of a device buffer starting `off` bytes in
+        def __init__(self, buf, off):
+            self.buf, self.ptr = buf, buf.ptr + off
+
+        def download(self, n):
+            return self.buf.download(n + (self.ptr - self.buf.ptr))[self.ptr - self.buf.ptr:]
+
     for pad in (int(p) for p in args.pads.split(",")):
         for spad in (int(p) for p in args.spads.split(",")):
-            fs = F + pad
-            ss = fs * (k + m) + spad
-            buf = D.DeviceBuffer(ss * S)
-            lay = D.Layout(buf, k + m, F, S, fs, ss)
-            lay.fill_splitmix(nfrags=k, stream=st)
-            lays[(pad, spad)] = lay
+            for off in (int(p) for p in args.offs.split(",")):
+                fs = F + pad
+                ss = fs * (k + m) + spad
+                buf = D.DeviceBuffer(ss * S + 256)
+                lay = D.Layout(Shifted(buf, off), k + m, F, S, fs, ss)
+                lay.fill_splitmix(nfrags=k, stream=st)
+                lays[(pad, spad, off)] = lay
     ref = None
     for key, lay in lays.items():
         D.rs_encode(k, m, lay, stream=st)
@@ -61,7 +70,8 @@ def main():
                 times.setdefault((op,) + key, []).append(a.elapsed_ms(b) / 3)
     for key, ts in sorted(times.items(), key=lambda kv: statistics.median(kv[1])):
         med = statistics.median(ts)
-        print(json.dumps({"op": key[0], "frag_pad": key[1], "stripe_pad": key[2], "ms": round(med, 4),
+        print(json.dumps({"op": key[0], "frag_pad": key[1], "stripe_pad": key[2], "base_off": key[3],
+                          "ms": round(med, 4),
                           "TBps": round(algo / med / 1e9, 3)}), flush=True)
 
 
