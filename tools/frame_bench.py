@@ -78,8 +78,8 @@ def main():
     d.ecamd_tune(b"frame_unfused", 0)
     if args.fused_sweep:  # fused CRC encode geometry: workgroups per CU x work units per CU
         fb.checksum = frame.CHKSUM_CRC32
-        for wgs in (1, 2, 3):
-            for units in (2, 4, 8, 16):
+        for wgs, units in [(w, u) for _ in range(2) for w in (2, 3, 4) for u in (2, 3, 4, 6, 8)]:
+            if True:
                 d.ecamd_tune(b"frame_crc_wgs", wgs)
                 d.ecamd_tune(b"frame_crc_units", units)
                 ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
