@@ -161,8 +161,10 @@ int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t b
                 const void* ctx, Launch launch)
 {
     const int64_t nfr = K + R;
-    int64_t chunk = std::max<int64_t>(16, (kChunkTarget / nfr) / 16 * 16);
-    const int64_t padded = (bs + 15) / 16 * 16;
+    // The chunk is also the fragment pitch in the slab: a multiple of 128 puts every fragment
+    // on a cache line (16-byte-aligned pitches cost the codec 13-19%).
+    int64_t chunk = std::max<int64_t>(128, (kChunkTarget / nfr) / 128 * 128);
+    const int64_t padded = (bs + 127) / 128 * 128;
     chunk = std::min(chunk, padded);
     int rc = 0;
     // Below ~16 KiB of fragments the extra launch + copy costs more than zlib on the host

@@ -343,7 +343,7 @@ def test_stream_kernel_variants(tune, R, K, variant):
 
 
 @pytest.mark.parametrize("stream,multi_list", [(0, 0), (1, 0), (1, 1)])
-@pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 24), (20, 8, 8192 + 2, 10)])
+@pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 24), (20, 8, 8192 + 2, 10), (24, 4, 4096 + 10, 6)])
 def test_decode_multi_pointer_kernels(tune, stream, multi_list, k, m, bs, S):
     """Heterogeneous batch decode on the stripe-list stream launches, the pointer-table stream
     kernel and the first-version pointer kernel, checked against the oracle on garbage-filled
