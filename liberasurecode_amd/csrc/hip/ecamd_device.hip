@@ -108,12 +108,12 @@ int ensure_device(int* dev_out)
 #undef KP_
         for (const void* k : pk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
-#define KF_(W) reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 1>),                   \
-               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 2>),                   \
-               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 3>),                   \
-               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4>),                   \
-               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5>)
-        const void* fk[] = {KF_(2), KF_(4), KF_(8),
+#define KF_(W, MB) reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 1, MB>),           \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 2, MB>),               \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 3, MB>),               \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4, MB>),               \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5, MB>)
+        const void* fk[] = {KF_(2, 1), KF_(4, 1), KF_(8, 1), KF_(2, 4), KF_(4, 4), KF_(8, 4),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<1>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
@@ -154,6 +154,7 @@ struct Tuning {
     int frame_copy_padded = 1;  // framed encode: copy-through also for objects shorter than k*bs
     int frame_crc_wgs = 0;    //   512-thread workgroups per CU (0 = 2)
     int frame_crc_units = 0;  //   work units (stripe ranges) per CU to aim for (0 = 4)
+    int frame_crc_mb = 0;     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
     int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
     int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     int crc_span_kib = 128; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
@@ -200,6 +201,7 @@ int dev_tune(const char* key)
     if (k == "frame_copy_padded") return g_tune.frame_copy_padded;
     if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
+    if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
     return 0;
 }
 
@@ -734,12 +736,21 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
                           &in_len);
 }
 
+// LDS bytes of gf16_frame_crc_kernel for an RS(k, m) encode: the pass's split tables, the CRC image
+// (byte tables for the first mb piece dwords) and the waves' state exchange.
+size_t fused_crc_lds(int k, int m, int mb)
+{
+    const int w = m <= 2 ? 2 : (m <= 4 ? 4 : 8);
+    const int ns = 4 * ((k + 3) / 4) + w;
+    return static_cast<size_t>(k) * 512 * 2 * w + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4;
+}
+
 // rs_encode_copy with the payload CRC32 folded in (gf16_frame_crc_kernel): r0 of range r of
 // payload f of stripe s lands in d_partial[(s*(k+m) + f)*q + r].  Returns ECAMD_EINVAL without
 // launching when the shape does not fit the fused kernel (the caller then runs the split path).
 int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                        int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream)
+                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb)
 {
     constexpr int kThreads = 512;
     constexpr int64_t kTile = kThreads * 16;
@@ -775,7 +786,9 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     if (k > 4 * kStreamGroups || !stream_offsets(a, bs) || !stream_copy_offsets(a, bs)) return ECAMD_EINVAL;
     const int kg = (k + 3) / 4;
     const int ns = 4 * kg + p.width;
-    const size_t lds = p.bytes + (static_cast<size_t>(crc_fused_words()) + 8 * ns) * 4;
+    if (mb != 1 && mb != 4) return ECAMD_EINVAL;
+    const size_t lds = fused_crc_lds(k, m, mb);
+    if (lds != p.bytes + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4) return ECAMD_EINVAL;
     if (lds > static_cast<size_t>(kLdsBytes)) return ECAMD_EINVAL;
     a.tiles_per_stripe = static_cast<uint32_t>(bs / kTile);
     a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
@@ -786,20 +799,20 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     const dim3 grid(static_cast<unsigned>(std::min<int64_t>(units, static_cast<int64_t>(cu_count(map->device)) * wgs)));
     const dim3 block(kThreads);
     hipStream_t st = static_cast<hipStream_t>(stream);
-#define ECAMD_FUSED(W)                                                                                      \
+#define ECAMD_FUSED(W, MB)                                                                                  \
     switch (kg) {                                                                                           \
-    case 1: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 1>), grid, block, lds, st, a, c); break;            \
-    case 2: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 2>), grid, block, lds, st, a, c); break;            \
-    case 3: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 3>), grid, block, lds, st, a, c); break;            \
-    case 4: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 4>), grid, block, lds, st, a, c); break;            \
-    default: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 5>), grid, block, lds, st, a, c); break;           \
+    case 1: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 1, MB>), grid, block, lds, st, a, c); break;        \
+    case 2: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 2, MB>), grid, block, lds, st, a, c); break;        \
+    case 3: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 3, MB>), grid, block, lds, st, a, c); break;        \
+    case 4: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 4, MB>), grid, block, lds, st, a, c); break;        \
+    default: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 5, MB>), grid, block, lds, st, a, c); break;       \
     }
     if (p.width == 2) {
-        ECAMD_FUSED(2)
+        if (mb == 4) { ECAMD_FUSED(2, 4) } else { ECAMD_FUSED(2, 1) }
     } else if (p.width == 4) {
-        ECAMD_FUSED(4)
+        if (mb == 4) { ECAMD_FUSED(4, 4) } else { ECAMD_FUSED(4, 1) }
     } else {
-        ECAMD_FUSED(8)
+        if (mb == 4) { ECAMD_FUSED(8, 4) } else { ECAMD_FUSED(8, 1) }
     }
 #undef ECAMD_FUSED
     HIP_TRY(hipGetLastError());
@@ -875,6 +888,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_pos = value;  // 0 off, anything else on
     } else if (k == "frame_crc_wgs") {
         g_tune.frame_crc_wgs = std::max(0, std::min(value, 4));
+    } else if (k == "frame_crc_mb") {
+        g_tune.frame_crc_mb = value;
     } else if (k == "frame_crc_units") {
         g_tune.frame_crc_units = std::max(0, std::min(value, 64));
     } else if (k == "frame_copy_padded") {

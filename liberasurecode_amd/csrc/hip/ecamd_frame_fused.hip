@@ -30,10 +30,10 @@ namespace {
 using crcdev::lmap;
 using crcdev::piece_r0;
 
-constexpr int kPieceWords = crcdev::piece_words(1);  // byte tables for dword 0, nibble for 1..3
-constexpr int kMap4 = 128;                           // one G=4 field-table map (8 x 16 words)
+constexpr int kMap4 = 128;  // one G=4 field-table map (8 x 16 words)
 
-template <int W, int G, int KG>
+// MB: byte tables for the first MB dwords of a piece, nibble tables for the rest (crcdev).
+template <int W, int G, int KG, int MB>
 __device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* lds, const uint32_t* ctab,
                                             const uint32_t* gap, const StreamTile& t,
                                             uint32_t (&acc)[8][W / 2], uint32_t (&st)[4 * KG + W])
@@ -50,21 +50,22 @@ __device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* l
         const int j = 4 * G + i;
         if (j < a.ncols) {  // wave-uniform
             __builtin_amdgcn_raw_buffer_store_b128(x[i], t.rcopy, a.copy_off32[j] + t.off, 0, 2);
-            st[j] = lmap<4>(gap, st[j]) ^ piece_r0<1>(ctab, x[i]);
+            st[j] = lmap<4>(gap, st[j]) ^ piece_r0<MB>(ctab, x[i]);
         }
     }
     if (4 * G + 0 < a.ncols) mac_chunk_imm<W, 4 * G + 0>(lds, x[0], acc);
     if (4 * G + 1 < a.ncols) mac_chunk_imm<W, 4 * G + 1>(lds, x[1], acc);
     if (4 * G + 2 < a.ncols) mac_chunk_imm<W, 4 * G + 2>(lds, x[2], acc);
     if (4 * G + 3 < a.ncols) mac_chunk_imm<W, 4 * G + 3>(lds, x[3], acc);
-    if constexpr (G + 1 < KG) fused_group<W, G + 1, KG>(a, lds, ctab, gap, t, acc, st);
+    if constexpr (G + 1 < KG) fused_group<W, G + 1, KG, MB>(a, lds, ctab, gap, t, acc, st);
 }
 
 }  // namespace
 
-template <int W, int KG>
+template <int W, int KG, int MB>
 __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c)
 {
+    constexpr int kPieceWords = crcdev::piece_words(MB);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int D = W / 2;
     constexpr int EB = 2 * W;
@@ -109,7 +110,7 @@ __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, 
             for (int w = 0; w < 8; w++)
 #pragma unroll
                 for (int d = 0; d < D; d++) acc[w][d] = 0u;
-            fused_group<W, 0, KG>(a, lds, ctab, gap, tile, acc, st);
+            fused_group<W, 0, KG, MB>(a, lds, ctab, gap, tile, acc, st);
 #pragma unroll
             for (int o = 0; o < W; o++) {
                 if (o >= a.nrows) break;
@@ -120,7 +121,7 @@ __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, 
                     v[d] = (o & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
                 }
                 __builtin_amdgcn_raw_buffer_store_b128(v, rout, a.out_off32[o] + tile.off, 0, 2);
-                st[4 * KG + o] = lmap<4>(gap, st[4 * KG + o]) ^ piece_r0<1>(ctab, v);
+                st[4 * KG + o] = lmap<4>(gap, st[4 * KG + o]) ^ piece_r0<MB>(ctab, v);
             }
         }
         // lanes of a wave -> the wave's 1 KiB segment end (the crc_partial_kernel butterfly)
@@ -149,13 +150,14 @@ __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, 
     }
 }
 
-#define ECAMD_FUSED_INST(W)                                                                   \
-    template __global__ void gf16_frame_crc_kernel<W, 1>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 2>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 3>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 4>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 5>(const ApplyArgs, const FusedCrcArgs);
-ECAMD_FUSED_INST(2) ECAMD_FUSED_INST(4) ECAMD_FUSED_INST(8)
+#define ECAMD_FUSED_INST(W, MB)                                                                   \
+    template __global__ void gf16_frame_crc_kernel<W, 1, MB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 2, MB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 3, MB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 4, MB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 5, MB>(const ApplyArgs, const FusedCrcArgs);
+ECAMD_FUSED_INST(2, 1) ECAMD_FUSED_INST(4, 1) ECAMD_FUSED_INST(8, 1)
+ECAMD_FUSED_INST(2, 4) ECAMD_FUSED_INST(4, 4) ECAMD_FUSED_INST(8, 4)
 #undef ECAMD_FUSED_INST
 
 }  // namespace ecamd

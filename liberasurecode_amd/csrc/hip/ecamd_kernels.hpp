@@ -70,7 +70,7 @@ __global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
 template <int KG>
 __global__ void gf16_hybrid_kernel(const ApplyArgs a);
 struct FusedCrcArgs;
-template <int W, int KG>
+template <int W, int KG, int MB>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);
 template <int CH, bool ABLATE>
 __global__ void gf16_apply_exp_kernel(const ApplyArgs a);

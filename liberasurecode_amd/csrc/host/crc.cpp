@@ -89,10 +89,11 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
     return img;
 }
 
-std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes)
+std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb)
 {
-    const CrcImage pieces = build_crc_image(m, 5, 4, 4, false);  // MB = 1 piece tables first
-    size_t pw = 4 * 256 + 3 * 8 * 16;
+    // piece tables first: byte tables for the first mb dwords (B = 4 + mb; 8 = all four)
+    const CrcImage pieces = build_crc_image(m, mb == 4 ? 8 : 4 + mb, 4, 4, false);
+    size_t pw = static_cast<size_t>(mb) * 4 * 256 + static_cast<size_t>(4 - mb) * 8 * 16;
     std::vector<uint32_t> w(pw + 8 * 128, 0);
     std::copy(pieces.words.begin(), pieces.words.begin() + static_cast<std::ptrdiff_t>(pw), w.begin());
     field_tables(zero_shift(m, tile_bytes), 4, w.data() + pw);

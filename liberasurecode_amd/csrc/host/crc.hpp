@@ -80,6 +80,6 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos = fa
 // Image of the fused framed-encode checksum (hip/ecamd_frame_fused.hip): piece tables with byte
 // tables for dword 0 and nibble tables for dwords 1-3, then four G = 4 maps: A^tile_bytes (the
 // step between a lane's pieces), A^(16*2^t) for t < 6 (in-wave butterfly), A^1024 (across waves).
-std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes);
+std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb = 1);
 
 }  // namespace ecamd

@@ -78,13 +78,16 @@ def main():
     d.ecamd_tune(b"frame_unfused", 0)
     if args.fused_sweep:  # fused CRC encode geometry: workgroups per CU x work units per CU
         fb.checksum = frame.CHKSUM_CRC32
-        for wgs, units in [(w, u) for _ in range(2) for w in (2, 3, 4) for u in (2, 3, 4, 6, 8)]:
+        for mb, wgs, units in [(b, w, u) for _ in range(2) for b in (1, 4) for w in (2, 3)
+                               for u in (2, 4)]:
             if True:
+                d.ecamd_tune(b"frame_crc_mb", mb)
                 d.ecamd_tune(b"frame_crc_wgs", wgs)
                 d.ecamd_tune(b"frame_crc_units", units)
                 ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
-                print(json.dumps({"op": "frame_encode_fused_crc", "wgs": wgs, "units_per_cu": units,
+                print(json.dumps({"op": "frame_encode_fused_crc", "mb": mb, "wgs": wgs, "units_per_cu": units,
                                   "ms": round(ms, 3)}), flush=True)
+        d.ecamd_tune(b"frame_crc_mb", 0)
         d.ecamd_tune(b"frame_crc_wgs", 0)
         d.ecamd_tune(b"frame_crc_units", 0)
     # objects that do not fill the payloads: Swift's default 1 MiB EC segments (bs = 104858) and a
