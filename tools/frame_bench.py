@@ -49,7 +49,8 @@ def main():
                                      fb.blocksize, S, 0, 0x5EED, st.handle), "fill")
     payload_bytes = S * (k + m) * fb.blocksize
     for bits, gap, pos, span in (() if args.no_crc_sweep else
-                                 ((4, 8, 0, 16), (5, 8, 1, 64), (5, 8, 1, 128), (4, 8, 1, 64), (7, 8, 1, 64))):
+                                 ((4, 8, 0, 16), (5, 8, 1, 64), (5, 8, 1, 128), (4, 8, 1, 64), (7, 8, 1, 64),
+                                  (6, 8, 1, 128), (7, 8, 1, 128), (8, 8, 1, 64), (8, 8, 1, 128))):
         for wgs in (0, 4):
             d.ecamd_tune(b"crc_span_kib", span)
             d.ecamd_tune(b"crc_pos", pos)
