@@ -163,6 +163,8 @@ struct Tuning {
     int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
                             // measured best, tools/xor_sweep.py)
+    int grid_mult = 0;      // stream launches: workgroups per resident slot (0: 2 for 4-output
+                            //   passes, else 1; tools/grid_sweep.py)
     int multi_list = 1;     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     int stream_hybrid = 1;  //   8-output passes: one input in 4 looks its hi table up via L1
     int stream_order = 0;   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
@@ -261,7 +263,7 @@ struct Geometry {
 };
 
 int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chunks = 1,
-             int max_threads = 1024, int max_wgs = 8)
+             int max_threads = 1024, int max_wgs = 8, int grid_mult = 1)
 {
     int wgs = lds ? static_cast<int>(std::min<size_t>(max_wgs, std::max<size_t>(1, kLdsBytes / lds))) : 8;
     int threads = lds ? std::min(1024, std::max(256, (1024 / wgs) / 64 * 64)) : 256;
@@ -276,7 +278,7 @@ int geometry(int dev, size_t lds, int64_t bs, int nstripes, Geometry& g, int chu
     g.lds = lds;
     g.tiles_per_stripe = static_cast<uint32_t>(tps);
     g.ntiles = static_cast<uint32_t>(nt);
-    int64_t grid = std::min<int64_t>(nt, static_cast<int64_t>(cu_count(dev)) * wgs);
+    int64_t grid = std::min<int64_t>(nt, static_cast<int64_t>(cu_count(dev)) * wgs * std::max(1, grid_mult));
     g.grid = static_cast<int>(std::max<int64_t>(grid, 1));
     return 0;
 }
@@ -429,8 +431,11 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             const int ch = (p.width <= 4 && !nib) ? g_tune.stream_ch : 1;
             if (nib) a.tables = map->d_tables + p.nib_offset;
             // 16 waves per CU (4 x 256 threads, or fewer, larger workgroups when the tables
-            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5
-            rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4);
+            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5.  4-output
+            // passes launch twice the resident workgroups (C3 encode / decode 1.2-2.7% faster;
+            // C2 7% and C5 2-4% slower that way, so only there)
+            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult : (p.width == 4 ? 2 : 1);
+            rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4, gm);
             if (rc) return rc;
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
@@ -904,6 +909,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_ch = value == 2 ? 2 : 1;
     } else if (k == "xor_wgs") {
         g_tune.xor_wgs = std::max(0, std::min(value, 8));
+    } else if (k == "grid_mult") {
+        g_tune.grid_mult = std::max(0, std::min(value, 64));
     } else if (k == "multi_list") {
         g_tune.multi_list = value;
     } else if (k == "stream_hybrid") {
