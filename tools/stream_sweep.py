@@ -22,7 +22,7 @@ CFGS = {"c3": (10, 4, 1 << 20, 256, [0, 1, 2, 3]),
 
 
 # (stream, ch, pf, nib, order, hybrid)
-VARIANTS = [(0, 1, 0, 0, 0, 0), (1, 1, 0, 0, 0, 0), (1, 1, 0, 0, 0, 1), (1, 1, 0, 0, 1, 1)]
+VARIANTS = [(0, 1, 0, 0, 0, 0), (1, 1, 0, 0, 0, 1), (1, 1, 0, 0, 1, 1), (1, 1, 0, 0, 2, 1), (1, 1, 0, 0, 3, 1)]
 
 
 def main():
