@@ -665,7 +665,8 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         int rc;
         if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs) &&
             (p.row0 != 0 || stream_copy_offsets(a, bs))) {
-            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4);
+            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult : (p.width == 4 ? 2 : 1);
+            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4, gm);
             if (rc) return rc;
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;

@@ -33,9 +33,11 @@ def main():
     ap.add_argument("--fused-sweep", action="store_true")
     ap.add_argument("--align", type=int, default=128, help="payload alignment of the fragment batch")
     ap.add_argument("--no-crc-sweep", action="store_true")
+    ap.add_argument("--grid-mult", type=int, default=0, help="grid_mult tuning (0 = library default)")
     args = ap.parse_args()
     S, k, m, size = args.stripes, 10, 4, 10 * 1048576
     d = _lib.dev()
+    d.ecamd_tune(b"grid_mult", args.grid_mult)
     st = D.Stream()
     fb = frame.FrameBatch(frame.RS_VAND, k, m, size, S, align=args.align)
     print(json.dumps({"align": args.align, "frag_stride": fb.frag_stride, "head": fb.head}), flush=True)
