@@ -77,8 +77,9 @@ int ecamd_rs_decode(int k, int m, const int *missing, int rebuild_parity, void *
                     void *stream);
 /* Heterogeneous batch decode: stripe s has its own -1 terminated erasure list at
  * missing + s*missing_stride (at most missing_stride entries).  Stripes are grouped by erasure
- * set; each group is one launch over a device pointer table, so a batch of stripes that lost
- * different fragments still costs one launch per distinct pattern, not per stripe. */
+ * set; each group is one launch over a device stripe list (a pointer table when k > 20 or a
+ * stripe spans 2 GiB), so a batch of stripes that lost different fragments costs one launch per
+ * distinct pattern, not per stripe. */
 int ecamd_rs_decode_multi(int k, int m, const int *missing, int missing_stride,
                           int rebuild_parity, void *base, int64_t stripe_stride,
                           int64_t frag_stride, int64_t blocksize, int nstripes, void *stream);
@@ -93,6 +94,26 @@ int ecamd_scatter_fragments(const void *d_src, int64_t stripe_stride, int64_t fr
 int ecamd_rs_reconstruct(int k, int m, const int *missing, int dest, void *base,
                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
                          int nstripes, void *stream);
+
+/* ---- flat_xor_hd on strided batches: the reference's xor_code_encode,
+ * xor_hd_decode (decode_parity as its argument) and xor_reconstruct_one
+ * (src/builtin/xor_codes/xor_code.c:180-314, xor_hd_code.c:574-662) replayed exactly per erasure
+ * list, missing slots read as zero (the frontend's zero-filled buffers); (k, m, hd) one of the
+ * codes init_xor_hd_code accepts.  encode overwrites the parity slots (the reference accumulates
+ * into the zeroed parity the frontend allocates: the same bytes).  decode_multi groups stripes by
+ * identical erasure lists and runs one stripe-list launch per group.  ECAMD_EINVAL for patterns
+ * the code cannot recover. */
+int ecamd_xor_encode(int k, int m, int hd, void *base, int64_t stripe_stride, int64_t frag_stride,
+                     int64_t blocksize, int nstripes, void *stream);
+int ecamd_xor_decode(int k, int m, int hd, const int *missing, int decode_parity, void *base,
+                     int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
+                     void *stream);
+int ecamd_xor_reconstruct(int k, int m, int hd, const int *missing, int dest, void *base,
+                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
+                          void *stream);
+int ecamd_xor_decode_multi(int k, int m, int hd, const int *missing, int missing_stride,
+                           int decode_parity, void *base, int64_t stripe_stride, int64_t frag_stride,
+                           int64_t blocksize, int nstripes, void *stream);
 
 /* ---- synchronous host-buffer execution (used by the per-call drop-in ABIs) ----
  * Pooled pinned staging + two streams, chunked so host copies overlap PCIe and the kernel.

@@ -87,6 +87,17 @@ def dev():
                 C.c_int, VP])
         _proto(d, "ecamd_rs_reconstruct", C.c_int,
                [C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
+        _proto(d, "ecamd_xor_encode", C.c_int,
+               [C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, VP])
+        _proto(d, "ecamd_xor_decode", C.c_int,
+               [C.c_int, C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64,
+                C.c_int, VP])
+        _proto(d, "ecamd_xor_reconstruct", C.c_int,
+               [C.c_int, C.c_int, C.c_int, IP, C.c_int, VP, C.c_int64, C.c_int64, C.c_int64,
+                C.c_int, VP])
+        _proto(d, "ecamd_xor_decode_multi", C.c_int,
+               [C.c_int, C.c_int, C.c_int, IP, C.c_int, C.c_int, VP, C.c_int64, C.c_int64,
+                C.c_int64, C.c_int, VP])
         _proto(d, "ecamd_fill_splitmix", C.c_int,
                [VP, C.c_int64, C.c_int64, C.c_int, C.c_int64, C.c_int, C.c_int, C.c_uint64, VP])
         _proto(d, "ecamd_frame_geometry", C.c_int,

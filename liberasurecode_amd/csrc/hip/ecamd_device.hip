@@ -527,6 +527,8 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                 default: hipLaunchKernelGGL((xor_stream_kernel<8>), grid, block, 0, st, a); break;
                 }
             } else {
+                if (a.stripe_list)  // only the stream kernel reads a stripe list
+                    return fail(ECAMD_EINVAL, "stripe list on a non-stream xor launch");
                 hipLaunchKernelGGL((xor_apply_kernel<8, PTRS>), dim3(g.grid), dim3(g.threads), 0, st,
                                    a);
             }
@@ -859,6 +861,86 @@ int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64
 
 }  // namespace ecamd
 
+namespace ecamd {
+
+// StagedUpload: a small host table (stripe list / pointer table) goes up asynchronously on the
+// caller's stream, ahead of the launches that read it, from one of kStagedSlots (pinned host,
+// device) buffer pairs per (device, stream); a slot is reused only after the event recorded behind
+// its launches (end()) has fired, so back-to-back calls do not drain the stream.  The rings' lock
+// is held from begin() to end().
+namespace {
+struct StagedSlot {
+    void* host = nullptr;
+    void* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+};
+constexpr int kStagedSlots = 4;
+struct StagedRing {
+    StagedSlot slot[kStagedSlots];
+    int next = 0;
+};
+std::mutex g_staged_mu;
+std::map<std::pair<int, void*>, StagedRing> g_staged;  // (device, stream)
+}  // namespace
+
+int StagedUpload::begin(int device, void* stream, const void* src, size_t bytes)
+{
+    lock_ = std::unique_lock<std::mutex>(g_staged_mu);
+    StagedRing& ring = g_staged[{device, stream}];
+    StagedSlot& sc = ring.slot[ring.next];
+    ring.next = (ring.next + 1) % kStagedSlots;
+    if (sc.done) HIP_TRY(hipEventSynchronize(sc.done));
+    else HIP_TRY(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
+    const size_t need = std::max<size_t>(bytes, 16);
+    if (sc.cap < need) {
+        if (sc.host) HIP_TRY(hipHostFree(sc.host));
+        if (sc.dev) HIP_TRY(hipFree(sc.dev));
+        sc.host = sc.dev = nullptr;
+        sc.cap = 0;
+        HIP_TRY(hipHostMalloc(&sc.host, need, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&sc.dev, need));
+        sc.cap = need;
+    }
+    std::memcpy(sc.host, src, bytes);
+    HIP_TRY(hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
+    done_ = static_cast<void*>(sc.done);
+    dev = sc.dev;
+    return 0;
+}
+
+int StagedUpload::end(void* stream)
+{
+    if (done_) {
+        HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(done_), static_cast<hipStream_t>(stream)));
+        done_ = nullptr;
+    }
+    if (lock_.owns_lock()) lock_.unlock();
+    return 0;
+}
+
+}  // namespace ecamd
+
+namespace ecamd {
+
+int xor_apply_list(const uint32_t* masks, int R, int K, void* base, int64_t stripe_stride,
+                   const int64_t* in_off, const int64_t* out_off, int64_t blocksize, int nstripes,
+                   const int32_t* d_list, void* stream)
+{
+    if (!masks || !in_off || !out_off || R <= 0 || K <= 0 || K > 32 || !d_list)
+        return fail(ECAMD_EINVAL, "bad xor map R=%d K=%d", R, K);
+    if (nstripes <= 0 || blocksize <= 0) return 0;
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(base);
+    a.out_base = static_cast<uint8_t*>(base);
+    a.in_stride = a.out_stride = stripe_stride;
+    a.stripe_list = d_list;
+    return launch_xor<false>(masks, R, K, a, in_off, out_off, blocksize, nstripes,
+                             static_cast<hipStream_t>(stream));
+}
+
+}  // namespace ecamd
+
 extern "C" {
 
 int ecamd_init(void) { return ensure_device(nullptr); }
@@ -1134,43 +1216,12 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
                 for (int f = 0; f < row; f++)
                     table.push_back(static_cast<uint8_t*>(base) + s * stripe_stride + f * frag_stride);
     }
-    // The table goes up asynchronously on the caller's stream, ahead of the launches that read it,
-    // from one of kSlots (pinned host, device) buffer pairs per (device, stream): a slot is reused
-    // only after the event recorded behind its last launches has fired, so back-to-back calls do
-    // not drain the stream (the GPU stays busy while the host plans the next call).
-    struct Slot {
-        void* host = nullptr;
-        void* dev = nullptr;
-        size_t cap = 0;
-        hipEvent_t done = nullptr;
-    };
-    constexpr int kSlots = 4;
-    struct Ring {
-        Slot slot[kSlots];
-        int next = 0;
-    };
-    static std::mutex mu;
-    static std::map<std::pair<int, void*>, Ring> rings;  // (device, stream)
-    std::lock_guard<std::mutex> lk(mu);
-    Ring& ring = rings[{dev, stream}];
-    Slot& sc = ring.slot[ring.next];
-    ring.next = (ring.next + 1) % kSlots;
     const size_t bytes = use_list ? list.size() * sizeof(int32_t) : table.size() * sizeof(uint8_t*);
-    if (sc.done) HIP_TRY(hipEventSynchronize(sc.done));
-    else HIP_TRY(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
-    if (sc.cap < bytes) {
-        if (sc.host) HIP_TRY(hipHostFree(sc.host));
-        if (sc.dev) HIP_TRY(hipFree(sc.dev));
-        sc.host = sc.dev = nullptr;
-        sc.cap = 0;
-        HIP_TRY(hipHostMalloc(&sc.host, bytes, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(&sc.dev, bytes));
-        sc.cap = bytes;
-    }
-    std::memcpy(sc.host, use_list ? static_cast<const void*>(list.data()) : table.data(), bytes);
-    HIP_TRY(hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
-    auto* d_table = static_cast<uint8_t**>(sc.dev);
-    auto* d_list = static_cast<const int32_t*>(sc.dev);
+    StagedUpload up;
+    rc = up.begin(dev, stream, use_list ? static_cast<const void*>(list.data()) : table.data(), bytes);
+    if (rc) return rc;
+    auto* d_table = static_cast<uint8_t**>(up.dev);
+    auto* d_list = static_cast<const int32_t*>(up.dev);
     size_t at = 0;
     for (const auto& g : groups) {
         const int G = static_cast<int>(g.second.size());
@@ -1210,8 +1261,8 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
         }
         if (rc) break;
     }
-    HIP_TRY(hipEventRecord(sc.done, static_cast<hipStream_t>(stream)));
-    return rc;
+    const int rc2 = up.end(stream);
+    return rc ? rc : rc2;
 }
 
 int ecamd_scatter_fragments(const void* d_src, int64_t stripe_stride, int64_t frag_stride,

@@ -242,7 +242,8 @@ int grid_for(int dev, int64_t work)
 
 // XOR plan of a reference operation applied in place on the payloads of every stripe.
 int xor_plan_apply(const Code& c, int op, const int* missing, int arg, uint8_t* payload0,
-                   int64_t ss, int64_t fs, int64_t bs, int nstripes, void* stream)
+                   int64_t ss, int64_t fs, int64_t bs, int nstripes, void* stream,
+                   const int32_t* d_list = nullptr)
 {
     unsigned pb[32], db[32];
     ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db);
@@ -280,8 +281,22 @@ int xor_plan_apply(const Code& c, int op, const int* missing, int arg, uint8_t* 
         masks.push_back(mk);
         out_off.push_back(outs[i] * fs);
     }
+    if (d_list)
+        return xor_apply_list(masks.data(), n, static_cast<int>(in_off.size()), payload0, ss, in_off.data(),
+                              out_off.data(), bs, nstripes, d_list, stream);
     return ecamd_xor_apply_strided(masks.data(), n, static_cast<int>(in_off.size()), payload0, ss,
                                    in_off.data(), payload0, ss, out_off.data(), bs, nstripes, stream);
+}
+
+// Strided flat_xor_hd batches (fragment f of stripe s at base + s*ss + f*fs, bs bytes).
+int xor_batch_check(const Code& c, const void* base, int64_t ss, int64_t fs, int64_t bs, int nstripes)
+{
+    int rc = check_code(c);
+    if (rc) return rc;
+    if (!base || nstripes < 0 || bs < 0) return dev_fail(ECAMD_EINVAL, "null base or negative sizes");
+    if (!a16(base) || ss % 16 || fs % 16) return dev_fail(ECAMD_EINVAL, "fragment addresses must be 16-byte aligned");
+    if (fs < bs) return dev_fail(ECAMD_EINVAL, "frag_stride < blocksize");
+    return 0;
 }
 
 // ---- fused CHKSUM_CRC32 framed encode (hip/ecamd_frame_fused.hip) ----
@@ -579,6 +594,107 @@ int ecamd_crc32(int legacy, const void* d_base, int64_t stripe_stride, int64_t f
     HeaderArgs none{};
     return run_crc(dev, legacy != 0, true, static_cast<const uint8_t*>(d_base), stripe_stride,
                    frag_stride, 0, nfrag, len, nstripes, d_crc, none, stream);
+}
+
+// ---- flat_xor_hd on strided batches (no framing): encode / decode / reconstruct in place ----
+
+int ecamd_xor_encode(int k, int m, int hd, void* base, int64_t stripe_stride, int64_t frag_stride,
+                     int64_t blocksize, int nstripes, void* stream)
+{
+    int rc = dev_ensure(nullptr);
+    if (rc) return rc;
+    const Code c = make_code(kBackendXor, k, m, hd);
+    if ((rc = xor_batch_check(c, base, stripe_stride, frag_stride, blocksize, nstripes))) return rc;
+    if (nstripes == 0 || blocksize == 0) return 0;
+    // xor_code_encode (src/builtin/xor_codes/xor_code.c:180-191) accumulates into the zeroed
+    // parity the frontend allocates: parity j = XOR of the data fragments in parity_bms[j], which
+    // is written here (overwriting whatever the parity slots held)
+    unsigned pb[32], db[32];
+    ecamd_xor_code_tables(k, m, hd, pb, db);
+    std::vector<int64_t> in_off(k), out_off(m);
+    for (int j = 0; j < k; j++) in_off[j] = j * frag_stride;
+    for (int r = 0; r < m; r++) out_off[r] = (k + r) * frag_stride;
+    return ecamd_xor_apply_strided(pb, m, k, base, stripe_stride, in_off.data(), base, stripe_stride,
+                                   out_off.data(), blocksize, nstripes, stream);
+}
+
+int ecamd_xor_decode(int k, int m, int hd, const int* missing, int decode_parity, void* base,
+                     int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
+                     void* stream)
+{
+    int rc = dev_ensure(nullptr);
+    if (rc) return rc;
+    const Code c = make_code(kBackendXor, k, m, hd);
+    if ((rc = xor_batch_check(c, base, stripe_stride, frag_stride, blocksize, nstripes))) return rc;
+    if (!missing) return dev_fail(ECAMD_EINVAL, "null missing list");
+    for (int i = 0; missing[i] >= 0; i++)
+        if (missing[i] >= k + m) return dev_fail(ECAMD_EINVAL, "missing index %d out of range", missing[i]);
+    if (nstripes == 0 || blocksize == 0) return 0;
+    return xor_plan_apply(c, 1, missing, decode_parity ? 1 : 0, static_cast<uint8_t*>(base), stripe_stride,
+                          frag_stride, blocksize, nstripes, stream);
+}
+
+int ecamd_xor_reconstruct(int k, int m, int hd, const int* missing, int dest, void* base,
+                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize, int nstripes,
+                          void* stream)
+{
+    int rc = dev_ensure(nullptr);
+    if (rc) return rc;
+    const Code c = make_code(kBackendXor, k, m, hd);
+    if ((rc = xor_batch_check(c, base, stripe_stride, frag_stride, blocksize, nstripes))) return rc;
+    if (!missing || dest < 0 || dest >= k + m) return dev_fail(ECAMD_EINVAL, "bad missing list / destination");
+    for (int i = 0; missing[i] >= 0; i++)
+        if (missing[i] >= k + m) return dev_fail(ECAMD_EINVAL, "missing index %d out of range", missing[i]);
+    if (nstripes == 0 || blocksize == 0) return 0;
+    return xor_plan_apply(c, 2, missing, dest, static_cast<uint8_t*>(base), stripe_stride, frag_stride,
+                          blocksize, nstripes, stream);
+}
+
+int ecamd_xor_decode_multi(int k, int m, int hd, const int* missing, int missing_stride, int decode_parity,
+                           void* base, int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
+                           int nstripes, void* stream)
+{
+    int dev = 0;
+    int rc = dev_ensure(&dev);
+    if (rc) return rc;
+    const Code c = make_code(kBackendXor, k, m, hd);
+    if ((rc = xor_batch_check(c, base, stripe_stride, frag_stride, blocksize, nstripes))) return rc;
+    if (!missing || missing_stride < 1) return dev_fail(ECAMD_EINVAL, "bad missing lists");
+    if (nstripes == 0 || blocksize == 0) return 0;
+    if ((k + m - 1) * frag_stride + blocksize >= (int64_t(1) << 31))
+        return dev_fail(ECAMD_EINVAL, "stripes wider than 2 GiB");
+    // Group stripes by their erasure list as given: xor_hd_decode's control flow (which equation
+    // rebuilds what) follows the list, so stripes share a launch only with identical lists.
+    std::map<std::vector<int>, std::vector<int32_t>> groups;
+    for (int s = 0; s < nstripes; s++) {
+        const int* row = missing + static_cast<int64_t>(s) * missing_stride;
+        std::vector<int> pat;
+        for (int i = 0; i < missing_stride && row[i] >= 0; i++) {
+            if (row[i] >= k + m) return dev_fail(ECAMD_EINVAL, "stripe %d: missing index %d", s, row[i]);
+            pat.push_back(row[i]);
+        }
+        groups[pat].push_back(s);
+    }
+    std::vector<int32_t> list;
+    list.reserve(nstripes);
+    for (const auto& g : groups) list.insert(list.end(), g.second.begin(), g.second.end());
+    StagedUpload up;
+    if ((rc = up.begin(dev, stream, list.data(), list.size() * sizeof(int32_t)))) return rc;
+    const auto* d_list = static_cast<const int32_t*>(up.dev);
+    size_t at = 0;
+    for (const auto& g : groups) {
+        const int G = static_cast<int>(g.second.size());
+        const int32_t* sl = d_list + at;
+        at += static_cast<size_t>(G);
+        if (g.first.empty()) continue;
+        std::vector<int> pat(g.first);
+        pat.push_back(-1);
+        rc = xor_plan_apply(c, 1, pat.data(), decode_parity ? 1 : 0, static_cast<uint8_t*>(base), stripe_stride,
+                            frag_stride, blocksize, G, stream, sl);
+        if (rc) break;
+    }
+    const int rc2 = up.end(stream);
+    return rc ? rc : rc2;
 }
 
 }  // extern "C"

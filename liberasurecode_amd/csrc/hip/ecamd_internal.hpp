@@ -1,8 +1,32 @@
 // ecamd_internal.hpp -- helpers ecamd_device.hip shares with the other launch files.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+
 namespace ecamd {
+
+// Asynchronous upload of a small host table (stripe list, pointer table) on `stream` through a
+// ring of pinned slots per (device, stream); call end() after enqueuing the launches that read
+// `dev` (ecamd_device.hip).
+struct StagedUpload {
+    void* dev = nullptr;
+    int begin(int device, void* stream, const void* src, size_t bytes);
+    int end(void* stream);
+    ~StagedUpload() { if (lock_.owns_lock()) lock_.unlock(); }
+
+private:
+    void* done_ = nullptr;
+    std::unique_lock<std::mutex> lock_;
+};
+
+// Strided flat-XOR apply (ecamd_xor_apply_strided) over the stripes listed in the device array
+// d_list (logical stripe i is stripe d_list[i] of the layout); ECAMD_EINVAL when the stream
+// kernel cannot take the shape.
+int xor_apply_list(const uint32_t* masks, int R, int K, void* base, int64_t stripe_stride,
+                   const int64_t* in_off, const int64_t* out_off, int64_t blocksize, int nstripes,
+                   const int32_t* d_list, void* stream);
 
 int dev_ensure(int* dev_out);                       // 0, or ECAMD_ENODEV / ECAMD_EHIP
 int dev_cu_count(int dev);

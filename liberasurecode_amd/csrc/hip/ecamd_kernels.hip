@@ -158,8 +158,9 @@ __global__ void __launch_bounds__(256) xor_stream_kernel(const ApplyArgs a)
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
     const int cstride = static_cast<int>(blockDim.x) * 16;
     for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-        const uint32_t s = t / a.tiles_per_stripe;
-        const int64_t toff = static_cast<int64_t>(t - s * a.tiles_per_stripe) * cstride;
+        const uint32_t sl = t / a.tiles_per_stripe;
+        const int64_t toff = static_cast<int64_t>(t - sl * a.tiles_per_stripe) * cstride;
+        const uint32_t s = a.stripe_list ? static_cast<uint32_t>(a.stripe_list[sl]) : sl;
         const int64_t o64 = toff + static_cast<int64_t>(threadIdx.x) * 16;
         if (toff + cstride > a.bs) {  // last, partial tile of each fragment
             const int64_t rem = a.bs - o64;

@@ -173,6 +173,37 @@ class GF16Map:
             lay.blocksize, lay.nstripes, _s(stream)), "map_apply")
 
 
+def xor_encode(k, m, hd, lay: Layout, stream=None):
+    """flat_xor_hd encode of a strided batch in place (ecamd_xor_encode)."""
+    check(dev().ecamd_xor_encode(k, m, hd, lay.buf.ptr, lay.stripe_stride, lay.frag_stride,
+                                 lay.blocksize, lay.nstripes, _s(stream)), "xor_encode")
+
+
+def xor_decode(k, m, hd, missing, lay: Layout, decode_parity=True, stream=None):
+    """xor_hd_decode replayed on every stripe (missing slots read as zero)."""
+    check(dev().ecamd_xor_decode(k, m, hd, ints(list(missing) + [-1]), int(decode_parity),
+                                 lay.buf.ptr, lay.stripe_stride, lay.frag_stride, lay.blocksize,
+                                 lay.nstripes, _s(stream)), "xor_decode")
+
+
+def xor_reconstruct(k, m, hd, missing, dest, lay: Layout, stream=None):
+    """xor_reconstruct_one of fragment `dest` on every stripe."""
+    check(dev().ecamd_xor_reconstruct(k, m, hd, ints(list(missing) + [-1]), dest, lay.buf.ptr,
+                                      lay.stripe_stride, lay.frag_stride, lay.blocksize,
+                                      lay.nstripes, _s(stream)), "xor_reconstruct")
+
+
+def xor_decode_multi(k, m, hd, missing_per_stripe, lay: Layout, decode_parity=True, stream=None):
+    """One erasure list per stripe; stripes with identical lists share a launch."""
+    width = k + m + 1
+    flat = []
+    for pat in missing_per_stripe:
+        flat += list(pat)[:width - 1] + [-1] * (width - min(len(pat), width - 1))
+    check(dev().ecamd_xor_decode_multi(k, m, hd, ints(flat), width, int(decode_parity), lay.buf.ptr,
+                                       lay.stripe_stride, lay.frag_stride, lay.blocksize,
+                                       lay.nstripes, _s(stream)), "xor_decode_multi")
+
+
 def xor_apply(masks, lay: Layout, inputs, outputs, stream=None):
     check(dev().ecamd_xor_apply_strided(
         u32s(masks), len(outputs), len(inputs), lay.buf.ptr, lay.stripe_stride,

@@ -55,6 +55,23 @@ def main():
                               "ms": round(ms, 4), "GBps": round(algo / ms / 1e6, 1)}), flush=True)
     ms = timed(lambda: D.rs_decode(k, m, allpats[0], lay, stream=st))
     print(json.dumps({"decode_strided": allpats[0], "ms": round(ms, 4), "GBps": round(algo / ms / 1e6, 1)}))
+    lay.buf.free()
+
+    # flat_xor_hd (10, 6, 4): encode, single-pattern decode and a 4-pattern batch (stripe lists);
+    # bytes = the fragments each launch reads and writes (read set differs per pattern: the sum
+    # over the launch's plan inputs + outputs, counted per stripe)
+    xk, xm, hd = 10, 6, 4
+    lay = D.Layout.alloc(xk + xm, F, S)
+    lay.fill_splitmix(nfrags=xk, stream=st)
+    D.xor_encode(xk, xm, hd, lay, stream=st)
+    xpats = [[0, 1, 2], [3, 7, 12], [4, 5, 6], [0, 9, 15]]
+    per = [xpats[s % len(xpats)] for s in range(S)]
+    for name, fn in (("xor_encode", lambda: D.xor_encode(xk, xm, hd, lay, stream=st)),
+                     ("xor_decode_1pattern", lambda: D.xor_decode(xk, xm, hd, xpats[0], lay, stream=st)),
+                     ("xor_decode_multi_4patterns", lambda: D.xor_decode_multi(xk, xm, hd, per, lay, stream=st))):
+        ms = timed(fn)
+        print(json.dumps({name: [xk, xm, hd], "ms": round(ms, 4),
+                          "GiBps_object": round(S * xk * F / ms / 1e6 / 1.073741824, 1)}), flush=True)
 
 
 if __name__ == "__main__":
