@@ -4,35 +4,40 @@
 One step = one pass of the hot path over one batch: RS(k=10, m=4) encode of S stripes of 1 MiB
 fragments (BASELINE.json configs[2], "C3"), then decode of the same S stripes with data fragments
 {0,1,2,3} erased (every rebuilt fragment needs a full 10-term GF(2^16) dot product).  Inputs are
-resident in HBM before the timed region.  value = object bytes (2 * S * k * F per step per GPU,
-summed over GPUs) / wall time of the K timed steps (max over ranks), in GiB/s.
+resident in HBM before the timed region.  value = object bytes (2 * S * k * F per step, summed
+over ranks) / wall time of the K timed steps (max over ranks), in GiB/s.
 
-Multi-GPU: one process per GPU (torch.distributed.run); stripes are independent, each rank owns
-its own S stripes (weak scaling) and there is no data-path collective -- the process group is used
-for the start barrier and the max-over-ranks of the elapsed time only.
+Multi-GPU (C4): one process per GPU.  Stripes are independent (src/erasurecode.c:383-477), so each
+rank owns its own stripes -- S per GPU (--scaling weak, default) or an even split of a fixed total
+(--scaling strong, 2048 stripes) -- and there is no data-path collective: the process group
+carries the start barrier, the max-over-ranks of the elapsed time and the per-rank rates only.
+Ranks come from torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*), or, when
+`--gpus N` > 1 is given without them, bench.py starts the N rank processes itself before anything
+touches the GPU (fresh child processes, no exec) and relays rank 0's line.
 
-Extra fields: "roofline" (gf16_stream_kernel, HIP-event timed per launch on the launch stream; peak =
-8 TB/s spec, plus a copy peak measured live) and "cpu_baseline" (the reference codec compiled from
-its sources -- or the oracle restatement when that build is absent -- on the host cores; rank 0).
+Extra fields: "roofline" (the dominant kernel, HIP-event timed per launch on its launch stream; peak =
+8 TB/s spec, plus a live copy probe; "trace" = the same figure from the committed rocprofv3 kernel
+trace of this command), "cpu_baseline" (the reference codec compiled from its sources -- or the
+oracle restatement when that build is absent -- on the host's usable cores; rank 0 at N=1), and
+"c5" (BASELINE configs[4], k=20 m=8 4 MiB: rebuild of 8 lost fragments, outside the timed steps).
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402  (before libecamd: one HIP runtime per process)
-
-from liberasurecode_amd import device as D  # noqa: E402
-from liberasurecode_amd.shard import Coordinator, stripe_range  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 # second decode pattern per config, data and parity mixed (SURVEY.md §8d)
 MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}
 GIB = float(1 << 30)
+ROUND = "r02"  # profiles/<round>_* written by tools/gpu_prof.sh for this bench
 
 CONFIGS = {
     # name: (k, m, fragment bytes, stripes per GPU, decode erasures, description)
@@ -43,15 +48,103 @@ CONFIGS = {
     "c5": (20, 8, 4 << 20, 32, list(range(8)),
            "C5 liberasurecode_rs_vand k=20 m=8, 4 MiB fragments, encode + decode(8 data missing)"),
 }
+STRONG_TOTAL = 2048  # C4 strong scaling, 2048 C3 stripes over all GPUs
 
 
-def cpu_baseline(k, m, F, missing, threads, stripes):
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--stripes", type=int, default=0,
+                    help="stripes per GPU (weak) or in total (strong); 0 = the config's")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 rebuild-8 fields")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0,
+                    help="target wall seconds of the multi-thread CPU-baseline leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="GPU-less rehearsal of the rank / shard plumbing (gloo, no kernels)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ rank launcher ----
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (fresh interpreters; this process never touches
+    the GPU) and return the highest exit code.  A failing rank takes the others down with it."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        out = None if r == 0 else subprocess.DEVNULL  # rank 0 prints the line
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env, stdout=out))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = max(rc, abs(code))
+                for q in live:  # the others would wait forever at the next barrier
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+def world_from_env(gpus):
+    """(world, launched_by_us) -- fails loudly when --gpus disagrees with the launcher's world."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; they must agree")
+        return world
+    return 1 if gpus <= 1 else None
+
+
+# ------------------------------------------------------------------ CPU baseline ----
+
+def usable_cores():
+    """(usable, visible, quota): CPUs this process may run on -- the affinity set, capped by a
+    cgroup v2 CPU quota when one is set (cpu.max) -- and what os.cpu_count() shows."""
+    visible = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = visible
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, math.floor(quota)))
+    return usable, visible, aff, quota
+
+
+def cpu_baseline(k, m, F, missing, threads, target_s):
     """Host-CPU baseline of the same hot path on this machine.
 
     Uses the REFERENCE codec itself (oracle/_ref/liberasurecode_rs_vand.so.1, compiled from the
     reference sources by oracle/Makefile, kind "reference") when it is present, else the oracle
-    restatement (oracle/ec_oracle.c, same log/antilog algorithm, kind "port").  One stripe per task,
-    `threads` threads (ctypes releases the GIL), and separately one thread."""
+    restatement (oracle/ec_oracle.c, same log/antilog algorithm, kind "port").  One stripe per task
+    on `threads` threads (ctypes releases the GIL), sized from a 1-thread calibration so the
+    multi-thread leg runs about target_s seconds; also reported per core."""
     import ctypes as C
     from concurrent.futures import ThreadPoolExecutor
 
@@ -101,8 +194,10 @@ def cpu_baseline(k, m, F, missing, threads, stripes):
         total = sum(n for n, _ in res)
         return 2 * total * k * F / GIB / wall, total, sum(t for _, t in res)
 
-    value, total, cpu_s = run(threads, stripes)
-    one, one_total, one_s = run(1, max(2, stripes // 4))
+    one, one_total, one_s = run(1, 4)
+    per_stripe_s = one_s / one_total
+    per = max(2, int(round(target_s / per_stripe_s)))
+    value, total, cpu_s = run(threads, per)
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -111,74 +206,150 @@ def cpu_baseline(k, m, F, missing, threads, stripes):
                 break
     except OSError:
         pass
+    usable, visible, aff, quota = usable_cores()
     return {"value": round(value, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
             "value_1core": round(one, 4),
-            "sample": f"{total} stripes x (encode + decode {list(missing)}) of k={k} m={m} F={F} on "
-                      f"{threads} threads, plus {one_total} on 1 thread; {what}",
+            "sample": f"{total} stripes x (encode + decode {list(missing)}) of k={k} m={m} F={F} "
+                      f"on {threads} threads, plus {one_total} on 1 thread; {what}",
             "cpu_seconds": round(cpu_s + one_s, 2), "cpu_model": model,
-            "host_cpus_visible": os.cpu_count()}
+            "cores_usable": usable, "host_cpus_visible": visible, "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota,
+            "note": "cores = the CPUs this job may use (affinity capped by the cgroup CPU quota); "
+                    "host_cpus_visible is the whole machine"}
 
 
-def measured_copy_peak(stream, nbytes=1 << 30):
-    """Second roofline denominator: non-temporal 16 B/lane copy of 1 GiB on this GPU (GB/s)."""
-    import ctypes as C
+# ------------------------------------------------------------------ GPU helpers ----
 
+def measured_copy_peak(D, stream, nbytes=1 << 30):
+    """Second roofline denominator: non-temporal 16 B/lane copy of 1 GiB on this GPU (GB/s), from
+    the measurement library (liberasurecode_amd/lib/libecamd_probe.so, not the product)."""
     from liberasurecode_amd import _lib
-    d = _lib.dev()
-    d.ecamd_debug_bw_probe.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                       C.c_int64, C.c_void_p]
+    p = _lib.probe()
     buf = D.DeviceBuffer(2 * nbytes)
     a, b = D.Event(), D.Event()
     best = 0.0
     for _ in range(3):
-        _lib.check(d.ecamd_debug_bw_probe(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes,
-                                          stream.handle), "copy probe")
+        _lib.check(p.ecamd_probe_bw(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes, stream.handle),
+                   "copy probe")
         a.record(stream)
         for _ in range(4):
-            d.ecamd_debug_bw_probe(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes, stream.handle)
+            p.ecamd_probe_bw(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes, stream.handle)
         b.record(stream)
         best = max(best, 2 * nbytes * 4 / (a.elapsed_ms(b) * 1e-3) / 1e9)
     buf.free()
     return best
 
 
-def pmc_traffic(cfg, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this same
-    command (profiles/<round>_<cfg>_summary.json, built by tools/summarize_prof.py from separate
-    FETCH_SIZE / WRITE_SIZE passes with the gfx950 FETCH_SIZE x2 correction)."""
+def profile_summary(cfg):
+    """The committed rocprofv3 evidence for this command (tools/gpu_prof.sh ->
+    tools/summarize_prof.py): profiles/<round>_<cfg>_summary.json, newest round first."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_summary.json")),
                        reverse=True):
         try:
-            summ = json.load(open(path))
+            return json.load(open(path)), os.path.relpath(path, ROOT)
         except Exception:
             continue
-        for name, d in summ.get("kernels", {}).items():
-            if kernel in name and "hbm_bytes_per_launch" in d:
-                return int(d["hbm_bytes_per_launch"]), os.path.relpath(path, ROOT)
     return None, None
 
 
+def kernel_entry(summ, kernel):
+    for name, d in (summ or {}).get("kernels", {}).items():
+        if kernel in name:
+            return d
+    return None
+
+
+def c5_rebuild(D, stream, reps=5):
+    """BASELINE configs[4]: k=20 m=8, 4 MiB fragments, 8 fragments lost, 32 stripes in HBM.
+    'reconstruct with 8 missing' two ways: one pass that rebuilds all 8 (ecamd_rs_decode with
+    rebuild_parity: the k inputs are read once, inverse / composite rows from one host-side
+    inversion) and 8 single-destination ecamd_rs_reconstruct launches (what 8
+    liberasurecode_reconstruct_fragment calls do, src/erasurecode.c:748)."""
+    k, m, F, S, lost, _ = CONFIGS["c5"]
+    lay = D.Layout.alloc(k + m, F, S)
+    lay.fill_splitmix(nfrags=k, stream=stream)
+    D.rs_encode(k, m, lay, stream=stream)
+    out = {"workload": "C5 k=20 m=8, 4 MiB fragments, 32 stripes, 8 lost", "stripes": S}
+    a, b = D.Event(), D.Event()
+
+    def timed(fn):
+        fn()
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        stream.synchronize()
+        return a.elapsed_ms(b) / reps
+
+    # per launch: k inputs read + 8 outputs written per stripe (algorithmic bytes)
+    algo = S * (k + 8) * F
+    for name, pat in (("data", lost), ("mixed", MIXED_PATTERNS["c5"])):
+        ms = timed(lambda: D.rs_decode(k, m, pat, lay, stream=stream))
+        out[f"rebuild8_{name}_pattern"] = pat
+        out[f"rebuild8_{name}_ms"] = round(ms, 4)
+        out[f"rebuild8_{name}_gibs"] = round(S * k * F / GIB / (ms * 1e-3), 2)
+        out[f"rebuild8_{name}_frac"] = round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    ms = timed(lambda: [D.rs_reconstruct(k, m, lost, d, lay, stream=stream) for d in lost])
+    out["reconstruct_x8_ms"] = round(ms, 4)
+    out["reconstruct_x8_gibs"] = round(S * k * F / GIB / (ms * 1e-3), 2)
+    ms = timed(lambda: D.rs_encode(k, m, lay, stream=stream))
+    out["encode_ms"] = round(ms, 4)
+    out["encode_frac"] = round(S * (k + m) * F / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    lay.buf.free()
+    return out
+
+
+# ------------------------------------------------------------------ main ----
+
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-stripes", type=int, default=32, help="stripes per CPU thread")
-    args = ap.parse_args()
+    args = parse_args()
+    world = world_from_env(args.gpus)
+    if world is None:  # --gpus N > 1 without a launcher: start the ranks (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+
+    if args.dry_run:
+        os.environ.setdefault("ECAMD_DIST_BACKEND", "gloo")
+    from liberasurecode_amd.shard import Coordinator, split_range, stripe_range
 
     co = Coordinator()  # one process per GPU; RCCL only for the barrier and time reductions
     world, rank = co.world, co.rank
+    ranks_seen = int(co.reduce([1.0], op="sum")[0])
+    if ranks_seen != world:
+        raise SystemExit(f"bench.py: process group has {ranks_seen} ranks, expected {world}")
 
-    k, m, F, S, missing, desc = CONFIGS[args.config]
-    if args.stripes:
-        S = args.stripes
+    k, m, F, S_cfg, missing, desc = CONFIGS[args.config]
+    if args.scaling == "weak":
+        first, S = stripe_range(rank, world, args.stripes or S_cfg)
+    else:
+        first, S = split_range(rank, world, args.stripes or STRONG_TOTAL)
+    total_stripes = int(co.reduce([float(S)], op="sum")[0])
+    # every stripe exactly once over the ranks (independent shards, no data-path collective)
+    cover = [0.0] * total_stripes
+    for s in range(first, first + S):
+        cover[s] = 1.0
+    cover = co.reduce(cover, op="sum")
+    if any(c != 1.0 for c in cover):
+        raise SystemExit("bench.py: stripe shards do not cover the batch exactly once")
+
+    if args.dry_run:
+        co.barrier()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": ranks_seen,
+                              "scaling": args.scaling, "total_stripes": total_stripes,
+                              "stripes_per_rank": [int(x) for x in co.reduce(
+                                  [float(S) if r == rank else 0.0 for r in range(world)], "sum")],
+                              "covered_once": True}), flush=True)
+        else:
+            co.reduce([float(S) if r == rank else 0.0 for r in range(world)], "sum")
+        co.close()
+        return
+
+    import torch
+
+    from liberasurecode_amd import device as D
+
     assert D.available(), "no HIP device"
-    first, S = stripe_range(rank, world, S)  # this rank's shard of independent stripes
     lay = D.Layout.alloc(k + m, F, S)
     stream = D.Stream()
     lay.fill_splitmix(nfrags=k, stripe0=first, stream=stream)
@@ -217,38 +388,53 @@ def main():
 
     enc_ms = [a.elapsed_ms(b) for a, b, _ in ev]
     dec_ms = [b.elapsed_ms(c) for _, b, c in ev]
-    obj_bytes = S * k * F  # object bytes per stripe batch per GPU
-    value = 2 * obj_bytes * args.steps * world / GIB / elapsed
+    obj_bytes = S * k * F  # object bytes per batch on this rank
+    value = 2 * total_stripes * k * F * args.steps / GIB / elapsed
+    enc_gibs = obj_bytes / GIB / (sum(enc_ms) / len(enc_ms) / 1e3)
+    dec_gibs = obj_bytes / GIB / (sum(dec_ms) / len(dec_ms) / 1e3)
+    per_rank = co.reduce([enc_gibs if r == rank else 0.0 for r in range(world)] +
+                         [dec_gibs if r == rank else 0.0 for r in range(world)], op="sum")
     # dominant kernel: the stream kernel (C3 encode and decode: 10 in, 4 out per launch)
     launch_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
     # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
-    # <W outputs per pass, KG groups of 4 inputs, CH chunks per lane, PF prefetch, NIB nibble tables>;
-    # 8-output passes run its hybrid LDS + L1 lookup form <KG>
     kernel = (f"gf16_hybrid_kernel<{(k + 3) // 4}>" if width == 8 else
               f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>")
-    traffic, traffic_src = pmc_traffic(args.config, kernel)
-    if traffic is not None and S != CONFIGS[args.config][3]:
-        traffic = int(traffic * S / CONFIGS[args.config][3])  # profile ran at the default S
 
-    copy_gbs = measured_copy_peak(stream)
-
-    # The survey's second decode pattern per config, outside the timed steps:
-    # erasures mixing data and parity (fewer full dot products than all-data erasures).
-    mixed = MIXED_PATTERNS.get(args.config)
-    mixed_gibs = None
-    if mixed is not None:
-        a, b = D.Event(), D.Event()
-        D.rs_decode(k, m, mixed, lay, stream=stream)
-        a.record(stream)
-        for _ in range(5):
-            D.rs_decode(k, m, mixed, lay, stream=stream)
-        b.record(stream)
-        mixed_gibs = round(obj_bytes / GIB / (a.elapsed_ms(b) / 5 / 1e3), 3)
-
+    out = None
     if rank == 0:
+        copy_gbs = measured_copy_peak(D, stream)
+        # The survey's second decode pattern per config, outside the timed steps:
+        # erasures mixing data and parity (fewer full dot products than all-data erasures).
+        mixed = MIXED_PATTERNS.get(args.config)
+        mixed_gibs = None
+        if mixed is not None:
+            a, b = D.Event(), D.Event()
+            D.rs_decode(k, m, mixed, lay, stream=stream)
+            a.record(stream)
+            for _ in range(5):
+                D.rs_decode(k, m, mixed, lay, stream=stream)
+            b.record(stream)
+            mixed_gibs = round(obj_bytes / GIB / (a.elapsed_ms(b) / 5 / 1e3), 3)
+
+        summ, summ_src = profile_summary(args.config)
+        kd = kernel_entry(summ, kernel) or {}
+        traffic = kd.get("hbm_bytes_per_launch")
+        prof_stripes = (summ or {}).get("stripes_per_gpu", S_cfg)
+        if traffic is not None and S != prof_stripes:
+            traffic = int(traffic * S / prof_stripes)  # profile ran at its own S
+        trace = None
+        timed_ns = kd.get("timed_avg_ns")
+        if timed_ns:
+            t_algo = algo_bytes * prof_stripes // S
+            trace = {"source": summ_src, "timed_launches": kd.get("timed_calls"),
+                     "launch_ms": round(timed_ns / 1e6, 4),
+                     "achieved": round(t_algo / timed_ns, 1),
+                     "frac": round(t_algo / timed_ns / HBM_PEAK_GBS, 4),
+                     "kernel_ms_per_step": round(2 * timed_ns / 1e6, 4),
+                     "profiled_ms_per_step": (summ or {}).get("ms_per_step")}
         out = {
             "metric": "device-resident encode+decode GiB/s (RS k=10 m=4, 1 MiB frags), 1/2/4/8 GPU"
             if args.config == "c3" else f"device-resident encode+decode GiB/s ({desc})",
@@ -259,30 +445,43 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u16 (GF(2^16) words)",
             "data": "synthetic (splitmix64 fragments generated in HBM)",
             "config": {"workload": desc, "k": k, "m": m, "fragment_bytes": F,
-                       "stripes_per_gpu": S, "decode_missing": missing,
+                       "stripes_per_gpu": S, "stripes_total": total_stripes,
+                       "decode_missing": missing,
                        "parallelism": f"stripe-sharded x{world} (no data-path collective)"},
-            "encode_gibs_per_gpu": round(obj_bytes / GIB / (sum(enc_ms) / len(enc_ms) / 1e3), 3),
-            "decode_gibs_per_gpu": round(obj_bytes / GIB / (sum(dec_ms) / len(dec_ms) / 1e3), 3),
+            "ranks_seen": ranks_seen,
+            "per_rank_encode_gibs": [round(x, 2) for x in per_rank[:world]],
+            "per_rank_decode_gibs": [round(x, 2) for x in per_rank[world:]],
+            "encode_gibs_per_gpu": round(enc_gibs, 3),
+            "decode_gibs_per_gpu": round(dec_gibs, 3),
             "decode_mixed_pattern": mixed,
             "decode_mixed_gibs_per_gpu": mixed_gibs,
             "roofline": {"bound": "hbm", "kernel": kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
+                         "traffic_source": summ_src,
                          "launch_ms": round(launch_ms, 4),
+                         "encode_launch_ms": round(sum(enc_ms) / len(enc_ms), 4),
+                         "decode_launch_ms": round(sum(dec_ms) / len(dec_ms), 4),
                          "copy_peak_measured": round(copy_gbs, 1),
                          "frac_of_measured_copy": round(achieved / copy_gbs, 4),
-                         "algorithmic_bytes_per_launch": algo_bytes},
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "trace": trace},
         }
+    lay.buf.free()
+    if rank == 0:
+        if not args.no_c5 and args.config == "c3":
+            out["c5"] = c5_rebuild(D, stream)
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(k, m, F, missing, args.cpu_threads,
-                                               args.cpu_stripes)
+            usable = usable_cores()[0]
+            out["cpu_baseline"] = cpu_baseline(k, m, F, missing, args.cpu_threads or usable,
+                                               args.cpu_seconds)
         print(json.dumps(out), flush=True)
+    co.barrier()
     co.close()
 
 

@@ -34,8 +34,13 @@ extern "C" {
 /* 0 if a HIP device is usable, ECAMD_ENODEV otherwise. */
 int ecamd_init(void);
 int ecamd_device_count(void);
+/* The calling thread's current HIP device (every call below works on it). */
+int ecamd_get_device(int *dev);
+int ecamd_set_device(int dev);
 const char *ecamd_last_error(void);
-/* Launch-geometry knobs for sweeps ("threads", "wgs_per_cu", "nt"); 0 restores the default. */
+/* Launch-geometry knobs for sweeps ("threads", "wgs_per_cu", "nt", ...; every setting produces
+ * bit-identical results, only the launch shape changes); 0 restores the default.  Safe to call
+ * while other threads launch: each launch reads each knob once. */
 int ecamd_tune(const char *key, int value);
 
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
@@ -90,6 +95,10 @@ int ecamd_rs_decode_multi(int k, int m, const int *missing, int missing_stride,
 int ecamd_scatter_fragments(const void *d_src, int64_t stripe_stride, int64_t frag_stride,
                             int64_t frag_len, int nfrags, int nstripes, const int *dst_dev,
                             void *const *d_dst, const int64_t *dst_stride, void *stream);
+/* The rs_* calls above cache one prepared map (device coefficient tables) per (device, k, m,
+ * erasure pattern, destination), least recently used first out once the tables exceed `limit`
+ * bytes: entries and bytes currently held. */
+int ecamd_map_cache_stats(int64_t *entries, int64_t *bytes, int64_t *limit);
 /* Reconstruct one destination, as liberasurecode_rs_vand_reconstruct does. */
 int ecamd_rs_reconstruct(int k, int m, const int *missing, int dest, void *base,
                          int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
@@ -117,6 +126,9 @@ int ecamd_xor_decode_multi(int k, int m, int hd, const int *missing, int missing
 
 /* ---- synchronous host-buffer execution (used by the per-call drop-in ABIs) ----
  * Pooled pinned staging + two streams, chunked so host copies overlap PCIe and the kernel.
+ * Calls are spread round-robin over the visible devices (or ECAMD_PERCALL_DEVICES, see
+ * ecamd_percall_device_plan in ecamd_host.h), each with its own staging pool; the caller's
+ * current device is restored on return.
  * ecamd_host_map_apply: out[r] = sum_j coeff[r*K+j] * in[j] over GF(2^16).
  * ecamd_host_xor_apply: out[r] = XOR of bufs[b] for bits b of sources[r] (nbuf <= 64, at most 32
  * distinct buffers referenced); outputs may alias bufs, every output sees the original inputs. */
@@ -132,6 +144,16 @@ int ecamd_host_xor_apply(const uint64_t *sources, int R, int nbuf, const void *c
 int ecamd_percall_crc_arm(int legacy);
 int ecamd_percall_crc_lookup(const void *ptr, int64_t len, uint32_t *crc);
 void ecamd_percall_crc_disarm(void);
+/* Per-call execution status: the first failure (staging allocation, copy, launch) of the two
+ * synchronous calls above on the calling thread since ecamd_percall_reset(), 0 if none.  The
+ * reference codec cannot fail mid-call and its shims discard the codec's return code
+ * (src/backends/rs_vand/liberasurecode_rs_vand.c:86-90); liberasurecode.so.1 reads this around
+ * each codec call and fails the call (-EIO) instead of stamping unwritten fragments. */
+void ecamd_percall_reset(void);
+int ecamd_percall_status(void);
+/* Fault injection for tests: site "staging" makes the next `count` staging acquisitions of the
+ * synchronous host-buffer calls fail with ECAMD_ENOMEM (0 disarms). */
+int ecamd_fault_inject(const char *site, int count);
 
 /* ---- on-device framing: the wire format of liberasurecode_encode, in HBM ----
  * backend 6 = liberasurecode_rs_vand, 3 = flat_xor_hd (hd used only there); checksum is the
@@ -180,29 +202,6 @@ int ecamd_crc32(int legacy, const void *d_base, int64_t stripe_stride, int64_t f
 int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, int nfrags,
                         int64_t blocksize, int nstripes, int stripe0, uint64_t seed_base,
                         void *stream);
-
-/* ---- measurement helper: non-temporal 16 B/lane streaming copy (HBM ceiling probe) ---- */
-int ecamd_debug_stream_copy(void *d_dst, const void *d_src, int64_t bytes, void *stream);
-/* kind 0 copy / 1 read-only / 2 write-only over `bytes`, unroll in {1,4,8} 16-B loads per lane in
- * flight, grid = CUs x wgs_per_cu workgroups of 256 lanes (bandwidth ceilings for DESIGN.md). */
-int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void *d_dst, const void *d_src,
-                         int64_t bytes, void *stream);
-/* Codec-shaped streaming probe: K fragment reads and R fragment writes per tile over nstripes
- * stripes of (K+R) fragments of blocksize bytes at d_base (stripe stride (K+R)*blocksize), the tile
- * order of gf16_apply_kernel, no table work.  lp / sp: buffer-load / store cache policy (gfx950
- * cpol: 1 sc0, 2 nt, 16 sc1; pairs listed in ECAMD_MIX_POLICIES), ch: 16-B chunks per lane (1, 2).
- * blocksize must be a multiple of threads*16*ch; stripe stride < 2 GiB. */
-int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d_base,
-                          int64_t blocksize, int K, int R, int nstripes, void *stream);
-/* Lookup-engine probe: random 16-byte lookups into four 4 KiB tables (d_table, 16 KiB) from LDS
- * (mode 0), from global memory through the vector L1 (1) or half each (2); grid = CUs x wgs_per_cu
- * workgroups of 256 lanes, iters x 4 lookups per lane. */
-int ecamd_debug_lookup_probe(int mode, int wgs_per_cu, int iters, const void *d_table, void *stream);
-/* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup) and the
- * chunk layout (wave_contig 1: a wave's ch chunks are 1 KiB apart, contiguous) as parameters. */
-int ecamd_debug_mix_probe2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
-                           int wave_contig, void *d_base, int64_t blocksize, int K, int R,
-                           int nstripes, void *stream);
 
 /* ---- device memory helpers for C / ctypes callers ---- */
 int ecamd_malloc(void **d_ptr, int64_t bytes);

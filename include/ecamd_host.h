@@ -78,6 +78,13 @@ int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int *r
                                  const int *excl, int list_stride, int nstripes, int *needed,
                                  int *rcs);
 
+/* Devices the per-call path (ecamd_host_map_apply / ecamd_host_xor_apply) spreads calls over:
+ * every one of ndev visible devices, or the comma-separated subset named by spec (the
+ * ECAMD_PERCALL_DEVICES environment variable; NULL or "" = all; out-of-range or repeated ids are
+ * dropped, and a spec naming none of them means all).  Writes up to max ids to devs, returns the
+ * count.  Call n of a process goes to devs[n % count]. */
+int ecamd_percall_device_plan(int ndev, const char *spec, int *devs, int max);
+
 #ifdef __cplusplus
 }
 #endif

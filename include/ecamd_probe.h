@@ -1,0 +1,46 @@
+/*
+ * ecamd_probe.h -- libecamd_probe.so: MI355X measurement probes (NOT the codec product).
+ *
+ * HBM ceilings and lookup-engine rates that DESIGN.md judges the codec kernels against; bench.py
+ * uses ecamd_probe_bw for its live copy-peak denominator, tools/ for sweeps.  Pointers are device
+ * pointers, `stream` a hipStream_t; every call returns 0 or a negative code
+ * (ecamd_probe_last_error() gives the reason).
+ */
+#ifndef ECAMD_PROBE_H
+#define ECAMD_PROBE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char *ecamd_probe_last_error(void);
+
+/* ---- non-temporal 16 B/lane streaming copy (HBM ceiling probe) ---- */
+int ecamd_probe_stream_copy(void *d_dst, const void *d_src, int64_t bytes, void *stream);
+/* kind 0 copy / 1 read-only / 2 write-only over `bytes`, unroll in {1,4,8} 16-B loads per lane in
+ * flight, grid = CUs x wgs_per_cu workgroups of 256 lanes (bandwidth ceilings for DESIGN.md). */
+int ecamd_probe_bw(int kind, int unroll, int wgs_per_cu, void *d_dst, const void *d_src,
+                         int64_t bytes, void *stream);
+/* Codec-shaped streaming probe: K fragment reads and R fragment writes per tile over nstripes
+ * stripes of (K+R) fragments of blocksize bytes at d_base (stripe stride (K+R)*blocksize), the tile
+ * order of gf16_apply_kernel, no table work.  lp / sp: buffer-load / store cache policy (gfx950
+ * cpol: 1 sc0, 2 nt, 16 sc1; pairs listed in ECAMD_MIX_POLICIES), ch: 16-B chunks per lane (1, 2).
+ * blocksize must be a multiple of threads*16*ch; stripe stride < 2 GiB. */
+int ecamd_probe_mix(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d_base,
+                          int64_t blocksize, int K, int R, int nstripes, void *stream);
+/* Lookup-engine probe: random 16-byte lookups into four 4 KiB tables (d_table, 16 KiB) from LDS
+ * (mode 0), from global memory through the vector L1 (1) or half each (2); grid = CUs x wgs_per_cu
+ * workgroups of 256 lanes, iters x 4 lookups per lane. */
+int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void *d_table, void *stream);
+/* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup) and the
+ * chunk layout (wave_contig 1: a wave's ch chunks are 1 KiB apart, contiguous) as parameters. */
+int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
+                           int wave_contig, void *d_base, int64_t blocksize, int K, int R,
+                           int nstripes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -25,6 +25,14 @@ extern "C" {
 #define _VERSION(x, y, z) (((x) << 16) | ((y) << 8) | (z))
 #define LIBERASURECODE_VERSION _VERSION(1, 8, 0) /* the reference release this API mirrors */
 
+/* Build-time suffix of every backend library name the frontend dlopen()s, e.g. "-amd" gives
+ * "liberasurecode_rs_vand-amd.so.1" (include/erasurecode/erasurecode_version.h:35-37 and each
+ * backend's SO_NAME, e.g. src/backends/rs_vand/liberasurecode_rs_vand.c:43).  Set with
+ * `make SO_SUFFIX=...`; the codec libraries of this build carry it in their sonames too. */
+#ifndef LIBERASURECODE_SO_SUFFIX
+#define LIBERASURECODE_SO_SUFFIX ""
+#endif
+
 typedef enum {
     EC_BACKEND_NULL = 0,
     EC_BACKEND_JERASURE_RS_VAND = 1,

@@ -119,7 +119,9 @@ def dev():
         _proto(d, "ecamd_percall_crc_arm", C.c_int, [C.c_int])
         _proto(d, "ecamd_percall_crc_lookup", C.c_int, [VP, C.c_int64, C.POINTER(C.c_uint32)])
         _proto(d, "ecamd_percall_crc_disarm", None, [])
-        _proto(d, "ecamd_debug_stream_copy", C.c_int, [VP, VP, C.c_int64, VP])
+        _proto(d, "ecamd_percall_reset", None, [])
+        _proto(d, "ecamd_percall_status", C.c_int, [])
+        _proto(d, "ecamd_fault_inject", C.c_int, [C.c_char_p, C.c_int])
         _proto(d, "ecamd_malloc", C.c_int, [C.POINTER(VP), C.c_int64])
         _proto(d, "ecamd_free", C.c_int, [VP])
         _proto(d, "ecamd_memcpy_h2d", C.c_int, [VP, VP, C.c_int64])
@@ -138,6 +140,30 @@ def dev():
         _proto(d, "ecamd_event_elapsed_ms", C.c_int, [VP, VP, C.POINTER(C.c_float)])
         _dev = d
     return _dev
+
+
+_probe = None
+
+
+def probe():
+    """libecamd_probe.so: HBM / lookup-engine measurement probes (not the codec product)."""
+    global _probe
+    if _probe is None:
+        dev()  # same HIP runtime, device selection and memory helpers
+        p = _load("libecamd_probe.so")
+        _proto(p, "ecamd_probe_last_error", C.c_char_p, [])
+        _proto(p, "ecamd_probe_stream_copy", C.c_int, [VP, VP, C.c_int64, VP])
+        _proto(p, "ecamd_probe_bw", C.c_int,
+               [C.c_int, C.c_int, C.c_int, VP, VP, C.c_int64, VP])
+        _proto(p, "ecamd_probe_lookup", C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP])
+        _proto(p, "ecamd_probe_mix", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int, C.c_int,
+                C.c_int, VP])
+        _proto(p, "ecamd_probe_mix2", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64,
+                C.c_int, C.c_int, C.c_int, VP])
+        _probe = p
+    return _probe
 
 
 class ECAmdError(RuntimeError):

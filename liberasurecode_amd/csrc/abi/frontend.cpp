@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "erasurecode.h"
@@ -117,28 +118,84 @@ int new_desc()
 size_t zero_metadata(void*, int) { return 0; }
 size_t zero_offset(void*, int) { return 0; }
 
+// ------------------------------------------------ codec hooks of this repo's libraries ----
+
+// Resolved with dlsym through the codec library's dependencies (libecamd.so, include/ecamd.h);
+// a foreign codec library (e.g. the reference's own) has none of them and gets the reference
+// behaviour: host zlib checksums, codec return codes discarded as the reference shims do.
+struct CodecHooks {
+    int (*crc_arm)(int) = nullptr;                               // ecamd_percall_crc_*
+    int (*crc_lookup)(const void*, int64_t, uint32_t*) = nullptr;
+    void (*crc_disarm)(void) = nullptr;
+    void (*exec_reset)(void) = nullptr;                          // ecamd_percall_reset / _status
+    int (*exec_status)(void) = nullptr;
+    bool crc() const { return crc_arm && crc_lookup && crc_disarm; }
+    bool ours() const { return exec_reset && exec_status; }
+};
+
+CodecHooks resolve_hooks(void* so)
+{
+    CodecHooks h;
+    if (!so) return h;
+    h.crc_arm = reinterpret_cast<int (*)(int)>(dlsym(so, "ecamd_percall_crc_arm"));
+    h.crc_lookup = reinterpret_cast<int (*)(const void*, int64_t, uint32_t*)>(
+        dlsym(so, "ecamd_percall_crc_lookup"));
+    h.crc_disarm = reinterpret_cast<void (*)(void)>(dlsym(so, "ecamd_percall_crc_disarm"));
+    h.exec_reset = reinterpret_cast<void (*)(void)>(dlsym(so, "ecamd_percall_reset"));
+    h.exec_status = reinterpret_cast<int (*)(void)>(dlsym(so, "ecamd_percall_status"));
+    dlerror();
+    return h;
+}
+
+// Every backend_desc this frontend creates starts with its hooks, resolved once at init and
+// living exactly as long as the instance (no shared cache to reallocate or go stale on dlclose).
+struct ShimBase {
+    CodecHooks hooks;
+};
+
+const CodecHooks& hooks_of(ec_backend* be) { return static_cast<ShimBase*>(be->desc.backend_desc)->hooks; }
+
+// Brackets one codec call: true when this repo's codec failed to EXECUTE it (staging, copy,
+// launch).  The reference shims discard codec return codes (flat_xor_hd.c:65-72,
+// liberasurecode_rs_vand.c:86-90) because a CPU codec cannot fail mid-call; a GPU codec can, and
+// a failed call must not come back as success with unwritten fragments.
+struct ExecCheck {
+    const CodecHooks& h;
+    explicit ExecCheck(const CodecHooks& hooks) : h(hooks)
+    {
+        if (h.ours()) h.exec_reset();
+    }
+    bool failed() const { return h.ours() && h.exec_status() != 0; }
+};
+
 // ------------------------------------------------ flat_xor_hd shim (flat_xor_hd.c:65-226) ----
 
-struct XorDesc {
-    xor_code_t* code;
+struct XorDesc : ShimBase {
+    xor_code_t* code = nullptr;
 };
 
 int fx_encode(void* d, char** data, char** parity, int bs)
 {
-    xor_code_t* c = static_cast<XorDesc*>(d)->code;
-    c->encode(c, data, parity, bs);
-    return 0;
+    auto* x = static_cast<XorDesc*>(d);
+    ExecCheck ex(x->hooks);
+    x->code->encode(x->code, data, parity, bs);
+    return ex.failed() ? -EIO : 0;
 }
 
 int fx_decode(void* d, char** data, char** parity, int* missing, int bs)
 {
-    xor_code_t* c = static_cast<XorDesc*>(d)->code;
-    return c->decode(c, data, parity, missing, bs, 1);
+    auto* x = static_cast<XorDesc*>(d);
+    ExecCheck ex(x->hooks);
+    const int rc = x->code->decode(x->code, data, parity, missing, bs, 1);
+    return ex.failed() ? -EIO : rc;
 }
 
 int fx_reconstruct(void* d, char** data, char** parity, int* missing, int dest, int bs)
 {
-    return xor_reconstruct_one(static_cast<XorDesc*>(d)->code, data, parity, missing, dest, bs);
+    auto* x = static_cast<XorDesc*>(d);
+    ExecCheck ex(x->hooks);
+    const int rc = xor_reconstruct_one(x->code, data, parity, missing, dest, bs);
+    return ex.failed() ? -EIO : rc;
 }
 
 int fx_needed(void* d, int* missing, int* exclude, int* needed)
@@ -175,24 +232,26 @@ int fx_check_reconstruct(void* d, int* missing, int)
 
 int fx_element_size(void*) { return 32; }
 
-void* fx_init(ec_backend_args* args, void*)
+void* fx_init(ec_backend_args* args, void* so)
 {
     args->uargs.w = 32;
     xor_code_t* c = init_xor_hd_code(args->uargs.k, args->uargs.m, args->uargs.hd);
     if (!c) return nullptr;
-    auto* d = static_cast<XorDesc*>(std::malloc(sizeof(XorDesc)));
+    auto* d = new (std::nothrow) XorDesc();
     if (!d) {
         std::free(c);
         return nullptr;
     }
+    d->hooks = resolve_hooks(so);
     d->code = c;
     return d;
 }
 
 int fx_exit(void* d)
 {
-    std::free(static_cast<XorDesc*>(d)->code);
-    std::free(d);
+    auto* x = static_cast<XorDesc*>(d);
+    std::free(x->code);
+    delete x;
     return 0;
 }
 
@@ -204,36 +263,54 @@ ec_backend_op_stubs g_xor_ops = {fx_init, fx_exit, true, fx_encode, fx_decode, f
 
 // ---------------------------------- liberasurecode_rs_vand shim (rs_vand.c:82-311) ----
 
-struct RsDesc {
-    void (*init)(int, int);
-    void (*deinit)(void);
-    void (*free_matrix)(int*);
-    int* (*make_matrix)(int, int);
-    int (*encode)(int*, char**, char**, int, int, int);
-    int (*decode)(int*, char**, char**, int, int, int*, int, int);
-    int (*reconstruct)(int*, char**, char**, int, int, int*, int, int);
-    int* matrix;
-    int k, m, w;
+struct RsDesc : ShimBase {
+    void (*init)(int, int) = nullptr;
+    void (*deinit)(void) = nullptr;
+    void (*free_matrix)(int*) = nullptr;
+    int* (*make_matrix)(int, int) = nullptr;
+    int (*encode)(int*, char**, char**, int, int, int) = nullptr;
+    int (*decode)(int*, char**, char**, int, int, int*, int, int) = nullptr;
+    int (*reconstruct)(int*, char**, char**, int, int, int*, int, int) = nullptr;
+    int* matrix = nullptr;
+    int k = 0, m = 0, w = 0;
 };
+
+// The codec refused the call (more than m missing, e.g. k fragments with duplicate indices):
+// liberasurecode_rs_vand.c:444-447 / 502-505 return -1 before writing anything, so the missing
+// slots keep the zeros the reference frontend allocated them with.  This frontend skips that
+// zeroing in front of its own codec (prepare_decode, realign = false), so it zeroes them here.
+void zero_missing(char** data, char** parity, int k, const int* missing, int bs)
+{
+    for (int i = 0; missing[i] >= 0; i++)
+        std::memset(missing[i] < k ? data[missing[i]] : parity[missing[i] - k], 0,
+                    static_cast<size_t>(bs));
+}
 
 int rs_encode(void* d, char** data, char** parity, int bs)
 {
     auto* r = static_cast<RsDesc*>(d);
+    ExecCheck ex(r->hooks);
     r->encode(r->matrix, data, parity, r->k, r->m, bs);
-    return 0;  // the reference shim discards the codec's return code
+    return ex.failed() ? -EIO : 0;  // otherwise the reference shim discards the codec's rc
 }
 
 int rs_decode(void* d, char** data, char** parity, int* missing, int bs)
 {
     auto* r = static_cast<RsDesc*>(d);
-    r->decode(r->matrix, data, parity, r->k, r->m, missing, bs, 1);
+    ExecCheck ex(r->hooks);
+    const int rc = r->decode(r->matrix, data, parity, r->k, r->m, missing, bs, 1);
+    if (ex.failed()) return -EIO;
+    if (rc != 0) zero_missing(data, parity, r->k, missing, bs);
     return 0;
 }
 
 int rs_reconstruct(void* d, char** data, char** parity, int* missing, int dest, int bs)
 {
     auto* r = static_cast<RsDesc*>(d);
-    r->reconstruct(r->matrix, data, parity, r->k, r->m, missing, dest, bs);
+    ExecCheck ex(r->hooks);
+    const int rc = r->reconstruct(r->matrix, data, parity, r->k, r->m, missing, dest, bs);
+    if (ex.failed()) return -EIO;
+    if (rc != 0) zero_missing(data, parity, r->k, missing, bs);
     return 0;
 }
 
@@ -267,8 +344,9 @@ bool bind(void* so, const char* name, F& fn)
 
 void* rs_init(ec_backend_args* args, void* so)
 {
-    auto* r = static_cast<RsDesc*>(std::calloc(1, sizeof(RsDesc)));
+    auto* r = new (std::nothrow) RsDesc();
     if (!r) return nullptr;
+    r->hooks = resolve_hooks(so);
     r->k = args->uargs.k;
     r->m = args->uargs.m;
     args->uargs.w = r->w = 16;
@@ -285,7 +363,7 @@ void* rs_init(ec_backend_args* args, void* so)
         ok = r->matrix != nullptr;
     }
     if (!ok) {
-        std::free(r);
+        delete r;
         return nullptr;
     }
     return r;
@@ -296,7 +374,7 @@ int rs_exit(void* d)
     auto* r = static_cast<RsDesc*>(d);
     r->free_matrix(r->matrix);
     r->deinit();
-    std::free(r);
+    delete r;
     return 0;
 }
 
@@ -315,20 +393,22 @@ struct TableEntry {
     ec_backend_op_stubs* ops;  // nullptr: no shim in this build (reported as not available)
 };
 
+#define SONAME(base, ver) base LIBERASURECODE_SO_SUFFIX ver
 const TableEntry kBackends[EC_BACKENDS_MAX] = {
-    {EC_BACKEND_NULL, "null", "libnullcode.so.1", nullptr},
-    {EC_BACKEND_JERASURE_RS_VAND, "jerasure_rs_vand", "libJerasure.so.2", nullptr},
-    {EC_BACKEND_JERASURE_RS_CAUCHY, "jerasure_rs_cauchy", "libJerasure.so.2", nullptr},
-    {EC_BACKEND_FLAT_XOR_HD, "flat_xor_hd", "libXorcode.so.1", &g_xor_ops},
-    {EC_BACKEND_ISA_L_RS_VAND, "isa_l_rs_vand", "libisal.so.2", nullptr},
-    {EC_BACKEND_SHSS, "shss", "libshss.so.1", nullptr},
-    {EC_BACKEND_LIBERASURECODE_RS_VAND, "liberasurecode_rs_vand", "liberasurecode_rs_vand.so.1",
-     &g_rs_ops},
-    {EC_BACKEND_ISA_L_RS_CAUCHY, "isa_l_rs_cauchy", "libisal.so.2", nullptr},
-    {EC_BACKEND_LIBPHAZR, "libphazr", "libphazr.so.1", nullptr},
-    {EC_BACKEND_ISA_L_RS_VAND_INV, "isa_l_rs_vand_inv", "libisal.so.2", nullptr},
-    {EC_BACKEND_ISA_L_RS_LRC, "isa_l_rs_lrc", "libisal.so.2", nullptr},
+    {EC_BACKEND_NULL, "null", SONAME("libnullcode", ".so.1"), nullptr},
+    {EC_BACKEND_JERASURE_RS_VAND, "jerasure_rs_vand", SONAME("libJerasure", ".so.2"), nullptr},
+    {EC_BACKEND_JERASURE_RS_CAUCHY, "jerasure_rs_cauchy", SONAME("libJerasure", ".so.2"), nullptr},
+    {EC_BACKEND_FLAT_XOR_HD, "flat_xor_hd", SONAME("libXorcode", ".so.1"), &g_xor_ops},
+    {EC_BACKEND_ISA_L_RS_VAND, "isa_l_rs_vand", SONAME("libisal", ".so.2"), nullptr},
+    {EC_BACKEND_SHSS, "shss", SONAME("libshss", ".so.1"), nullptr},
+    {EC_BACKEND_LIBERASURECODE_RS_VAND, "liberasurecode_rs_vand",
+     SONAME("liberasurecode_rs_vand", ".so.1"), &g_rs_ops},
+    {EC_BACKEND_ISA_L_RS_CAUCHY, "isa_l_rs_cauchy", SONAME("libisal", ".so.2"), nullptr},
+    {EC_BACKEND_LIBPHAZR, "libphazr", SONAME("libphazr", ".so.1"), nullptr},
+    {EC_BACKEND_ISA_L_RS_VAND_INV, "isa_l_rs_vand_inv", SONAME("libisal", ".so.2"), nullptr},
+    {EC_BACKEND_ISA_L_RS_LRC, "isa_l_rs_lrc", SONAME("libisal", ".so.2"), nullptr},
 };
+#undef SONAME
 
 void fill_common(ec_backend_common& c, const TableEntry& e)
 {
@@ -356,54 +436,25 @@ int aligned_size(ec_backend* be, int data_len)
     return ((data_len + a - 1) / a) * a;
 }
 
-// GPU checksum handoff (include/ecamd.h ecamd_percall_crc_*): found in the dependency chain of
-// this repo's codec libraries; with a foreign codec library it is absent and zlib runs here.
-struct CrcHooks {
-    int (*arm)(int);
-    int (*lookup)(const void*, int64_t, uint32_t*);
-    void (*disarm)(void);
-};
-thread_local const CrcHooks* t_hooks = nullptr;
+// GPU checksum handoff (include/ecamd.h ecamd_percall_crc_*), armed for one encode / reconstruct
+// call when the instance stores CRC32 checksums: the codec call then checksums the fragments on
+// the GPU while they are resident.  With a foreign codec library zlib runs here.
+thread_local const CodecHooks* t_hooks = nullptr;
 
-const CrcHooks* crc_hooks(ec_backend* be)
-{
-    static pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
-    static std::vector<std::pair<void*, CrcHooks>> cache;
-    void* so = be->desc.backend_sohandle;
-    if (!so) return nullptr;
-    pthread_mutex_lock(&mu);
-    const CrcHooks* found = nullptr;
-    for (auto& e : cache)
-        if (e.first == so) found = &e.second;
-    if (!found) {
-        CrcHooks h;
-        h.arm = reinterpret_cast<int (*)(int)>(dlsym(so, "ecamd_percall_crc_arm"));
-        h.lookup = reinterpret_cast<int (*)(const void*, int64_t, uint32_t*)>(
-            dlsym(so, "ecamd_percall_crc_lookup"));
-        h.disarm = reinterpret_cast<void (*)(void)>(dlsym(so, "ecamd_percall_crc_disarm"));
-        cache.emplace_back(so, h);
-        found = &cache.back().second;
-    }
-    const CrcHooks* r = (found->arm && found->lookup && found->disarm) ? found : nullptr;
-    pthread_mutex_unlock(&mu);
-    return r;
-}
-
-// Armed for one encode / reconstruct call when the instance stores CRC32 checksums: the codec
-// call then checksums the fragments on the GPU while they are resident.
 struct CrcArm {
-    const CrcHooks* h = nullptr;
+    const CodecHooks* h = nullptr;
     CrcArm(ec_backend* be, bool want)
     {
-        if (want && (h = crc_hooks(be)) != nullptr) {
-            h->arm(env_legacy_crc() ? 1 : 0);
+        if (want && hooks_of(be).crc()) {
+            h = &hooks_of(be);  // lives in the instance, which the read lock keeps alive
+            h->crc_arm(env_legacy_crc() ? 1 : 0);
             t_hooks = h;
         }
     }
     ~CrcArm()
     {
         if (h) {
-            h->disarm();
+            h->crc_disarm();
             t_hooks = nullptr;
         }
     }
@@ -416,7 +467,7 @@ void write_checksum(char* f, ec_checksum_type_t ct, int bs)
     h->meta.chksum_mismatch = 0;
     if (ct != CHKSUM_CRC32) return;
     uint32_t c = 0;
-    if (t_hooks && t_hooks->lookup(payload(f), bs, &c) == 0)
+    if (t_hooks && t_hooks->crc_lookup(payload(f), bs, &c) == 0)
         h->meta.chksum[0] = c;
     else
         h->meta.chksum[0] = env_legacy_crc()
@@ -570,16 +621,19 @@ int liberasurecode_crc32_alt(int crc, const void* buf, size_t size)
 {
     // The legacy checksum of bug 1666320 (src/utils/chksum/crc32.c:79-91): reflected CRC-32
     // whose 8-bit shift sign-extends from bit 23.
-    static uint32_t tab[256];
-    static bool ready = false;
-    if (!ready) {
-        for (uint32_t n = 0; n < 256; n++) {
-            uint32_t c = n;
-            for (int b = 0; b < 8; b++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-            tab[n] = c;
+    struct Table {
+        uint32_t t[256];
+        Table()
+        {
+            for (uint32_t n = 0; n < 256; n++) {
+                uint32_t c = n;
+                for (int b = 0; b < 8; b++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+                t[n] = c;
+            }
         }
-        ready = true;
-    }
+    };
+    static const Table table;  // thread-safe one-time initialisation
+    const uint32_t* tab = table.t;
     const signed char* p = static_cast<const signed char*>(buf);
     int32_t c = crc ^ ~0;
     while (size--) {
@@ -863,7 +917,7 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
     int ret = get_fragment_partition(k, m, available_fragments, num_fragments, data.data(),
                                      parity.data(), missing.data());
     int orig = 0, bs = 0;
-    const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && crc_hooks(be));
+    const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && hooks_of(be).ours());
     if (ret == 0)
         ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
                              fragment_len, owned, realign);
@@ -928,7 +982,7 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
         if (ret < 0) return ret;
     }
     int orig = 0, bs = 0;
-    const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && crc_hooks(be));
+    const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && hooks_of(be).ours());
     ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
                          fragment_len, owned, realign);
     CrcArm arm(be, be->args.uargs.ct == CHKSUM_CRC32);  // through the stamping below

@@ -4,9 +4,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <list>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -81,11 +84,7 @@ int ensure_device(int* dev_out)
                             K_(2, true, true),   K_(4, true, true),   K_(8, true, true),
                             reinterpret_cast<const void*>(&gf16_copy_apply_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_copy_apply_kernel<4>),
-                            reinterpret_cast<const void*>(&gf16_copy_apply_kernel<8>),
-                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<1, false>),
-                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<1, true>),
-                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<2, false>),
-                            reinterpret_cast<const void*>(&gf16_apply_exp_kernel<2, true>)};
+                            reinterpret_cast<const void*>(&gf16_copy_apply_kernel<8>)};
 #undef K_
         for (const void* k : ks)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
@@ -140,36 +139,47 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 
 // Launch-geometry knobs (0 = automatic).  Set through ecamd_tune() for sweeps; defaults are the
 // measured best on MI355X ("Tuning").
+// A launch knob: written by ecamd_tune from any thread, read by launches on others (each launch
+// reads each knob once; every setting gives bit-identical results, only the launch shape changes).
+struct Knob {
+    std::atomic<int> v;
+    explicit Knob(int x) : v(x) {}
+    operator int() const { return v.load(std::memory_order_relaxed); }
+    Knob& operator=(int x)
+    {
+        v.store(x, std::memory_order_relaxed);
+        return *this;
+    }
+};
+
 struct Tuning {
-    int threads = 0;     // threads per workgroup of the gf16 kernel
-    int wgs_per_cu = 0;  // resident workgroups per CU the grid is sized for
-    int nt = 1;          // 1: non-temporal global loads/stores in the gf16 kernel (+7% on MI355X)
-    int exp_ch = 0;      // sweeps: experimental W=4 kernel with 1 or 2 chunks per lane
-    int ablate = 0;      // sweeps: experimental kernel without LDS lookups (wrong results)
-    int nib = 0;         // gf16 kernel: 1 = nibble tables (4 conflict-free lookups per word)
-    int crc_bits = 5;    // CRC32 kernel piece tables: 4 nibble, 8 byte, 5..7 byte tables for the first
+    Knob threads{0};     // threads per workgroup of the gf16 kernel
+    Knob wgs_per_cu{0};  // resident workgroups per CU the grid is sized for
+    Knob nt{1};          // 1: non-temporal global loads/stores in the gf16 kernel (+7% on MI355X)
+    Knob nib{0};         // gf16 kernel: 1 = nibble tables (4 conflict-free lookups per word)
+    Knob crc_bits{5};    // CRC32 kernel piece tables: 4 nibble, 8 byte, 5..7 byte tables for the first
                          // bits-4 dwords of a piece (5 measured best with crc_pos, tools/frame_bench.py)
-    int crc_wgs = 0;     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
-    int frame_crc_fused = 1;  // framed encode with CRC32: codec + checksums in one launch
-    int frame_copy_padded = 1;  // framed encode: copy-through also for objects shorter than k*bs
-    int frame_crc_wgs = 0;    //   512-thread workgroups per CU (0 = 2)
-    int frame_crc_units = 0;  //   work units (stripe ranges) per CU to aim for (0 = 4)
-    int frame_crc_mb = 0;     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
-    int frame_unfused = 0;  // framed encode: 1 = always split then encode (A/B against copy-through)
-    int crc_gap_bits = 8;   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
-    int crc_span_kib = 128; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
-    int crc_pos = 1;        // CRC32 kernel: position-specific piece tables (one gap step per 4 pieces)
-    int stream = 1;         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
-    int stream_ch = 1;      //   16-byte chunks per lane (1, 2; W = 8 always 1)
-    int xor_wgs = 0;        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
+    Knob crc_wgs{0};     // CRC32 kernel: resident 512-thread workgroups per CU (0 = by LDS)
+    Knob frame_crc_fused{1};  // framed encode with CRC32: codec + checksums in one launch
+    Knob frame_copy_padded{1};  // framed encode: copy-through also for objects shorter than k*bs
+    Knob frame_crc_wgs{0};    //   512-thread workgroups per CU (0 = 2)
+    Knob frame_crc_units{0};  //   work units (stripe ranges) per CU to aim for (0 = 4)
+    Knob frame_crc_mb{0};     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
+    Knob frame_unfused{0};  // framed encode: 1 = always split then encode (A/B against copy-through)
+    Knob crc_gap_bits{8};   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
+    Knob crc_span_kib{128}; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
+    Knob crc_pos{1};        // CRC32 kernel: position-specific piece tables (one gap step per 4 pieces)
+    Knob stream{1};         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
+    Knob stream_ch{1};      //   16-byte chunks per lane (1, 2; W = 8 always 1)
+    Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
                             // measured best, tools/xor_sweep.py)
-    int grid_mult = 0;      // stream launches: workgroups per resident slot (0: 2 for 4-output
+    Knob grid_mult{0};      // stream launches: workgroups per resident slot (0: 2 for 4-output
                             //   passes, else 1; tools/grid_sweep.py)
-    int multi_list = 1;     // heterogeneous decode: stripe-list stream launches (else pointer tables)
-    int stream_hybrid = 1;  //   8-output passes: one input in 4 looks its hi table up via L1
-    int stream_order = 0;   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
-    int stream_nib = 0;     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
-    int stream_pf = 0;      //   next group's loads issued before the lookups (1) or after (0);
+    Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
+    Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
+    Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
+    Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
+    Knob stream_pf{0};      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
 };
 Tuning g_tune;
@@ -407,24 +417,12 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
         for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[p.col0 + j];
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
         Geometry g;
-        const bool exp = g_tune.exp_ch > 0 && p.width == 4 && !PTRS;
-        int rc = geometry(map->device, p.bytes, bs, nstripes, g, exp ? g_tune.exp_ch : 1);
+        int rc = geometry(map->device, p.bytes, bs, nstripes, g, 1);
         if (rc) return rc;
         a.ntiles = g.ntiles;
         a.tiles_per_stripe = g.tiles_per_stripe;
         dim3 grid(g.grid), block(g.threads);
-        if (exp) {
-            const int v = (g_tune.exp_ch == 2 ? 2 : 0) + (g_tune.ablate ? 1 : 0);
-            switch (v) {
-            case 0: hipLaunchKernelGGL((gf16_apply_exp_kernel<1, false>), grid, block, g.lds, st, a); break;
-            case 1: hipLaunchKernelGGL((gf16_apply_exp_kernel<1, true>), grid, block, g.lds, st, a); break;
-            case 2: hipLaunchKernelGGL((gf16_apply_exp_kernel<2, false>), grid, block, g.lds, st, a); break;
-            default: hipLaunchKernelGGL((gf16_apply_exp_kernel<2, true>), grid, block, g.lds, st, a); break;
-            }
-            HIP_TRY(hipGetLastError());
-            continue;
-        }
-        if (!PTRS && g_tune.nt && !exp && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
+        if (!PTRS && g_tune.nt && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
             stream_offsets(a, bs)) {
             const bool nib = g_tune.stream_nib == 1 || (g_tune.stream_nib == 2 && p.width == 8) ||
                              (g_tune.nib != 0);
@@ -447,7 +445,7 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
         }
         if (a.stripe_list)  // only the stream kernel reads a stripe list
             return fail(ECAMD_EINVAL, "stripe list on a non-stream launch");
-        if (PTRS && g_tune.nt && !exp && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
+        if (PTRS && g_tune.nt && g_tune.stream && p.ncols <= 4 * kStreamGroups &&
             bs < (int64_t(1) << 31)) {
             rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4);
             if (rc) return rc;
@@ -545,8 +543,47 @@ struct RsEntry {
     std::vector<int> inputs, outputs;
 };
 
+// Bounded LRU of prepared maps keyed by (device, kind, k, m, rebuild, dest, erasures): a long-lived
+// process that sees many distinct erasure patterns (k+m up to 256) keeps at most
+// kCacheBytes of coefficient tables on each device.  Evicted entries stay alive while a launch
+// still holds them (shared_ptr); their device tables are freed with the last reference.
+constexpr size_t kCacheBytes = size_t(64) << 20;
+struct CacheSlot {
+    std::shared_ptr<RsEntry> entry;
+    std::list<std::vector<int>>::iterator lru;
+    size_t bytes;
+};
 std::mutex g_cache_mu;
-std::map<std::vector<int>, std::shared_ptr<RsEntry>> g_cache;
+std::map<std::vector<int>, CacheSlot> g_cache;
+std::list<std::vector<int>> g_lru;  // most recent first
+size_t g_cache_bytes = 0;
+
+size_t map_bytes(const ecamd_map* mp)
+{
+    if (!mp || mp->passes.empty()) return 0;
+    const auto& p = mp->passes.back();
+    return std::max(p.offset + p.bytes, p.nib_offset + p.nib_bytes);
+}
+
+// caller holds g_cache_mu
+void cache_insert(const std::vector<int>& key, std::shared_ptr<RsEntry>& e)
+{
+    auto it = g_cache.find(key);
+    if (it != g_cache.end()) {  // another thread prepared it meanwhile
+        e = it->second.entry;
+        return;
+    }
+    g_lru.push_front(key);
+    const size_t b = map_bytes(e->map.get()) + 256;
+    g_cache.emplace(key, CacheSlot{e, g_lru.begin(), b});
+    g_cache_bytes += b;
+    while (g_cache_bytes > kCacheBytes && g_lru.size() > 1) {
+        auto victim = g_cache.find(g_lru.back());
+        g_cache_bytes -= victim->second.bytes;
+        g_cache.erase(victim);
+        g_lru.pop_back();
+    }
+}
 
 int rs_entry(int kind, int k, int m, const int* missing, int rebuild, int dest,
              std::shared_ptr<RsEntry>& out)
@@ -564,7 +601,8 @@ int rs_entry(int kind, int k, int m, const int* missing, int rebuild, int dest,
         std::lock_guard<std::mutex> lk(g_cache_mu);
         auto it = g_cache.find(key);
         if (it != g_cache.end()) {
-            out = it->second;
+            g_lru.splice(g_lru.begin(), g_lru, it->second.lru);
+            out = it->second.entry;
             return 0;
         }
     }
@@ -591,8 +629,8 @@ int rs_entry(int kind, int k, int m, const int* missing, int rebuild, int dest,
         e->map.reset(mp);
     }
     std::lock_guard<std::mutex> lk(g_cache_mu);
-    auto ins = g_cache.emplace(key, e);
-    out = ins.first->second;
+    cache_insert(key, e);
+    out = e;
     return 0;
 }
 
@@ -866,30 +904,47 @@ namespace ecamd {
 // StagedUpload: a small host table (stripe list / pointer table) goes up asynchronously on the
 // caller's stream, ahead of the launches that read it, from one of kStagedSlots (pinned host,
 // device) buffer pairs per (device, stream); a slot is reused only after the event recorded behind
-// its launches (end()) has fired, so back-to-back calls do not drain the stream.  The rings' lock
-// is held from begin() to end().
-namespace {
+// its launches (end()) has fired, so back-to-back calls do not drain the stream.  Locking is per
+// ring and only around claiming / releasing a slot: the event wait, the upload and the launches
+// run unlocked, so batches on other streams or devices never wait behind this one.
 struct StagedSlot {
     void* host = nullptr;
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t done = nullptr;
+    bool busy = false;  // claimed by a StagedUpload between begin() and end()
 };
 constexpr int kStagedSlots = 4;
 struct StagedRing {
+    std::mutex mu;
+    std::condition_variable freed;
     StagedSlot slot[kStagedSlots];
     int next = 0;
 };
+namespace {
 std::mutex g_staged_mu;
-std::map<std::pair<int, void*>, StagedRing> g_staged;  // (device, stream)
+std::map<std::pair<int, void*>, std::unique_ptr<StagedRing>> g_staged;  // (device, stream)
 }  // namespace
 
 int StagedUpload::begin(int device, void* stream, const void* src, size_t bytes)
 {
-    lock_ = std::unique_lock<std::mutex>(g_staged_mu);
-    StagedRing& ring = g_staged[{device, stream}];
-    StagedSlot& sc = ring.slot[ring.next];
-    ring.next = (ring.next + 1) % kStagedSlots;
+    end(stream_);  // a second begin() releases the first slot
+    {
+        std::lock_guard<std::mutex> lk(g_staged_mu);
+        auto& r = g_staged[{device, stream}];
+        if (!r) r.reset(new StagedRing());
+        ring_ = r.get();
+    }
+    {
+        std::unique_lock<std::mutex> lk(ring_->mu);
+        StagedSlot* sc = &ring_->slot[ring_->next];
+        ring_->next = (ring_->next + 1) % kStagedSlots;
+        ring_->freed.wait(lk, [sc] { return !sc->busy; });
+        sc->busy = true;
+        slot_ = sc;
+        stream_ = stream;
+    }
+    StagedSlot& sc = *slot_;
     if (sc.done) HIP_TRY(hipEventSynchronize(sc.done));
     else HIP_TRY(hipEventCreateWithFlags(&sc.done, hipEventDisableTiming));
     const size_t need = std::max<size_t>(bytes, 16);
@@ -904,18 +959,24 @@ int StagedUpload::begin(int device, void* stream, const void* src, size_t bytes)
     }
     std::memcpy(sc.host, src, bytes);
     HIP_TRY(hipMemcpyAsync(sc.dev, sc.host, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
-    done_ = static_cast<void*>(sc.done);
     dev = sc.dev;
     return 0;
 }
 
 int StagedUpload::end(void* stream)
 {
-    if (done_) {
-        HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(done_), static_cast<hipStream_t>(stream)));
-        done_ = nullptr;
+    if (!slot_) return 0;
+    hipError_t e = hipSuccess;
+    if (slot_->done) e = hipEventRecord(slot_->done, static_cast<hipStream_t>(stream));
+    {
+        std::lock_guard<std::mutex> lk(ring_->mu);
+        slot_->busy = false;
     }
-    if (lock_.owns_lock()) lock_.unlock();
+    ring_->freed.notify_all();
+    slot_ = nullptr;
+    ring_ = nullptr;
+    dev = nullptr;
+    if (e != hipSuccess) return fail(ECAMD_EHIP, "hipEventRecord: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -945,6 +1006,15 @@ extern "C" {
 
 int ecamd_init(void) { return ensure_device(nullptr); }
 
+int ecamd_map_cache_stats(int64_t* entries, int64_t* bytes, int64_t* limit)
+{
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    if (entries) *entries = static_cast<int64_t>(g_cache.size());
+    if (bytes) *bytes = static_cast<int64_t>(g_cache_bytes);
+    if (limit) *limit = static_cast<int64_t>(kCacheBytes);
+    return 0;
+}
+
 int ecamd_tune(const char* key, int value)
 {
     if (!key) return fail(ECAMD_EINVAL, "null key");
@@ -957,10 +1027,6 @@ int ecamd_tune(const char* key, int value)
         g_tune.wgs_per_cu = std::max(0, std::min(value, 8));
     } else if (k == "nt") {
         g_tune.nt = value != 0;  // note: the default is 1; ecamd_tune("nt", 0) turns it off
-    } else if (k == "exp_ch") {
-        g_tune.exp_ch = (value == 1 || value == 2) ? value : 0;
-    } else if (k == "ablate") {
-        g_tune.ablate = value != 0;
     } else if (k == "nib") {
         g_tune.nib = value != 0;
     } else if (k == "crc_bits") {
@@ -1015,6 +1081,19 @@ int ecamd_device_count(void)
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+int ecamd_get_device(int* dev)
+{
+    if (!dev) return fail(ECAMD_EINVAL, "null device pointer");
+    HIP_TRY(hipGetDevice(dev));
+    return 0;
+}
+
+int ecamd_set_device(int dev)
+{
+    HIP_TRY(hipSetDevice(dev));
+    return 0;
 }
 
 const char* ecamd_last_error(void) { return g_err.c_str(); }
@@ -1201,7 +1280,7 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
     // wider than 2 GiB -- one pointer table row (k+m fragment addresses) per stripe. Both are
     // laid out group by group.
     const int row = k + m;
-    const bool use_list = g_tune.multi_list && g_tune.stream && g_tune.nt && g_tune.exp_ch <= 0 &&
+    const bool use_list = g_tune.multi_list && g_tune.stream && g_tune.nt &&
                           k <= 4 * kStreamGroups &&
                           (row - 1) * frag_stride + blocksize < (int64_t(1) << 31);
     std::vector<uint8_t*> table;
@@ -1288,21 +1367,26 @@ int ecamd_scatter_fragments(const void* d_src, int64_t stripe_stride, int64_t fr
             std::lock_guard<std::mutex> lk(mu);
             if (std::find(enabled.begin(), enabled.end(), std::make_pair(dev, to)) == enabled.end()) {
                 int can = 0;
-                HIP_TRY(hipDeviceCanAccessPeer(&can, dev, to));
-                if (!can) return fail(ECAMD_EINVAL, "no peer path from device %d to %d", dev, to);
+                if (hipDeviceCanAccessPeer(&can, dev, to) != hipSuccess || !can)
+                    return fail(ECAMD_EINVAL, "fragment %d: no peer path from device %d to %d", f,
+                                dev, to);
                 hipError_t e = hipDeviceEnablePeerAccess(to, 0);
                 if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-                    return fail(ECAMD_EHIP, "hipDeviceEnablePeerAccess(%d): %s", to, hipGetErrorString(e));
+                    return fail(ECAMD_EHIP, "fragment %d: hipDeviceEnablePeerAccess(%d -> %d): %s",
+                                f, dev, to, hipGetErrorString(e));
                 (void)hipGetLastError();
                 enabled.emplace_back(dev, to);
             }
         }
         // One strided copy per fragment: nstripes rows of frag_len bytes (xGMI DMA when to != dev).
-        HIP_TRY(hipMemcpy2DAsync(d_dst[f], static_cast<size_t>(dst_stride[f]),
-                                 static_cast<const uint8_t*>(d_src) + f * frag_stride,
-                                 static_cast<size_t>(stripe_stride), static_cast<size_t>(frag_len),
-                                 static_cast<size_t>(nstripes), hipMemcpyDefault,
-                                 static_cast<hipStream_t>(stream)));
+        const hipError_t e = hipMemcpy2DAsync(
+            d_dst[f], static_cast<size_t>(dst_stride[f]),
+            static_cast<const uint8_t*>(d_src) + f * frag_stride, static_cast<size_t>(stripe_stride),
+            static_cast<size_t>(frag_len), static_cast<size_t>(nstripes), hipMemcpyDefault,
+            static_cast<hipStream_t>(stream));
+        if (e != hipSuccess)
+            return fail(ECAMD_EHIP, "fragment %d -> device %d: hipMemcpy2DAsync: %s", f, to,
+                        hipGetErrorString(e));
     }
     return 0;
 }
@@ -1332,105 +1416,6 @@ int ecamd_fill_splitmix(void* base, int64_t stripe_stride, int64_t frag_stride, 
     int64_t grid = std::min<int64_t>((total + 255) / 256, static_cast<int64_t>(cu_count(dev)) * 16);
     hipLaunchKernelGGL(splitmix_fill_kernel, dim3(static_cast<int>(std::max<int64_t>(grid, 1))),
                        dim3(256), 0, static_cast<hipStream_t>(stream), f);
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
-int ecamd_debug_stream_copy(void* dst, const void* src, int64_t bytes, void* stream)
-{
-    int dev = 0;
-    int rc = ensure_device(&dev);
-    if (rc) return rc;
-    if (!aligned16(dst) || !aligned16(src) || bytes % 16)
-        return fail(ECAMD_EINVAL, "stream copy needs 16-byte aligned pointers and size");
-    hipLaunchKernelGGL(stream_copy_kernel, dim3(cu_count(dev) * 8), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), static_cast<uint4*>(dst),
-                       static_cast<const uint4*>(src), bytes / 16);
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
-int ecamd_debug_bw_probe(int kind, int unroll, int wgs_per_cu, void* dst, const void* src,
-                         int64_t bytes, void* stream)
-{
-    int dev = 0;
-    int rc = ensure_device(&dev);
-    if (rc) return rc;
-    static uint32_t* sink = nullptr;
-    if (!sink) HIP_TRY(hipMalloc(&sink, 1024 * sizeof(uint32_t)));
-    dim3 grid(cu_count(dev) * std::max(1, wgs_per_cu)), block(256);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    auto* d = static_cast<uint8_t*>(dst);
-    auto* s = static_cast<const uint8_t*>(src);
-    switch (unroll) {
-    case 1: hipLaunchKernelGGL(bw_probe_kernel<1>, grid, block, 0, st, d, s, bytes, kind, sink); break;
-    case 4: hipLaunchKernelGGL(bw_probe_kernel<4>, grid, block, 0, st, d, s, bytes, kind, sink); break;
-    default: hipLaunchKernelGGL(bw_probe_kernel<8>, grid, block, 0, st, d, s, bytes, kind, sink); break;
-    }
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
-int ecamd_debug_lookup_probe(int mode, int wgs_per_cu, int iters, const void* d_table, void* stream)
-{
-    int dev = 0;
-    int rc = ensure_device(&dev);
-    if (rc) return rc;
-    static uint32_t* sink = nullptr;
-    if (!sink) HIP_TRY(hipMalloc(&sink, 64));
-    const dim3 grid(cu_count(dev) * std::max(1, wgs_per_cu)), block(256);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    const auto* t = static_cast<const uint4*>(d_table);
-    switch (mode) {
-    case 0: hipLaunchKernelGGL(lookup_probe_kernel<0>, grid, block, 0, st, t, iters, sink); break;
-    case 1: hipLaunchKernelGGL(lookup_probe_kernel<1>, grid, block, 0, st, t, iters, sink); break;
-    case 2: hipLaunchKernelGGL(lookup_probe_kernel<2>, grid, block, 0, st, t, iters, sink); break;
-    case 3: hipLaunchKernelGGL(lookup_probe_kernel<3>, grid, block, 0, st, t, iters, sink); break;
-    case 4: hipLaunchKernelGGL(lookup_probe_kernel<4>, grid, block, 0, st, t, iters, sink); break;
-    default: hipLaunchKernelGGL(lookup_probe_kernel<5>, grid, block, 0, st, t, iters, sink); break;
-    }
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
-int ecamd_debug_mix_probe(int lp, int sp, int ch, int threads, int wgs_per_cu, void* base,
-                          int64_t bs, int K, int R, int nstripes, void* stream)
-{
-    return ecamd_debug_mix_probe2(lp, sp, ch, threads, wgs_per_cu, 0, 0, base, bs, K, R, nstripes, stream);
-}
-
-int ecamd_debug_mix_probe2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
-                           int wave_contig, void* base, int64_t bs, int K, int R, int nstripes,
-                           void* stream)
-{
-    int dev = 0;
-    int rc = ensure_device(&dev);
-    if (rc) return rc;
-    if (ch != 1 && ch != 2) return fail(ECAMD_EINVAL, "mix probe: ch must be 1 or 2");
-    if (threads < 64 || threads > 1024 || threads % 64) return fail(ECAMD_EINVAL, "mix probe: threads");
-    const int64_t span = static_cast<int64_t>(threads) * 16 * ch;
-    const int64_t sstride = bs * (K + R);
-    if (K < 1 || R < 0 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
-        return fail(ECAMD_EINVAL, "mix probe: bad shape");
-    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0, order != 0,
-              wave_contig != 0};
-    a.tiles_per_stripe = static_cast<uint32_t>(bs / span);
-    a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
-    const int grid = static_cast<int>(std::min<int64_t>(a.ntiles,
-                                                        static_cast<int64_t>(cu_count(dev)) * std::max(1, wgs_per_cu)));
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    bool launched = false;
-#define ECAMD_MIX(LP, SP)                                                                         \
-    if (!launched && lp == LP && sp == SP) {                                                      \
-        if (ch == 1)                                                                              \
-            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 1>), dim3(grid), dim3(threads), 0, st, a); \
-        else                                                                                      \
-            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 2>), dim3(grid), dim3(threads), 0, st, a); \
-        launched = true;                                                                          \
-    }
-    ECAMD_MIX_POLICIES(ECAMD_MIX)
-#undef ECAMD_MIX
-    if (!launched) return fail(ECAMD_EINVAL, "mix probe: policy pair (%d, %d) not instantiated", lp, sp);
     HIP_TRY(hipGetLastError());
     return 0;
 }

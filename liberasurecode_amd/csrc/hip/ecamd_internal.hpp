@@ -10,15 +10,18 @@ namespace ecamd {
 // Asynchronous upload of a small host table (stripe list, pointer table) on `stream` through a
 // ring of pinned slots per (device, stream); call end() after enqueuing the launches that read
 // `dev` (ecamd_device.hip).
+struct StagedSlot;
+struct StagedRing;
 struct StagedUpload {
     void* dev = nullptr;
     int begin(int device, void* stream, const void* src, size_t bytes);
-    int end(void* stream);
-    ~StagedUpload() { if (lock_.owns_lock()) lock_.unlock(); }
+    int end(void* stream);  // records the slot's event behind the launches and releases it
+    ~StagedUpload() { end(stream_); }
 
 private:
-    void* done_ = nullptr;
-    std::unique_lock<std::mutex> lock_;
+    StagedRing* ring_ = nullptr;
+    StagedSlot* slot_ = nullptr;
+    void* stream_ = nullptr;
 };
 
 // Strided flat-XOR apply (ecamd_xor_apply_strided) over the stripes listed in the device array

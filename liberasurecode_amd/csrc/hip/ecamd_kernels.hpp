@@ -72,39 +72,9 @@ __global__ void gf16_hybrid_kernel(const ApplyArgs a);
 struct FusedCrcArgs;
 template <int W, int KG, int MB>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);
-template <int CH, bool ABLATE>
-__global__ void gf16_apply_exp_kernel(const ApplyArgs a);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);
 template <int KG>
 __global__ void xor_stream_kernel(const ApplyArgs a);
 __global__ void splitmix_fill_kernel(FillArgs f);
-struct MixArgs {
-    uint8_t* base;
-    int64_t stripe_stride;
-    int frag_stride;
-    int K, R;
-    uint32_t ntiles;
-    uint32_t tiles_per_stripe;
-    int order;        // 0: grid-stride tile order, 1: contiguous tile range per workgroup
-    int wave_contig;  // 1: a wave's CH chunks are contiguous (1 KiB apart)
-};
-
-// (load policy, store policy) pairs instantiated for mix_probe_kernel; gfx950 cpol bits
-// 1 = sc0, 2 = nt, 16 = sc1.
-#define ECAMD_MIX_POLICIES(X) \
-    X(0, 0) X(0, 2) X(0, 16) X(0, 18) X(0, 1) \
-    X(2, 0) X(2, 2) X(2, 16) X(2, 18) X(2, 1) \
-    X(1, 0) X(1, 2) X(16, 2) X(18, 2) X(3, 2) X(18, 18)
-template <int LP, int SP, int CH>
-__global__ void mix_probe_kernel(MixArgs a);
-
-template <int MODE>
-__global__ void lookup_probe_kernel(const uint4* __restrict__ table, int iters, uint32_t* sink);
-
-template <int U>
-__global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int kind,
-                                uint32_t* sink);
-__global__ void stream_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n);
-
 }  // namespace ecamd

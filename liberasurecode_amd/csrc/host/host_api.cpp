@@ -1,6 +1,8 @@
 // host_api.cpp -- extern "C" surface of libecamd_host.so (include/ecamd_host.h).
 #include "ecamd_host.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -181,6 +183,31 @@ int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int* r
         }
     }
     return 0;
+}
+
+int ecamd_percall_device_plan(int ndev, const char* spec, int* devs, int max)
+{
+    if (ndev <= 0 || !devs || max <= 0) return 0;
+    std::vector<int> ids;
+    std::vector<bool> seen(static_cast<size_t>(ndev), false);
+    for (const char* p = spec; p && *p;) {
+        char* end = nullptr;
+        const long v = std::strtol(p, &end, 10);
+        if (end == p) {  // not a number: skip one character (separators, spaces)
+            p++;
+            continue;
+        }
+        if (v >= 0 && v < ndev && !seen[static_cast<size_t>(v)]) {
+            seen[static_cast<size_t>(v)] = true;
+            ids.push_back(static_cast<int>(v));
+        }
+        p = end;
+    }
+    if (ids.empty())
+        for (int d = 0; d < ndev; d++) ids.push_back(d);
+    const int n = std::min(static_cast<int>(ids.size()), max);
+    for (int i = 0; i < n; i++) devs[i] = ids[static_cast<size_t>(i)];
+    return n;
 }
 
 }  // extern "C"

@@ -8,7 +8,9 @@
 // c&1), the CPU packs chunk c+1 into the other pinned slab and unpacks chunk c-1.  Fragment maps
 // are cached by content, so callers may free() and rebuild matrices at will.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -17,6 +19,7 @@
 
 #include "crc.hpp"
 #include "ecamd.h"
+#include "ecamd_host.h"
 
 namespace {
 
@@ -33,6 +36,22 @@ struct CrcRecord {
     std::vector<Entry> entries;
 };
 thread_local CrcRecord t_crc;
+
+// Per-call execution status (ecamd_percall_status): the first staging / copy / launch failure on
+// this thread since ecamd_percall_reset.  The reference codec cannot fail mid-call, so its shim
+// discards return codes (src/backends/rs_vand/liberasurecode_rs_vand.c:86-90); a GPU codec can,
+// and the frontend reads this to fail the call instead of stamping stale parity.
+thread_local int t_exec_rc = 0;
+
+int note_exec(int rc)
+{
+    if (rc != 0 && t_exec_rc == 0) t_exec_rc = rc;
+    return rc;
+}
+
+// Fault injection (ecamd_fault_inject): the next N staging acquisitions fail as an allocation
+// failure would, before any GPU work.
+std::atomic<int> g_fail_staging{0};
 
 // zlib crc32_combine: crc(A || B) = A^|B| crc(A) ^ crc(B) for both checksum machines.
 uint32_t crc_combine(bool legacy, uint32_t a, uint32_t b, int64_t len_b)
@@ -63,9 +82,9 @@ struct MapHolder {
 std::mutex g_map_mu;
 std::map<std::vector<int>, std::shared_ptr<MapHolder>> g_maps;
 
-std::shared_ptr<MapHolder> cached_map(const int* coeff, int R, int K, int* rc)
+std::shared_ptr<MapHolder> cached_map(int dev, const int* coeff, int R, int K, int* rc)
 {
-    std::vector<int> key = {R, K};
+    std::vector<int> key = {dev, R, K};
     key.insert(key.end(), coeff, coeff + static_cast<size_t>(R) * K);
     {
         std::lock_guard<std::mutex> lk(g_map_mu);
@@ -90,7 +109,7 @@ struct Slot {
 struct Staging {
     Slot slot[2];
     int64_t cap = 0;  // bytes per slab
-    bool ok = false;
+    int device = 0;   // every stream, event and buffer of this context lives there
     ~Staging()
     {
         for (auto& s : slot) {
@@ -100,8 +119,45 @@ struct Staging {
     }
 };
 
+// One pool of staging contexts per device; calls go round-robin over the planned devices
+// (ecamd_percall_device_plan), so concurrent callers on an 8-GPU node use 8 PCIe links.
 std::mutex g_pool_mu;
-std::vector<Staging*> g_pool;
+std::vector<std::vector<Staging*>> g_pool;  // by device
+
+struct DevicePlan {
+    std::vector<int> devs;
+    std::atomic<unsigned> next{0};
+    DevicePlan()
+    {
+        const int n = ecamd_device_count();
+        if (n <= 0) return;
+        devs.resize(static_cast<size_t>(n));
+        devs.resize(static_cast<size_t>(
+            ecamd_percall_device_plan(n, std::getenv("ECAMD_PERCALL_DEVICES"), devs.data(), n)));
+    }
+};
+
+int pick_device()
+{
+    static DevicePlan plan;  // thread-safe one-time initialisation
+    if (plan.devs.empty()) return -1;
+    return plan.devs[plan.next.fetch_add(1, std::memory_order_relaxed) % plan.devs.size()];
+}
+
+// Makes `dev` current for one call and restores the caller's device afterwards.
+struct DeviceScope {
+    int prev = -1;
+    int rc = 0;
+    explicit DeviceScope(int dev)
+    {
+        if ((rc = ecamd_get_device(&prev)) == 0 && prev != dev) rc = ecamd_set_device(dev);
+    }
+    ~DeviceScope()
+    {
+        int cur = -1;
+        if (prev >= 0 && ecamd_get_device(&cur) == 0 && cur != prev) ecamd_set_device(prev);
+    }
+};
 
 int grow(Staging* st, int64_t bytes)
 {
@@ -122,18 +178,25 @@ int grow(Staging* st, int64_t bytes)
     return 0;
 }
 
-Staging* acquire(int64_t bytes, int* rc)
+Staging* acquire(int dev, int64_t bytes, int* rc)
 {
+    for (int left = g_fail_staging.load(); left > 0; left = g_fail_staging.load())
+        if (g_fail_staging.compare_exchange_weak(left, left - 1)) {
+            *rc = ECAMD_ENOMEM;
+            return nullptr;
+        }
     Staging* st = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (!g_pool.empty()) {
-            st = g_pool.back();
-            g_pool.pop_back();
+        if (static_cast<int>(g_pool.size()) <= dev) g_pool.resize(static_cast<size_t>(dev) + 1);
+        if (!g_pool[dev].empty()) {
+            st = g_pool[dev].back();
+            g_pool[dev].pop_back();
         }
     }
     if (!st) {
         st = new Staging();
+        st->device = dev;
         for (auto& s : st->slot) {
             if ((*rc = ecamd_stream_create(&s.stream)) || (*rc = ecamd_event_create(&s.event))) {
                 delete st;
@@ -151,13 +214,13 @@ Staging* acquire(int64_t bytes, int* rc)
 void release(Staging* st)
 {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.push_back(st);
+    g_pool[st->device].push_back(st);
 }
 
 // Kernel launcher for one chunk: inputs at d + j*pitch, outputs at d + (K+r)*pitch.
 using Launch = int (*)(const void* ctx, char* d, int64_t pitch, int64_t bytes, void* stream);
 
-int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t bs,
+int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, int64_t bs,
                 const void* ctx, Launch launch)
 {
     const int64_t nfr = K + R;
@@ -170,7 +233,7 @@ int run_chunked(int K, int R, const char* const* in, char* const* out, int64_t b
     // Below ~16 KiB of fragments the extra launch + copy costs more than zlib on the host
     // (4 KiB object: 47 vs 38 us); the frontend then falls back to the CPU for the missing entries.
     const bool want_crc = t_crc.armed && nfr <= 64 && bs * nfr >= (16 << 10);
-    Staging* st = acquire(chunk * nfr + 256, &rc);  // last 256 B of each slab: chunk CRCs
+    Staging* st = acquire(dev, chunk * nfr + 256, &rc);  // last 256 B of each slab: chunk CRCs
     if (!st) return rc;
     const int64_t crc_off = st->cap - 256;
     std::vector<uint32_t> crc(want_crc ? nfr : 0, 0u);
@@ -269,12 +332,16 @@ int ecamd_host_map_apply(const int* coeff, int R, int K, const void* const* in,
         for (int r = 0; r < R; r++) std::memset(out[r], 0, static_cast<size_t>(blocksize));
         return 0;
     }
+    const int dev = pick_device();
+    if (dev < 0) return note_exec(ECAMD_ENODEV);
+    DeviceScope scope(dev);
+    if (scope.rc) return note_exec(scope.rc);
     int rc = 0;
-    auto mh = cached_map(coeff, R, K, &rc);
-    if (!mh) return rc ? rc : ECAMD_EINVAL;
+    auto mh = cached_map(dev, coeff, R, K, &rc);
+    if (!mh) return note_exec(rc ? rc : ECAMD_EINVAL);
     MapCtx ctx{mh->map, K, R};
-    return run_chunked(K, R, reinterpret_cast<const char* const*>(in),
-                       reinterpret_cast<char* const*>(out), blocksize, &ctx, launch_map);
+    return note_exec(run_chunked(dev, K, R, reinterpret_cast<const char* const*>(in),
+                                 reinterpret_cast<char* const*>(out), blocksize, &ctx, launch_map));
 }
 
 int ecamd_host_xor_apply(const uint64_t* sources, int R, int nbuf, const void* const* bufs,
@@ -307,8 +374,12 @@ int ecamd_host_xor_apply(const uint64_t* sources, int R, int nbuf, const void* c
     }
     // outputs may alias inputs: results land in pinned memory first and are copied back only
     // after the whole chunk's inputs were packed, so every output sees the ORIGINAL inputs.
-    return run_chunked(ctx.K, R, in.data(), reinterpret_cast<char* const*>(out), blocksize, &ctx,
-                       launch_xor);
+    const int dev = pick_device();
+    if (dev < 0) return note_exec(ECAMD_ENODEV);
+    DeviceScope scope(dev);
+    if (scope.rc) return note_exec(scope.rc);
+    return note_exec(run_chunked(dev, ctx.K, R, in.data(), reinterpret_cast<char* const*>(out),
+                                 blocksize, &ctx, launch_xor));
 }
 
 int ecamd_percall_crc_arm(int legacy)
@@ -333,6 +404,17 @@ void ecamd_percall_crc_disarm(void)
 {
     t_crc.armed = false;
     t_crc.entries.clear();
+}
+
+void ecamd_percall_reset(void) { t_exec_rc = 0; }
+
+int ecamd_percall_status(void) { return t_exec_rc; }
+
+int ecamd_fault_inject(const char* site, int count)
+{
+    if (!site || std::strcmp(site, "staging") != 0 || count < 0) return ECAMD_EINVAL;
+    g_fail_staging.store(count);
+    return 0;
 }
 
 }  // extern "C"

@@ -1,0 +1,161 @@
+// probe_api.hip -- C ABI of libecamd_probe.so (include/ecamd_probe.h): bandwidth and lookup-engine
+// probes used by bench.py (live copy-peak denominator) and tools/ sweeps.  Kept out of libecamd.so
+// so the codec library carries no experiment code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "ecamd_probe.h"
+#include "probe.hpp"
+
+using namespace ecamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return fail(-5, "%s: %s", #expr, hipGetErrorString(e_));     \
+    } while (0)
+
+int ensure_device(int* dev)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(-19, "no HIP device");
+    HIP_TRY(hipGetDevice(dev));
+    return 0;
+}
+
+int cu_count(int dev)
+{
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+        cus = 256;
+    return cus;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+const char* ecamd_probe_last_error(void) { return g_err.c_str(); }
+
+int ecamd_probe_stream_copy(void* dst, const void* src, int64_t bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!aligned16(dst) || !aligned16(src) || bytes % 16)
+        return fail(-22, "stream copy needs 16-byte aligned pointers and size");
+    hipLaunchKernelGGL(stream_copy_kernel, dim3(cu_count(dev) * 8), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), static_cast<uint4*>(dst),
+                       static_cast<const uint4*>(src), bytes / 16);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_probe_bw(int kind, int unroll, int wgs_per_cu, void* dst, const void* src,
+                         int64_t bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    static uint32_t* sink = nullptr;
+    if (!sink) HIP_TRY(hipMalloc(&sink, 1024 * sizeof(uint32_t)));
+    dim3 grid(cu_count(dev) * std::max(1, wgs_per_cu)), block(256);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    auto* d = static_cast<uint8_t*>(dst);
+    auto* s = static_cast<const uint8_t*>(src);
+    switch (unroll) {
+    case 1: hipLaunchKernelGGL(bw_probe_kernel<1>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    case 4: hipLaunchKernelGGL(bw_probe_kernel<4>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    default: hipLaunchKernelGGL(bw_probe_kernel<8>, grid, block, 0, st, d, s, bytes, kind, sink); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void* d_table, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    static uint32_t* sink = nullptr;
+    if (!sink) HIP_TRY(hipMalloc(&sink, 64));
+    const dim3 grid(cu_count(dev) * std::max(1, wgs_per_cu)), block(256);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const auto* t = static_cast<const uint4*>(d_table);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(lookup_probe_kernel<0>, grid, block, 0, st, t, iters, sink); break;
+    case 1: hipLaunchKernelGGL(lookup_probe_kernel<1>, grid, block, 0, st, t, iters, sink); break;
+    case 2: hipLaunchKernelGGL(lookup_probe_kernel<2>, grid, block, 0, st, t, iters, sink); break;
+    case 3: hipLaunchKernelGGL(lookup_probe_kernel<3>, grid, block, 0, st, t, iters, sink); break;
+    case 4: hipLaunchKernelGGL(lookup_probe_kernel<4>, grid, block, 0, st, t, iters, sink); break;
+    default: hipLaunchKernelGGL(lookup_probe_kernel<5>, grid, block, 0, st, t, iters, sink); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecamd_probe_mix(int lp, int sp, int ch, int threads, int wgs_per_cu, void* base,
+                          int64_t bs, int K, int R, int nstripes, void* stream)
+{
+    return ecamd_probe_mix2(lp, sp, ch, threads, wgs_per_cu, 0, 0, base, bs, K, R, nstripes, stream);
+}
+
+int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
+                           int wave_contig, void* base, int64_t bs, int K, int R, int nstripes,
+                           void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (ch != 1 && ch != 2) return fail(-22, "mix probe: ch must be 1 or 2");
+    if (threads < 64 || threads > 1024 || threads % 64) return fail(-22, "mix probe: threads");
+    const int64_t span = static_cast<int64_t>(threads) * 16 * ch;
+    const int64_t sstride = bs * (K + R);
+    if (K < 1 || R < 0 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
+        return fail(-22, "mix probe: bad shape");
+    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0, order != 0,
+              wave_contig != 0};
+    a.tiles_per_stripe = static_cast<uint32_t>(bs / span);
+    a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
+    const int grid = static_cast<int>(std::min<int64_t>(a.ntiles,
+                                                        static_cast<int64_t>(cu_count(dev)) * std::max(1, wgs_per_cu)));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    bool launched = false;
+#define ECAMD_MIX(LP, SP)                                                                         \
+    if (!launched && lp == LP && sp == SP) {                                                      \
+        if (ch == 1)                                                                              \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 1>), dim3(grid), dim3(threads), 0, st, a); \
+        else                                                                                      \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 2>), dim3(grid), dim3(threads), 0, st, a); \
+        launched = true;                                                                          \
+    }
+    ECAMD_MIX_POLICIES(ECAMD_MIX)
+#undef ECAMD_MIX
+    if (!launched) return fail(-22, "mix probe: policy pair (%d, %d) not instantiated", lp, sp);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

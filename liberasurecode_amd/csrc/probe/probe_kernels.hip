@@ -1,14 +1,11 @@
-// ecamd_kernels_exp.hip -- tuning variants of the W=4 strided GF(2^16) kernel (sweeps only).
-//
-// CH     : 16-byte chunks per lane per tile (1 or 2); 2 doubles the bytes each lane has in
-//          flight and halves the tile bookkeeping.
-// ABLATE : skip the LDS lookups (acc ^= input) -- WRONG RESULTS, used only to price the LDS
-//          work against pure streaming on the same launch geometry (cdna_hip_programming.md §7
-//          "ablate").  Never reachable from the codec entry points: only ecamd_tune("ablate").
+// probe_kernels.hip -- measurement kernels of libecamd_probe.so (NOT part of the codec product):
+// HBM ceilings (bw_probe_kernel, stream_copy_kernel), the codec's exact read/write pattern with no
+// table work (mix_probe_kernel) and the LDS / L1 lookup engines (lookup_probe_kernel).  DESIGN.md
+// §4 cites their numbers as the denominators the codec kernels are judged against.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "ecamd_kernels.hpp"
+#include "probe.hpp"
 
 namespace ecamd {
 namespace {
@@ -27,97 +24,9 @@ __device__ __forceinline__ void stnt(uint8_t* p, uint4 v)
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
-template <bool ABLATE>
-__device__ __forceinline__ void mac4(const uint8_t* tl, uint4 x, uint32_t (&acc)[8][2])
-{
-    const uint8_t* th = tl + 256 * 8;
-    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int w = 0; w < 8; w++) {
-        const uint32_t v = xs[w >> 1] >> ((w & 1) * 16);
-        if constexpr (ABLATE) {
-            acc[w][0] ^= v;
-            acc[w][1] ^= v;
-        } else {
-            uint2 e0 = *reinterpret_cast<const uint2*>(tl + (v & 0xffu) * 8);
-            uint2 e1 = *reinterpret_cast<const uint2*>(th + ((v >> 8) & 0xffu) * 8);
-            acc[w][0] ^= e0.x ^ e1.x;
-            acc[w][1] ^= e0.y ^ e1.y;
-        }
-    }
-}
-
 }  // namespace
 
-template <int CH, bool ABLATE>
-__global__ void __launch_bounds__(1024) gf16_apply_exp_kernel(const ApplyArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int tbytes = a.ncols * 512 * 8;
-    for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
-        *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
-    __syncthreads();
-    const int K = a.ncols;
-    const int64_t cstride = static_cast<int64_t>(blockDim.x) * 16;
-    const int64_t span = cstride * CH;
-    for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-        const uint32_t s = t / a.tiles_per_stripe;
-        const int64_t off = static_cast<int64_t>(t - s * a.tiles_per_stripe) * span +
-                            static_cast<int64_t>(threadIdx.x) * 16;
-        // sweeps run on 16-byte multiples of the tile span only
-        if (off + (CH - 1) * cstride + 16 > a.bs) continue;
-        const uint8_t* ib = a.in_base + static_cast<int64_t>(s) * a.in_stride + off;
-        uint32_t acc[CH][8][2];
-#pragma unroll
-        for (int c = 0; c < CH; c++)
-#pragma unroll
-            for (int w = 0; w < 8; w++) acc[c][w][0] = acc[c][w][1] = 0u;
-        uint4 cur[4][CH], nxt[4][CH];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-            for (int c = 0; c < CH; c++)
-                cur[i][c] = (i < K) ? ldnt(ib + a.in_off[i] + c * cstride) : make_uint4(0, 0, 0, 0);
-        for (int j0 = 0; j0 < K; j0 += 4) {
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int c = 0; c < CH; c++)
-                    nxt[i][c] = (j0 + 4 + i < K) ? ldnt(ib + a.in_off[j0 + 4 + i] + c * cstride)
-                                                 : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-                if (j0 + i < K)
-#pragma unroll
-                    for (int c = 0; c < CH; c++)
-                        mac4<ABLATE>(lds + static_cast<size_t>(j0 + i) * 4096, cur[i][c], acc[c]);
-#pragma unroll
-            for (int i = 0; i < 4; i++)
-#pragma unroll
-                for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
-        }
-        uint8_t* ob = a.out_base + static_cast<int64_t>(s) * a.out_stride + off;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            if (r >= a.nrows) break;
-#pragma unroll
-            for (int c = 0; c < CH; c++) {
-                uint32_t o[4];
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    const uint32_t A = acc[c][2 * d][r >> 1], B = acc[c][2 * d + 1][r >> 1];
-                    o[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
-                }
-                stnt(ob + a.out_off[r] + c * cstride, make_uint4(o[0], o[1], o[2], o[3]));
-            }
-        }
-    }
-}
 
-template __global__ void gf16_apply_exp_kernel<1, false>(const ApplyArgs);
-template __global__ void gf16_apply_exp_kernel<2, false>(const ApplyArgs);
-template __global__ void gf16_apply_exp_kernel<1, true>(const ApplyArgs);
-template __global__ void gf16_apply_exp_kernel<2, true>(const ApplyArgs);
 
 }  // namespace ecamd
 

@@ -1,0 +1,49 @@
+"""CPU: bench.py's multi-rank launcher and stripe sharding (C4), rehearsed without a GPU.
+
+`bench.py --gpus N` with no WORLD_SIZE in the environment starts N rank processes itself (fresh
+interpreters, before anything touches the GPU) with RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*;
+`--dry-run` runs the same rank / shard plumbing on gloo and skips the kernels.  Stripes are
+independent (src/erasurecode.c:383-477): the shards must cover the batch exactly once."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(*args, env=None):
+    e = dict(os.environ)
+    for key in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(key, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + list(args),
+                          capture_output=True, text=True, timeout=300, env=e, cwd=ROOT)
+
+
+@pytest.mark.parametrize("gpus,scaling,per_rank", [(2, "weak", [256, 256]),
+                                                    (2, "strong", [1024, 1024]),
+                                                    (3, "strong", [683, 683, 682])])
+def test_launcher_starts_ranks_and_covers_every_stripe(gpus, scaling, per_rank):
+    r = run_bench("--gpus", str(gpus), "--dry-run", "--scaling", scaling)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["dry_run"] and line["covered_once"]
+    assert line["n_gpus"] == gpus and line["ranks_seen"] == gpus
+    assert line["stripes_per_rank"] == per_rank
+    assert line["total_stripes"] == sum(per_rank)
+
+
+def test_mismatched_world_fails_loudly():
+    r = run_bench("--gpus", "1", "--dry-run", env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_single_rank_dry_run():
+    r = run_bench("--dry-run")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["stripes_per_rank"] == [256]

@@ -16,8 +16,7 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 def main():
     d = _lib.dev()
-    d.ecamd_debug_bw_probe.argtypes = [_lib.C.c_int, _lib.C.c_int, _lib.C.c_int, _lib.VP, _lib.VP,
-                                       _lib.C.c_int64, _lib.VP]
+    p = _lib.probe()
     half = 2 << 30
     buf = D.DeviceBuffer(2 * half)
     buf.zero()
@@ -28,10 +27,10 @@ def main():
     for _ in range(3):
         for v in variants:
             kind, u, w = v
-            _lib.check(d.ecamd_debug_bw_probe(kind, u, w, buf.ptr + half, buf.ptr, half, st.handle), "probe")
+            _lib.check(p.ecamd_probe_bw(kind, u, w, buf.ptr + half, buf.ptr, half, st.handle), "probe")
             a.record(st)
             for _ in range(3):
-                d.ecamd_debug_bw_probe(kind, u, w, buf.ptr + half, buf.ptr, half, st.handle)
+                p.ecamd_probe_bw(kind, u, w, buf.ptr + half, buf.ptr, half, st.handle)
             b.record(st)
             times[v].append(a.elapsed_ms(b) / 3)
     best = {}

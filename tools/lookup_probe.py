@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Lookup engines on one MI355X (development tool): random 16-byte table lookups per clock per CU
 from LDS, from global memory through the vector L1, and half each; 16-entry (nibble-sized) tables from each
-(ecamd_debug_lookup_probe)."""
+(ecamd_probe_lookup)."""
 import ctypes as C
 import json
 import os
@@ -18,21 +18,14 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 def main():
     d = _lib.dev()
-    d.ecamd_debug_lookup_probe.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
-    tab = D.DeviceBuffer(16 << 10)
-    tab.zero()
-    st = D.Stream()
-    iters = 4096
-    a, b = D.Event(), D.Event()
-    cus = 256
-    names = ["lds", "l1", "half", "l1_16ent", "lds_16ent", "lds_byte+l1_16ent"]
+    p = _lib.probe()
     for mode in range(6):
         for wgs in (2, 4, 8):
             ts = []
             for _ in range(5):
-                _lib.check(d.ecamd_debug_lookup_probe(mode, wgs, iters, tab.ptr, st.handle), "probe")
+                _lib.check(p.ecamd_probe_lookup(mode, wgs, iters, tab.ptr, st.handle), "probe")
                 a.record(st)
-                d.ecamd_debug_lookup_probe(mode, wgs, iters, tab.ptr, st.handle)
+                p.ecamd_probe_lookup(mode, wgs, iters, tab.ptr, st.handle)
                 b.record(st)
                 ts.append(a.elapsed_ms(b))
             ms = statistics.median(ts)

@@ -38,8 +38,7 @@ def main():
     k, m, F, S = args.k, args.m, args.F, args.S
     C = _lib.C
     d = _lib.dev()
-    d.ecamd_debug_mix_probe2.argtypes = [C.c_int] * 7 + [_lib.VP, C.c_int64, C.c_int, C.c_int,
-                                                          C.c_int, _lib.VP]
+    p = _lib.probe()
     lay = D.Layout.alloc(k + m, F, S)
     st = D.Stream()
     lay.fill_splitmix(nfrags=k, stream=st)
@@ -55,7 +54,7 @@ def main():
             for threads, wgs in geoms:
                 for order, wc in lays:
                     def fn(lp=lp, sp=sp, ch=ch, threads=threads, wgs=wgs, order=order, wc=wc):
-                        _lib.check(d.ecamd_debug_mix_probe2(lp, sp, ch, threads, wgs, order, wc,
+                        _lib.check(p.ecamd_probe_mix2(lp, sp, ch, threads, wgs, order, wc,
                                                             lay.buf.ptr, F, k, m, S, st.handle),
                                    "mix probe")
                     variants[f"mix_l{lp}_s{sp}_ch{ch}_t{threads}_w{wgs}_o{order}_wc{wc}"] = fn

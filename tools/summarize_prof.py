@@ -1,46 +1,120 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 CSVs from gpurun_out/prof_*_<cfg>/ into profiles/<round>_<cfg>_*.
+"""Summarise rocprofv3 output of tools/gpu_prof.sh into profiles/<round>_<cfg>_summary.json.
+
+Per kernel: launch count and duration statistics from the kernel trace (per-dispatch start / end
+timestamps), plus -- for the bench's dominant kernel -- the same statistics over the TIMED steps
+only: the bench launches it once before the warm-up, twice per warm-up step, twice per timed step,
+then for the untimed mixed-pattern decodes; the timed launches are dispatches
+[1 + 2*warmup, 1 + 2*warmup + 2*steps) of that kernel in dispatch order.  bench.py reads
+"timed_avg_ns" to put the trace-derived roofline fraction beside its HIP-event one.
 
 HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and
-WRITE_SIZE are in KiB, collected in separate passes; on gfx950 FETCH_SIZE reports exactly half the
-bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact for 16 B/lane
-streaming stores.
+WRITE_SIZE are in KiB, collected in separate passes; on gfx950 FETCH_SIZE reports half the bytes
+of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact for 16 B/lane streaming
+stores.  Counter values are averaged over the same timed dispatches when the kernel is the
+dominant one, else over all its dispatches.
+
+usage: summarize_prof.py <cfg> <round> [--kernel NAME --warmup W --steps K --stripes S --bench LOG]
 """
+import argparse
 import csv
+import glob
 import json
 import os
 import shutil
 import statistics
-import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counters(path):
-    agg = defaultdict(list)
+def find_csv(d, suffix):
+    hits = sorted(glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True))
+    return hits[0] if hits else None
+
+
+def col(row, *names):
+    for n in names:
+        if n in row:
+            return row[n]
+    raise KeyError(names)
+
+
+def trace_rows(path):
+    """(kernel, dispatch id, duration ns) per dispatch, in dispatch order."""
+    out = []
     for r in csv.DictReader(open(path)):
-        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
-    return agg
+        name = col(r, "Kernel_Name", "KernelName")
+        start = int(col(r, "Start_Timestamp", "BeginNs"))
+        end = int(col(r, "End_Timestamp", "EndNs"))
+        did = int(col(r, "Dispatch_Id", "Index", "Correlation_Id"))
+        out.append((name, did, end - start))
+    out.sort(key=lambda x: x[1])
+    return out
 
 
-def main(cfg, rnd="r01"):
+def stats(durs):
+    return {"calls": len(durs), "avg_ns": round(statistics.mean(durs), 1),
+            "min_ns": min(durs), "max_ns": max(durs),
+            "median_ns": round(statistics.median(durs), 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cfg")
+    ap.add_argument("round")
+    ap.add_argument("--kernel", default="", help="dominant kernel (name prefix)")
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--stripes", type=int, default=256)
+    ap.add_argument("--bench", default="", help="bench JSON log of the profiled command")
+    ap.add_argument("--command", default="")
+    args = ap.parse_args()
     g = os.path.join(ROOT, "gpurun_out")
-    out = {"config": cfg, "round": rnd, "kernels": {}}
-    # cfg "frame": tools/gpu_prof_frame.sh (framing / CRC kernels), dirs gpurun_out/fprof_<tag>
-    d_of = (lambda tag: f"fprof_{tag}") if cfg == "frame" else (lambda tag: f"prof_{tag}_{cfg}")
-    stats = os.path.join(g, d_of("trace"), "run_kernel_stats.csv")
-    for r in csv.DictReader(open(stats)):
-        out["kernels"][r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                     "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
-                                     "pct": float(r["Percentage"])}
+    pre = f"prof_{{}}_{args.cfg}"
+    out = {"config": args.cfg, "round": args.round, "command": args.command,
+           "stripes_per_gpu": args.stripes, "warmup": args.warmup, "steps": args.steps,
+           "kernels": {}}
+
+    tpath = find_csv(os.path.join(g, pre.format("trace")), "kernel_trace.csv")
+    rows = trace_rows(tpath)
+    by = defaultdict(list)
+    for name, did, dur in rows:
+        by[name].append((did, dur))
+    timed_ids = set()
+    for name, lst in by.items():
+        d = stats([x[1] for x in lst])
+        if args.kernel and args.kernel in name:
+            lo = 1 + 2 * args.warmup
+            timed = lst[lo:lo + 2 * args.steps]
+            timed_ids = {x[0] for x in timed}
+            t = stats([x[1] for x in timed])
+            d.update({"timed_calls": t["calls"], "timed_avg_ns": t["avg_ns"],
+                      "timed_min_ns": t["min_ns"], "timed_max_ns": t["max_ns"],
+                      "timed_median_ns": t["median_ns"],
+                      "first_dispatch_ns": lst[0][1],
+                      "note": f"timed = dispatches {lo}..{lo + 2 * args.steps - 1} of this kernel"})
+        out["kernels"][name] = d
+
     for tag in ("fetch", "write", "lds"):
-        p = os.path.join(g, d_of(tag), "run_counter_collection.csv")
-        if not os.path.exists(p):
+        p = find_csv(os.path.join(g, pre.format(tag)), "counter_collection.csv")
+        if not p:
             continue
-        for (kern, cname), vals in counters(p).items():
+        per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [(dispatch, value)]
+        for r in csv.DictReader(open(p)):
+            per[col(r, "Kernel_Name")][col(r, "Counter_Name")].append(
+                (int(col(r, "Dispatch_Id")), float(col(r, "Counter_Value"))))
+        for kern, cs in per.items():
             d = out["kernels"].setdefault(kern, {})
-            d[cname] = statistics.mean(vals)
+            for cname, vals in cs.items():
+                # PMC runs are separate processes: use the same position-based timed window
+                vals.sort()
+                if args.kernel and args.kernel in kern:
+                    lo = 1 + 2 * args.warmup
+                    sel = [v for _, v in vals[lo:lo + 2 * args.steps]] or [v for _, v in vals]
+                else:
+                    sel = [v for _, v in vals]
+                d[cname] = statistics.mean(sel)
     for kern, d in out["kernels"].items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             rd = d["FETCH_SIZE"] * 1024 * 2   # gfx950: FETCH_SIZE = half the streamed bytes
@@ -48,17 +122,29 @@ def main(cfg, rnd="r01"):
             d["hbm_read_bytes"] = rd
             d["hbm_write_bytes"] = wr
             d["hbm_bytes_per_launch"] = rd + wr
-            if d.get("avg_ns"):
-                d["hbm_GBps"] = round((rd + wr) / d["avg_ns"], 1)
+            ns = d.get("timed_avg_ns") or d.get("avg_ns")
+            if ns:
+                d["hbm_GBps"] = round((rd + wr) / ns, 1)
+        if "SQ_LDS_BANK_CONFLICT" in d and d.get("SQ_LDS_IDX_ACTIVE"):
+            d["lds_conflict_ratio"] = round(d["SQ_LDS_BANK_CONFLICT"] / d["SQ_LDS_IDX_ACTIVE"], 4)
+    if args.bench and os.path.exists(args.bench):
+        for line in open(args.bench):
+            line = line.strip()
+            if line.startswith("{"):
+                try:
+                    b = json.loads(line)
+                    out["ms_per_step"] = b.get("ms_per_step")
+                    out["bench_value"] = b.get("value")
+                except json.JSONDecodeError:
+                    pass
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    dst = os.path.join(ROOT, "profiles", f"{rnd}_{cfg}_summary.json")
+    dst = os.path.join(ROOT, "profiles", f"{args.round}_{args.cfg}_summary.json")
     json.dump(out, open(dst, "w"), indent=1)
-    shutil.copy(stats, os.path.join(ROOT, "profiles", f"{rnd}_{cfg}_kernel_stats.csv"))
-    blog = os.path.join(g, f"bench_full_{cfg}.log")
-    if os.path.exists(blog):
-        shutil.copy(blog, os.path.join(ROOT, "profiles", f"{rnd}_{cfg}_bench.log"))
+    spath = find_csv(os.path.join(g, pre.format("trace")), "kernel_stats.csv")
+    if spath:
+        shutil.copy(spath, os.path.join(ROOT, "profiles", f"{args.round}_{args.cfg}_kernel_stats.csv"))
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "c3", sys.argv[2] if len(sys.argv) > 2 else "r01")
+    main()
