@@ -43,6 +43,12 @@ const char *ecamd_last_error(void);
  * while other threads launch: each launch reads each knob once. */
 int ecamd_tune(const char *key, int value);
 
+/* Bitsliced 8-output passes (hip/ecamd_jit.hip): 1 if run-time compilation (hiprtc) is usable;
+ * ecamd_bitslice_wait() blocks until every kernel compile started so far has finished and returns
+ * how many failed (their maps keep using the LDS-table kernels). */
+int ecamd_bitslice_available(void);
+int ecamd_bitslice_wait(void);
+
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
 typedef struct ecamd_map ecamd_map;
 

@@ -52,6 +52,10 @@ def host():
         _proto(h, "ecamd_gf16_invert", C.c_int, [IP, IP, C.c_int])
         _proto(h, "ecamd_rs_decode_map", C.c_int, [IP, C.c_int, C.c_int, IP, C.c_int, IP, IP, IP, IP])
         _proto(h, "ecamd_rs_reconstruct_map", C.c_int, [IP, C.c_int, C.c_int, IP, C.c_int, IP, IP, IP])
+        _proto(h, "ecamd_bitslice_eval", C.c_int,
+               [IP, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, IP])
+        _proto(h, "ecamd_bitslice_source", C.c_int64,
+               [IP, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int64])
         _proto(h, "ecamd_split_tables", C.c_int,
                [IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p])
         _host = h
@@ -119,6 +123,8 @@ def dev():
         _proto(d, "ecamd_percall_crc_arm", C.c_int, [C.c_int])
         _proto(d, "ecamd_percall_crc_lookup", C.c_int, [VP, C.c_int64, C.POINTER(C.c_uint32)])
         _proto(d, "ecamd_percall_crc_disarm", None, [])
+        _proto(d, "ecamd_bitslice_available", C.c_int, [])
+        _proto(d, "ecamd_bitslice_wait", C.c_int, [])
         _proto(d, "ecamd_percall_reset", None, [])
         _proto(d, "ecamd_percall_status", C.c_int, [])
         _proto(d, "ecamd_fault_inject", C.c_int, [C.c_char_p, C.c_int])
@@ -162,6 +168,9 @@ def probe():
         _proto(p, "ecamd_probe_mix2", C.c_int,
                [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64,
                 C.c_int, C.c_int, C.c_int, VP])
+        _proto(p, "ecamd_probe_valu", C.c_int, [C.c_int, C.c_int, C.c_int, VP])
+        _proto(p, "ecamd_probe_bs_c5_encode", C.c_int,
+               [VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, VP])
         _probe = p
     return _probe
 

@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "../host/bitslice.hpp"
 #include "../host/gf16.hpp"
 #include "../host/tables.hpp"
 #include "ecamd.h"
@@ -117,7 +118,14 @@ int ensure_device(int* dev_out)
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<4>),
-                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>)};
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>),
+#define KD_(PF) reinterpret_cast<const void*>(&gf16_deep_kernel<1, 3, PF>),                    \
+                reinterpret_cast<const void*>(&gf16_deep_kernel<2, 3, PF>),                    \
+                reinterpret_cast<const void*>(&gf16_deep_kernel<3, 3, PF>),                    \
+                reinterpret_cast<const void*>(&gf16_deep_kernel<4, 3, PF>),                    \
+                reinterpret_cast<const void*>(&gf16_deep_kernel<5, 3, PF>)
+                            KD_(false), KD_(true)};
+#undef KD_
 #undef KF_
         for (const void* k : fk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
@@ -176,6 +184,9 @@ struct Tuning {
     Knob grid_mult{0};      // stream launches: workgroups per resident slot (0: 2 for 4-output
                             //   passes, else 1; tools/grid_sweep.py)
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
+    Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
+                            //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
+    Knob stream_deep{0};    //   8-output passes: all lookups of an input chunk in flight at once
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
@@ -231,7 +242,13 @@ struct ecamd_map {
     int R = 0, K = 0;
     std::vector<Pass> passes;
     uint8_t* d_tables = nullptr;
+    std::vector<int> coeff;  // R x K (host copy: the bitsliced kernels are generated from it)
 };
+
+namespace ecamd {
+hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, bool wait);
+int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st);
+}  // namespace ecamd
 
 namespace {
 
@@ -349,6 +366,26 @@ int launch_stream_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipSt
 int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3 grid, dim3 block,
                   size_t lds, hipStream_t st)
 {
+    const int deep = g_tune.stream_deep;
+    if (width == 8 && !nib && deep) {  // deep lookups (gf16_deep_kernel), with L1 share if hybrid
+#define ECAMD_DEEP(KG)                                                                     \
+    do {                                                                                   \
+        if (pf)                                                                            \
+            hipLaunchKernelGGL((gf16_deep_kernel<KG, 3, true>), grid, block, lds, st, a);  \
+        else                                                                               \
+            hipLaunchKernelGGL((gf16_deep_kernel<KG, 3, false>), grid, block, lds, st, a); \
+    } while (0)
+        switch ((a.ncols + 3) / 4) {
+        case 1: ECAMD_DEEP(1); break;
+        case 2: ECAMD_DEEP(2); break;
+        case 3: ECAMD_DEEP(3); break;
+        case 4: ECAMD_DEEP(4); break;
+        default: ECAMD_DEEP(5); break;
+        }
+#undef ECAMD_DEEP
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (width == 8 && !nib && g_tune.stream_hybrid) {  // LDS + L1 lookups (gf16_hybrid_kernel)
         switch ((a.ncols + 3) / 4) {
         case 1: hipLaunchKernelGGL((gf16_hybrid_kernel<1>), grid, block, lds, st, a); break;
@@ -403,12 +440,49 @@ int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, siz
     return launch_ptrs_w<8>(a, grid, block, lds, st);
 }
 
+// The bitsliced form of an 8-output pass (host/bitslice.hpp, hip/ecamd_jit.hip) over the whole
+// 16 KiB tiles of every fragment; returns the bytes it covered (0: not taken -- shape, knob, or the
+// kernel is still compiling), the rest of each fragment goes to the LDS-table kernels.
+int64_t launch_bitslice(const ecamd_map* map, const ecamd_map::Pass& p, ApplyArgs a, int64_t bs,
+                        int nstripes, hipStream_t st, int* rc)
+{
+    *rc = 0;
+    const int mode = g_tune.bitslice;
+    if (!mode || p.width != 8 || a.nrows < 5 || p.col0 != 0 || p.ncols != map->K || a.copy_records ||
+        a.limited || bs < kBsTile || p.ncols > kBsMaxK || !stream_offsets(a, bs))
+        return 0;
+    std::vector<int> sub(static_cast<size_t>(a.nrows) * p.ncols);
+    for (int r = 0; r < a.nrows; r++)
+        for (int j = 0; j < p.ncols; j++)
+            sub[static_cast<size_t>(r) * p.ncols + j] =
+                map->coeff[static_cast<size_t>(p.row0 + r) * map->K + p.col0 + j];
+    hipFunction_t fn = bitslice_function(map->device, sub, a.nrows, p.ncols, mode == 2);
+    if (!fn) return 0;
+    BsArgs b{};
+    b.in_base = a.in_base;
+    b.out_base = a.out_base;
+    b.in_stride = a.in_stride;
+    b.out_stride = a.out_stride;
+    b.stripe_list = a.stripe_list;
+    b.in_records = a.in_records;
+    b.out_records = a.out_records;
+    b.tiles_per_stripe = static_cast<uint32_t>(bs / kBsTile);
+    b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
+    for (int j = 0; j < p.ncols; j++) b.in_off[j] = a.in_off32[j];
+    for (int r = 0; r < a.nrows; r++) b.out_off[r] = a.out_off32[r];
+    // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
+    const int grid = static_cast<int>(std::min<int64_t>(b.ntiles, static_cast<int64_t>(cu_count(map->device)) * 2));
+    *rc = bitslice_launch(fn, b, grid, st);
+    return *rc ? 0 : bs / kBsTile * kBsTile;
+}
+
 template <bool PTRS>
 int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off,
-                const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st)
+                const int64_t* out_off, int64_t bs_all, int nstripes, hipStream_t st)
 {
     for (const auto& p : map->passes) {
         ApplyArgs a = base_args;
+        int64_t bs = bs_all;
         a.tables = map->d_tables + p.offset;
         a.bs = bs;
         a.ncols = p.ncols;
@@ -416,6 +490,18 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
         a.accumulate = p.col0 > 0;
         for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[p.col0 + j];
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
+        if constexpr (!PTRS) {
+            int brc = 0;
+            const int64_t done = launch_bitslice(map, p, a, bs, nstripes, st, &brc);
+            if (brc) return brc;
+            if (done == bs) continue;
+            if (done > 0) {  // the tail of every fragment through the LDS-table kernels
+                for (int j = 0; j < p.ncols; j++) a.in_off[j] += done;
+                for (int r = 0; r < a.nrows; r++) a.out_off[r] += done;
+                bs -= done;
+                a.bs = bs;
+            }
+        }
         Geometry g;
         int rc = geometry(map->device, p.bytes, bs, nstripes, g, 1);
         if (rc) return rc;
@@ -1062,6 +1148,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.grid_mult = std::max(0, std::min(value, 64));
     } else if (k == "multi_list") {
         g_tune.multi_list = value;
+    } else if (k == "bitslice") {
+        g_tune.bitslice = value;
+    } else if (k == "stream_deep") {
+        g_tune.stream_deep = value;
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
     } else if (k == "stream_order") {
@@ -1125,6 +1215,7 @@ int ecamd_map_create(const int* coeff, int R, int K, ecamd_map** out)
     map->R = R;
     map->K = K;
     map->passes = passes;
+    map->coeff = c;
     if (hipMalloc(&map->d_tables, total) != hipSuccess) {
         delete map;
         return fail(ECAMD_ENOMEM, "hipMalloc(%zu) for tables failed", total);

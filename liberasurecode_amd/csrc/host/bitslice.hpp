@@ -1,0 +1,69 @@
+// bitslice.hpp -- bitsliced GF(2^16) fragment maps (host side): the XOR network of an R x K
+// coefficient matrix and the HIP source of a kernel specialised to it (compiled at run time by
+// hip/ecamd_jit.hip).
+//
+// c*x over GF(2^16) is the 16x16 GF(2) matrix M_c applied to the bits of x (rs_galois_mult is
+// carry-less multiplication mod 0x1100b, src/builtin/rs_vand/rs_galois.c:90-100).
+// A lane holds 32 words of each fragment; a 16x16 bit transpose inside each 16-bit half of its 16
+// dwords turns them into 16 bit planes (plane of bit b in register 15 - b; word w at bit
+// (15 - w/2) + 16*(w%2); the transpose is an involution, so the same code maps output planes back
+// to words).  Output plane (r, p) is the XOR over inputs j and bits b with M_{A[r][j]}[p][b] = 1 of
+// the input planes: VALU XORs only, no table lookups, so the 8-output passes that the LDS tables
+// bound (C5: random 16-byte lookups conflict ~2.9-way in the LDS banks) run at VALU rate.  Output
+// planes accumulate through three-input XORs (v_bitop3), so a row of n terms costs ceil(n/2) ops;
+// per input, sums shared by several rows are computed once first -- greedy common-subexpression
+// elimination in the spirit of Paar's algorithm, but priced in three-input XORs: a shared triple
+// saves one op in every row holding it, a shared pair one op in every odd-length row holding it,
+// each costs one op -- with at most `cap` such temporaries, so the network fits the register file
+// at 2 waves per SIMD.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ecamd {
+
+// The 16 rows of M_c: bit b of row p is set when bit p of c*(1<<b) is.
+void gf16_bitmatrix(int c, uint16_t (&rows)[16]);
+
+struct BitsliceNet {
+    int R = 0, K = 0;
+    // per input j: temporaries (XOR of 2 or 3 variables -- third < 0 for a pair; variables
+    // 0..15 are the input planes by bit, 16+ the temps in order) and, per output plane r*16+p,
+    // the variables XORed into it
+    struct Input {
+        std::vector<std::array<int, 3>> temps;
+        std::vector<std::vector<int>> rows;
+    };
+    std::vector<Input> inputs;
+    int xor_ops() const;  // VALU ops of the network (temps + 3-input accumulation)
+};
+
+BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap);
+
+// Evaluate the network on 32 words per input (host check of the construction).
+void bitslice_eval(const BitsliceNet& net, const uint16_t* in /* K x 32 */, uint16_t* out /* R x 32 */);
+
+// HIP source of `extern "C" __global__ void ecamd_bs_kernel(ecamd_bs_args)` for the network.
+std::string bitslice_source(const BitsliceNet& net);
+
+// Kernel arguments (layout shared by the generated source and the launcher).
+constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)
+constexpr int kBsMaxK = 32;
+constexpr int kBsMaxR = 8;
+struct BsArgs {
+    const uint8_t* in_base;
+    uint8_t* out_base;
+    int64_t in_stride;
+    int64_t out_stride;
+    const int32_t* stripe_list;  // logical stripe s is stripe_list[s] (null: s)
+    uint32_t in_records;
+    uint32_t out_records;
+    uint32_t ntiles;
+    uint32_t tiles_per_stripe;
+    int32_t in_off[kBsMaxK];
+    int32_t out_off[kBsMaxR];
+};
+
+}  // namespace ecamd

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <vector>
 
+#include "bitslice.hpp"
 #include "gf16.hpp"
 #include "tables.hpp"
 #include "xor_plan.hpp"
@@ -208,6 +209,30 @@ int ecamd_percall_device_plan(int ndev, const char* spec, int* devs, int max)
     const int n = std::min(static_cast<int>(ids.size()), max);
     for (int i = 0; i < n; i++) devs[i] = ids[static_cast<size_t>(i)];
     return n;
+}
+
+int ecamd_bitslice_eval(const int* coeff, int R, int K, int cap, const uint16_t* in, uint16_t* out,
+                        int* ops)
+{
+    if (!coeff || !in || !out || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK) return -1;
+    std::vector<int> c(coeff, coeff + static_cast<size_t>(R) * K);
+    const BitsliceNet net = bitslice_network(c, R, K, cap);
+    bitslice_eval(net, in, out);
+    if (ops) *ops = net.xor_ops();
+    return 0;
+}
+
+int64_t ecamd_bitslice_source(const int* coeff, int R, int K, int cap, char* buf, int64_t size)
+{
+    if (!coeff || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK) return -1;
+    std::vector<int> c(coeff, coeff + static_cast<size_t>(R) * K);
+    const std::string src = bitslice_source(bitslice_network(c, R, K, cap));
+    if (buf && size > 0) {
+        const size_t n = std::min(static_cast<size_t>(size - 1), src.size());
+        std::memcpy(buf, src.data(), n);
+        buf[n] = 0;
+    }
+    return static_cast<int64_t>(src.size());
 }
 
 }  // extern "C"

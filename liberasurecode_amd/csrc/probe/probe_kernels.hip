@@ -213,3 +213,65 @@ template __global__ void lookup_probe_kernel<4>(const uint4*, int, uint32_t*);
 template __global__ void lookup_probe_kernel<5>(const uint4*, int, uint32_t*);
 
 }  // namespace ecamd
+
+namespace ecamd {
+
+// VALU issue-cost probe: each lane runs `iters` rounds of 8 independent chains of one
+// instruction form (OP), so the SIMD sees back-to-back independent VALU work from every wave;
+// cycles per wave-instruction = wall cycles x waves per SIMD / (iters x 8).  OP: 0 v_xor_b32,
+// 1 v_bitop3_b32 (XOR3), 2 v_lshlrev_b32_sdwa (byte select), 3 v_bfe_u32, 4 v_and_b32,
+// 5 v_perm_b32, 6 v_lshl_or_b32, 7 ds_read_b128 from a 16-entry table (conflict-free).
+template <int OP>
+__global__ void __launch_bounds__(256) valu_probe_kernel(int iters, uint32_t seed, uint32_t* sink)
+{
+    __shared__ uint4 tab[16];
+    if (threadIdx.x < 16) tab[threadIdx.x] = make_uint4(threadIdx.x, seed, 3, 4);
+    __syncthreads();
+    uint32_t a[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) a[i] = seed * (threadIdx.x + 1 + i);
+    const uint32_t k = seed | 1u;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            uint32_t r;
+            if constexpr (OP == 0) {
+                asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a[i]), "v"(k));
+            } else if constexpr (OP == 1) {
+                asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a[i]), "v"(k), "v"(a[(i + 1) & 7]));
+            } else if constexpr (OP == 2) {
+                asm volatile("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+                             : "=v"(r) : "v"(a[i]));
+                r ^= 0;
+            } else if constexpr (OP == 3) {
+                asm volatile("v_bfe_u32 %0, %1, 8, 4" : "=v"(r) : "v"(a[i]));
+            } else if constexpr (OP == 4) {
+                asm volatile("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(a[i]), "v"(k));
+            } else if constexpr (OP == 5) {
+                asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a[i]), "v"(k), "v"(a[(i + 3) & 7]));
+            } else if constexpr (OP == 6) {
+                asm volatile("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(r) : "v"(a[i]), "v"(k));
+            } else {
+                uint4 v;
+                asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((a[i] & 15u) * 16u));
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                r = v.x;
+            }
+            a[i] = r;
+        }
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) x ^= a[i];
+    if (x == 0x12345678u) sink[0] = x;
+}
+template __global__ void valu_probe_kernel<0>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<1>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<2>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<3>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<4>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<5>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<6>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<7>(int, uint32_t, uint32_t*);
+
+}  // namespace ecamd

@@ -14,13 +14,16 @@ import torch  # noqa: E402,F401
 from liberasurecode_amd import _lib  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
-K, M, F, S = 20, 8, 4 << 20, 32
+K, M = 20, 8
+F = int(os.environ.get("C5_F", 4 << 20))
+S = int(os.environ.get("C5_S", 32))
 LOST = list(range(8))
-DEFAULTS = {"stream_hybrid": 1, "stream_nib": 0, "stream_mixed": 0, "stream_ch": 1, "stream_pf": 0}
+DEFAULTS = {"stream_hybrid": 1, "stream_nib": 0, "stream_deep": 0, "stream_ch": 1, "stream_pf": 0,
+            "bitslice": 0}
 VARIANTS = {
+    "bitslice": {"bitslice": 2},
     "hybrid": {},
     "byte": {"stream_hybrid": 0},
-    "nib": {"stream_hybrid": 0, "stream_nib": 1},
 }
 for extra in sys.argv[1:]:  # name=key:val,key:val
     name, kv = extra.split("=", 1)
@@ -32,7 +35,7 @@ def setv(d, v):
         d.ecamd_tune(key.encode(), v.get(key, val))
 
 
-def main(reps=8):
+def main(reps=8, rounds=3):
     d = _lib.dev()
     lay = D.Layout.alloc(K + M, F, S)
     st = D.Stream()
@@ -42,9 +45,9 @@ def main(reps=8):
     st.synchronize()
     want = lay.buf.download(lay.stripe_stride * 2)
     algo = S * (K + M) * F
-    for name, v in VARIANTS.items():
+    for rnd, (name, v) in [(r, nv) for r in range(rounds) for nv in VARIANTS.items()]:
         setv(d, v)
-        res = {"variant": name, "knobs": v}
+        res = {"round": rnd, "variant": name, "knobs": v}
         for op, fn in (("encode", lambda: D.rs_encode(K, M, lay, stream=st)),
                        ("decode", lambda: D.rs_decode(K, M, LOST, lay, stream=st))):
             fn()
