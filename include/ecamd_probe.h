@@ -45,11 +45,6 @@ int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
  * shift, 3 v_bfe_u32, 4 v_and_b32, 5 v_perm_b32, 6 v_lshl_or_b32, 7 conflict-free ds_read_b128 +
  * wait). */
 int ecamd_probe_valu(int op, int wgs_per_cu, int iters, void *stream);
-/* Experiment: bitsliced C5 encode (k=20, m=8) over a strided batch (fragment f of stripe s at
- * base + s*stripe_stride + f*frag_stride), blocksize a multiple of 16 KiB. */
-int ecamd_probe_bs_c5_encode(void *base, int64_t stripe_stride, int64_t frag_stride, int64_t blocksize,
-                             int nstripes, int wgs_per_cu, void *stream);
-
 #ifdef __cplusplus
 }
 #endif

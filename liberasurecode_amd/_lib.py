@@ -169,8 +169,6 @@ def probe():
                [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64,
                 C.c_int, C.c_int, C.c_int, VP])
         _proto(p, "ecamd_probe_valu", C.c_int, [C.c_int, C.c_int, C.c_int, VP])
-        _proto(p, "ecamd_probe_bs_c5_encode", C.c_int,
-               [VP, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, VP])
         _probe = p
     return _probe
 

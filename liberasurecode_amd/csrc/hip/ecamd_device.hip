@@ -118,14 +118,7 @@ int ensure_device(int* dev_out)
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<4>),
-                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>),
-#define KD_(PF) reinterpret_cast<const void*>(&gf16_deep_kernel<1, 3, PF>),                    \
-                reinterpret_cast<const void*>(&gf16_deep_kernel<2, 3, PF>),                    \
-                reinterpret_cast<const void*>(&gf16_deep_kernel<3, 3, PF>),                    \
-                reinterpret_cast<const void*>(&gf16_deep_kernel<4, 3, PF>),                    \
-                reinterpret_cast<const void*>(&gf16_deep_kernel<5, 3, PF>)
-                            KD_(false), KD_(true)};
-#undef KD_
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>)};
 #undef KF_
         for (const void* k : fk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
@@ -186,7 +179,6 @@ struct Tuning {
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
-    Knob stream_deep{0};    //   8-output passes: all lookups of an input chunk in flight at once
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
@@ -366,26 +358,6 @@ int launch_stream_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipSt
 int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3 grid, dim3 block,
                   size_t lds, hipStream_t st)
 {
-    const int deep = g_tune.stream_deep;
-    if (width == 8 && !nib && deep) {  // deep lookups (gf16_deep_kernel), with L1 share if hybrid
-#define ECAMD_DEEP(KG)                                                                     \
-    do {                                                                                   \
-        if (pf)                                                                            \
-            hipLaunchKernelGGL((gf16_deep_kernel<KG, 3, true>), grid, block, lds, st, a);  \
-        else                                                                               \
-            hipLaunchKernelGGL((gf16_deep_kernel<KG, 3, false>), grid, block, lds, st, a); \
-    } while (0)
-        switch ((a.ncols + 3) / 4) {
-        case 1: ECAMD_DEEP(1); break;
-        case 2: ECAMD_DEEP(2); break;
-        case 3: ECAMD_DEEP(3); break;
-        case 4: ECAMD_DEEP(4); break;
-        default: ECAMD_DEEP(5); break;
-        }
-#undef ECAMD_DEEP
-        HIP_TRY(hipGetLastError());
-        return 0;
-    }
     if (width == 8 && !nib && g_tune.stream_hybrid) {  // LDS + L1 lookups (gf16_hybrid_kernel)
         switch ((a.ncols + 3) / 4) {
         case 1: hipLaunchKernelGGL((gf16_hybrid_kernel<1>), grid, block, lds, st, a); break;
@@ -1150,8 +1122,6 @@ int ecamd_tune(const char* key, int value)
         g_tune.multi_list = value;
     } else if (k == "bitslice") {
         g_tune.bitslice = value;
-    } else if (k == "stream_deep") {
-        g_tune.stream_deep = value;
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
     } else if (k == "stream_order") {

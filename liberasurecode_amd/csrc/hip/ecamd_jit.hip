@@ -1,21 +1,30 @@
 // ecamd_jit.hip -- run-time specialised bitsliced GF(2^16) kernels (host/bitslice.hpp).
 //
 // The XOR network of a bitsliced map depends on every coefficient, so its kernel is generated for
-// the matrix and compiled with hiprtc (loaded with dlopen: without it the LDS-table kernels simply
-// keep running).  Compilation takes a few seconds and runs on a background thread the first time
-// a matrix is seen; launches use the LDS-table kernel until the code object is ready (knob
-// "bitslice" = 1, the default), or wait for it (= 2; tests, bench); ecamd_bitslice_wait() waits for
-// every pending compile.  Code objects are cached per matrix, modules per device.
+// the matrix and compiled at run time.  The compile runs in a child process (ecamd_jitc, next to
+// this library; hiprtc), never in this process: a GPU process that exits while a compile is in
+// flight simply abandons it, and hiprtc's runtime never shares an address space with the GPU
+// work.  Code objects land in a disk cache keyed by a hash of the source ($ECAMD_JIT_CACHE, else
+// /tmp/ecamd-jit-<uid>), so later processes load them at once.  Knob "bitslice": 1 (default)
+// launches the LDS-table kernel until the code object is ready, 2 waits for it (tests, bench), 0
+// never uses the bitsliced form; ecamd_bitslice_wait() waits for every compile started so far.
 #include <hip/hip_runtime.h>
-#include <hip/hiprtc.h>
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
-#include <chrono>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <future>
+#include <fstream>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -23,96 +32,128 @@
 #include "ecamd.h"
 #include "ecamd_internal.hpp"
 
+extern char** environ;
+
 namespace ecamd {
 namespace {
-
-struct Rtc {
-    hiprtcResult (*create)(hiprtcProgram*, const char*, const char*, int, const char* const*,
-                           const char* const*) = nullptr;
-    hiprtcResult (*compile)(hiprtcProgram, int, const char* const*) = nullptr;
-    hiprtcResult (*code_size)(hiprtcProgram, size_t*) = nullptr;
-    hiprtcResult (*code)(hiprtcProgram, char*) = nullptr;
-    hiprtcResult (*log_size)(hiprtcProgram, size_t*) = nullptr;
-    hiprtcResult (*log)(hiprtcProgram, char*) = nullptr;
-    hiprtcResult (*destroy)(hiprtcProgram*) = nullptr;
-    bool ok = false;
-};
-
-const Rtc& rtc()
-{
-    static Rtc r;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        void* h = nullptr;
-        for (const char* name : {"libhiprtc.so.7", "libhiprtc.so", "/opt/rocm/lib/libhiprtc.so"})
-            if ((h = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
-        if (!h) return;
-#define SYM(f, n) r.f = reinterpret_cast<decltype(r.f)>(dlsym(h, n))
-        SYM(create, "hiprtcCreateProgram");
-        SYM(compile, "hiprtcCompileProgram");
-        SYM(code_size, "hiprtcGetCodeSize");
-        SYM(code, "hiprtcGetCode");
-        SYM(log_size, "hiprtcGetProgramLogSize");
-        SYM(log, "hiprtcGetProgramLog");
-        SYM(destroy, "hiprtcDestroyProgram");
-#undef SYM
-        r.ok = r.create && r.compile && r.code_size && r.code && r.destroy;
-    });
-    return r;
-}
-
-// Code object of the kernel for one network ("" when the compile failed).
-std::string compile_network(const std::string& src)
-{
-    const Rtc& r = rtc();
-    if (!r.ok) return {};
-    hiprtcProgram prog = nullptr;
-    if (r.create(&prog, src.c_str(), "ecamd_bitslice.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
-        return {};
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    std::string out;
-    if (r.compile(prog, 3, opts) == HIPRTC_SUCCESS) {
-        size_t n = 0;
-        if (r.code_size(prog, &n) == HIPRTC_SUCCESS && n > 0) {
-            out.resize(n);
-            if (r.code(prog, &out[0]) != HIPRTC_SUCCESS) out.clear();
-        }
-    } else if (r.log_size && r.log) {
-        size_t n = 0;
-        r.log_size(prog, &n);
-        std::string log(n, '\0');
-        if (n) r.log(prog, &log[0]);
-        std::fprintf(stderr, "libecamd: bitslice kernel compile failed:\n%s\n", log.c_str());
-    }
-    r.destroy(&prog);
-    return out;
-}
-
-struct BsEntry {
-    std::vector<int> coeff;
-    int R = 0, K = 0;
-    int cap = 0;  // shared temporaries allowed in the network (fewer: fewer registers)
-    int gen = 0;  // bumped when the network is rebuilt
-    std::shared_future<std::string> code;
-    std::mutex mu;
-    std::map<int, hipFunction_t> fn;  // per device; nullptr: unusable there
-    std::vector<hipModule_t> modules;
-};
 
 // Temporaries per input: 40 fits the register file at 2 waves per SIMD for the C5 networks
 // (252 VGPRs, no scratch); a network that spills is rebuilt once with 16.
 constexpr int kCapFirst = 40;
 constexpr int kCapRetry = 16;
 
-void start_compile(BsEntry& e)
+std::string helper_path()
 {
-    const BitsliceNet net = bitslice_network(e.coeff, e.R, e.K, e.cap);
-    e.code = std::async(std::launch::async, compile_network, bitslice_source(net)).share();
-    e.gen++;
+    static std::string path;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        Dl_info info{};
+        if (dladdr(reinterpret_cast<void*>(&helper_path), &info) && info.dli_fname) {
+            std::string lib(info.dli_fname);
+            const size_t slash = lib.rfind('/');
+            path = (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/ecamd_jitc";
+        }
+        if (access(path.c_str(), X_OK) != 0) path.clear();
+    });
+    return path;
 }
 
-std::mutex g_jit_mu;
+std::string cache_dir()
+{
+    static std::string dir;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* env = std::getenv("ECAMD_JIT_CACHE");
+        dir = env && *env ? env : "/tmp/ecamd-jit-" + std::to_string(getuid());
+        mkdir(dir.c_str(), 0700);
+    });
+    return dir;
+}
+
+uint64_t fnv1a(const std::string& s)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    return h;
+}
+
+bool read_file(const std::string& path, std::string& out)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    out = ss.str();
+    return !out.empty();
+}
+
+struct BsEntry {
+    std::vector<int> coeff;
+    int R = 0, K = 0;
+    int cap = 0;          // shared temporaries allowed in the network (fewer: fewer registers)
+    std::string co_path;  // cache file of the code object
+    pid_t pid = -1;       // compiler child while running
+    int state = 0;        // 0 compiling, 1 code object ready, -1 failed
+    std::string code;
+    std::map<int, hipFunction_t> fn;  // per device; nullptr: unusable there
+    std::vector<hipModule_t> modules;
+};
+
+std::mutex g_jit_mu;  // guards g_jit and every entry
 std::map<std::vector<int>, std::shared_ptr<BsEntry>> g_jit;
+
+// Generate the source for e.cap and start (or skip, when cached) its compile.  Caller holds the lock.
+void start_compile(BsEntry& e)
+{
+    const std::string src = bitslice_source(bitslice_network(e.coeff, e.R, e.K, e.cap));
+    char name[32];
+    std::snprintf(name, sizeof(name), "%016llx", static_cast<unsigned long long>(fnv1a(src)));
+    const std::string base = cache_dir() + "/bs_" + name;
+    e.co_path = base + ".co";
+    e.pid = -1;
+    e.code.clear();
+    if (read_file(e.co_path, e.code)) {  // compiled before, here or by another process
+        e.state = 1;
+        return;
+    }
+    e.state = -1;
+    const std::string helper = helper_path();
+    if (helper.empty()) return;
+    const std::string src_path = base + ".hip";
+    {
+        const std::string tmp = src_path + ".tmp." + std::to_string(getpid());
+        std::ofstream f(tmp);
+        f << src;
+        f.close();
+        if (!f || std::rename(tmp.c_str(), src_path.c_str()) != 0) return;
+    }
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);  // keep our stdout clean
+    const char* argv[] = {helper.c_str(), src_path.c_str(), e.co_path.c_str(), nullptr};
+    pid_t pid = -1;
+    if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, const_cast<char* const*>(argv), environ) == 0) {
+        e.pid = pid;
+        e.state = 0;
+    }
+    posix_spawn_file_actions_destroy(&fa);
+}
+
+// Advance a compiling entry (reap the child; block when `wait`).  Caller holds the lock.
+void poll_compile(BsEntry& e, bool wait)
+{
+    if (e.state != 0) return;
+    int status = 0;
+    pid_t r;
+    do {
+        r = waitpid(e.pid, &status, wait ? 0 : WNOHANG);
+    } while (r < 0 && errno == EINTR);
+    if (r == 0) return;  // still running
+    const bool ok = r == e.pid && WIFEXITED(status) && WEXITSTATUS(status) == 0;
+    e.pid = -1;
+    // a child reaped elsewhere (r < 0) may still have produced the file
+    e.state = ((ok || r < 0) && read_file(e.co_path, e.code)) ? 1 : -1;
+}
 
 }  // namespace
 
@@ -120,46 +161,32 @@ std::map<std::vector<int>, std::shared_ptr<BsEntry>> g_jit;
 // bitsliced form is unavailable; starts the compile the first time the matrix is seen.
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, bool wait)
 {
-    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || !rtc().ok) return nullptr;
+    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
     std::vector<int> key = {R, K};
     key.insert(key.end(), coeff.begin(), coeff.end());
-    std::shared_ptr<BsEntry> e;
-    {
-        std::lock_guard<std::mutex> lk(g_jit_mu);
-        if (g_jit.size() >= 1024 && !g_jit.count(key)) g_jit.clear();  // bound; in-use entries live on
-        auto& slot = g_jit[key];
-        if (!slot) {
-            slot = std::make_shared<BsEntry>();
-            slot->coeff = coeff;
-            slot->R = R;
-            slot->K = K;
-            slot->cap = kCapFirst;
-            start_compile(*slot);
-        }
-        e = slot;
+    std::lock_guard<std::mutex> lk(g_jit_mu);
+    if (g_jit.size() >= 1024 && !g_jit.count(key)) g_jit.clear();  // bound; loaded modules stay valid
+    auto& slot = g_jit[key];
+    if (!slot) {
+        slot = std::make_shared<BsEntry>();
+        slot->coeff = coeff;
+        slot->R = R;
+        slot->K = K;
+        slot->cap = kCapFirst;
+        start_compile(*slot);
     }
+    BsEntry& e = *slot;
     for (;;) {
-        std::shared_future<std::string> code;
-        int gen = 0;
-        {
-            std::lock_guard<std::mutex> lk(e->mu);
-            auto it = e->fn.find(dev);
-            if (it != e->fn.end()) return it->second;
-            code = e->code;
-            gen = e->gen;
-        }
-        if (!wait && code.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return nullptr;
-        const std::string& co = code.get();
-        std::lock_guard<std::mutex> lk(e->mu);
-        if (e->gen != gen) continue;  // rebuilt meanwhile by another thread
-        auto it = e->fn.find(dev);
-        if (it != e->fn.end()) return it->second;
+        auto it = e.fn.find(dev);
+        if (it != e.fn.end()) return it->second;
+        poll_compile(e, wait);
+        if (e.state == 0) return nullptr;
         hipFunction_t fn = nullptr;
         int spill = 0;
-        if (!co.empty()) {
+        if (e.state == 1) {
             hipModule_t mod = nullptr;
-            if (hipModuleLoadData(&mod, co.data()) == hipSuccess) {
-                e->modules.push_back(mod);
+            if (hipModuleLoadData(&mod, e.code.data()) == hipSuccess) {
+                e.modules.push_back(mod);
                 if (hipModuleGetFunction(&fn, mod, "ecamd_bs_kernel") != hipSuccess) fn = nullptr;
                 if (fn && hipFuncGetAttribute(&spill, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) == hipSuccess &&
                     spill > 0)
@@ -167,13 +194,13 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
             }
             (void)hipGetLastError();
         }
-        if (!fn && spill > 0 && e->cap > kCapRetry) {  // rebuild with fewer temporaries
-            e->cap = kCapRetry;
-            start_compile(*e);
-            e->fn.clear();
+        if (!fn && spill > 0 && e.cap > kCapRetry) {  // rebuild with fewer temporaries
+            e.cap = kCapRetry;
+            e.fn.clear();
+            start_compile(e);
             continue;
         }
-        e->fn[dev] = fn;
+        e.fn[dev] = fn;
         return fn;
     }
 }
@@ -193,21 +220,13 @@ int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t 
 
 extern "C" int ecamd_bitslice_wait(void)
 {
-    std::vector<std::shared_ptr<ecamd::BsEntry>> all;
-    {
-        std::lock_guard<std::mutex> lk(ecamd::g_jit_mu);
-        for (auto& kv : ecamd::g_jit) all.push_back(kv.second);
-    }
+    std::lock_guard<std::mutex> lk(ecamd::g_jit_mu);
     int failed = 0;
-    for (auto& e : all) {
-        std::shared_future<std::string> code;
-        {
-            std::lock_guard<std::mutex> lk(e->mu);
-            code = e->code;
-        }
-        if (code.get().empty()) failed++;
+    for (auto& kv : ecamd::g_jit) {
+        ecamd::poll_compile(*kv.second, true);
+        if (kv.second->state != 1) failed++;
     }
     return failed;
 }
 
-extern "C" int ecamd_bitslice_available(void) { return ecamd::rtc().ok ? 1 : 0; }
+extern "C" int ecamd_bitslice_available(void) { return ecamd::helper_path().empty() ? 0 : 1; }

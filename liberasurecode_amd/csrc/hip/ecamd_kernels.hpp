@@ -69,8 +69,6 @@ template <int W, int KG>
 __global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
 template <int KG>
 __global__ void gf16_hybrid_kernel(const ApplyArgs a);
-template <int KG, int TM, bool PF>
-__global__ void gf16_deep_kernel(const ApplyArgs a);
 struct FusedCrcArgs;
 template <int W, int KG, int MB>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);

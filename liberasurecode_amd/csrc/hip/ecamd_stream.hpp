@@ -146,47 +146,6 @@ __device__ __forceinline__ void mac_chunk_mixed(const uint8_t* lds, v4u x, const
     }
 }
 
-// Deep lookups (TM 3 and 4, 8-output passes): all 16 lookups of one input chunk are issued
-// before any XOR consumes them, so a wave keeps up to 15 LDS reads in flight (counted lgkmcnt)
-// instead of the 2 that mac_chunk_imm's interleaving leaves the compiler (read, read, wait, XOR):
-// at 4 waves per SIMD -- C5's 160 KiB table image allows no more -- the LDS array otherwise idles
-// while waves wait on their 2 reads.  The first NH hi lookups come from registers (L1, TM 4).
-template <int W, int J, int NH>
-__device__ __forceinline__ void mac_chunk_deep(const uint8_t* lds, v4u x,
-                                               const uint32_t (&eh)[NH ? NH : 1][W / 2],
-                                               uint32_t (&acc)[8][W / 2])
-{
-    constexpr int D = W / 2;
-    constexpr int EB = 2 * W;
-    constexpr int S = log2i(EB);
-    constexpr int TL = J * 512 * EB;
-    constexpr int TH = TL + 256 * EB;
-    v4u e0[8], e1[8];
-#pragma unroll
-    for (int w = 0; w < 8; w++) {
-        const uint32_t v = x[w >> 1];
-        if (w & 1)
-            e0[w] = *reinterpret_cast<const v4u*>(lds + TL + byte_shl<2, S>(v));
-        else
-            e0[w] = *reinterpret_cast<const v4u*>(lds + TL + byte_shl<0, S>(v));
-        if (w < NH)
-            e1[w] = v4u{eh[w < NH ? w : 0][0], eh[w < NH ? w : 0][1], eh[w < NH ? w : 0][2],
-                        eh[w < NH ? w : 0][3]};
-        else if (w & 1)
-            e1[w] = *reinterpret_cast<const v4u*>(lds + TH + byte_shl<3, S>(v));
-        else
-            e1[w] = *reinterpret_cast<const v4u*>(lds + TH + byte_shl<1, S>(v));
-    }
-    // one fence over every lookup result: all reads are issued before the first is consumed
-    asm volatile("" : "+v"(e0[0]), "+v"(e0[1]), "+v"(e0[2]), "+v"(e0[3]), "+v"(e0[4]), "+v"(e0[5]),
-                 "+v"(e0[6]), "+v"(e0[7]), "+v"(e1[0]), "+v"(e1[1]), "+v"(e1[2]), "+v"(e1[3]),
-                 "+v"(e1[4]), "+v"(e1[5]), "+v"(e1[6]), "+v"(e1[7]));
-#pragma unroll
-    for (int w = 0; w < 8; w++)
-#pragma unroll
-        for (int d = 0; d < D; d++) acc[w][d] = xor3(acc[w][d], e0[w][d], e1[w][d]);
-}
-
 template <int W, int CH, int J, int TM>
 __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds, const StreamTile& t,
                                           const v4u (&x)[CH], uint32_t (&acc)[CH][8][W / 2])
@@ -200,14 +159,10 @@ __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds
         }
 #pragma unroll
         for (int c = 0; c < CH; c++) {
-            if constexpr (TM == 1) {
+            if constexpr (TM == 1)
                 mac_chunk_nib_imm<W, J>(lds, x[c], acc[c]);
-            } else if constexpr (TM >= 3) {
-                const uint32_t none[1][W / 2] = {};
-                mac_chunk_deep<W, J, 0>(lds, x[c], none, acc[c]);
-            } else {
+            else
                 mac_chunk_imm<W, J>(lds, x[c], acc[c]);
-            }
         }
     }
 }
@@ -233,7 +188,7 @@ __device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* 
 {
     v4u nxt[4][CH];
     if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG>(a, t, nxt);
-    if constexpr ((TM == 2 || TM == 4) && CH == 1) {
+    if constexpr (TM == 2 && CH == 1) {
         // input 0's hi table via L1 (12.5% of the lookups; taking 3/16 -- input 2's hi for words
         // 0..3, or input 0's lo for words 0..3 -- measured 12% slower than none: a 40 KiB table
         // footprint no longer fits the 32 KiB L1)
@@ -244,16 +199,10 @@ __device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* 
             if (a.copy_records && a.copy_off32[4 * G] >= 0)
                 __builtin_amdgcn_raw_buffer_store_b128(cur[0][0], t.rcopy, a.copy_off32[4 * G] + t.off, 0, 2);
         }
-        constexpr int TI = TM == 4 ? 3 : 0;  // the other inputs: deep (TM 4) or interleaved lookups
-        input_mac<W, CH, 4 * G + 1, TI>(a, lds, t, cur[1], acc);
-        input_mac<W, CH, 4 * G + 2, TI>(a, lds, t, cur[2], acc);
-        input_mac<W, CH, 4 * G + 3, TI>(a, lds, t, cur[3], acc);
-        if (live0) {
-            if constexpr (TM == 4)
-                mac_chunk_deep<W, 4 * G, 8>(lds, cur[0][0], eh0, acc[0]);
-            else
-                mac_chunk_mixed<W, 4 * G, 0, 8>(lds, cur[0][0], dummy, eh0, acc[0]);
-        }
+        input_mac<W, CH, 4 * G + 1, 0>(a, lds, t, cur[1], acc);
+        input_mac<W, CH, 4 * G + 2, 0>(a, lds, t, cur[2], acc);
+        input_mac<W, CH, 4 * G + 3, 0>(a, lds, t, cur[3], acc);
+        if (live0) mac_chunk_mixed<W, 4 * G, 0, 8>(lds, cur[0][0], dummy, eh0, acc[0]);
     } else {
         input_mac<W, CH, 4 * G + 0, TM>(a, lds, t, cur[0], acc);
         input_mac<W, CH, 4 * G + 1, TM>(a, lds, t, cur[1], acc);
@@ -377,16 +326,6 @@ __global__ void __launch_bounds__(1024) gf16_hybrid_kernel(const ApplyArgs a)
     gf16_stream_body<8, KG, 1, false, false, 2>(a);
 }
 
-// 8-output passes with deep lookups (TM 3), optionally beside the hybrid L1 lookups (TM 4).  The
-// waves-per-EU bound tells the compiler that 4 waves per SIMD is all this launch gets (the table
-// image fills the LDS), so it may hold the 16 lookups of an input chunk in registers.
-template <int KG, int TM, bool PF>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
-gf16_deep_kernel(const ApplyArgs a)
-{
-    gf16_stream_body<8, KG, 1, PF, false, TM>(a);
-}
-
 // One group of 4 inputs of gf16_ptrs_stream_kernel: a buffer resource per fragment, loads
 // unconditional (out-of-range offset past ncols), lookups at compile-time table offsets.
 template <int W, int G, int KG>
@@ -482,12 +421,6 @@ __global__ void __launch_bounds__(1024) gf16_ptrs_stream_kernel(const ApplyArgs 
     template __global__ void ecamd::gf16_hybrid_kernel<3>(const ecamd::ApplyArgs); \
     template __global__ void ecamd::gf16_hybrid_kernel<4>(const ecamd::ApplyArgs); \
     template __global__ void ecamd::gf16_hybrid_kernel<5>(const ecamd::ApplyArgs);
-#define ECAMD_DEEP_KG(TM, PF) \
-    template __global__ void ecamd::gf16_deep_kernel<1, TM, PF>(const ecamd::ApplyArgs); \
-    template __global__ void ecamd::gf16_deep_kernel<2, TM, PF>(const ecamd::ApplyArgs); \
-    template __global__ void ecamd::gf16_deep_kernel<3, TM, PF>(const ecamd::ApplyArgs); \
-    template __global__ void ecamd::gf16_deep_kernel<4, TM, PF>(const ecamd::ApplyArgs); \
-    template __global__ void ecamd::gf16_deep_kernel<5, TM, PF>(const ecamd::ApplyArgs);
 #define ECAMD_PTRS_KG(W)                                                                  \
     template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 1>(const ecamd::ApplyArgs);      \
     template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 2>(const ecamd::ApplyArgs);      \

@@ -6,5 +6,3 @@ ECAMD_STREAM_KG(8, 1, true, false)
 ECAMD_STREAM_KG(8, 1, false, true)
 ECAMD_PTRS_KG(8)
 ECAMD_HYBRID_KG
-ECAMD_DEEP_KG(3, false)
-ECAMD_DEEP_KG(3, true)

@@ -33,9 +33,6 @@ __global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes,
                                 uint32_t* sink);
 __global__ void stream_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n);
 
-template <int V>
-__global__ void bs_c5_encode_kernel(uint8_t* base, int64_t stripe_stride, int fstride,
-                                    uint32_t ntiles, uint32_t tiles_per_stripe);
 template <int OP>
 __global__ void valu_probe_kernel(int iters, uint32_t seed, uint32_t* sink);
 

@@ -181,28 +181,4 @@ int ecamd_probe_valu(int op, int wgs_per_cu, int iters, void* stream)
     return 0;
 }
 
-int ecamd_probe_bs_c5_encode(void* base, int64_t stripe_stride, int64_t frag_stride,
-                             int64_t blocksize, int nstripes, int wgs_per_cu, void* stream)
-{
-    int dev = 0;
-    int rc = ensure_device(&dev);
-    if (rc) return rc;
-    if (!aligned16(base) || blocksize % 16384 || frag_stride < blocksize || 28 * frag_stride >= (1ll << 31) ||
-        nstripes < 1)
-        return fail(-22, "bitslice probe: blocksize must be a multiple of 16 KiB, stripes < 2 GiB");
-    const uint32_t tps = static_cast<uint32_t>(blocksize / 16384);
-    const uint32_t ntiles = tps * static_cast<uint32_t>(nstripes);
-    const int variant = wgs_per_cu / 10;  // tens digit: 0 -> 24 temps, 1 -> 8 temps
-    wgs_per_cu %= 10;
-    const dim3 grid(std::min<uint32_t>(ntiles, cu_count(dev) * std::max(1, wgs_per_cu))), block(256);
-    if (variant == 1)
-        hipLaunchKernelGGL(bs_c5_encode_kernel<8>, grid, block, 0, static_cast<hipStream_t>(stream),
-                           static_cast<uint8_t*>(base), stripe_stride, static_cast<int>(frag_stride), ntiles, tps);
-    else
-        hipLaunchKernelGGL(bs_c5_encode_kernel<24>, grid, block, 0, static_cast<hipStream_t>(stream),
-                           static_cast<uint8_t*>(base), stripe_stride, static_cast<int>(frag_stride), ntiles, tps);
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
 }  // extern "C"

@@ -317,14 +317,14 @@ def tune():
     yield d.ecamd_tune
     for key, val in ((b"stream", 1), (b"stream_ch", 1), (b"stream_pf", 0), (b"stream_nib", 0),
                      (b"stream_order", 0), (b"stream_hybrid", 1), (b"multi_list", 1), (b"xor_wgs", 0),
-                     (b"stream_deep", 0)):
+                     (b"bitslice", 1)):
         d.ecamd_tune(key, val)
 
 
 @pytest.mark.parametrize("R,K", [(1, 1), (2, 4), (2, 5), (4, 10), (4, 13), (7, 16), (8, 20), (3, 21)])
 @pytest.mark.parametrize("variant", [(b"stream", 0), (b"stream", 1), (b"stream_pf", 1),
                                      (b"stream_nib", 1), (b"stream_ch", 2), (b"stream_order", 1),
-                                     (b"stream_hybrid", 0), (b"stream_deep", 1)])
+                                     (b"stream_hybrid", 0), (b"bitslice", 0)])
 def test_stream_kernel_variants(tune, R, K, variant):
     """Every gf16 kernel variant (the stream kernel and its tuning knobs, the first-version kernel,
     K = 21 falling back to it) against the numpy GF(2^16) reference on full 4 KiB tiles plus a

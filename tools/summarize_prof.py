@@ -69,6 +69,11 @@ def main():
     ap.add_argument("--stripes", type=int, default=256)
     ap.add_argument("--bench", default="", help="bench JSON log of the profiled command")
     ap.add_argument("--command", default="")
+    ap.add_argument("--algo-bytes", type=float, default=0,
+                    help="algorithmic bytes per launch of the windows' kernels (frac vs 8 TB/s)")
+    ap.add_argument("--window", action="append", default=[],
+                    help="label:kernel-substring:first:count -- stats over dispatches [first, "
+                         "first+count) of that kernel in dispatch order (repeatable)")
     args = ap.parse_args()
     g = os.path.join(ROOT, "gpurun_out")
     pre = f"prof_{{}}_{args.cfg}"
@@ -77,6 +82,7 @@ def main():
            "kernels": {}}
 
     tpath = find_csv(os.path.join(g, pre.format("trace")), "kernel_trace.csv")
+    win_pmc = None
     rows = trace_rows(tpath)
     by = defaultdict(list)
     for name, did, dur in rows:
@@ -96,6 +102,26 @@ def main():
                       "note": f"timed = dispatches {lo}..{lo + 2 * args.steps - 1} of this kernel"})
         out["kernels"][name] = d
 
+    # labelled windows (e.g. the steady-state launches of each C5 operation)
+    windows = []
+    for spec in args.window:
+        label, sub, first, count = spec.split(":")
+        windows.append((label, sub, int(first), int(count)))
+    out["windows"] = {}
+    for label, sub, first, count in windows:
+        for name, lst in by.items():
+            if sub in name:
+                sel = lst[first:first + count]
+                w = stats([x[1] for x in sel])
+                w["kernel"] = name
+                w["dispatch_ids"] = [sel[0][0], sel[-1][0]] if sel else []
+                if args.algo_bytes and sel:
+                    w["algo_bytes"] = args.algo_bytes
+                    w["achieved_GBps"] = round(args.algo_bytes / w["avg_ns"], 1)
+                    w["frac"] = round(args.algo_bytes / w["avg_ns"] / 8000, 4)
+                out["windows"][label] = w
+    win_pmc = {label: [] for label, *_ in windows}
+
     for tag in ("fetch", "write", "lds"):
         p = find_csv(os.path.join(g, pre.format(tag)), "counter_collection.csv")
         if not p:
@@ -104,6 +130,15 @@ def main():
         for r in csv.DictReader(open(p)):
             per[col(r, "Kernel_Name")][col(r, "Counter_Name")].append(
                 (int(col(r, "Dispatch_Id")), float(col(r, "Counter_Value"))))
+        for label, sub, first, count in windows:
+            for kern, cs in per.items():
+                if sub not in kern:
+                    continue
+                w = out["windows"].setdefault(label, {})
+                for cname, vals in cs.items():
+                    vv = sorted(vals)[first:first + count]
+                    if vv:
+                        w[cname] = statistics.mean(v for _, v in vv)
         for kern, cs in per.items():
             d = out["kernels"].setdefault(kern, {})
             for cname, vals in cs.items():
@@ -115,7 +150,7 @@ def main():
                 else:
                     sel = [v for _, v in vals]
                 d[cname] = statistics.mean(sel)
-    for kern, d in out["kernels"].items():
+    for kern, d in list(out["kernels"].items()) + list(out["windows"].items()):
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             rd = d["FETCH_SIZE"] * 1024 * 2   # gfx950: FETCH_SIZE = half the streamed bytes
             wr = d["WRITE_SIZE"] * 1024
