@@ -88,10 +88,12 @@ int ecamd_percall_device_plan(int ndev, const char *spec, int *devs, int max);
 /* Bitsliced GF(2^16) maps (host/bitslice.hpp): the XOR network built for an R x K matrix
  * (R <= 8, K <= 32, at most `cap` shared temporaries per input) evaluated on 32 words per input
  * (in: K x 32, out: R x 32; *ops = VALU ops of the network per tile), and the HIP source of the
- * kernel specialised to it (returns the source length; writes up to size-1 bytes + NUL). */
+ * kernel specialised to it, inputs loaded into registers (depth 0) or through a per-wave LDS ring
+ * of 2 or 4 inputs (returns the source length; writes up to size-1 bytes + NUL). */
 int ecamd_bitslice_eval(const int *coeff, int R, int K, int cap, const uint16_t *in, uint16_t *out,
                         int *ops);
-int64_t ecamd_bitslice_source(const int *coeff, int R, int K, int cap, char *buf, int64_t size);
+int64_t ecamd_bitslice_source(const int *coeff, int R, int K, int cap, int depth, char *buf,
+                              int64_t size);
 
 #ifdef __cplusplus
 }

@@ -55,7 +55,7 @@ def host():
         _proto(h, "ecamd_bitslice_eval", C.c_int,
                [IP, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, IP])
         _proto(h, "ecamd_bitslice_source", C.c_int64,
-               [IP, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int64])
+               [IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_int64])
         _proto(h, "ecamd_split_tables", C.c_int,
                [IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p])
         _host = h

@@ -179,6 +179,8 @@ struct Tuning {
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
+    Knob bitslice_depth{2}; //   inputs through a per-wave LDS ring 2 (default) / 4 deep, or straight
+                            //   into registers (0); tools/c5_prof.py C5_MODES A/B
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
@@ -238,7 +240,7 @@ struct ecamd_map {
 };
 
 namespace ecamd {
-hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, bool wait);
+hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st);
 }  // namespace ecamd
 
@@ -428,7 +430,7 @@ int64_t launch_bitslice(const ecamd_map* map, const ecamd_map::Pass& p, ApplyArg
         for (int j = 0; j < p.ncols; j++)
             sub[static_cast<size_t>(r) * p.ncols + j] =
                 map->coeff[static_cast<size_t>(p.row0 + r) * map->K + p.col0 + j];
-    hipFunction_t fn = bitslice_function(map->device, sub, a.nrows, p.ncols, mode == 2);
+    hipFunction_t fn = bitslice_function(map->device, sub, a.nrows, p.ncols, g_tune.bitslice_depth, mode == 2);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1122,6 +1124,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.multi_list = value;
     } else if (k == "bitslice") {
         g_tune.bitslice = value;
+    } else if (k == "bitslice_depth") {
+        g_tune.bitslice_depth = value >= 4 ? 4 : value >= 2 ? 2 : 0;
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
     } else if (k == "stream_order") {

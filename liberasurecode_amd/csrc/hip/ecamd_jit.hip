@@ -1,11 +1,12 @@
 // ecamd_jit.hip -- run-time specialised bitsliced GF(2^16) kernels (host/bitslice.hpp).
 //
 // The XOR network of a bitsliced map depends on every coefficient, so its kernel is generated for
-// the matrix and compiled at run time.  The compile runs in a child process (ecamd_jitc, next to
-// this library; hiprtc), never in this process: a GPU process that exits while a compile is in
+// the matrix and compiled at run time.  Both steps -- the network search (tens to hundreds of ms)
+// and the hiprtc compile (seconds) -- run in a child process (ecamd_jitc, next to this library),
+// never on a caller's thread or in this process: a GPU process that exits while a compile is in
 // flight simply abandons it, and hiprtc's runtime never shares an address space with the GPU
-// work.  Code objects land in a disk cache keyed by a hash of the source ($ECAMD_JIT_CACHE, else
-// /tmp/ecamd-jit-<uid>), so later processes load them at once.  Knob "bitslice": 1 (default)
+// work.  Code objects land in a disk cache ($ECAMD_JIT_CACHE, else /tmp/ecamd-jit-<uid>) keyed by
+// a hash of the request and of the generator itself, so later processes load them at once.  Knob "bitslice": 1 (default)
 // launches the LDS-table kernel until the code object is ready, 2 waits for it (tests, bench), 0
 // never uses the bitsliced form; ecamd_bitslice_wait() waits for every compile started so far.
 #include <hip/hip_runtime.h>
@@ -37,10 +38,12 @@ extern char** environ;
 namespace ecamd {
 namespace {
 
-// Temporaries per input: 40 fits the register file at 2 waves per SIMD for the C5 networks
-// (252 VGPRs, no scratch); a network that spills is rebuilt once with 16.
-constexpr int kCapFirst = 40;
-constexpr int kCapRetry = 16;
+// Shared temporaries per input, first choice first: 48 fits the register file at 2 waves per SIMD
+// for the C5 networks in the LDS-ring form (~250 VGPRs, no scratch; the register-load form holds
+// the next input's loads too and fits ~32); a network that spills (the compiler's schedule
+// decides, not the count alone) is rebuilt with the next.
+constexpr int kCaps[] = {48, 40, 32, 24, 16};
+constexpr int kNumCaps = static_cast<int>(sizeof(kCaps) / sizeof(kCaps[0]));
 
 std::string helper_path()
 {
@@ -90,7 +93,8 @@ bool read_file(const std::string& path, std::string& out)
 struct BsEntry {
     std::vector<int> coeff;
     int R = 0, K = 0;
-    int cap = 0;          // shared temporaries allowed in the network (fewer: fewer registers)
+    int depth = 0;        // bitslice_source: 0 register loads, 2 / 4 LDS ring
+    int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string co_path;  // cache file of the code object
     pid_t pid = -1;       // compiler child while running
     int state = 0;        // 0 compiling, 1 code object ready, -1 failed
@@ -102,12 +106,26 @@ struct BsEntry {
 std::mutex g_jit_mu;  // guards g_jit and every entry
 std::map<std::vector<int>, std::shared_ptr<BsEntry>> g_jit;
 
-// Generate the source for e.cap and start (or skip, when cached) its compile.  Caller holds the lock.
+// Identifies the generator: the sources it emits for a tiny map in both load modes, and the
+// search settings -- a changed generator never reuses an old cache entry.
+const std::string& generator_fingerprint()
+{
+    static std::string fp;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0, 1);
+        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + "trials=" + std::to_string(kBsTrials);
+    });
+    return fp;
+}
+
+// Start (or skip, when cached) the build of e's kernel at kCaps[e.cap_index].  Caller holds the lock.
 void start_compile(BsEntry& e)
 {
-    const std::string src = bitslice_source(bitslice_network(e.coeff, e.R, e.K, e.cap));
+    const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth);
     char name[32];
-    std::snprintf(name, sizeof(name), "%016llx", static_cast<unsigned long long>(fnv1a(src)));
+    std::snprintf(name, sizeof(name), "%016llx",
+                  static_cast<unsigned long long>(fnv1a(generator_fingerprint() + req)));
     const std::string base = cache_dir() + "/bs_" + name;
     e.co_path = base + ".co";
     e.pid = -1;
@@ -119,18 +137,18 @@ void start_compile(BsEntry& e)
     e.state = -1;
     const std::string helper = helper_path();
     if (helper.empty()) return;
-    const std::string src_path = base + ".hip";
+    const std::string req_path = base + ".req";
     {
-        const std::string tmp = src_path + ".tmp." + std::to_string(getpid());
+        const std::string tmp = req_path + ".tmp." + std::to_string(getpid());
         std::ofstream f(tmp);
-        f << src;
+        f << req;
         f.close();
-        if (!f || std::rename(tmp.c_str(), src_path.c_str()) != 0) return;
+        if (!f || std::rename(tmp.c_str(), req_path.c_str()) != 0) return;
     }
     posix_spawn_file_actions_t fa;
     posix_spawn_file_actions_init(&fa);
     posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);  // keep our stdout clean
-    const char* argv[] = {helper.c_str(), src_path.c_str(), e.co_path.c_str(), nullptr};
+    const char* argv[] = {helper.c_str(), req_path.c_str(), e.co_path.c_str(), nullptr};
     pid_t pid = -1;
     if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, const_cast<char* const*>(argv), environ) == 0) {
         e.pid = pid;
@@ -159,10 +177,11 @@ void poll_compile(BsEntry& e, bool wait)
 
 // Kernel for the R x K matrix on `dev`: nullptr while compiling (wait = false) or when the
 // bitsliced form is unavailable; starts the compile the first time the matrix is seen.
-hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, bool wait)
+hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
-    std::vector<int> key = {R, K};
+    depth = bitslice_depth(depth, K);
+    std::vector<int> key = {R, K, depth};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::lock_guard<std::mutex> lk(g_jit_mu);
     if (g_jit.size() >= 1024 && !g_jit.count(key)) g_jit.clear();  // bound; loaded modules stay valid
@@ -172,7 +191,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->coeff = coeff;
         slot->R = R;
         slot->K = K;
-        slot->cap = kCapFirst;
+        slot->depth = depth;
         start_compile(*slot);
     }
     BsEntry& e = *slot;
@@ -194,8 +213,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
             }
             (void)hipGetLastError();
         }
-        if (!fn && spill > 0 && e.cap > kCapRetry) {  // rebuild with fewer temporaries
-            e.cap = kCapRetry;
+        if (!fn && spill > 0 && e.cap_index + 1 < kNumCaps) {  // rebuild with fewer temporaries
+            e.cap_index++;
             e.fn.clear();
             start_compile(e);
             continue;

@@ -77,23 +77,56 @@ void share_terms(std::vector<std::vector<int>>& rows, std::vector<std::array<int
 
 }  // namespace
 
-BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap)
+BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap, int trials)
 {
     BitsliceNet net;
     net.R = R;
     net.K = K;
     net.inputs.resize(static_cast<size_t>(K));
     for (int j = 0; j < K; j++) {
-        auto& in = net.inputs[static_cast<size_t>(j)];
-        in.rows.assign(static_cast<size_t>(R) * 16, {});
+        std::vector<std::vector<int>> rows(static_cast<size_t>(R) * 16);
         for (int r = 0; r < R; r++) {
             uint16_t M[16];
             gf16_bitmatrix(coeff[static_cast<size_t>(r) * K + j], M);
             for (int p = 0; p < 16; p++)
                 for (int b = 0; b < 16; b++)
-                    if ((M[p] >> b) & 1) in.rows[static_cast<size_t>(r) * 16 + p].push_back(b);
+                    if ((M[p] >> b) & 1) rows[static_cast<size_t>(r) * 16 + p].push_back(b);
         }
-        share_terms(in.rows, in.temps, cap);
+        // The greedy is sensitive to its tie-breaks, which follow the plane labels: run it on
+        // `trials` relabelings (the first is the identity; the rest a fixed pseudo-random sequence,
+        // so the network stays a function of the matrix) and keep the cheapest.
+        auto& best = net.inputs[static_cast<size_t>(j)];
+        int best_ops = -1;
+        uint32_t rng = 0x9e3779b9u ^ static_cast<uint32_t>(j);
+        for (int t = 0; t < std::max(1, trials); t++) {
+            int perm[16];
+            for (int b = 0; b < 16; b++) perm[b] = b;
+            if (t)
+                for (int b = 15; b > 0; b--) {
+                    rng = rng * 1664525u + 1013904223u;
+                    std::swap(perm[b], perm[(rng >> 8) % static_cast<uint32_t>(b + 1)]);
+                }
+            BitsliceNet::Input cand;
+            cand.rows = rows;
+            for (auto& row : cand.rows) {
+                for (int& v : row) v = perm[v];
+                std::sort(row.begin(), row.end());
+            }
+            share_terms(cand.rows, cand.temps, cap);
+            int inv[16];
+            for (int b = 0; b < 16; b++) inv[perm[b]] = b;
+            auto back = [&](int v) { return v >= 0 && v < 16 ? inv[v] : v; };
+            for (auto& tm : cand.temps)
+                for (int& v : tm) v = back(v);
+            for (auto& row : cand.rows)
+                for (int& v : row) v = back(v);
+            int ops = static_cast<int>(cand.temps.size());
+            for (const auto& row : cand.rows) ops += static_cast<int>((row.size() + 1) / 2);
+            if (best_ops < 0 || ops < best_ops) {
+                best_ops = ops;
+                best = std::move(cand);
+            }
+        }
     }
     return net;
 }
@@ -189,27 +222,24 @@ __device__ __forceinline__ void tr16(u32 (&A)[16])
 
 }  // namespace
 
-std::string bitslice_source(const BitsliceNet& net)
+int bitslice_depth(int depth, int K)
 {
+    if (depth < 2) return 0;
+    int d = depth >= 4 ? 4 : 2;
+    while (d > 2 && d - 1 > K) d /= 2;  // prefetch reaches at most one tile ahead
+    return d;
+}
+
+std::string bitslice_source(const BitsliceNet& net, int depth)
+{
+    const int D = bitslice_depth(depth, net.K);
     std::ostringstream s;
     s << "// generated by liberasurecode_amd bitslice_source: " << net.R << " outputs x " << net.K
-      << " inputs, " << net.xor_ops() << " network ops per tile\n";
+      << " inputs, " << net.xor_ops() << " network ops per tile, "
+      << (D ? "LDS ring of " + std::to_string(D) + " inputs per wave" : std::string("register loads")) << "\n";
     s << kPrelude;
     s << "extern \"C\" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))\n"
-         "ecamd_bs_kernel(ecamd_bs_args a)\n{\n"
-         "    for (u32 t = blockIdx.x; t < a.ntiles; t += gridDim.x) {\n"
-         "        const u32 sl = t / a.tiles_per_stripe;\n"
-         "        const u32 s = a.stripe_list ? (u32)a.stripe_list[sl] : sl;\n"
-         "        const i32 off = (i32)(t - sl * a.tiles_per_stripe) * "
-      << kBsTile
-      << " + (i32)threadIdx.x * 16;\n"
-         "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
-         "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
-         "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
-         "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n"
-      << "        u32 acc[" << net.R << "][16];\n"
-      << "#pragma unroll\n        for (int r = 0; r < " << net.R
-      << "; r++)\n#pragma unroll\n            for (int p = 0; p < 16; p++) acc[r][p] = 0u;\n";
+         "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
     auto ref = [](int v) {
         char b[24];
         if (v < 16)
@@ -218,14 +248,10 @@ std::string bitslice_source(const BitsliceNet& net)
             std::snprintf(b, sizeof(b), "t%d", v);
         return std::string(b);
     };
-    for (int j = 0; j < net.K; j++) {
+    // the network of input j on P[16] (bit planes), accumulated into acc
+    auto network = [&](int j) {
         const auto& in = net.inputs[static_cast<size_t>(j)];
-        s << "        {  // input " << j << "\n            u32 P[16];\n"
-          << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
-          << "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
-          << "] + off + c * 4096, 0, 2);\n"
-          << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
-          << "            }\n            tr16(P);\n";
+        s << "            tr16(P);\n";
         for (size_t i = 0; i < in.temps.size(); i++) {
             const auto& t = in.temps[i];
             if (t[2] < 0)
@@ -245,20 +271,147 @@ std::string bitslice_source(const BitsliceNet& net)
                   << ref(terms[q + 1]) << ");\n";
             if (q < terms.size()) s << "            " << dst << " ^= " << ref(terms[q]) << ";\n";
         }
+    };
+    auto acc_init = [&]() {
+        s << "        u32 acc[" << net.R << "][16];\n"
+          << "#pragma unroll\n        for (int r = 0; r < " << net.R
+          << "; r++)\n#pragma unroll\n            for (int p = 0; p < 16; p++) acc[r][p] = 0u;\n";
+    };
+    auto outputs = [&](const char* rout, const char* off) {
+        s << "#pragma unroll\n        for (int r = 0; r < " << net.R
+          << "; r++) {\n"
+             "            tr16(acc[r]);\n"
+             "#pragma unroll\n"
+             "            for (int c = 0; c < 4; c++) {\n"
+             "                const v4u v = {acc[r][4 * c], acc[r][4 * c + 1], acc[r][4 * c + 2], acc[r][4 * c + 3]};\n"
+             "                __builtin_amdgcn_raw_buffer_store_b128(v, "
+          << rout << ", a.out_off[r] + " << off
+          << " + c * 4096, 0, 2);\n"
+             "            }\n"
+             "        }\n";
+    };
+    if (!D) {
+        s << "    for (u32 t = blockIdx.x; t < a.ntiles; t += gridDim.x) {\n"
+             "        const u32 sl = t / a.tiles_per_stripe;\n"
+             "        const u32 s = a.stripe_list ? (u32)a.stripe_list[sl] : sl;\n"
+             "        const i32 off = (i32)(t - sl * a.tiles_per_stripe) * "
+          << kBsTile
+          << " + (i32)threadIdx.x * 16;\n"
+             "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
+             "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n";
+        acc_init();
+        for (int j = 0; j < net.K; j++) {
+            s << "        {  // input " << j << "\n            u32 P[16];\n"
+              << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
+              << "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+              << "] + off + c * 4096, 0, 2);\n"
+              << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
+              << "            }\n";
+            network(j);
+            s << "        }\n";
+        }
+        outputs("rout", "off");
+        s << "    }\n}\n";
+        return s.str();
+    }
+    // LDS ring: each wave streams its 1 KiB share of the tile's four 4 KiB chunks of every input into
+    // a ring of D slots by LDS-DMA loads (no VGPRs), D - 1 inputs ahead of the network -- across the
+    // tile boundary too -- and reads its own 64 B per lane back (conflict-free ds_read_b128).  Loads
+    // return in order, so waiting until at most 4 (D - 1) vector-memory operations are outstanding
+    // retires the input about to be read whatever stores are in flight.  A slot is refilled only
+    // after the reads of its previous input have returned.  Past the last tile the prefetches go to a
+    // zero-length buffer (no memory traffic, still counted).
+    s << "    __shared__ __attribute__((aligned(16))) u8 ring[4 * " << D << " * 4096];\n"
+         "    typedef __attribute__((address_space(3))) u8 lds_u8;\n"
+         "    const u32 wring = (u32)(unsigned long)(lds_u8*)ring + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * "
+      << D * 4096
+      << "u;\n"
+         "    const u32 lane = (threadIdx.x & 63u) * 16u;\n"
+         "    u32 t = blockIdx.x;\n"
+         "    if (t >= a.ntiles) return;\n"
+         "    u32 sl = t / a.tiles_per_stripe;\n"
+         "    u32 s = a.stripe_list ? (u32)a.stripe_list[sl] : sl;\n"
+         "    i32 off = (i32)(t - sl * a.tiles_per_stripe) * "
+      << kBsTile
+      << " + (i32)threadIdx.x * 16;\n"
+         "    __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
+         "        (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
+         "    u32 base = 0;\n";
+    auto issue = [&](const char* rin, const std::string& voff, const std::string& slot) {
+        s << "#pragma unroll\n        for (int c = 0; c < 4; c++)\n"
+             "            __builtin_amdgcn_raw_ptr_buffer_load_lds("
+          << rin << ", (__attribute__((address_space(3))) void*)(unsigned long)(wring + ((" << slot
+          << ") & " << D - 1 << "u) * 4096u + c * 1024u), 16, " << voff << " + c * 4096, 0, 0, 2);\n";
+    };
+    for (int q = 0; q < D - 1; q++) issue("rin", "a.in_off[" + std::to_string(q) + "] + off", std::to_string(q));
+    s << "    for (;;) {\n"
+         "        const u32 t2 = t + gridDim.x;\n"
+         "        const bool more = t2 < a.ntiles;\n"
+         "        const u32 sl2 = more ? t2 / a.tiles_per_stripe : sl;\n"
+         "        const u32 s2 = more ? (a.stripe_list ? (u32)a.stripe_list[sl2] : sl2) : s;\n"
+         "        const i32 off2 = (i32)(t2 - sl2 * a.tiles_per_stripe) * "
+      << kBsTile
+      << " + (i32)threadIdx.x * 16;\n"
+         "        const __amdgpu_buffer_rsrc_t rin2 = __builtin_amdgcn_make_buffer_rsrc(\n"
+         "            (void*)(a.in_base + (i64)s2 * a.in_stride), 0, more ? (int)a.in_records : 0, 0x00020000);\n";
+    acc_init();
+    for (int j = 0; j < net.K; j++) {
+        const int jj = j + D - 1;
+        s << "        {  // input " << j << "\n";
+        if (jj < net.K)
+            issue("rin", "a.in_off[" + std::to_string(jj) + "] + off", "base + " + std::to_string(jj) + "u");
+        else
+            issue("rin2", "a.in_off[" + std::to_string(jj - net.K) + "] + off2", "base + " + std::to_string(jj) + "u");
+        s << "            asm volatile(\"s_waitcnt vmcnt(" << 4 * (D - 1) << ")\" ::: \"memory\");\n"
+          << "            const u32 rd = wring + ((base + " << j << "u) & " << D - 1 << "u) * 4096u + lane;\n"
+          << "            v4u q0, q1, q2, q3;\n"
+          << "            asm volatile(\"ds_read_b128 %0, %1\" : \"=v\"(q0) : \"v\"(rd) : \"memory\");\n"
+          << "            asm volatile(\"ds_read_b128 %0, %1 offset:1024\" : \"=v\"(q1) : \"v\"(rd) : \"memory\");\n"
+          << "            asm volatile(\"ds_read_b128 %0, %1 offset:2048\" : \"=v\"(q2) : \"v\"(rd) : \"memory\");\n"
+          << "            asm volatile(\"ds_read_b128 %0, %1 offset:3072\" : \"=v\"(q3) : \"v\"(rd) : \"memory\");\n"
+          << "            asm volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(q0), \"+v\"(q1), \"+v\"(q2), \"+v\"(q3));\n"
+          << "            u32 P[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],\n"
+          << "                         q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3]};\n";
+        network(j);
         s << "        }\n";
     }
-    s << "#pragma unroll\n        for (int r = 0; r < " << net.R
-      << "; r++) {\n"
-         "            tr16(acc[r]);\n"
-         "#pragma unroll\n"
-         "            for (int c = 0; c < 4; c++) {\n"
-         "                const v4u v = {acc[r][4 * c], acc[r][4 * c + 1], acc[r][4 * c + 2], acc[r][4 * c + 3]};\n"
-         "                __builtin_amdgcn_raw_buffer_store_b128(v, rout, a.out_off[r] + off + c * 4096, 0, 2);\n"
-         "            }\n"
-         "        }\n"
+    s << "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
+         "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n";
+    outputs("rout", "off");
+    s << "        if (!more) break;\n"
+         "        t = t2; sl = sl2; s = s2; off = off2; rin = rin2;\n"
+         "        base = (base + "
+      << net.K << "u) & " << D - 1
+      << "u;\n"
          "    }\n"
+         "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // no LDS-DMA outlives the workgroup\n"
          "}\n";
     return s.str();
+}
+
+std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth)
+{
+    std::ostringstream s;
+    s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
+    for (size_t i = 0; i < coeff.size(); i++) s << coeff[i] << ((i + 1) % static_cast<size_t>(K) ? " " : "\n");
+    return s.str();
+}
+
+bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
+                            int& depth)
+{
+    std::istringstream s(text);
+    std::string magic;
+    int version = 0;
+    if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version != 1) return false;
+    if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 48)
+        return false;
+    coeff.assign(static_cast<size_t>(R) * K, 0);
+    for (int& c : coeff)
+        if (!(s >> c) || c < 0 || c > 0xffff) return false;
+    return true;
 }
 
 }  // namespace ecamd

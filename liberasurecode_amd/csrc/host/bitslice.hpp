@@ -40,13 +40,23 @@ struct BitsliceNet {
     int xor_ops() const;  // VALU ops of the network (temps + 3-input accumulation)
 };
 
-BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap);
+// `trials` relabelings of the planes are tried per input and the cheapest network kept.
+constexpr int kBsTrials = 16;
+BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap, int trials = kBsTrials);
 
 // Evaluate the network on 32 words per input (host check of the construction).
 void bitslice_eval(const BitsliceNet& net, const uint16_t* in /* K x 32 */, uint16_t* out /* R x 32 */);
 
 // HIP source of `extern "C" __global__ void ecamd_bs_kernel(ecamd_bs_args)` for the network.
-std::string bitslice_source(const BitsliceNet& net);
+// depth 0: each input's 64 B per lane loaded straight into registers; 2 or 4: through a per-wave
+// LDS ring that many inputs deep, filled by LDS-DMA loads (bitslice_depth: the depth used for K).
+std::string bitslice_source(const BitsliceNet& net, int depth = 0);
+int bitslice_depth(int depth, int K);
+
+// A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
+std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth);
+bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
+                            int& depth);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

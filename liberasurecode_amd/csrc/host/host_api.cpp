@@ -222,11 +222,11 @@ int ecamd_bitslice_eval(const int* coeff, int R, int K, int cap, const uint16_t*
     return 0;
 }
 
-int64_t ecamd_bitslice_source(const int* coeff, int R, int K, int cap, char* buf, int64_t size)
+int64_t ecamd_bitslice_source(const int* coeff, int R, int K, int cap, int depth, char* buf, int64_t size)
 {
     if (!coeff || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK) return -1;
     std::vector<int> c(coeff, coeff + static_cast<size_t>(R) * K);
-    const std::string src = bitslice_source(bitslice_network(c, R, K, cap));
+    const std::string src = bitslice_source(bitslice_network(c, R, K, cap), depth);
     if (buf && size > 0) {
         const size_t n = std::min(static_cast<size_t>(size - 1), src.size());
         std::memcpy(buf, src.data(), n);

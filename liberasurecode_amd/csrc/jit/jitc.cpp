@@ -1,30 +1,58 @@
-// jitc.cpp -- ecamd_jitc: compiles one generated HIP kernel source to a gfx950 code object with
-// hiprtc, in its own process.  libecamd (hip/ecamd_jit.hip) starts it as a child process, so a
-// compile never shares a process with the GPU work and can outlive (or be abandoned by) its
-// parent harmlessly; the result is written to <out>.tmp.<pid> and renamed to <out>, so readers
-// only ever see a whole code object.  This program never touches the GPU.
+// jitc.cpp -- ecamd_jitc: builds the bitsliced kernel for one coefficient matrix (host/bitslice.cpp:
+// XOR network, then HIP source) and compiles it to a gfx950 code object with hiprtc, in its own
+// process.  libecamd (hip/ecamd_jit.hip) starts it as a child process, so neither the network
+// search nor the compile runs on a caller's thread or shares a process with the GPU work, and a
+// parent that exits abandons it harmlessly.  The code object is written to <out>.tmp.<pid> and
+// renamed to <out>, so readers only ever see a whole one; the source lands beside it as
+// <out minus .co>.hip for inspection.  This program never touches the GPU.
 //
-//   ecamd_jitc <source.hip> <out.co>      exit 0 on success
+//   ecamd_jitc <request> <out.co>      request: bitslice_request() text; exit 0 on success
 #include <hip/hiprtc.h>
-#include <dlfcn.h>
 #include <unistd.h>
 
 #include <cstdio>
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <vector>
+
+#include "bitslice.hpp"
+
+namespace {
+
+bool write_whole(const std::string& path, const std::string& bytes)
+{
+    const std::string tmp = path + ".tmp." + std::to_string(getpid());
+    {
+        std::ofstream out(tmp, std::ios::binary);
+        out.write(bytes.data(), static_cast<std::streamsize>(bytes.size()));
+        if (!out) return false;
+    }
+    return std::rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+}  // namespace
 
 int main(int argc, char** argv)
 {
     if (argc != 3) {
-        std::fprintf(stderr, "usage: %s <source.hip> <out.co>\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <request> <out.co>\n", argv[0]);
         return 2;
     }
     std::ifstream in(argv[1]);
     std::stringstream ss;
     ss << in.rdbuf();
-    const std::string src = ss.str();
-    if (src.empty()) return 2;
+    std::vector<int> coeff;
+    int R = 0, K = 0, cap = 0, depth = 0;
+    if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth)) {
+        std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
+        return 2;
+    }
+    const std::string src = ecamd::bitslice_source(ecamd::bitslice_network(coeff, R, K, cap), depth);
+    std::string out(argv[2]);
+    if (out.size() > 3 && out.compare(out.size() - 3, 3, ".co") == 0)
+        write_whole(out.substr(0, out.size() - 3) + ".hip", src);
+
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "ecamd_bitslice.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return 1;
@@ -42,11 +70,5 @@ int main(int argc, char** argv)
     std::string code(n, '\0');
     if (hiprtcGetCode(prog, &code[0]) != HIPRTC_SUCCESS) return 1;
     hiprtcDestroyProgram(&prog);
-    const std::string tmp = std::string(argv[2]) + ".tmp." + std::to_string(getpid());
-    {
-        std::ofstream out(tmp, std::ios::binary);
-        out.write(code.data(), static_cast<std::streamsize>(code.size()));
-        if (!out) return 1;
-    }
-    return std::rename(tmp.c_str(), argv[2]) == 0 ? 0 : 1;
+    return write_whole(out, code) ? 0 : 1;
 }

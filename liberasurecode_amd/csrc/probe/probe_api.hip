@@ -175,6 +175,10 @@ int ecamd_probe_valu(int op, int wgs_per_cu, int iters, void* stream)
     case 4: hipLaunchKernelGGL(valu_probe_kernel<4>, grid, block, 0, st, iters, 0x9e37u, sink); break;
     case 5: hipLaunchKernelGGL(valu_probe_kernel<5>, grid, block, 0, st, iters, 0x9e37u, sink); break;
     case 6: hipLaunchKernelGGL(valu_probe_kernel<6>, grid, block, 0, st, iters, 0x9e37u, sink); break;
+    case 8: hipLaunchKernelGGL(valu_probe_kernel<8>, grid, block, 0, st, iters, 0x9e37u, sink); break;
+    case 9: hipLaunchKernelGGL(valu_probe_kernel<9>, grid, block, 0, st, iters, 0x9e37u, sink); break;
+    case 10: hipLaunchKernelGGL(valu_probe_kernel<10>, grid, block, 0, st, iters, 0x9e37u, sink); break;
+    case 11: hipLaunchKernelGGL(valu_probe_kernel<11>, grid, block, 0, st, iters, 0x9e37u, sink); break;
     default: hipLaunchKernelGGL(valu_probe_kernel<7>, grid, block, 0, st, iters, 0x9e37u, sink); break;
     }
     HIP_TRY(hipGetLastError());

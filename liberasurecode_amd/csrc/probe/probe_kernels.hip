@@ -220,7 +220,9 @@ namespace ecamd {
 // instruction form (OP), so the SIMD sees back-to-back independent VALU work from every wave;
 // cycles per wave-instruction = wall cycles x waves per SIMD / (iters x 8).  OP: 0 v_xor_b32,
 // 1 v_bitop3_b32 (XOR3), 2 v_lshlrev_b32_sdwa (byte select), 3 v_bfe_u32, 4 v_and_b32,
-// 5 v_perm_b32, 6 v_lshl_or_b32, 7 ds_read_b128 from a 16-entry table (conflict-free).
+// 5 v_perm_b32, 6 v_lshl_or_b32, 7 ds_read_b128 from a 16-entry table (conflict-free),
+// 8 v_bfi_b32 (SGPR mask), 9 v_lshrrev_b32, 10 v_bitop3_b32 0xCA (select, SGPR mask),
+// 11 v_alignbit_b32.
 template <int OP>
 __global__ void __launch_bounds__(256) valu_probe_kernel(int iters, uint32_t seed, uint32_t* sink)
 {
@@ -251,6 +253,14 @@ __global__ void __launch_bounds__(256) valu_probe_kernel(int iters, uint32_t see
                 asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a[i]), "v"(k), "v"(a[(i + 3) & 7]));
             } else if constexpr (OP == 6) {
                 asm volatile("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(r) : "v"(a[i]), "v"(k));
+            } else if constexpr (OP == 8) {
+                asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(k), "v"(a[i]), "v"(a[(i + 3) & 7]));
+            } else if constexpr (OP == 9) {
+                asm volatile("v_lshrrev_b32 %0, 4, %1" : "=v"(r) : "v"(a[i]));
+            } else if constexpr (OP == 10) {
+                asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(k), "v"(a[i]), "v"(a[(i + 3) & 7]));
+            } else if constexpr (OP == 11) {
+                asm volatile("v_alignbit_b32 %0, %1, %2, 4" : "=v"(r) : "v"(a[i]), "v"(a[(i + 3) & 7]));
             } else {
                 uint4 v;
                 asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((a[i] & 15u) * 16u));
@@ -273,5 +283,9 @@ template __global__ void valu_probe_kernel<4>(int, uint32_t, uint32_t*);
 template __global__ void valu_probe_kernel<5>(int, uint32_t, uint32_t*);
 template __global__ void valu_probe_kernel<6>(int, uint32_t, uint32_t*);
 template __global__ void valu_probe_kernel<7>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<8>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<9>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<10>(int, uint32_t, uint32_t*);
+template __global__ void valu_probe_kernel<11>(int, uint32_t, uint32_t*);
 
 }  // namespace ecamd

@@ -57,12 +57,15 @@ def test_shared_pairs_cut_the_work():
 
 
 @pytest.mark.skipif(not shutil.which("/opt/rocm/bin/hipcc"), reason="needs hipcc")
-def test_generated_source_compiles_for_gfx950(tmp_path):
+@pytest.mark.parametrize("depth,cap", [(0, 32), (4, 40)])
+def test_generated_source_compiles_for_gfx950(tmp_path, depth, cap):
+    """C5 encode: the register-load form fits at cap 32, the LDS-ring form (fewer live registers) at
+    40; the JIT steps down through its caps when the compiler spills (hip/ecamd_jit.hip)."""
     G = orc.generator(20, 8)
     h = _lib.host()
-    n = h.ecamd_bitslice_source(_lib.ints(G[400:]), 8, 20, 24, None, 0)
+    n = h.ecamd_bitslice_source(_lib.ints(G[400:]), 8, 20, cap, depth, None, 0)
     buf = C.create_string_buffer(n + 1)
-    h.ecamd_bitslice_source(_lib.ints(G[400:]), 8, 20, 24, buf, n + 1)
+    h.ecamd_bitslice_source(_lib.ints(G[400:]), 8, 20, cap, depth, buf, n + 1)
     src = tmp_path / "bs.hip"
     src.write_text("#include <hip/hip_runtime.h>\n" + buf.value.decode())
     out = tmp_path / "bs.s"
@@ -72,3 +75,29 @@ def test_generated_source_compiles_for_gfx950(tmp_path):
     asm = out.read_text()
     assert "ScratchSize: 0" in asm          # the network fits the registers: no spills
     assert "Occupancy: 2" in asm            # 2 waves per SIMD
+    if depth:
+        assert " lds" in asm and "ds_read_b128" in asm   # LDS-DMA ring
+
+
+JITC = os.path.join(os.path.dirname(_lib.__file__), "lib", "ecamd_jitc")
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs hiprtc")
+def test_jitc_builds_a_request(tmp_path):
+    """The child-process compiler (csrc/jit/jitc.cpp) libecamd starts for each new matrix: the
+    network search and the hiprtc compile both run there; the code object appears whole."""
+    G = orc.generator(12, 5)
+    req = tmp_path / "bs.req"
+    rows = [" ".join(str(c) for c in G[12 * 12 + 12 * r:12 * 12 + 12 * (r + 1)]) for r in range(5)]
+    req.write_text("ecamd-bitslice-request 1\n5 12 40 0\n" + "\n".join(rows) + "\n")
+    out = tmp_path / "bs.co"
+    r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.read_bytes()[:4] == b"\x7fELF"
+    assert "5 outputs x 12 inputs" in (tmp_path / "bs.hip").read_text()
+    assert not [p for p in os.listdir(tmp_path) if ".tmp." in p]
+    bad = tmp_path / "bad.req"
+    for text in ("nonsense\n", "ecamd-bitslice-request 1\n9 12 40 0\n", "ecamd-bitslice-request 1\n1 1 40 0\n70000\n"):
+        bad.write_text(text)
+        assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2
+    assert not (tmp_path / "bad.co").exists()

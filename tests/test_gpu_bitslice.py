@@ -4,7 +4,10 @@ host/bitslice.cpp) against the CPU oracle, bit-exact.
 Covers encode (C5 shape: liberasurecode_rs_vand_encode, src/builtin/rs_vand/liberasurecode_rs_vand.c:399-410),
 decode / reconstruct of 5..8 lost fragments (:426-481, :483-558), fragments with a tail that is
 not a whole 16 KiB tile (the tail runs through the LDS-table kernel), heterogeneous batches over
-stripe lists, and the knob that turns the bitsliced form off (same bytes)."""
+stripe lists, and the knob that turns the bitsliced form off (same bytes).  Every test runs with
+the inputs loaded straight into registers (bitslice_depth 0) and through the per-wave LDS-DMA ring
+(2 and 4 inputs deep); batches with many more tiles than workgroups exercise the ring's prefetch
+across tile boundaries and its drain after the last tile."""
 import numpy as np
 import pytest
 
@@ -16,12 +19,17 @@ from liberasurecode_amd import device as D
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def sync_compile():
+@pytest.fixture(autouse=True, params=[0, 2, 4], ids=["regs", "ring2", "ring4"])
+def sync_compile(request):
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)  # wait for the compile: every launch below takes the JIT kernel
+    d.ecamd_tune(b"bitslice_depth", request.param)
     yield d
     d.ecamd_tune(b"bitslice", 1)
+    d.ecamd_tune(b"bitslice_depth", DEFAULT_DEPTH)
+
+
+DEFAULT_DEPTH = 2
 
 
 def test_hiprtc_available():
@@ -89,3 +97,32 @@ def test_knob_off_gives_the_same_bytes(sync_compile):
     lay.fill_splitmix(nfrags=k, stripe0=3)
     D.rs_encode(k, m, lay)
     assert (a == want).all() and (lay.download_stripes() == want).all()
+
+
+@pytest.mark.parametrize("k,m,lost", [(20, 8, None), (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]), (3, 5, None),
+                                      (1, 8, None)])
+def test_many_tiles_per_workgroup(sync_compile, k, m, lost):
+    """ntiles >> workgroups (2 per CU): the same bytes as the LDS-table kernels, which the tests
+    above pin to the oracle.  k = 1 and 3 take the shallower ring (prefetch stays within one tile
+    ahead)."""
+    bs, S = 1 << 20, 48
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix(nfrags=k if lost is None else k + m, stripe0=11)
+    if lost is not None:
+        sync_compile.ecamd_tune(b"bitslice", 0)
+        D.rs_encode(k, m, lay)
+    ref = None
+    for mode in (0, 2):
+        sync_compile.ecamd_tune(b"bitslice", mode)
+        if lost is None:
+            D.rs_encode(k, m, lay)
+        else:
+            D.rs_decode(k, m, lost, lay)
+        got = lay.download_stripes()
+        if ref is None:
+            ref = got
+            host = got.copy()  # the next pass must rewrite these slots itself
+            host[:, list(range(k, k + m)) if lost is None else lost] = 0x77
+            lay.upload_stripes(host)
+    assert (got == ref).all()
+    assert _lib.dev().ecamd_bitslice_wait() == 0

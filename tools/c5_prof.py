@@ -5,7 +5,8 @@ order: 30 encodes, 30 rebuilds of data {0..7}, 30 rebuilds of the mixed pattern
 {0,2,4,6,20,22,24,26}; then the same 90 launches on the LDS-table kernels (bitslice = 0).  Each
 run of 30 is one kernel (ecamd_bs_kernel / gf16_hybrid_kernel<5>) in dispatch order, so the
 summary takes launches 10..29 of each run as the steady state (the clock settles over the first
-few launches of a new mix).  Prints the HIP-event rate of each steady window too."""
+few launches of a new mix).  Prints the HIP-event rate of each steady window too.
+C5_MODES="2:0,2:4,0:0" picks other (bitslice, bitslice_depth) sequences, e.g. for A/B runs."""
 import json
 import os
 import sys
@@ -22,6 +23,7 @@ PATTERNS = {"rebuild8_data": list(range(8)), "rebuild8_mixed": [0, 2, 4, 6, 20, 
 
 
 def main(n=30, skip=10):
+    modes = [tuple(int(x) for x in m.split(":")) for m in os.environ.get("C5_MODES", "").split(",") if m]
     d = _lib.dev()
     lay = D.Layout.alloc(K + M, F, S)
     st = D.Stream()
@@ -30,14 +32,21 @@ def main(n=30, skip=10):
     D.rs_encode(K, M, lay, stream=st)
     # compile every bitsliced network before the profiled launches
     d.ecamd_tune(b"bitslice", 2)
+    for _, depth in modes:
+        d.ecamd_tune(b"bitslice_depth", depth)
+        D.rs_encode(K, M, lay, stream=st)
+        for pat in PATTERNS.values():
+            D.rs_decode(K, M, pat, lay, stream=st)
     D.rs_encode(K, M, lay, stream=st)
     for pat in PATTERNS.values():
         D.rs_decode(K, M, pat, lay, stream=st)
     st.synchronize()
     assert d.ecamd_bitslice_wait() == 0
     algo = S * (K + M) * F
-    for mode in (2, 0):
+    for mode, depth in modes or [(2, None), (0, None)]:
         d.ecamd_tune(b"bitslice", mode)
+        if depth is not None:
+            d.ecamd_tune(b"bitslice_depth", depth)
         ops = [("encode", lambda: D.rs_encode(K, M, lay, stream=st))]
         ops += [(name, (lambda p: lambda: D.rs_decode(K, M, p, lay, stream=st))(p)) for name, p in PATTERNS.items()]
         for name, fn in ops:
@@ -49,7 +58,7 @@ def main(n=30, skip=10):
             st.synchronize()
             ms = [ev[i].elapsed_ms(ev[i + 1]) for i in range(skip, n)]
             avg = sum(ms) / len(ms)
-            print(json.dumps({"kernel": "bitslice" if mode else "lds", "op": name,
+            print(json.dumps({"kernel": "bitslice" if mode else "lds", "depth": depth, "op": name,
                               "steady_ms": round(avg, 4), "TBps": round(algo / avg / 1e9, 3),
                               "frac": round(algo / avg / 1e9 / 8, 4)}), flush=True)
     d.ecamd_tune(b"bitslice", 1)

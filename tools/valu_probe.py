@@ -14,7 +14,8 @@ from liberasurecode_amd import _lib  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
 NAMES = ["v_xor_b32", "v_bitop3_b32", "v_lshlrev_b32_sdwa", "v_bfe_u32", "v_and_b32", "v_perm_b32",
-         "v_lshl_or_b32", "ds_read_b128+wait"]
+         "v_lshl_or_b32", "ds_read_b128+wait", "v_bfi_b32", "v_lshrrev_b32", "v_bitop3_b32 0xca",
+         "v_alignbit_b32"]
 
 
 def main(iters=4096):
@@ -23,7 +24,7 @@ def main(iters=4096):
     st = D.Stream()
     a, b = D.Event(), D.Event()
     base = None
-    for wpc in (4, 8):
+    for wpc in (2, 4, 8):
         for op, name in enumerate(NAMES):
             _lib.check(p.ecamd_probe_valu(op, wpc, iters, st.handle), "probe")
             a.record(st)
