@@ -17,6 +17,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -97,14 +98,27 @@ struct BsEntry {
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string co_path;  // cache file of the code object
     pid_t pid = -1;       // compiler child while running
-    int state = 0;        // 0 compiling, 1 code object ready, -1 failed
+    int state = 0;        // 0 compiling, 2 waiting for a compiler slot, 1 code object ready, -1 failed
     std::string code;
     std::map<int, hipFunction_t> fn;  // per device; nullptr: unusable there
     std::vector<hipModule_t> modules;
 };
 
-std::mutex g_jit_mu;  // guards g_jit and every entry
+std::mutex g_jit_mu;  // guards g_jit, g_running and every entry
 std::map<std::vector<int>, std::shared_ptr<BsEntry>> g_jit;
+std::vector<std::shared_ptr<BsEntry>> g_running;  // entries whose compiler child runs
+
+// Compiler children at once ($ECAMD_JIT_JOBS, default 2): a burst of new erasure patterns queues
+// rather than loading the host with one compile per pattern.
+size_t max_jobs()
+{
+    static size_t n = [] {
+        const char* env = std::getenv("ECAMD_JIT_JOBS");
+        const int v = env ? std::atoi(env) : 0;
+        return static_cast<size_t>(v >= 1 && v <= 64 ? v : 2);
+    }();
+    return n;
+}
 
 // Identifies the generator: the sources it emits for a tiny map in both load modes, and the
 // search settings -- a changed generator never reuses an old cache entry.
@@ -119,9 +133,11 @@ const std::string& generator_fingerprint()
     return fp;
 }
 
-// Start (or skip, when cached) the build of e's kernel at kCaps[e.cap_index].  Caller holds the lock.
-void start_compile(BsEntry& e)
+// Start (or skip, when cached) the build of e's kernel at kCaps[e.cap_index]; queue it (state 2)
+// while max_jobs() compilers run, unless `force`.  Caller holds the lock.
+void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
+    BsEntry& e = *ep;
     const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
@@ -137,6 +153,10 @@ void start_compile(BsEntry& e)
     e.state = -1;
     const std::string helper = helper_path();
     if (helper.empty()) return;
+    if (!force && g_running.size() >= max_jobs()) {
+        e.state = 2;
+        return;
+    }
     const std::string req_path = base + ".req";
     {
         const std::string tmp = req_path + ".tmp." + std::to_string(getpid());
@@ -153,13 +173,17 @@ void start_compile(BsEntry& e)
     if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, const_cast<char* const*>(argv), environ) == 0) {
         e.pid = pid;
         e.state = 0;
+        g_running.push_back(ep);
     }
     posix_spawn_file_actions_destroy(&fa);
 }
 
-// Advance a compiling entry (reap the child; block when `wait`).  Caller holds the lock.
-void poll_compile(BsEntry& e, bool wait)
+// Advance an entry: reap its compiler child (block when `wait`), or start a queued compile when a
+// slot is free (or at once when `wait`).  Caller holds the lock.
+void poll_compile(const std::shared_ptr<BsEntry>& ep, bool wait)
 {
+    BsEntry& e = *ep;
+    if (e.state == 2) start_compile(ep, wait);
     if (e.state != 0) return;
     int status = 0;
     pid_t r;
@@ -169,6 +193,7 @@ void poll_compile(BsEntry& e, bool wait)
     if (r == 0) return;  // still running
     const bool ok = r == e.pid && WIFEXITED(status) && WEXITSTATUS(status) == 0;
     e.pid = -1;
+    g_running.erase(std::remove(g_running.begin(), g_running.end(), ep), g_running.end());
     // a child reaped elsewhere (r < 0) may still have produced the file
     e.state = ((ok || r < 0) && read_file(e.co_path, e.code)) ? 1 : -1;
 }
@@ -184,7 +209,14 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     std::vector<int> key = {R, K, depth};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::lock_guard<std::mutex> lk(g_jit_mu);
-    if (g_jit.size() >= 1024 && !g_jit.count(key)) g_jit.clear();  // bound; loaded modules stay valid
+    for (size_t i = 0; i < g_running.size();) {  // reap finished compilers, freeing their slots
+        const auto ep = g_running[i];
+        poll_compile(ep, false);
+        if (ep->state == 0) i++;
+    }
+    if (g_jit.size() >= 1024 && !g_jit.count(key))  // bound; loaded modules stay valid
+        for (auto it = g_jit.begin(); it != g_jit.end();)
+            it = it->second->state == 0 ? std::next(it) : g_jit.erase(it);  // children stay reapable
     auto& slot = g_jit[key];
     if (!slot) {
         slot = std::make_shared<BsEntry>();
@@ -192,14 +224,15 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->R = R;
         slot->K = K;
         slot->depth = depth;
-        start_compile(*slot);
+        start_compile(slot, wait);
     }
-    BsEntry& e = *slot;
+    const std::shared_ptr<BsEntry> ep = slot;
+    BsEntry& e = *ep;
     for (;;) {
         auto it = e.fn.find(dev);
         if (it != e.fn.end()) return it->second;
-        poll_compile(e, wait);
-        if (e.state == 0) return nullptr;
+        poll_compile(ep, wait);
+        if (e.state == 0 || e.state == 2) return nullptr;
         hipFunction_t fn = nullptr;
         int spill = 0;
         if (e.state == 1) {
@@ -216,7 +249,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         if (!fn && spill > 0 && e.cap_index + 1 < kNumCaps) {  // rebuild with fewer temporaries
             e.cap_index++;
             e.fn.clear();
-            start_compile(e);
+            start_compile(ep, wait);
             continue;
         }
         e.fn[dev] = fn;
@@ -242,7 +275,7 @@ extern "C" int ecamd_bitslice_wait(void)
     std::lock_guard<std::mutex> lk(ecamd::g_jit_mu);
     int failed = 0;
     for (auto& kv : ecamd::g_jit) {
-        ecamd::poll_compile(*kv.second, true);
+        ecamd::poll_compile(kv.second, true);  // starts queued compiles too
         if (kv.second->state != 1) failed++;
     }
     return failed;

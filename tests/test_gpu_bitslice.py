@@ -126,3 +126,23 @@ def test_many_tiles_per_workgroup(sync_compile, k, m, lost):
             lay.upload_stripes(host)
     assert (got == ref).all()
     assert _lib.dev().ecamd_bitslice_wait() == 0
+
+
+def test_background_compiles_queue(sync_compile):
+    """Knob 1 (the default): new matrices run on the LDS tables while at most ECAMD_JIT_JOBS (2)
+    compiler children build their kernels, the rest queued; every result is exact throughout, and
+    once the queue has drained every pass takes the bitsliced kernel -- still exact."""
+    k, m, bs, S = 13, 7, 65536, 2
+    lay, want = _batch(k, m, bs, S, seed=21)
+    pats = [[0, 1, 2, 3, 4, 5, 6], [1, 2, 3, 4, 5, 6, 7], [2, 3, 4, 5, 6, 7, 8], [3, 4, 5, 6, 7, 8, 9],
+            [4, 5, 6, 7, 8, 9, 10], [0, 2, 4, 6, 13, 15, 17]]
+    sync_compile.ecamd_tune(b"bitslice", 1)
+    for rnd in range(2):
+        for p in pats:
+            host = want.copy()
+            host[:, p] = 0xC3
+            lay.upload_stripes(host)
+            D.rs_decode(k, m, p, lay)
+            assert (lay.download_stripes() == want).all(), (rnd, p)
+        if rnd == 0:
+            assert _lib.dev().ecamd_bitslice_wait() == 0
