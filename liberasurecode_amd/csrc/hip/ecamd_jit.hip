@@ -39,12 +39,25 @@ extern char** environ;
 namespace ecamd {
 namespace {
 
-// Shared temporaries per input, first choice first: 48 fits the register file at 2 waves per SIMD
-// for the C5 networks in the LDS-ring form (~250 VGPRs, no scratch; the register-load form holds
-// the next input's loads too and fits ~32); a network that spills (the compiler's schedule
-// decides, not the count alone) is rebuilt with the next.
-constexpr int kCaps[] = {48, 40, 32, 24, 16};
+// Shared temporaries per input, first choice first: 64 fits the register file at 2 waves per SIMD
+// for the C5 encode and decode networks in the LDS-ring form (225-245 VGPRs, no scratch: each
+// temporary is computed right before its first use); a network that spills (the compiler's
+// schedule decides, not the count alone) is rebuilt with the next.
+constexpr int kCaps[] = {64, 48, 32, 16};
 constexpr int kNumCaps = static_cast<int>(sizeof(kCaps) / sizeof(kCaps[0]));
+
+// First cap to try: the largest not above $ECAMD_JIT_CAP_MAX (A/B experiments), else kCaps[0].
+int first_cap_index()
+{
+    static const int idx = [] {
+        const char* env = std::getenv("ECAMD_JIT_CAP_MAX");
+        const int v = env ? std::atoi(env) : 0;
+        int i = 0;
+        while (v > 0 && i + 1 < kNumCaps && kCaps[i] > v) i++;
+        return i;
+    }();
+    return idx;
+}
 
 std::string helper_path()
 {
@@ -224,6 +237,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->R = R;
         slot->K = K;
         slot->depth = depth;
+        slot->cap_index = first_cap_index();
         start_compile(slot, wait);
     }
     const std::shared_ptr<BsEntry> ep = slot;

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <sstream>
 
 #include "gf16.hpp"
@@ -30,7 +31,7 @@ namespace {
 // saves at least one op and fewer than `cap` temporaries exist.  Deterministic in the matrix.
 void share_terms(std::vector<std::vector<int>>& rows, std::vector<std::array<int, 3>>& temps, int cap)
 {
-    constexpr int V = 64;  // variable ids < 16 + cap <= 64
+    constexpr int V = 80;  // variable ids < 16 + cap <= 80
     std::vector<int> c2(V * V), c3(V * V * V);
     std::vector<int> touched;
     int nvar = 16;
@@ -230,7 +231,7 @@ int bitslice_depth(int depth, int K)
     return d;
 }
 
-std::string bitslice_source(const BitsliceNet& net, int depth)
+std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle style)
 {
     const int D = bitslice_depth(depth, net.K);
     std::ostringstream s;
@@ -252,17 +253,34 @@ std::string bitslice_source(const BitsliceNet& net, int depth)
     auto network = [&](int j) {
         const auto& in = net.inputs[static_cast<size_t>(j)];
         s << "            tr16(P);\n";
-        for (size_t i = 0; i < in.temps.size(); i++) {
-            const auto& t = in.temps[i];
+        // each temporary is computed right before its first use, so it lives no longer than needed
+        std::vector<char> done(in.temps.size(), 0);
+        if (!style.lazy_temps)
+            for (size_t i = 0; i < in.temps.size(); i++) {
+                const auto& t = in.temps[i];
+                done[i] = 1;
+                if (t[2] < 0)
+                    s << "            const u32 t" << 16 + i << " = " << ref(t[0]) << " ^ " << ref(t[1]) << ";\n";
+                else
+                    s << "            const u32 t" << 16 + i << " = x3(" << ref(t[0]) << ", " << ref(t[1]) << ", "
+                      << ref(t[2]) << ");\n";
+            }
+        std::function<void(int)> need = [&](int v) {
+            if (v < 16 || done[static_cast<size_t>(v - 16)]) return;
+            const auto& t = in.temps[static_cast<size_t>(v - 16)];
+            for (int u : t)
+                if (u >= 0) need(u);
+            done[static_cast<size_t>(v - 16)] = 1;
             if (t[2] < 0)
-                s << "            const u32 t" << 16 + i << " = " << ref(t[0]) << " ^ " << ref(t[1]) << ";\n";
+                s << "            const u32 t" << v << " = " << ref(t[0]) << " ^ " << ref(t[1]) << ";\n";
             else
-                s << "            const u32 t" << 16 + i << " = x3(" << ref(t[0]) << ", " << ref(t[1]) << ", "
+                s << "            const u32 t" << v << " = x3(" << ref(t[0]) << ", " << ref(t[1]) << ", "
                   << ref(t[2]) << ");\n";
-        }
+        };
         for (size_t i = 0; i < in.rows.size(); i++) {
             const auto& terms = in.rows[i];
             if (terms.empty()) continue;
+            for (int v : terms) need(v);
             char dst[32];
             std::snprintf(dst, sizeof(dst), "acc[%zu][%zu]", i / 16, 15 - i % 16);
             size_t q = 0;
@@ -375,6 +393,9 @@ std::string bitslice_source(const BitsliceNet& net, int depth)
           << "            u32 P[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],\n"
           << "                         q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3]};\n";
         network(j);
+        // optional scheduling barrier between inputs (style.input_barrier): measured neutral once
+        // temporaries are computed lazily (profiles/r02_c5_experiments.log, tools/c5_ab.sh)
+        if (style.input_barrier) s << "            __builtin_amdgcn_sched_barrier(0);\n";
         s << "        }\n";
     }
     s << "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
@@ -406,7 +427,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     std::string magic;
     int version = 0;
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version != 1) return false;
-    if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 48)
+    if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 64)
         return false;
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)

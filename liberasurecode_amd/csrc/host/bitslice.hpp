@@ -50,7 +50,14 @@ void bitslice_eval(const BitsliceNet& net, const uint16_t* in /* K x 32 */, uint
 // HIP source of `extern "C" __global__ void ecamd_bs_kernel(ecamd_bs_args)` for the network.
 // depth 0: each input's 64 B per lane loaded straight into registers; 2 or 4: through a per-wave
 // LDS ring that many inputs deep, filled by LDS-DMA loads (bitslice_depth: the depth used for K).
-std::string bitslice_source(const BitsliceNet& net, int depth = 0);
+// Emission choices (A/B experiments through ecamd_jitc's environment; defaults are the product's):
+// temporaries computed right before first use (lazy) or all up front; a scheduling barrier after
+// each input's network in the LDS-ring form.
+struct BitsliceStyle {
+    bool lazy_temps = true;
+    bool input_barrier = false;
+};
+std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
 int bitslice_depth(int depth, int K);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.

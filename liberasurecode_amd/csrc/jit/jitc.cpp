@@ -11,6 +11,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -48,7 +49,10 @@ int main(int argc, char** argv)
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
-    const std::string src = ecamd::bitslice_source(ecamd::bitslice_network(coeff, R, K, cap), depth);
+    ecamd::BitsliceStyle style;  // experiments only: the parent's cache key does not see these
+    if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
+    if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
+    const std::string src = ecamd::bitslice_source(ecamd::bitslice_network(coeff, R, K, cap), depth, style);
     std::string out(argv[2]);
     if (out.size() > 3 && out.compare(out.size() - 3, 3, ".co") == 0)
         write_whole(out.substr(0, out.size() - 3) + ".hip", src);
