@@ -10,5 +10,6 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_trace_
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/prof_fetch_c5" -o run --output-format csv -- $B > gpurun_out/prof_fetch_c5.log 2>&1 || { echo "FETCH FAILED rc=$?"; tail -20 gpurun_out/prof_fetch_c5.log; exit 1; }
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/prof_write_c5" -o run --output-format csv -- $B > gpurun_out/prof_write_c5.log 2>&1 || { echo "WRITE FAILED rc=$?"; tail -20 gpurun_out/prof_write_c5.log; exit 1; }
 timeout -k 10 200 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace -d "$R/gpurun_out/prof_lds_c5" -o run --output-format csv -- $B > gpurun_out/prof_lds_c5.log 2>&1 || { echo "LDS FAILED rc=$?"; tail -20 gpurun_out/prof_lds_c5.log; exit 1; }
+timeout -k 10 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_IFETCH SQ_INSTS_VMEM SQ_INSTS_SALU --kernel-trace -d "$R/gpurun_out/prof_stall_c5" -o run --output-format csv -- $B > gpurun_out/prof_stall_c5.log 2>&1 || { echo "STALL FAILED rc=$?"; tail -20 gpurun_out/prof_stall_c5.log; exit 1; }
 grep '^{' gpurun_out/prof_trace_c5.log
 echo PROF_C5_OK

@@ -122,7 +122,7 @@ def main():
                 out["windows"][label] = w
     win_pmc = {label: [] for label, *_ in windows}
 
-    for tag in ("fetch", "write", "lds"):
+    for tag in ("fetch", "write", "lds", "stall"):
         p = find_csv(os.path.join(g, pre.format(tag)), "counter_collection.csv")
         if not p:
             continue
@@ -160,6 +160,11 @@ def main():
             ns = d.get("timed_avg_ns") or d.get("avg_ns")
             if ns:
                 d["hbm_GBps"] = round((rd + wr) / ns, 1)
+        if d.get("SQ_WAVE_CYCLES"):  # shares of wave time: parked on s_waitcnt / issue-stalled / issuing
+            for c, k in (("SQ_WAIT_ANY", "wait_any_share"), ("SQ_WAIT_INST_ANY", "wait_inst_share"),
+                         ("SQ_ACTIVE_INST_ANY", "active_inst_share"), ("SQ_ACTIVE_INST_VALU", "active_valu_share")):
+                if c in d:
+                    d[k] = round(d[c] / d["SQ_WAVE_CYCLES"], 4)
         if "SQ_LDS_BANK_CONFLICT" in d and d.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_conflict_ratio"] = round(d["SQ_LDS_BANK_CONFLICT"] / d["SQ_LDS_IDX_ACTIVE"], 4)
     if args.bench and os.path.exists(args.bench):
