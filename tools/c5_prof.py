@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """C5 workload for rocprofv3 (tools/gpu_prof_c5.sh): k=20 m=8, 4 MiB fragments, 32 stripes in HBM.
 With the bitsliced kernels (knob bitslice = 2: compile on first use, then always taken), in this
-order: 30 encodes, 30 rebuilds of data {0..7}, 30 rebuilds of the mixed pattern
-{0,2,4,6,20,22,24,26}; then the same 90 launches on the LDS-table kernels (bitslice = 0).  Each
-run of 30 is one kernel (ecamd_bs_kernel / gf16_hybrid_kernel<5>) in dispatch order, so the
-summary takes launches 10..29 of each run as the steady state (the clock settles over the first
-few launches of a new mix).  Prints the HIP-event rate of each steady window too.
+order: 25 untimed warm-up encodes, 30 encodes, 30 rebuilds of data {0..7}, 30 rebuilds of the
+mixed pattern {0,2,4,6,20,22,24,26}; then the same 115 launches on the LDS-table kernels
+(bitslice = 0).  Each run of 30 is one kernel (ecamd_bs_kernel / gf16_hybrid_kernel<5>) in
+dispatch order, so the summary takes launches 10..29 of each run as the steady state (the clock
+settles over the first ~20 launches of a VALU-dense kernel): ecamd_bs_kernel dispatches 38, 68, 98
+(after 3 compile-time launches), gf16_hybrid_kernel 36, 66, 96 (after 1).  Prints the HIP-event rate of each steady window too.
 C5_MODES="2:0,2:4,0:0" picks other (bitslice, bitslice_depth) sequences, e.g. for A/B runs."""
 import json
 import os
@@ -19,6 +20,7 @@ from liberasurecode_amd import _lib  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
 K, M, F, S = 20, 8, 4 << 20, 32
+WARM = 25
 PATTERNS = {"rebuild8_data": list(range(8)), "rebuild8_mixed": [0, 2, 4, 6, 20, 22, 24, 26]}
 
 
@@ -47,6 +49,8 @@ def main(n=30, skip=10):
         d.ecamd_tune(b"bitslice", mode)
         if depth is not None:
             d.ecamd_tune(b"bitslice_depth", depth)
+        for _ in range(WARM):
+            D.rs_encode(K, M, lay, stream=st)
         ops = [("encode", lambda: D.rs_encode(K, M, lay, stream=st))]
         ops += [(name, (lambda p: lambda: D.rs_decode(K, M, p, lay, stream=st))(p)) for name, p in PATTERNS.items()]
         for name, fn in ops:

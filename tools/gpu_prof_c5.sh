@@ -1,6 +1,11 @@
 #!/bin/bash
 # rocprofv3 kernel trace + separate PMC passes of tools/c5_prof.py (C5 steady state, bitsliced and
 # LDS-table kernels), summarised into profiles/<round>_c5_summary.json.  Usage: gpu_prof_c5.sh
+# then, where gpurun_out/ was merged back (windows = the steady launches, tools/c5_prof.py docstring):
+#   tools/summarize_prof.py c5 r02 --command "python3 tools/c5_prof.py" --algo-bytes 3758096384 \
+#     --window bs_encode:ecamd_bs_kernel:38:20 --window bs_rebuild8_data:ecamd_bs_kernel:68:20 \
+#     --window bs_rebuild8_mixed:ecamd_bs_kernel:98:20 --window lds_encode:gf16_hybrid_kernel:36:20 \
+#     --window lds_rebuild8_data:gf16_hybrid_kernel:66:20 --window lds_rebuild8_mixed:gf16_hybrid_kernel:96:20
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
