@@ -414,23 +414,32 @@ int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, siz
     return launch_ptrs_w<8>(a, grid, block, lds, st);
 }
 
-// The bitsliced form of an 8-output pass (host/bitslice.hpp, hip/ecamd_jit.hip) over the whole
-// 16 KiB tiles of every fragment; returns the bytes it covered (0: not taken -- shape, knob, or the
-// kernel is still compiling), the rest of each fragment goes to the LDS-table kernels.
-int64_t launch_bitslice(const ecamd_map* map, const ecamd_map::Pass& p, ApplyArgs a, int64_t bs,
-                        int nstripes, hipStream_t st, int* rc)
+// The bitsliced form (host/bitslice.hpp, hip/ecamd_jit.hip) of output rows row0 .. row0+nrows-1
+// (5..8 of them) over ALL K <= 32 inputs -- whatever column chunks and row widths the LDS-table
+// passes use -- on the whole 16 KiB tiles of every fragment; returns the bytes it covered (0: not
+// taken -- shape, knob, or the kernel is still compiling); the LDS-table passes of those rows then
+// run on the rest of each fragment only.
+int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyArgs& base,
+                        const int64_t* in_off, const int64_t* out_off, int64_t bs, int nstripes,
+                        hipStream_t st, int* rc)
 {
     *rc = 0;
     const int mode = g_tune.bitslice;
-    if (!mode || p.width != 8 || a.nrows < 5 || p.col0 != 0 || p.ncols != map->K || a.copy_records ||
-        a.limited || bs < kBsTile || p.ncols > kBsMaxK || !stream_offsets(a, bs))
+    const int K = map->K;
+    if (!mode || nrows < 5 || nrows > kBsMaxR || K > kBsMaxK || base.copy_records || base.limited ||
+        bs < kBsTile)
         return 0;
-    std::vector<int> sub(static_cast<size_t>(a.nrows) * p.ncols);
-    for (int r = 0; r < a.nrows; r++)
-        for (int j = 0; j < p.ncols; j++)
-            sub[static_cast<size_t>(r) * p.ncols + j] =
-                map->coeff[static_cast<size_t>(p.row0 + r) * map->K + p.col0 + j];
-    hipFunction_t fn = bitslice_function(map->device, sub, a.nrows, p.ncols, g_tune.bitslice_depth, mode == 2);
+    ApplyArgs a = base;
+    a.ncols = K;
+    a.nrows = nrows;
+    for (int j = 0; j < K; j++) a.in_off[j] = in_off[j];
+    for (int r = 0; r < nrows; r++) a.out_off[r] = out_off[row0 + r];
+    if (!stream_offsets(a, bs)) return 0;
+    std::vector<int> sub(static_cast<size_t>(nrows) * K);
+    for (int r = 0; r < nrows; r++)
+        for (int j = 0; j < K; j++)
+            sub[static_cast<size_t>(r) * K + j] = map->coeff[static_cast<size_t>(row0 + r) * K + j];
+    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, g_tune.bitslice_depth, mode == 2);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -442,8 +451,8 @@ int64_t launch_bitslice(const ecamd_map* map, const ecamd_map::Pass& p, ApplyArg
     b.out_records = a.out_records;
     b.tiles_per_stripe = static_cast<uint32_t>(bs / kBsTile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
-    for (int j = 0; j < p.ncols; j++) b.in_off[j] = a.in_off32[j];
-    for (int r = 0; r < a.nrows; r++) b.out_off[r] = a.out_off32[r];
+    for (int j = 0; j < K; j++) b.in_off[j] = a.in_off32[j];
+    for (int r = 0; r < nrows; r++) b.out_off[r] = a.out_off32[r];
     // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
     const int grid = static_cast<int>(std::min<int64_t>(b.ntiles, static_cast<int64_t>(cu_count(map->device)) * 2));
     *rc = bitslice_launch(fn, b, grid, st);
@@ -454,9 +463,22 @@ template <bool PTRS>
 int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off,
                 const int64_t* out_off, int64_t bs_all, int nstripes, hipStream_t st)
 {
+    // bytes of each fragment the bitsliced kernel covered, per group of 8 output rows (the LDS-table
+    // row widths 2 / 4 / 8 divide 8, so a pass lies in one group)
+    std::vector<int64_t> bs_done(static_cast<size_t>((map->R + 7) / 8), 0);
+    if constexpr (!PTRS) {
+        for (int g = 0; g * 8 < map->R; g++) {
+            int brc = 0;
+            bs_done[static_cast<size_t>(g)] = launch_bitslice(map, g * 8, std::min(8, map->R - g * 8), base_args, in_off, out_off,
+                                         bs_all, nstripes, st, &brc);
+            if (brc) return brc;
+        }
+    }
     for (const auto& p : map->passes) {
         ApplyArgs a = base_args;
         int64_t bs = bs_all;
+        const int64_t done = bs_done[static_cast<size_t>(p.row0 / 8)];
+        if (done == bs_all) continue;
         a.tables = map->d_tables + p.offset;
         a.bs = bs;
         a.ncols = p.ncols;
@@ -465,10 +487,6 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
         for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[p.col0 + j];
         for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
         if constexpr (!PTRS) {
-            int brc = 0;
-            const int64_t done = launch_bitslice(map, p, a, bs, nstripes, st, &brc);
-            if (brc) return brc;
-            if (done == bs) continue;
             if (done > 0) {  // the tail of every fragment through the LDS-table kernels
                 for (int j = 0; j < p.ncols; j++) a.in_off[j] += done;
                 for (int r = 0; r < a.nrows; r++) a.out_off[r] += done;

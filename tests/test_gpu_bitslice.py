@@ -2,7 +2,9 @@
 host/bitslice.cpp) against the CPU oracle, bit-exact.
 
 Covers encode (C5 shape: liberasurecode_rs_vand_encode, src/builtin/rs_vand/liberasurecode_rs_vand.c:399-410),
-decode / reconstruct of 5..8 lost fragments (:426-481, :483-558), fragments with a tail that is
+decode / reconstruct of 5..8 lost fragments (:426-481, :483-558) -- also k > 20, where the
+LDS-table passes split rows and columns but the bitsliced kernel takes all k inputs of each group of
+8 outputs, and more than 8 outputs (the rows past 8 stay on the tables) --, fragments with a tail that is
 not a whole 16 KiB tile (the tail runs through the LDS-table kernel), heterogeneous batches over
 stripe lists, and the knob that turns the bitsliced form off (same bytes).  Every test runs with
 the inputs loaded straight into registers (bitslice_depth 0) and through the per-wave LDS-DMA ring
@@ -46,7 +48,8 @@ def _batch(k, m, bs, S, seed=3):
 
 
 @pytest.mark.parametrize("k,m,bs", [(20, 8, 65536), (20, 8, 65536 + 4096 + 48), (10, 6, 16384 * 3),
-                                    (12, 5, 16384 + 2), (32, 8, 32768)])
+                                    (12, 5, 16384 + 2), (32, 8, 32768), (24, 8, 65536 + 16384 + 6),
+                                    (6, 10, 32768), (25, 13, 49152)])
 def test_encode_exact(k, m, bs):
     lay, want = _batch(k, m, bs, 3)
     D.rs_encode(k, m, lay)
@@ -56,7 +59,9 @@ def test_encode_exact(k, m, bs):
 
 @pytest.mark.parametrize("k,m,lost", [(20, 8, list(range(8))), (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]),
                                       (20, 8, [1, 3, 5, 7, 9]), (10, 6, [0, 1, 2, 3, 4, 5]),
-                                      (16, 7, [15, 14, 13, 16, 18, 20, 22])])
+                                      (16, 7, [15, 14, 13, 16, 18, 20, 22]),
+                                      (24, 8, [0, 1, 2, 3, 4, 5, 6, 7]), (10, 12, list(range(10))),
+                                      (32, 8, [1, 3, 5, 7, 32, 34, 36, 38])])
 def test_decode_exact(k, m, lost):
     bs = 49152 + 80
     lay, want = _batch(k, m, bs, 4)
