@@ -7,7 +7,8 @@ mixed pattern {0,2,4,6,20,22,24,26}; then the same 115 launches on the LDS-table
 dispatch order, so the summary takes launches 10..29 of each run as the steady state (the clock
 settles over the first ~20 launches of a VALU-dense kernel): ecamd_bs_kernel dispatches 38, 68, 98
 (after 3 compile-time launches), gf16_hybrid_kernel 36, 66, 96 (after 1).  Prints the HIP-event rate of each steady window too.
-C5_MODES="2:0,2:4,0:0" picks other (bitslice, bitslice_depth) sequences, e.g. for A/B runs."""
+C5_MODES="2:0,2:4,0:0" picks other (bitslice, bitslice_depth) sequences, e.g. for A/B runs;
+C5_K / C5_M / C5_S other shapes (m = 8)."""
 import json
 import os
 import sys
@@ -19,9 +20,10 @@ import torch  # noqa: E402,F401
 from liberasurecode_amd import _lib  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
-K, M, F, S = 20, 8, 4 << 20, 32
+K, M = int(os.environ.get("C5_K", 20)), int(os.environ.get("C5_M", 8))  # other shapes: A/B only
+F, S = 4 << 20, int(os.environ.get("C5_S", 32))
 WARM = 25
-PATTERNS = {"rebuild8_data": list(range(8)), "rebuild8_mixed": [0, 2, 4, 6, 20, 22, 24, 26]}
+PATTERNS = {"rebuild8_data": list(range(8)), "rebuild8_mixed": [0, 2, 4, 6, K, K + 2, K + 4, K + 6]}
 
 
 def main(n=30, skip=10):
