@@ -181,6 +181,7 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     posix_spawn_file_actions_t fa;
     posix_spawn_file_actions_init(&fa);
     posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);  // keep our stdout clean
+    posix_spawn_file_actions_addclosefrom_np(&fa, 3);  // no GPU / socket descriptors in the child
     const char* argv[] = {helper.c_str(), req_path.c_str(), e.co_path.c_str(), nullptr};
     pid_t pid = -1;
     if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, const_cast<char* const*>(argv), environ) == 0) {
