@@ -35,9 +35,11 @@ class Coordinator:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.on_gpu = False
+        self.device = None
         if torch.cuda.is_available() and torch.cuda.device_count() > 0:
             # one GPU per rank; ranks beyond the visible GPUs share them (rehearsal only)
-            torch.cuda.set_device(self.local % torch.cuda.device_count())
+            self.device = self.local % torch.cuda.device_count()
+            torch.cuda.set_device(self.device)
         if self.world > 1:
             backend = backend or os.environ.get("ECAMD_DIST_BACKEND")
             if backend is None:
@@ -45,7 +47,7 @@ class Coordinator:
             self.on_gpu = backend == "nccl"
             if self.on_gpu:
                 dist.init_process_group(backend=backend,
-                                        device_id=torch.device("cuda", self.local))
+                                        device_id=torch.device("cuda", self.device or 0))
             else:
                 dist.init_process_group(backend=backend)
 
