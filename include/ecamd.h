@@ -45,9 +45,12 @@ int ecamd_tune(const char *key, int value);
 
 /* Bitsliced 8-output passes (hip/ecamd_jit.hip): 1 if run-time compilation (hiprtc) is usable;
  * ecamd_bitslice_wait() blocks until every kernel compile started so far has finished and returns
- * how many failed (their maps keep using the LDS-table kernels). */
+ * how many failed (their maps keep using the LDS-table kernels); ecamd_bitslice_entries() is the
+ * number of matrices held (bounded by the "bitslice_entries" knob, least recently used evicted and
+ * their modules unloaded once no launch can still use them). */
 int ecamd_bitslice_available(void);
 int ecamd_bitslice_wait(void);
+int ecamd_bitslice_entries(void);
 
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
 typedef struct ecamd_map ecamd_map;

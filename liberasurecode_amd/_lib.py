@@ -125,6 +125,7 @@ def dev():
         _proto(d, "ecamd_percall_crc_disarm", None, [])
         _proto(d, "ecamd_bitslice_available", C.c_int, [])
         _proto(d, "ecamd_bitslice_wait", C.c_int, [])
+        _proto(d, "ecamd_bitslice_entries", C.c_int, [])
         _proto(d, "ecamd_percall_reset", None, [])
         _proto(d, "ecamd_percall_status", C.c_int, [])
         _proto(d, "ecamd_fault_inject", C.c_int, [C.c_char_p, C.c_int])

@@ -179,6 +179,7 @@ struct Tuning {
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
+    Knob bitslice_entries{256};  // matrices with a loaded bitsliced kernel kept (LRU beyond)
     Knob bitslice_depth{2}; //   inputs through a per-wave LDS ring 2 (default) / 4 deep, or straight
                             //   into registers (0); tools/c5_prof.py C5_MODES A/B
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
@@ -219,6 +220,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
     if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
+    if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
 }
 
@@ -240,7 +242,8 @@ struct ecamd_map {
 };
 
 namespace ecamd {
-hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait);
+hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
+                                std::shared_ptr<void>& hold);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st);
 }  // namespace ecamd
 
@@ -439,7 +442,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     for (int r = 0; r < nrows; r++)
         for (int j = 0; j < K; j++)
             sub[static_cast<size_t>(r) * K + j] = map->coeff[static_cast<size_t>(row0 + r) * K + j];
-    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, g_tune.bitslice_depth, mode == 2);
+    std::shared_ptr<void> hold;  // the kernel's module stays loaded until the launch is enqueued
+    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, g_tune.bitslice_depth, mode == 2, hold);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1142,6 +1146,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.multi_list = value;
     } else if (k == "bitslice") {
         g_tune.bitslice = value;
+    } else if (k == "bitslice_entries") {
+        g_tune.bitslice_entries = value >= 1 && value <= 4096 ? value : 256;  // 0 restores the default
     } else if (k == "bitslice_depth") {
         g_tune.bitslice_depth = value >= 4 ? 4 : value >= 2 ? 2 : 0;
     } else if (k == "stream_hybrid") {

@@ -114,12 +114,38 @@ struct BsEntry {
     int state = 0;        // 0 compiling, 2 waiting for a compiler slot, 1 code object ready, -1 failed
     std::string code;
     std::map<int, hipFunction_t> fn;  // per device; nullptr: unusable there
-    std::vector<hipModule_t> modules;
+    std::vector<std::pair<int, hipModule_t>> modules;  // (device, module), spilled ones included
+    uint64_t last_use = 0;
+
+    // Reached only for an entry evicted from the cache (the cache itself is never destroyed, so
+    // nothing here runs at process exit) once its last holder -- a launch in progress keeps one --
+    // has let go: no launch of its functions can still be enqueued; wait for those in flight on
+    // each device the modules live on, then unload them.
+    ~BsEntry()
+    {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        std::vector<int> synced;
+        for (const auto& dm : modules) {
+            if (hipSetDevice(dm.first) != hipSuccess) continue;
+            if (std::find(synced.begin(), synced.end(), dm.first) == synced.end()) {
+                (void)hipDeviceSynchronize();
+                synced.push_back(dm.first);
+            }
+            (void)hipModuleUnload(dm.second);
+        }
+        if (cur >= 0) (void)hipSetDevice(cur);
+        (void)hipGetLastError();
+    }
 };
 
-std::mutex g_jit_mu;  // guards g_jit, g_running and every entry
-std::map<std::vector<int>, std::shared_ptr<BsEntry>> g_jit;
-std::vector<std::shared_ptr<BsEntry>> g_running;  // entries whose compiler child runs
+// Matrices with a bitsliced kernel (or one on the way), the least recently used evicted past the
+// "bitslice_entries" knob (256); heap objects never destroyed, so no HIP call runs during static
+// destruction.
+std::mutex g_jit_mu;  // guards g_jit, g_running, g_clock and every entry
+auto& g_jit = *new std::map<std::vector<int>, std::shared_ptr<BsEntry>>();
+auto& g_running = *new std::vector<std::shared_ptr<BsEntry>>();  // entries whose compiler child runs
+uint64_t g_clock = 0;
 
 // Compiler children at once ($ECAMD_JIT_JOBS, default 2): a burst of new erasure patterns queues
 // rather than loading the host with one compile per pattern.
@@ -215,8 +241,10 @@ void poll_compile(const std::shared_ptr<BsEntry>& ep, bool wait)
 }  // namespace
 
 // Kernel for the R x K matrix on `dev`: nullptr while compiling (wait = false) or when the
-// bitsliced form is unavailable; starts the compile the first time the matrix is seen.
-hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait)
+// bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
+// keeps the kernel's module loaded until the caller has enqueued its launch.
+hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
+                                std::shared_ptr<void>& hold)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
     depth = bitslice_depth(depth, K);
@@ -228,9 +256,15 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         poll_compile(ep, false);
         if (ep->state == 0) i++;
     }
-    if (g_jit.size() >= 1024 && !g_jit.count(key))  // bound; loaded modules stay valid
-        for (auto it = g_jit.begin(); it != g_jit.end();)
-            it = it->second->state == 0 ? std::next(it) : g_jit.erase(it);  // children stay reapable
+    const size_t max_entries = static_cast<size_t>(std::max(1, dev_tune("bitslice_entries")));
+    while (g_jit.size() >= max_entries && !g_jit.count(key)) {  // evict the least recently used
+        auto victim = g_jit.end();
+        for (auto it = g_jit.begin(); it != g_jit.end(); ++it)
+            if (it->second->state != 0 && (victim == g_jit.end() || it->second->last_use < victim->second->last_use))
+                victim = it;
+        if (victim == g_jit.end()) break;  // all compiling: let the map grow until they finish
+        g_jit.erase(victim);
+    }
     auto& slot = g_jit[key];
     if (!slot) {
         slot = std::make_shared<BsEntry>();
@@ -243,6 +277,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     }
     const std::shared_ptr<BsEntry> ep = slot;
     BsEntry& e = *ep;
+    e.last_use = ++g_clock;
+    hold = ep;
     for (;;) {
         auto it = e.fn.find(dev);
         if (it != e.fn.end()) return it->second;
@@ -253,7 +289,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         if (e.state == 1) {
             hipModule_t mod = nullptr;
             if (hipModuleLoadData(&mod, e.code.data()) == hipSuccess) {
-                e.modules.push_back(mod);
+                e.modules.emplace_back(dev, mod);
                 if (hipModuleGetFunction(&fn, mod, "ecamd_bs_kernel") != hipSuccess) fn = nullptr;
                 if (fn && hipFuncGetAttribute(&spill, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) == hipSuccess &&
                     spill > 0)
@@ -294,6 +330,12 @@ extern "C" int ecamd_bitslice_wait(void)
         if (kv.second->state != 1) failed++;
     }
     return failed;
+}
+
+extern "C" int ecamd_bitslice_entries(void)
+{
+    std::lock_guard<std::mutex> lk(ecamd::g_jit_mu);
+    return static_cast<int>(ecamd::g_jit.size());
 }
 
 extern "C" int ecamd_bitslice_available(void) { return ecamd::helper_path().empty() ? 0 : 1; }

@@ -151,3 +151,24 @@ def test_background_compiles_queue(sync_compile):
             assert (lay.download_stripes() == want).all(), (rnd, p)
         if rnd == 0:
             assert _lib.dev().ecamd_bitslice_wait() == 0
+
+
+def test_entries_bounded_and_evicted_kernels_reload(sync_compile):
+    """More distinct 8-output matrices than the "bitslice_entries" bound: the least recently used
+    are evicted (modules unloaded after their launches drained) and a pattern seen again is
+    rebuilt from the disk cache; every result exact."""
+    k, m, bs, S = 20, 8, 32768, 2
+    lay, want = _batch(k, m, bs, S, seed=31)
+    pats = [[j, j + 1, j + 2, j + 3, j + 4, 20, 21, 22] for j in range(5)]
+    d = sync_compile
+    d.ecamd_tune(b"bitslice_entries", 2)
+    try:
+        for p in pats + pats[:2]:
+            host = want.copy()
+            host[:, p] = 0x5C
+            lay.upload_stripes(host)
+            D.rs_decode(k, m, p, lay)
+            assert (lay.download_stripes() == want).all(), p
+            assert d.ecamd_bitslice_entries() <= 2
+    finally:
+        d.ecamd_tune(b"bitslice_entries", 0)
