@@ -10,6 +10,7 @@
 // launches the LDS-table kernel until the code object is ready, 2 waits for it (tests, bench), 0
 // never uses the bitsliced form; ecamd_bitslice_wait() waits for every compile started so far.
 #include <hip/hip_runtime.h>
+#include <dirent.h>
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <spawn.h>
@@ -75,6 +76,31 @@ std::string helper_path()
     return path;
 }
 
+// Keep the disk cache to the newest $ECAMD_JIT_CACHE_MAX (4096) code objects: run once per process.
+void prune_cache(const std::string& dir)
+{
+    const char* env = std::getenv("ECAMD_JIT_CACHE_MAX");
+    const long cap = env && std::atol(env) > 0 ? std::atol(env) : 4096;
+    std::vector<std::pair<time_t, std::string>> cos;
+    if (DIR* d = opendir(dir.c_str())) {
+        while (const dirent* ent = readdir(d)) {
+            const std::string name(ent->d_name);
+            if (name.size() < 4 || name.compare(0, 3, "bs_") != 0 || name.compare(name.size() - 3, 3, ".co") != 0)
+                continue;
+            struct stat st {};
+            const std::string path = dir + "/" + name;
+            if (stat(path.c_str(), &st) == 0) cos.emplace_back(st.st_mtime, path);
+        }
+        closedir(d);
+    }
+    if (static_cast<long>(cos.size()) <= cap) return;
+    std::sort(cos.begin(), cos.end());
+    for (size_t i = 0; i + static_cast<size_t>(cap) < cos.size(); i++) {
+        std::remove(cos[i].second.c_str());
+        std::remove((cos[i].second.substr(0, cos[i].second.size() - 3) + ".hip").c_str());
+    }
+}
+
 std::string cache_dir()
 {
     static std::string dir;
@@ -83,6 +109,7 @@ std::string cache_dir()
         const char* env = std::getenv("ECAMD_JIT_CACHE");
         dir = env && *env ? env : "/tmp/ecamd-jit-" + std::to_string(getuid());
         mkdir(dir.c_str(), 0700);
+        prune_cache(dir);
     });
     return dir;
 }
@@ -196,7 +223,7 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
         e.state = 2;
         return;
     }
-    const std::string req_path = base + ".req";
+    const std::string req_path = base + ".req." + std::to_string(getpid());  // this process's; jitc consumes it
     {
         const std::string tmp = req_path + ".tmp." + std::to_string(getpid());
         std::ofstream f(tmp);
@@ -231,11 +258,11 @@ void poll_compile(const std::shared_ptr<BsEntry>& ep, bool wait)
         r = waitpid(e.pid, &status, wait ? 0 : WNOHANG);
     } while (r < 0 && errno == EINTR);
     if (r == 0) return;  // still running
-    const bool ok = r == e.pid && WIFEXITED(status) && WEXITSTATUS(status) == 0;
     e.pid = -1;
     g_running.erase(std::remove(g_running.begin(), g_running.end(), ep), g_running.end());
-    // a child reaped elsewhere (r < 0) may still have produced the file
-    e.state = ((ok || r < 0) && read_file(e.co_path, e.code)) ? 1 : -1;
+    // a child reaped elsewhere (r < 0), or another process compiling the same request, may still
+    // have produced the code object
+    e.state = read_file(e.co_path, e.code) ? 1 : -1;
 }
 
 }  // namespace

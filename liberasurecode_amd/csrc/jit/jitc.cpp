@@ -3,7 +3,8 @@
 // process.  libecamd (hip/ecamd_jit.hip) starts it as a child process, so neither the network
 // search nor the compile runs on a caller's thread or shares a process with the GPU work, and a
 // parent that exits abandons it harmlessly.  The code object is written to <out>.tmp.<pid> and
-// renamed to <out>, so readers only ever see a whole one; the source lands beside it as
+// renamed to <out>, so readers only ever see a whole one; the request file is removed once read,
+// and with ECAMD_JIT_KEEP_SOURCE=1 the generated source lands beside the code object as
 // <out minus .co>.hip for inspection.  This program never touches the GPU.
 //
 //   ecamd_jitc <request> <out.co>      request: bitslice_request() text; exit 0 on success
@@ -52,9 +53,11 @@ int main(int argc, char** argv)
     ecamd::BitsliceStyle style;  // experiments only: the parent's cache key does not see these
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
+    std::remove(argv[1]);
     const std::string src = ecamd::bitslice_source(ecamd::bitslice_network(coeff, R, K, cap), depth, style);
     std::string out(argv[2]);
-    if (out.size() > 3 && out.compare(out.size() - 3, 3, ".co") == 0)
+    const char* keep = std::getenv("ECAMD_JIT_KEEP_SOURCE");
+    if (keep && std::atoi(keep) && out.size() > 3 && out.compare(out.size() - 3, 3, ".co") == 0)
         write_whole(out.substr(0, out.size() - 3) + ".hip", src);
 
     hiprtcProgram prog = nullptr;

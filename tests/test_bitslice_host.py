@@ -91,10 +91,12 @@ def test_jitc_builds_a_request(tmp_path):
     rows = [" ".join(str(c) for c in G[12 * 12 + 12 * r:12 * 12 + 12 * (r + 1)]) for r in range(5)]
     req.write_text("ecamd-bitslice-request 1\n5 12 40 0\n" + "\n".join(rows) + "\n")
     out = tmp_path / "bs.co"
-    r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, ECAMD_JIT_KEEP_SOURCE="1")
+    r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     assert out.read_bytes()[:4] == b"\x7fELF"
     assert "5 outputs x 12 inputs" in (tmp_path / "bs.hip").read_text()
+    assert not req.exists()  # the request is consumed
     assert not [p for p in os.listdir(tmp_path) if ".tmp." in p]
     bad = tmp_path / "bad.req"
     for text in ("nonsense\n", "ecamd-bitslice-request 1\n9 12 40 0\n", "ecamd-bitslice-request 1\n1 1 40 0\n70000\n"):
