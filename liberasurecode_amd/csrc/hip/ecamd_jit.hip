@@ -40,11 +40,12 @@ extern char** environ;
 namespace ecamd {
 namespace {
 
-// Shared temporaries per input, first choice first: 64 fits the register file at 2 waves per SIMD
-// for the C5 encode and decode networks in the LDS-ring form (225-245 VGPRs, no scratch: each
-// temporary is computed right before its first use); a network that spills (the compiler's
-// schedule decides, not the count alone) is rebuilt with the next.
-constexpr int kCaps[] = {64, 48, 32, 16};
+// Temporaries per input, first choice first: 96 (the search stops by itself near 80 on C5 maps)
+// fits the register file at 2 waves per SIMD for the C5 encode and decode networks in the
+// LDS-ring form (230-245 VGPRs, no scratch: each temporary is computed right before its first use);
+// a network that spills (the compiler's schedule decides, not the count alone) is rebuilt with the
+// next.
+constexpr int kCaps[] = {96, 64, 40, 16};
 constexpr int kNumCaps = static_cast<int>(sizeof(kCaps) / sizeof(kCaps[0]));
 
 // First cap to try: the largest not above $ECAMD_JIT_CAP_MAX (A/B experiments), else kCaps[0].
@@ -193,8 +194,8 @@ const std::string& generator_fingerprint()
     static std::string fp;
     static std::once_flag once;
     std::call_once(once, [] {
-        const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0, 1);
-        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + "trials=" + std::to_string(kBsTrials);
+        const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0);
+        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + kBsNetworkVersion;
     });
     return fp;
 }

@@ -26,108 +26,96 @@ void gf16_bitmatrix(int c, uint16_t (&rows)[16])
 
 namespace {
 
-// Greedy common-subexpression elimination priced in three-input XORs (bitslice.hpp): take the
-// shared pair or triple with the largest saving (ties: pairs first, then the smallest ids) while it
-// saves at least one op and fewer than `cap` temporaries exist.  Deterministic in the matrix.
-void share_terms(std::vector<std::vector<int>>& rows, std::vector<std::array<int, 3>>& temps, int cap)
+// The network of one input: its R*16 target rows (16-bit masks over the input's planes) built from
+// the 16 planes plus up to `cap` temporaries, priced as the kernel runs it -- a row that is the XOR
+// of d available variables costs ceil(d/2) three-input XORs into its accumulator, a temporary one
+// op (the XOR of 2 or 3 available variables).
+//
+// Distance-guided greedy in the manner of Boyar and Peralta's circuit heuristic, made exact by the
+// small space: dist[v] is the fewest available variables XORing to v, for every v of the 2^16, so
+// adding a variable c updates it in one pass (dist'[v] = min(dist[v], dist[v^c] + 1): a minimal
+// sum uses c at most once) and the saving of a candidate c is sum over rows t of
+// ceil(dist[t]/2) - ceil(min(dist[t], dist[t^c] + 1)/2).  Each step adds the one-op candidate
+// (dist 2 or 3) with the largest saving above its own cost; ties go to the smallest mask, so the
+// network is a function of the matrix.  Rows are then spelled out along parent links (each v
+// remembers the variable its current minimal sum ends with).
+void distance_network(const std::vector<uint16_t>& rows, int cap, BitsliceNet::Input& out)
 {
-    constexpr int V = 80;  // variable ids < 16 + cap <= 80
-    std::vector<int> c2(V * V), c3(V * V * V);
-    std::vector<int> touched;
-    int nvar = 16;
-    while (static_cast<int>(temps.size()) < cap && nvar < V) {
-        std::fill(c2.begin(), c2.end(), 0);
-        for (int t : touched) c3[static_cast<size_t>(t)] = 0;
-        touched.clear();
-        for (const auto& r : rows) {
-            const size_t n = r.size();
-            for (size_t i = 0; i < n; i++)
-                for (size_t k = i + 1; k < n; k++) {
-                    if (n & 1) c2[static_cast<size_t>(r[i]) * V + r[k]]++;
-                    for (size_t l = k + 1; l < n; l++) {
-                        const int key = (r[i] * V + r[k]) * V + r[l];
-                        if (c3[static_cast<size_t>(key)]++ == 0) touched.push_back(key);
-                    }
-                }
-        }
-        int best = 1, ba = -1, bb = -1, bc = -1;
-        for (int a = 0; a < nvar; a++)
-            for (int b = a + 1; b < nvar; b++)
-                if (c2[static_cast<size_t>(a) * V + b] > best) {
-                    best = c2[static_cast<size_t>(a) * V + b];
-                    ba = a, bb = b, bc = -1;
-                }
-        std::sort(touched.begin(), touched.end());
-        for (int key : touched)
-            if (c3[static_cast<size_t>(key)] > best) {
-                best = c3[static_cast<size_t>(key)];
-                ba = key / (V * V), bb = (key / V) % V, bc = key % V;
-            }
-        if (ba < 0) break;  // nothing saves an op
-        temps.push_back({ba, bb, bc});
-        for (auto& r : rows) {
-            auto has = [&](int v) { return v < 0 || std::find(r.begin(), r.end(), v) != r.end(); };
-            if (!has(ba) || !has(bb) || !has(bc)) continue;
-            r.erase(std::remove_if(r.begin(), r.end(), [&](int v) { return v == ba || v == bb || v == bc; }),
-                    r.end());
-            r.push_back(nvar);  // rows stay sorted: new variables are the largest
-        }
-        nvar++;
+    constexpr int N = 1 << 16;
+    std::vector<uint8_t> dist(N);
+    std::vector<uint8_t> par(N);  // variable id whose removal leaves a minimal sum for v ^ var
+    std::vector<uint16_t> var;    // variable id -> mask over the planes
+    for (int b = 0; b < 16; b++) var.push_back(static_cast<uint16_t>(1u << b));
+    for (int v = 0; v < N; v++) {
+        dist[static_cast<size_t>(v)] = static_cast<uint8_t>(__builtin_popcount(static_cast<unsigned>(v)));
+        par[static_cast<size_t>(v)] = static_cast<uint8_t>(v ? __builtin_ctz(static_cast<unsigned>(v)) : 0);
     }
+    auto spell = [&](uint16_t v) {
+        std::vector<int> ids;
+        while (v) {
+            const int e = par[v];
+            ids.push_back(e);
+            v = static_cast<uint16_t>(v ^ var[static_cast<size_t>(e)]);
+        }
+        return ids;
+    };
+    auto cost = [](int d) { return (d + 1) / 2; };
+    std::vector<uint16_t> open;  // rows that a new variable could still make cheaper (dist >= 2)
+    out.temps.clear();
+    while (static_cast<int>(out.temps.size()) < cap) {
+        open.clear();
+        for (uint16_t t : rows)
+            if (dist[t] >= 2) open.push_back(t);
+        if (open.empty()) break;
+        int best = 1, bc = -1;  // a temporary costs one op: it must save at least two
+        for (int c = 1; c < N; c++) {
+            const int dc = dist[static_cast<size_t>(c)];
+            if (dc < 2 || dc > 3) continue;
+            int g = 0;
+            for (uint16_t t : open) {
+                const int d = dist[t], d2 = dist[static_cast<size_t>(t ^ c)] + 1;
+                if (d2 < d) g += cost(d) - cost(d2);
+            }
+            if (g > best) {
+                best = g;
+                bc = c;
+            }
+        }
+        if (bc < 0) break;
+        const std::vector<int> def = spell(static_cast<uint16_t>(bc));
+        out.temps.push_back({def[0], def[1], def.size() > 2 ? def[2] : -1});
+        const int id = static_cast<int>(var.size());
+        var.push_back(static_cast<uint16_t>(bc));
+        // v ^ bc then v: ascending v would read entries already updated in this pass, so use a copy
+        const std::vector<uint8_t> old = dist;
+        for (int v = 0; v < N; v++) {
+            const int d2 = old[static_cast<size_t>(v ^ bc)] + 1;
+            if (d2 < old[static_cast<size_t>(v)]) {
+                dist[static_cast<size_t>(v)] = static_cast<uint8_t>(d2);
+                par[static_cast<size_t>(v)] = static_cast<uint8_t>(id);
+            }
+        }
+    }
+    out.rows.clear();
+    for (uint16_t t : rows) out.rows.push_back(spell(t));
 }
 
 }  // namespace
 
-BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap, int trials)
+BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap)
 {
     BitsliceNet net;
     net.R = R;
     net.K = K;
     net.inputs.resize(static_cast<size_t>(K));
     for (int j = 0; j < K; j++) {
-        std::vector<std::vector<int>> rows(static_cast<size_t>(R) * 16);
+        std::vector<uint16_t> rows(static_cast<size_t>(R) * 16);
         for (int r = 0; r < R; r++) {
             uint16_t M[16];
             gf16_bitmatrix(coeff[static_cast<size_t>(r) * K + j], M);
-            for (int p = 0; p < 16; p++)
-                for (int b = 0; b < 16; b++)
-                    if ((M[p] >> b) & 1) rows[static_cast<size_t>(r) * 16 + p].push_back(b);
+            for (int p = 0; p < 16; p++) rows[static_cast<size_t>(r) * 16 + p] = M[p];
         }
-        // The greedy is sensitive to its tie-breaks, which follow the plane labels: run it on
-        // `trials` relabelings (the first is the identity; the rest a fixed pseudo-random sequence,
-        // so the network stays a function of the matrix) and keep the cheapest.
-        auto& best = net.inputs[static_cast<size_t>(j)];
-        int best_ops = -1;
-        uint32_t rng = 0x9e3779b9u ^ static_cast<uint32_t>(j);
-        for (int t = 0; t < std::max(1, trials); t++) {
-            int perm[16];
-            for (int b = 0; b < 16; b++) perm[b] = b;
-            if (t)
-                for (int b = 15; b > 0; b--) {
-                    rng = rng * 1664525u + 1013904223u;
-                    std::swap(perm[b], perm[(rng >> 8) % static_cast<uint32_t>(b + 1)]);
-                }
-            BitsliceNet::Input cand;
-            cand.rows = rows;
-            for (auto& row : cand.rows) {
-                for (int& v : row) v = perm[v];
-                std::sort(row.begin(), row.end());
-            }
-            share_terms(cand.rows, cand.temps, cap);
-            int inv[16];
-            for (int b = 0; b < 16; b++) inv[perm[b]] = b;
-            auto back = [&](int v) { return v >= 0 && v < 16 ? inv[v] : v; };
-            for (auto& tm : cand.temps)
-                for (int& v : tm) v = back(v);
-            for (auto& row : cand.rows)
-                for (int& v : row) v = back(v);
-            int ops = static_cast<int>(cand.temps.size());
-            for (const auto& row : cand.rows) ops += static_cast<int>((row.size() + 1) / 2);
-            if (best_ops < 0 || ops < best_ops) {
-                best_ops = ops;
-                best = std::move(cand);
-            }
-        }
+        distance_network(rows, cap, net.inputs[static_cast<size_t>(j)]);
     }
     return net;
 }
@@ -427,7 +415,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     std::string magic;
     int version = 0;
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version != 1) return false;
-    if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 64)
+    if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)

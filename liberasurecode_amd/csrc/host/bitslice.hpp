@@ -11,11 +11,9 @@
 // the input planes: VALU XORs only, no table lookups, so the 8-output passes that the LDS tables
 // bound (C5: random 16-byte lookups conflict ~2.9-way in the LDS banks) run at VALU rate.  Output
 // planes accumulate through three-input XORs (v_bitop3), so a row of n terms costs ceil(n/2) ops;
-// per input, sums shared by several rows are computed once first -- greedy common-subexpression
-// elimination in the spirit of Paar's algorithm, but priced in three-input XORs: a shared triple
-// saves one op in every row holding it, a shared pair one op in every odd-length row holding it,
-// each costs one op -- with at most `cap` such temporaries, so the network fits the register file
-// at 2 waves per SIMD.
+// per input, up to `cap` temporaries (XORs of 2 or 3 available variables, one op each) are chosen
+// by a distance-guided greedy (bitslice.cpp, distance_network) so that the rows become short sums,
+// few enough that the network fits the register file at 2 waves per SIMD.
 #pragma once
 #include <array>
 #include <cstdint>
@@ -40,9 +38,9 @@ struct BitsliceNet {
     int xor_ops() const;  // VALU ops of the network (temps + 3-input accumulation)
 };
 
-// `trials` relabelings of the planes are tried per input and the cheapest network kept.
-constexpr int kBsTrials = 16;
-BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap, int trials = kBsTrials);
+// Bumped whenever the network search changes (part of the JIT cache key).
+constexpr const char* kBsNetworkVersion = "distance-1";
+BitsliceNet bitslice_network(const std::vector<int>& coeff, int R, int K, int cap);
 
 // Evaluate the network on 32 words per input (host check of the construction).
 void bitslice_eval(const BitsliceNet& net, const uint16_t* in /* K x 32 */, uint16_t* out /* R x 32 */);
