@@ -180,8 +180,8 @@ struct Tuning {
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
     Knob bitslice_entries{256};  // matrices with a loaded bitsliced kernel kept (LRU beyond)
-    Knob bitslice_depth{2}; //   inputs through a per-wave LDS ring 2 (default) / 4 deep, or straight
-                            //   into registers (0); tools/c5_prof.py C5_MODES A/B
+    Knob bitslice_depth{0}; //   inputs straight into registers (0, default) or through a per-wave
+                            //   LDS ring 2 / 4 deep; tools/c5_prof.py C5_MODES A/B
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only

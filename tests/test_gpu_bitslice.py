@@ -31,7 +31,7 @@ def sync_compile(request):
     d.ecamd_tune(b"bitslice_depth", DEFAULT_DEPTH)
 
 
-DEFAULT_DEPTH = 2
+DEFAULT_DEPTH = 0
 
 
 def test_hiprtc_available():
