@@ -41,10 +41,9 @@ namespace ecamd {
 namespace {
 
 // Temporaries per input, first choice first: 96 (the search stops by itself near 80 on C5 maps)
-// fits the register file at 2 waves per SIMD for the C5 encode and decode networks in the
-// LDS-ring form (230-245 VGPRs, no scratch: each temporary is computed right before its first use);
-// a network that spills (the compiler's schedule decides, not the count alone) is rebuilt with the
-// next.
+// fits the register file at 2 waves per SIMD for the C5 encode and decode networks (230-248 VGPRs,
+// no scratch: each temporary is computed right before its first use); a network that spills (the
+// compiler's schedule decides, not the count alone) is rebuilt with the next.
 constexpr int kCaps[] = {96, 64, 40, 16};
 constexpr int kNumCaps = static_cast<int>(sizeof(kCaps) / sizeof(kCaps[0]));
 
@@ -110,7 +109,14 @@ std::string cache_dir()
         const char* env = std::getenv("ECAMD_JIT_CACHE");
         dir = env && *env ? env : "/tmp/ecamd-jit-" + std::to_string(getuid());
         mkdir(dir.c_str(), 0700);
-        prune_cache(dir);
+        // Code objects from this directory run on the GPU: use it only if it is a real directory of
+        // ours that nobody else can write; otherwise a fresh private one (no sharing across processes).
+        struct stat st {};
+        if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != getuid() || (st.st_mode & 022)) {
+            char tmpl[] = "/tmp/ecamd-jit-XXXXXX";
+            dir = mkdtemp(tmpl) ? tmpl : "";
+        }
+        if (!dir.empty()) prune_cache(dir);
     });
     return dir;
 }
@@ -209,7 +215,12 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + req)));
-    const std::string base = cache_dir() + "/bs_" + name;
+    const std::string dir = cache_dir();
+    if (dir.empty()) {  // no usable cache directory: the LDS tables serve this matrix
+        e.state = -1;
+        return;
+    }
+    const std::string base = dir + "/bs_" + name;
     e.co_path = base + ".co";
     e.pid = -1;
     e.code.clear();
