@@ -8,8 +8,8 @@ LDS-table passes split rows and columns but the bitsliced kernel takes all k inp
 not a whole 16 KiB tile (the tail runs through the LDS-table kernel), heterogeneous batches over
 stripe lists, and the knob that turns the bitsliced form off (same bytes).  Every test runs with
 the inputs loaded straight into registers (bitslice_depth 0) and through the per-wave LDS-DMA ring
-(2 and 4 inputs deep); batches with many more tiles than workgroups exercise the ring's prefetch
-across tile boundaries and its drain after the last tile."""
+(2 inputs deep; the 4-deep ring in test_ring4_many_tiles); batches with many more tiles than
+workgroups exercise the ring's prefetch across tile boundaries and its drain after the last tile."""
 import numpy as np
 import pytest
 
@@ -21,7 +21,7 @@ from liberasurecode_amd import device as D
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=[0, 2, 4], ids=["regs", "ring2", "ring4"])
+@pytest.fixture(autouse=True, params=[0, 2], ids=["regs", "ring2"])
 def sync_compile(request):
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)  # wait for the compile: every launch below takes the JIT kernel
@@ -172,3 +172,10 @@ def test_entries_bounded_and_evicted_kernels_reload(sync_compile):
             assert d.ecamd_bitslice_entries() <= 2
     finally:
         d.ecamd_tune(b"bitslice_entries", 0)
+
+
+@pytest.mark.parametrize("k,m,lost", [(20, 8, None), (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]), (3, 5, None)])
+def test_ring4_many_tiles(sync_compile, k, m, lost):
+    """The 4-deep LDS ring (prefetch three inputs ahead, across tile boundaries)."""
+    sync_compile.ecamd_tune(b"bitslice_depth", 4)
+    test_many_tiles_per_workgroup(sync_compile, k, m, lost)
