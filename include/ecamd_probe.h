@@ -39,6 +39,10 @@ int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void *d_table,
 int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
                            int wave_contig, void *d_base, int64_t blocksize, int K, int R,
                            int nstripes, void *stream);
+/* The same with an explicit slot per logical fragment: frag[i] (i < K) is read, frag[K + r] is
+ * written (a permutation of 0..K+R-1; NULL = identity). */
+int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int order, int wave_contig,
+                     void *base, int64_t bs, int K, int R, int nstripes, const int *frag, void *stream);
 
 /* VALU / LDS issue-cost probe: grid = CUs x wgs_per_cu workgroups of 256 lanes, each lane `iters`
  * rounds of 8 independent instructions of form op (0 v_xor_b32, 1 v_bitop3_b32, 2 SDWA byte-select

@@ -169,6 +169,9 @@ def probe():
         _proto(p, "ecamd_probe_mix2", C.c_int,
                [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64,
                 C.c_int, C.c_int, C.c_int, VP])
+        _proto(p, "ecamd_probe_mix3", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int,
+                C.c_int, C.c_int, IP, VP])
         _proto(p, "ecamd_probe_valu", C.c_int, [C.c_int, C.c_int, C.c_int, VP])
         _probe = p
     return _probe

@@ -126,6 +126,13 @@ int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
                            int wave_contig, void* base, int64_t bs, int K, int R, int nstripes,
                            void* stream)
 {
+    return ecamd_probe_mix3(lp, sp, ch, threads, wgs_per_cu, order, wave_contig, base, bs, K, R, nstripes,
+                            nullptr, stream);
+}
+
+int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int order, int wave_contig,
+                     void* base, int64_t bs, int K, int R, int nstripes, const int* frag, void* stream)
+{
     int dev = 0;
     int rc = ensure_device(&dev);
     if (rc) return rc;
@@ -133,10 +140,14 @@ int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
     if (threads < 64 || threads > 1024 || threads % 64) return fail(-22, "mix probe: threads");
     const int64_t span = static_cast<int64_t>(threads) * 16 * ch;
     const int64_t sstride = bs * (K + R);
-    if (K < 1 || R < 0 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
+    if (K < 1 || R < 0 || K + R > 64 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
         return fail(-22, "mix probe: bad shape");
     MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0, order != 0,
-              wave_contig != 0};
+              wave_contig != 0, {}};
+    for (int i = 0; i < K + R; i++) {
+        a.frag[i] = frag ? frag[i] : i;
+        if (a.frag[i] < 0 || a.frag[i] >= K + R) return fail(-22, "mix probe: fragment slot out of range");
+    }
     a.tiles_per_stripe = static_cast<uint32_t>(bs / span);
     a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     const int grid = static_cast<int>(std::min<int64_t>(a.ntiles,

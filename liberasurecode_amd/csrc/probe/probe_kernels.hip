@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
 #pragma unroll
             for (int c = 0; c < CH; c++)
                 cur[i][c] = (i < a.K) ? __builtin_amdgcn_raw_buffer_load_b128(
-                                            rsrc, i * a.frag_stride + off + c * cstride, 0, LP)
+                                            rsrc, a.frag[i] * a.frag_stride + off + c * cstride, 0, LP)
                                       : v4{0u, 0u, 0u, 0u};
         for (int j0 = 0; j0 < a.K; j0 += 4) {
 #pragma unroll
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
                 for (int c = 0; c < CH; c++)
                     nxt[i][c] = (j0 + 4 + i < a.K)
                                     ? __builtin_amdgcn_raw_buffer_load_b128(
-                                          rsrc, (j0 + 4 + i) * a.frag_stride + off + c * cstride, 0, LP)
+                                          rsrc, a.frag[j0 + 4 + i] * a.frag_stride + off + c * cstride, 0, LP)
                                     : v4{0u, 0u, 0u, 0u};
 #pragma unroll
             for (int i = 0; i < 4; i++)
@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
 #pragma unroll
             for (int c = 0; c < CH; c++)
                 __builtin_amdgcn_raw_buffer_store_b128(acc[c] + static_cast<unsigned>(r), rsrc,
-                                                       (a.K + r) * a.frag_stride + off + c * cstride,
+                                                       a.frag[a.K + r] * a.frag_stride + off + c * cstride,
                                                        0, SP);
     }
 }
