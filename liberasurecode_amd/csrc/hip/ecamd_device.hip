@@ -179,6 +179,7 @@ struct Tuning {
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
+    Knob bitslice_min_rows{5};   // fewest outputs of a row group that take the bitsliced kernel
     Knob bitslice_entries{256};  // matrices with a loaded bitsliced kernel kept (LRU beyond)
     Knob bitslice_depth{0}; //   inputs straight into registers (0, default) or through a per-wave
                             //   LDS ring 2 / 4 deep; tools/c5_prof.py C5_MODES A/B
@@ -429,7 +430,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     *rc = 0;
     const int mode = g_tune.bitslice;
     const int K = map->K;
-    if (!mode || nrows < 5 || nrows > kBsMaxR || K > kBsMaxK || base.copy_records || base.limited ||
+    if (!mode || nrows < g_tune.bitslice_min_rows || nrows > kBsMaxR || K > kBsMaxK || base.copy_records || base.limited ||
         bs < kBsTile)
         return 0;
     ApplyArgs a = base;
@@ -458,7 +459,9 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     for (int j = 0; j < K; j++) b.in_off[j] = a.in_off32[j];
     for (int r = 0; r < nrows; r++) b.out_off[r] = a.out_off32[r];
     // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
-    const int grid = static_cast<int>(std::min<int64_t>(b.ntiles, static_cast<int64_t>(cu_count(map->device)) * 2));
+    // one 4-wave workgroup per wave per SIMD the kernel is built for (2 for 5..8 outputs)
+    const int grid = static_cast<int>(std::min<int64_t>(
+        b.ntiles, static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows)));
     *rc = bitslice_launch(fn, b, grid, st);
     return *rc ? 0 : bs / kBsTile * kBsTile;
 }
@@ -1146,6 +1149,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.multi_list = value;
     } else if (k == "bitslice") {
         g_tune.bitslice = value;
+    } else if (k == "bitslice_min_rows") {
+        g_tune.bitslice_min_rows = value >= 1 && value <= 8 ? value : 5;  // 0 restores the default
     } else if (k == "bitslice_entries") {
         g_tune.bitslice_entries = value >= 1 && value <= 4096 ? value : 256;  // 0 restores the default
     } else if (k == "bitslice_depth") {

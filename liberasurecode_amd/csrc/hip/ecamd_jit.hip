@@ -311,7 +311,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->R = R;
         slot->K = K;
         slot->depth = depth;
-        slot->cap_index = first_cap_index();
+        // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
+        slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R) > 2 ? 2 : 0);
         start_compile(slot, wait);
     }
     const std::shared_ptr<BsEntry> ep = slot;

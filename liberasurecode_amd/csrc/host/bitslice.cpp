@@ -211,6 +211,8 @@ __device__ __forceinline__ void tr16(u32 (&A)[16])
 
 }  // namespace
 
+int bitslice_waves_per_simd(int R) { return R <= 4 ? 4 : 2; }
+
 int bitslice_depth(int depth, int K)
 {
     if (depth < 2) return 0;
@@ -227,7 +229,9 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
       << " inputs, " << net.xor_ops() << " network ops per tile, "
       << (D ? "LDS ring of " + std::to_string(D) + " inputs per wave" : std::string("register loads")) << "\n";
     s << kPrelude;
-    s << "extern \"C\" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))\n"
+    const int wpe = bitslice_waves_per_simd(net.R);
+    s << "extern \"C\" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
+      << wpe << ")))\n"
          "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
     auto ref = [](int v) {
         char b[24];

@@ -57,6 +57,9 @@ struct BitsliceStyle {
 };
 std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
 int bitslice_depth(int depth, int K);
+// Waves per SIMD the kernel of an R-output map is built for: 2 (16 R accumulators + the network
+// in <= 256 VGPRs) for 5..8 outputs, 4 (<= 128 VGPRs) for up to 4.
+int bitslice_waves_per_simd(int R);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth);

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""A/B at C3 (k=10 m=4, 1 MiB, 256 stripes): the LDS-table stream kernel (default for <= 4 outputs)
+against the bitsliced kernel built for 4 waves per SIMD (knob bitslice_min_rows 4), encode and
+decode of data {0,1,2,3}, interleaved rounds, steady launches (HIP events)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+
+from liberasurecode_amd import _lib  # noqa: E402
+from liberasurecode_amd import device as D  # noqa: E402
+
+K, M, F, S = 10, 4, 1 << 20, 256
+LOST = [0, 1, 2, 3]
+
+
+def main(rounds=3, n=30, skip=10):
+    d = _lib.dev()
+    lay = D.Layout.alloc(K + M, F, S)
+    st = D.Stream()
+    lay.fill_splitmix(nfrags=K, stream=st)
+    d.ecamd_tune(b"bitslice", 2)
+    d.ecamd_tune(b"bitslice_min_rows", 4)
+    D.rs_encode(K, M, lay, stream=st)
+    D.rs_decode(K, M, LOST, lay, stream=st)
+    ref = lay.download_stripes()
+    d.ecamd_tune(b"bitslice_min_rows", 0)
+    D.rs_encode(K, M, lay, stream=st)
+    D.rs_decode(K, M, LOST, lay, stream=st)
+    assert (lay.download_stripes() == ref).all()
+    algo = S * (K + M) * F
+    for rnd in range(rounds):
+        for name, rows in (("lds", 0), ("bitslice", 4)):
+            d.ecamd_tune(b"bitslice_min_rows", rows)
+            for op, fn in (("encode", lambda: D.rs_encode(K, M, lay, stream=st)),
+                           ("decode", lambda: D.rs_decode(K, M, LOST, lay, stream=st))):
+                ev = [D.Event() for _ in range(n + 1)]
+                ev[0].record(st)
+                for i in range(n):
+                    fn()
+                    ev[i + 1].record(st)
+                st.synchronize()
+                ms = [ev[i].elapsed_ms(ev[i + 1]) for i in range(skip, n)]
+                avg = sum(ms) / len(ms)
+                print(json.dumps({"round": rnd, "kernel": name, "op": op, "ms": round(avg, 4),
+                                  "frac": round(algo / (avg * 1e-3) / 8e12, 4)}), flush=True)
+    d.ecamd_tune(b"bitslice_min_rows", 0)
+    d.ecamd_tune(b"bitslice", 1)
+
+
+if __name__ == "__main__":
+    main()
