@@ -179,3 +179,22 @@ def test_ring4_many_tiles(sync_compile, k, m, lost):
     """The 4-deep LDS ring (prefetch three inputs ahead, across tile boundaries)."""
     sync_compile.ecamd_tune(b"bitslice_depth", 4)
     test_many_tiles_per_workgroup(sync_compile, k, m, lost)
+
+
+@pytest.mark.parametrize("k,m,bs,rows", [(10, 4, 65536 + 100, 4), (6, 3, 49152, 3)])
+def test_few_output_builds_exact(sync_compile, k, m, bs, rows):
+    """Maps of up to 4 outputs (knob bitslice_min_rows lowered) get the 4-waves-per-SIMD build."""
+    d = sync_compile
+    d.ecamd_tune(b"bitslice_min_rows", rows)
+    try:
+        lay, want = _batch(k, m, bs, 3, seed=41)
+        D.rs_encode(k, m, lay)
+        assert (lay.download_stripes() == want).all()
+        lost = list(range(m))
+        host = want.copy()
+        host[:, lost] = 0x99
+        lay.upload_stripes(host)
+        D.rs_decode(k, m, lost, lay)
+        assert (lay.download_stripes() == want).all()
+    finally:
+        d.ecamd_tune(b"bitslice_min_rows", 0)
