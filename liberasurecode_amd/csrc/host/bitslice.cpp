@@ -1,7 +1,7 @@
 // bitslice.cpp -- network construction and kernel source for bitsliced GF(2^16) maps
 // (bitslice.hpp).  The generated kernel is verified bit-exact against the CPU oracle by
 // tests/test_gpu_bitslice.py; the network itself against GF16 products by
-// tests/test_host_planning.py (ecamd_bitslice_eval).
+// tests/test_bitslice_host.py (ecamd_bitslice_eval).
 #include "bitslice.hpp"
 
 #include <algorithm>
