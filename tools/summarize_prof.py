@@ -3,9 +3,10 @@
 
 Per kernel: launch count and duration statistics from the kernel trace (per-dispatch start / end
 timestamps), plus -- for the bench's dominant kernel -- the same statistics over the TIMED steps
-only: the bench launches it once before the warm-up, twice per warm-up step, twice per timed step,
+only: the bench launches it `--pre` times before the warm-up (2: an encode and a decode, which
+also compile any bitsliced kernel the config needs), twice per warm-up step, twice per timed step,
 then for the untimed mixed-pattern decodes; the timed launches are dispatches
-[1 + 2*warmup, 1 + 2*warmup + 2*steps) of that kernel in dispatch order.  bench.py reads
+[pre + 2*warmup, pre + 2*warmup + 2*steps) of that kernel in dispatch order.  bench.py reads
 "timed_avg_ns" to put the trace-derived roofline fraction beside its HIP-event one.
 
 HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and
@@ -65,6 +66,7 @@ def main():
     ap.add_argument("round")
     ap.add_argument("--kernel", default="", help="dominant kernel (name prefix)")
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--pre", type=int, default=2, help="launches of the kernel before the warm-up")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--stripes", type=int, default=256)
     ap.add_argument("--bench", default="", help="bench JSON log of the profiled command")
@@ -91,7 +93,7 @@ def main():
     for name, lst in by.items():
         d = stats([x[1] for x in lst])
         if args.kernel and args.kernel in name:
-            lo = 1 + 2 * args.warmup
+            lo = args.pre + 2 * args.warmup
             timed = lst[lo:lo + 2 * args.steps]
             timed_ids = {x[0] for x in timed}
             t = stats([x[1] for x in timed])
@@ -145,7 +147,7 @@ def main():
                 # PMC runs are separate processes: use the same position-based timed window
                 vals.sort()
                 if args.kernel and args.kernel in kern:
-                    lo = 1 + 2 * args.warmup
+                    lo = args.pre + 2 * args.warmup
                     sel = [v for _, v in vals[lo:lo + 2 * args.steps]] or [v for _, v in vals]
                 else:
                     sel = [v for _, v in vals]
