@@ -328,7 +328,12 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         int spill = 0;
         if (e.state == 1) {
             hipModule_t mod = nullptr;
-            if (hipModuleLoadData(&mod, e.code.data()) == hipSuccess) {
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            if (cur != dev) (void)hipSetDevice(dev);  // the module belongs to the map's device
+            const hipError_t lrc = hipModuleLoadData(&mod, e.code.data());
+            if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+            if (lrc == hipSuccess) {
                 e.modules.emplace_back(dev, mod);
                 if (hipModuleGetFunction(&fn, mod, "ecamd_bs_kernel") != hipSuccess) fn = nullptr;
                 if (fn && hipFuncGetAttribute(&spill, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) == hipSuccess &&
