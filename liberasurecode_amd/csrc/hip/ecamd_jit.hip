@@ -14,6 +14,7 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <spawn.h>
+#include <signal.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -23,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <fstream>
 #include <map>
 #include <memory>
@@ -76,7 +78,8 @@ std::string helper_path()
     return path;
 }
 
-// Keep the disk cache to the newest $ECAMD_JIT_CACHE_MAX (4096) code objects: run once per process.
+// Keep the disk cache to the newest $ECAMD_JIT_CACHE_MAX (4096) code objects and drop temporaries
+// older than an hour (a compile stopped mid-way): run once per process.
 void prune_cache(const std::string& dir)
 {
     const char* env = std::getenv("ECAMD_JIT_CACHE_MAX");
@@ -85,11 +88,15 @@ void prune_cache(const std::string& dir)
     if (DIR* d = opendir(dir.c_str())) {
         while (const dirent* ent = readdir(d)) {
             const std::string name(ent->d_name);
-            if (name.size() < 4 || name.compare(0, 3, "bs_") != 0 || name.compare(name.size() - 3, 3, ".co") != 0)
-                continue;
+            if (name.compare(0, 3, "bs_") != 0) continue;
             struct stat st {};
             const std::string path = dir + "/" + name;
-            if (stat(path.c_str(), &st) == 0) cos.emplace_back(st.st_mtime, path);
+            if (stat(path.c_str(), &st) != 0) continue;
+            if (name.find(".tmp.") != std::string::npos || name.find(".req.") != std::string::npos) {
+                if (st.st_mtime + 3600 < time(nullptr)) std::remove(path.c_str());  // left by a killed compile
+                continue;
+            }
+            if (name.size() > 3 && name.compare(name.size() - 3, 3, ".co") == 0) cos.emplace_back(st.st_mtime, path);
         }
         closedir(d);
     }
@@ -206,6 +213,17 @@ const std::string& generator_fingerprint()
     return fp;
 }
 
+// At exit, stop the compilers this process started and has not reaped (their results would only
+// land in the cache; a half-written one never does -- jitc renames whole files into place).  The
+// exact PIDs, never a pattern; skipped if another thread holds the lock.
+void stop_children_at_exit()
+{
+    if (!g_jit_mu.try_lock()) return;
+    for (const auto& ep : g_running)
+        if (ep->pid > 0) kill(ep->pid, SIGTERM);
+    g_jit_mu.unlock();
+}
+
 // Start (or skip, when cached) the build of e's kernel at kCaps[e.cap_index]; queue it (state 2)
 // while max_jobs() compilers run, unless `force`.  Caller holds the lock.
 void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
@@ -253,6 +271,8 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
         e.pid = pid;
         e.state = 0;
         g_running.push_back(ep);
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(stop_children_at_exit); });
     }
     posix_spawn_file_actions_destroy(&fa);
 }
