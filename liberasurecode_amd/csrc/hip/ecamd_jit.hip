@@ -215,10 +215,12 @@ const std::string& generator_fingerprint()
 
 // At exit, stop the compilers this process started and has not reaped (their results would only
 // land in the cache; a half-written one never does -- jitc renames whole files into place).  The
-// exact PIDs, never a pattern; skipped if another thread holds the lock.
+// exact PIDs, never a pattern; skipped if another thread holds the lock, or with
+// ECAMD_JIT_DETACH=1 (short-lived processes that want later ones to find the kernels compiled).
 void stop_children_at_exit()
 {
-    if (!g_jit_mu.try_lock()) return;
+    const char* detach = std::getenv("ECAMD_JIT_DETACH");
+    if ((detach && std::atoi(detach)) || !g_jit_mu.try_lock()) return;
     for (const auto& ep : g_running)
         if (ep->pid > 0) kill(ep->pid, SIGTERM);
     g_jit_mu.unlock();
