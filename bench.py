@@ -62,6 +62,8 @@ def parse_args(argv=None):
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 rebuild-8 fields")
+    ap.add_argument("--no-scatter", action="store_true",
+                    help="skip the peer-scatter fields of multi-GPU runs")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--cpu-seconds", type=float, default=2.0,
                     help="target wall seconds of the multi-thread CPU-baseline leg")
@@ -322,6 +324,67 @@ def c5_rebuild(D, stream, reps=20, warm=25):
     return out
 
 
+def peer_scatter(D, stream, home, ndev, S=8, reps=5):
+    """SURVEY §8f f4 on a multi-GPU node (rank 0, after the timed steps): S encoded C3 stripes on
+    this rank's GPU, fragment f of every stripe placed on device f % ndev with
+    ecamd_scatter_fragments (per-destination copy lanes over xGMI), every destination byte checked
+    against the source, then `reps` timed scatters.  Reference anchor: the placement the rs_vand
+    shim's callers do per fragment (src/backends/rs_vand/liberasurecode_rs_vand.c:119-145)."""
+    import ctypes as C
+
+    import torch
+
+    from liberasurecode_amd import _lib
+    k, m, F = 10, 4, 1 << 20
+    h = _lib.dev()
+    f_scatter = h.ecamd_scatter_fragments
+    f_scatter.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lay = D.Layout.alloc(k + m, F, S)
+    lay.fill_splitmix(nfrags=k, stream=stream)
+    D.rs_encode(k, m, lay, stream=stream)
+    stream.synchronize()
+    src = lay.download_stripes()
+    devs = [(home + f) % ndev for f in range(k + m)]
+    bufs = []
+    try:
+        for f in range(k + m):
+            torch.cuda.set_device(devs[f])
+            bufs.append(D.DeviceBuffer(S * F))
+        torch.cuda.set_device(home)
+        args = (lay.buf.ptr, lay.stripe_stride, lay.frag_stride, F, k + m, S, _lib.ints(devs),
+                (C.c_void_p * (k + m))(*[b.ptr for b in bufs]), _lib.i64s([F] * (k + m)),
+                stream.handle)
+
+        def run():
+            _lib.check(f_scatter(*args), "ecamd_scatter_fragments")
+
+        run()
+        stream.synchronize()
+        exact = True
+        for f in range(k + m):
+            torch.cuda.set_device(devs[f])
+            got = bufs[f].download(S * F).reshape(S, F)
+            exact = exact and bool((got == src[:, f]).all())
+        torch.cuda.set_device(home)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        stream.synchronize()
+        dt = time.perf_counter() - t0
+        remote = sum(1 for d in devs if d != home)
+        return {"devices": ndev, "stripes": S, "fragment_bytes": F, "dst_devices": devs,
+                "bytes_exact": exact, "ms": round(dt * 1e3 / reps, 4),
+                "gbs_total": round(reps * S * (k + m) * F / dt / 1e9, 2),
+                "gbs_over_xgmi": round(reps * S * remote * F / dt / 1e9, 2)}
+    finally:
+        for f, b in enumerate(bufs):
+            torch.cuda.set_device(devs[f])
+            b.free()
+        torch.cuda.set_device(home)
+        lay.buf.free()
+
+
 # ------------------------------------------------------------------ main ----
 
 def main():
@@ -504,6 +567,12 @@ def main():
     if rank == 0:
         if not args.no_c5 and args.config == "c3":
             out["c5"] = c5_rebuild(D, stream)
+        ndev = torch.cuda.device_count()
+        if world > 1 and not args.no_scatter:  # (one visible GPU: the all-local rehearsal)
+            try:
+                out["peer_scatter"] = peer_scatter(D, stream, co.device or 0, ndev)
+            except Exception as e:  # evidence only: never costs the bench line
+                out["peer_scatter"] = {"error": str(e)[:300]}
         if not args.no_cpu_baseline and world == 1:
             usable = usable_cores()[0]
             out["cpu_baseline"] = cpu_baseline(k, m, F, missing, args.cpu_threads or usable,

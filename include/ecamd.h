@@ -100,7 +100,9 @@ int ecamd_rs_decode_multi(int k, int m, const int *missing, int missing_stride,
 /* Fragment placement across GPUs: fragment f of every stripe (frag_len bytes at
  * d_src + s*stripe_stride + f*frag_stride on the current device) goes to d_dst[f] +
  * s*dst_stride[f] on device dst_dev[f]: one strided DMA per fragment, over xGMI when dst_dev[f]
- * is a peer (peer access is enabled on first use).  Asynchronous on `stream`. */
+ * is a peer (peer access is enabled on first use).  Copies to different peers run at once on
+ * per-destination copy lanes forked from and joined back into `stream`; every destination is
+ * checked before anything is queued.  Asynchronous on `stream`. */
 int ecamd_scatter_fragments(const void *d_src, int64_t stripe_stride, int64_t frag_stride,
                             int64_t frag_len, int nfrags, int nstripes, const int *dst_dev,
                             void *const *d_dst, const int64_t *dst_stride, void *stream);

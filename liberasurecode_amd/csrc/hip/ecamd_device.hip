@@ -188,6 +188,9 @@ struct Tuning {
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     Knob stream_pf{0};      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
+    Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
+                            //   peers (0), for every destination incl. local ones (1, exercises the
+                            //   fork / join on one-GPU boxes), or none: all on the caller's stream (2)
 };
 Tuning g_tune;
 
@@ -1163,6 +1166,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_nib = std::max(0, std::min(value, 2));
     } else if (k == "stream_pf") {
         g_tune.stream_pf = value != 0;
+    } else if (k == "scatter_lanes") {
+        g_tune.scatter_lanes = std::max(0, std::min(value, 2));
     } else {
         return fail(ECAMD_EINVAL, "unknown tuning key %s", key);
     }
@@ -1450,39 +1455,103 @@ int ecamd_scatter_fragments(const void* d_src, int64_t stripe_stride, int64_t fr
     if (nfrags == 0 || nstripes == 0 || frag_len == 0) return 0;
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
-    static std::mutex mu;
-    static std::vector<std::pair<int, int>> enabled;  // (from, to) peer links already opened
+    // Check every destination before anything is queued: a bad request copies nothing.
     for (int f = 0; f < nfrags; f++) {
         const int to = dst_dev[f];
         if (to < 0 || to >= ndev) return fail(ECAMD_EINVAL, "fragment %d: bad device %d", f, to);
         if (!d_dst[f] || dst_stride[f] < frag_len)
             return fail(ECAMD_EINVAL, "fragment %d: bad destination / stride", f);
-        if (to != dev) {
-            std::lock_guard<std::mutex> lk(mu);
-            if (std::find(enabled.begin(), enabled.end(), std::make_pair(dev, to)) == enabled.end()) {
+    }
+    // Peer links (from, to) opened once per process; copy lanes are per (from, to) streams created
+    // on the source device, so copies to different peers run at once, one xGMI link each, instead
+    // of one after another on the caller's stream.
+    static std::mutex mu;
+    static std::vector<std::pair<int, int>> enabled;
+    static std::map<std::pair<int, int>, hipStream_t> lanes;
+    const int mode = g_tune.scatter_lanes;
+    std::vector<int> order;  // destination devices in first-use order
+    for (int f = 0; f < nfrags; f++)
+        if (std::find(order.begin(), order.end(), dst_dev[f]) == order.end()) order.push_back(dst_dev[f]);
+    std::vector<std::pair<int, hipStream_t>> used;  // (destination, lane) of this call
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (const int to : order) {
+            if (to != dev && std::find(enabled.begin(), enabled.end(), std::make_pair(dev, to)) == enabled.end()) {
                 int can = 0;
-                if (hipDeviceCanAccessPeer(&can, dev, to) != hipSuccess || !can)
-                    return fail(ECAMD_EINVAL, "fragment %d: no peer path from device %d to %d", f,
-                                dev, to);
+                if (hipDeviceCanAccessPeer(&can, dev, to) != hipSuccess || !can) {
+                    int f = 0;
+                    while (dst_dev[f] != to) f++;
+                    return fail(ECAMD_EINVAL, "fragment %d: no peer path from device %d to %d", f, dev, to);
+                }
                 hipError_t e = hipDeviceEnablePeerAccess(to, 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-                    return fail(ECAMD_EHIP, "fragment %d: hipDeviceEnablePeerAccess(%d -> %d): %s",
-                                f, dev, to, hipGetErrorString(e));
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                    int f = 0;
+                    while (dst_dev[f] != to) f++;
+                    return fail(ECAMD_EHIP, "fragment %d: hipDeviceEnablePeerAccess(%d -> %d): %s", f, dev,
+                                to, hipGetErrorString(e));
+                }
                 (void)hipGetLastError();
                 enabled.emplace_back(dev, to);
             }
+            const bool lane = mode == 1 || (mode == 0 && to != dev);
+            if (!lane) continue;
+            hipStream_t& s = lanes[std::make_pair(dev, to)];
+            if (!s) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            used.emplace_back(to, s);
         }
-        // One strided copy per fragment: nstripes rows of frag_len bytes (xGMI DMA when to != dev).
-        const hipError_t e = hipMemcpy2DAsync(
-            d_dst[f], static_cast<size_t>(dst_stride[f]),
-            static_cast<const uint8_t*>(d_src) + f * frag_stride, static_cast<size_t>(stripe_stride),
-            static_cast<size_t>(frag_len), static_cast<size_t>(nstripes), hipMemcpyDefault,
-            static_cast<hipStream_t>(stream));
-        if (e != hipSuccess)
-            return fail(ECAMD_EHIP, "fragment %d -> device %d: hipMemcpy2DAsync: %s", f, to,
-                        hipGetErrorString(e));
     }
-    return 0;
+    const hipStream_t caller = static_cast<hipStream_t>(stream);
+    // fork: every lane starts after the work already queued on the caller's stream
+    hipEvent_t fork = nullptr;
+    if (!used.empty()) {
+        HIP_TRY(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        const hipError_t e = hipEventRecord(fork, caller);
+        if (e != hipSuccess) {
+            (void)hipEventDestroy(fork);
+            return fail(ECAMD_EHIP, "scatter fork: %s", hipGetErrorString(e));
+        }
+    }
+    std::vector<hipEvent_t> joins;
+    auto lane_of = [&](int to) -> hipStream_t {
+        for (const auto& u : used)
+            if (u.first == to) return u.second;
+        return caller;
+    };
+    for (const int to : order) {
+        const hipStream_t s = lane_of(to);
+        if (s != caller) {
+            const hipError_t e = hipStreamWaitEvent(s, fork, 0);
+            if (e != hipSuccess) {
+                rc = fail(ECAMD_EHIP, "device %d lane: hipStreamWaitEvent: %s", to, hipGetErrorString(e));
+                break;
+            }
+        }
+        for (int f = 0; f < nfrags && rc == 0; f++) {
+            if (dst_dev[f] != to) continue;
+            // One strided copy per fragment: nstripes rows of frag_len bytes (xGMI DMA when to != dev).
+            const hipError_t e = hipMemcpy2DAsync(
+                d_dst[f], static_cast<size_t>(dst_stride[f]),
+                static_cast<const uint8_t*>(d_src) + f * frag_stride, static_cast<size_t>(stripe_stride),
+                static_cast<size_t>(frag_len), static_cast<size_t>(nstripes), hipMemcpyDefault, s);
+            if (e != hipSuccess)
+                rc = fail(ECAMD_EHIP, "fragment %d -> device %d: hipMemcpy2DAsync: %s", f, to,
+                          hipGetErrorString(e));
+        }
+        if (s != caller) {  // join: the caller's stream continues once this lane's copies landed
+            hipEvent_t j = nullptr;
+            hipError_t e = hipEventCreateWithFlags(&j, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(j, s);
+            if (e == hipSuccess) e = hipStreamWaitEvent(caller, j, 0);
+            if (j) joins.push_back(j);
+            if (e != hipSuccess && rc == 0)
+                rc = fail(ECAMD_EHIP, "device %d lane: join: %s", to, hipGetErrorString(e));
+        }
+        if (rc) break;
+    }
+    // events may be destroyed while pending: their resources go once they complete
+    for (hipEvent_t j : joins) (void)hipEventDestroy(j);
+    if (fork) (void)hipEventDestroy(fork);
+    return rc;
 }
 
 int ecamd_rs_reconstruct(int k, int m, const int* missing, int dest, void* base,

@@ -31,12 +31,17 @@ def _scatter():
     return f
 
 
-def test_scatter_fragments_round_robin_devices():
+@pytest.mark.parametrize("lanes", [0, 1, 2])
+def test_scatter_fragments_round_robin_devices(lanes):
+    """lanes: copy lanes for peer destinations (0, default), for every destination (1: the
+    fork / join on one-GPU boxes too), none (2: everything on the caller's stream)."""
     ndev = torch.cuda.device_count()
     k, m, bs, S = 10, 4, 65536 + 48, 5
     lay = D.Layout.alloc(k + m, bs, S)
-    lay.fill_splitmix()
-    D.rs_encode(k, m, lay)
+    stream = D.Stream()
+    lay.fill_splitmix(stream=stream)
+    D.rs_encode(k, m, lay, stream=stream)
+    stream.synchronize()
     src = lay.download_stripes()
     devs = [f % ndev for f in range(k + m)]
     strides = [bs + 16 * (f + 1) for f in range(k + m)]
@@ -44,14 +49,22 @@ def test_scatter_fragments_round_robin_devices():
     for f in range(k + m):
         torch.cuda.set_device(devs[f])
         bufs.append(D.DeviceBuffer(S * strides[f]))
+        bufs[-1].zero()
     torch.cuda.set_device(0)
-    rc = _scatter()(lay.buf.ptr, lay.stripe_stride, lay.frag_stride, bs, k + m, S, _lib.ints(devs),
-                    (C.c_void_p * (k + m))(*[b.ptr for b in bufs]), _lib.i64s(strides), None)
-    assert rc == 0, _lib.dev().ecamd_last_error()
-    for d in range(ndev):
-        torch.cuda.set_device(d)
-        D.synchronize()
-    torch.cuda.set_device(0)
+    h = _lib.dev()
+    assert h.ecamd_tune(b"scatter_lanes", lanes) == 0
+    try:
+        # re-encode right before the scatter on the same stream: the lanes must wait for it
+        D.rs_encode(k, m, lay, stream=stream)
+        rc = _scatter()(lay.buf.ptr, lay.stripe_stride, lay.frag_stride, bs, k + m, S,
+                        _lib.ints(devs), (C.c_void_p * (k + m))(*[b.ptr for b in bufs]),
+                        _lib.i64s(strides), stream.handle)
+        assert rc == 0, h.ecamd_last_error()
+        stream.synchronize()  # the join: the caller's stream covers every lane's copies
+    finally:
+        h.ecamd_tune(b"scatter_lanes", 0)
+    # no device-wide synchronize here: the lanes are non-blocking streams, so only the join into
+    # `stream` orders them before these reads
     for f in range(k + m):
         torch.cuda.set_device(devs[f])
         got = bufs[f].download(S * strides[f]).reshape(S, strides[f])[:, :bs]
