@@ -175,7 +175,8 @@ struct Tuning {
     Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
                             // measured best, tools/xor_sweep.py)
     Knob grid_mult{0};      // stream launches: workgroups per resident slot (0: 2 for 4-output
-                            //   passes, else 1; tools/grid_sweep.py)
+                            //   passes of at most 64 tiles per slot, else 1; tools/grid_sweep.py,
+                            //   tools/c3_size_sweep.py)
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
@@ -520,7 +521,13 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             // allow fewer than 4): measured best for this kernel at C2 / C3 / C5.  4-output
             // passes launch twice the resident workgroups (C3 encode / decode 1.2-2.7% faster;
             // C2 7% and C5 2-4% slower that way, so only there)
-            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult : (p.width == 4 ? 2 : 1);
+            // -- up to 64 tiles per resident slot: beyond that (C3 with 512 stripes and more) the
+            // two-pass order loses 2-5% to the single pass (tools/c3_size_sweep.py,
+            // profiles/r02_c3_size_sweep.log)
+            rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4, 1);
+            if (rc) return rc;
+            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
+                                                : (p.width == 4 && g.ntiles <= 64ull * g.grid ? 2 : 1);
             rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4, gm);
             if (rc) return rc;
             a.ntiles = g.ntiles;
@@ -793,7 +800,10 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         int rc;
         if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs) &&
             (p.row0 != 0 || stream_copy_offsets(a, bs))) {
-            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult : (p.width == 4 ? 2 : 1);
+            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4, 1);
+            if (rc) return rc;
+            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
+                                                : (p.width == 4 && g.ntiles <= 64ull * g.grid ? 2 : 1);
             rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4, gm);
             if (rc) return rc;
             a.ntiles = g.ntiles;
