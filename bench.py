@@ -242,6 +242,18 @@ def measured_copy_peak(D, stream, nbytes=1 << 30):
     return best
 
 
+def dispatches_per_pass(k, width, F, S, cus):
+    """Launches of the stream kernel one strided rs_encode / rs_decode pass makes
+    (ecamd_device.hip launch_stream_pass): at most 32 (4-output passes) or 64 tiles per resident
+    workgroup per launch -- a tile is 256 lanes x 16 B of every fragment, 4 workgroups per CU --
+    split as evenly as the stripes allow.  C3 (256 stripes of 1 MiB, 256 CUs): 2."""
+    if width == 8:
+        return 1  # 8-output passes: the bitsliced kernel
+    tiles = S * -(-F // 4096)
+    limit = (32 if width == 4 else 64) * cus * 4
+    return max(1, -(-tiles // limit))
+
+
 def profile_summary(cfg):
     """The committed rocprofv3 evidence for this command (tools/gpu_prof.sh ->
     tools/summarize_prof.py): profiles/<round>_<cfg>_summary.json, newest round first."""
@@ -484,12 +496,16 @@ def main():
     dec_gibs = obj_bytes / GIB / (sum(dec_ms) / len(dec_ms) / 1e3)
     per_rank = co.reduce([enc_gibs if r == rank else 0.0 for r in range(world)] +
                          [dec_gibs if r == rank else 0.0 for r in range(world)], op="sum")
-    # dominant kernel: the stream kernel (C3 encode and decode: 10 in, 4 out per launch)
-    launch_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
-    # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
-    algo_bytes = S * (2 * k + m + len(missing)) * F // 2
-    achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+    # dominant kernel: the stream kernel (C3 encode and decode: 10 in, 4 out per launch); a pass
+    # (one rs_encode / rs_decode call) may run as several launches of it, see dispatches_per_pass
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
+    per_pass = dispatches_per_pass(k, width, F, S, torch.cuda.get_device_properties(
+        torch.cuda.current_device()).multi_processor_count)
+    pass_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
+    launch_ms = pass_ms / per_pass  # HIP events bracket whole passes: gaps between launches count
+    # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
+    algo_bytes = S * (2 * k + m + len(missing)) * F // 2 // per_pass
+    achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     bitsliced = width == 8 and _lib.dev().ecamd_bitslice_available()
     kernel = ("ecamd_bs_kernel" if bitsliced else f"gf16_hybrid_kernel<{(k + 3) // 4}>" if width == 8 else
               f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>")
@@ -519,12 +535,14 @@ def main():
         trace = None
         timed_ns = kd.get("timed_avg_ns")
         if timed_ns:
-            t_algo = algo_bytes * prof_stripes // S
+            t_pass = kd.get("dispatches_per_pass", 1)
+            t_algo = algo_bytes * per_pass // t_pass * prof_stripes // S
             trace = {"source": summ_src, "timed_launches": kd.get("timed_calls"),
+                     "dispatches_per_pass": t_pass,
                      "launch_ms": round(timed_ns / 1e6, 4),
                      "achieved": round(t_algo / timed_ns, 1),
                      "frac": round(t_algo / timed_ns / HBM_PEAK_GBS, 4),
-                     "kernel_ms_per_step": round(2 * timed_ns / 1e6, 4),
+                     "kernel_ms_per_step": round(2 * t_pass * timed_ns / 1e6, 4),
                      "profiled_ms_per_step": (summ or {}).get("ms_per_step")}
         out = {
             "metric": "device-resident encode+decode GiB/s (RS k=10 m=4, 1 MiB frags), 1/2/4/8 GPU"
@@ -556,8 +574,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": summ_src,
                          "launch_ms": round(launch_ms, 4),
-                         "encode_launch_ms": round(sum(enc_ms) / len(enc_ms), 4),
-                         "decode_launch_ms": round(sum(dec_ms) / len(dec_ms), 4),
+                         "dispatches_per_pass": per_pass,
+                         "encode_pass_ms": round(sum(enc_ms) / len(enc_ms), 4),
+                         "decode_pass_ms": round(sum(dec_ms) / len(dec_ms), 4),
                          "copy_peak_measured": round(copy_gbs, 1),
                          "frac_of_measured_copy": round(achieved / copy_gbs, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,

@@ -189,6 +189,9 @@ struct Tuning {
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     Knob stream_pf{0};      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
+    Knob tiles_per_slot{0};   // stream passes: most tiles per resident workgroup in one launch
+                              //   (longer batches run as several launches; 0: 32 for 4-output
+                              //   passes, else 64; tools/slot_sweep.py)
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
                             //   peers (0), for every destination incl. local ones (1, exercises the
                             //   fork / join on one-GPU boxes), or none: all on the caller's stream (2)
@@ -401,6 +404,55 @@ int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3
     return launch_stream_w<8, 1, false>(a, grid, block, lds, st);
 }
 
+// One strided stream pass over a batch.  Within one launch the workgroups drift apart as they go
+// and the tiles in flight spread over more and more of the batch, which costs HBM rate (C3, 2048
+// stripes: one launch 5.34 TB/s, launches of 32 tiles per resident workgroup 5.85; 256 stripes
+// spread over the span of 2048: 5.06-5.22, tools/span_probe.py, tools/slot_sweep.py,
+// profiles/r02_{span_probe,slot_sweep}.log).  So a pass runs as launches of at most tiles_per_slot
+// tiles per resident workgroup -- 32 for 4-output passes (C3 256 stripes: two launches, 0-2%
+// faster than one), 64 for the others (C2 loses 1.5% at 32: its launches are short) -- each
+// starting its workgroups in step again; 4-output launches of at most 64 tiles per slot take
+// twice the resident workgroups (C3 +1.2-2.7%; C2 -7% and C5 -2-4% that way, so only there).
+int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch, bool nib,
+                       int64_t bs, int nstripes, hipStream_t st)
+{
+    const int knob = g_tune.tiles_per_slot;
+    const uint64_t kTilesPerSlot = knob > 0 ? static_cast<uint64_t>(knob) : (width == 4 ? 32 : 64);
+    Geometry g;
+    int rc = geometry(dev, lds_bytes, bs, nstripes, g, ch, 1024, 4, 1);
+    if (rc) return rc;
+    int per = nstripes;  // stripes per launch, as even as the split allows
+    if (g.ntiles > kTilesPerSlot * g.grid) {
+        const uint64_t launches = (g.ntiles + kTilesPerSlot * g.grid - 1) / (kTilesPerSlot * g.grid);
+        per = static_cast<int>((static_cast<uint64_t>(nstripes) + launches - 1) / launches);
+    }
+    for (int s0 = 0; s0 < nstripes; s0 += per) {
+        const int n = std::min(per, nstripes - s0);
+        ApplyArgs c = a;
+        if (a.stripe_list) {
+            c.stripe_list = a.stripe_list + s0;  // stripe indices stay absolute
+        } else {
+            c.in_base = a.in_base + s0 * a.in_stride;
+            c.out_base = a.out_base + s0 * a.out_stride;
+            if (a.copy_records) c.copy_base = a.copy_base + s0 * a.copy_stride;
+        }
+        rc = geometry(dev, lds_bytes, bs, n, g, ch, 1024, 4, 1);
+        if (rc) return rc;
+        const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
+                                            : (width == 4 && g.ntiles <= 64ull * g.grid ? 2 : 1);
+        if (gm != 1) {
+            rc = geometry(dev, lds_bytes, bs, n, g, ch, 1024, 4, gm);
+            if (rc) return rc;
+        }
+        c.ntiles = g.ntiles;
+        c.tiles_per_stripe = g.tiles_per_stripe;
+        c.tile_order = g_tune.stream_order;
+        rc = launch_stream(c, width, ch, g_tune.stream_pf != 0, nib, dim3(g.grid), dim3(g.threads), g.lds, st);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
 template <int W>
 int launch_ptrs_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipStream_t st)
 {
@@ -518,23 +570,9 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             const int ch = (p.width <= 4 && !nib) ? g_tune.stream_ch : 1;
             if (nib) a.tables = map->d_tables + p.nib_offset;
             // 16 waves per CU (4 x 256 threads, or fewer, larger workgroups when the tables
-            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5.  4-output
-            // passes launch twice the resident workgroups (C3 encode / decode 1.2-2.7% faster;
-            // C2 7% and C5 2-4% slower that way, so only there)
-            // -- up to 64 tiles per resident slot: beyond that (C3 with 512 stripes and more) the
-            // two-pass order loses 2-5% to the single pass (tools/c3_size_sweep.py,
-            // profiles/r02_c3_size_sweep.log)
-            rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4, 1);
-            if (rc) return rc;
-            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
-                                                : (p.width == 4 && g.ntiles <= 64ull * g.grid ? 2 : 1);
-            rc = geometry(map->device, nib ? p.nib_bytes : p.bytes, bs, nstripes, g, ch, 1024, 4, gm);
-            if (rc) return rc;
-            a.ntiles = g.ntiles;
-            a.tiles_per_stripe = g.tiles_per_stripe;
-            a.tile_order = g_tune.stream_order;
-            rc = launch_stream(a, p.width, ch, g_tune.stream_pf != 0, nib, dim3(g.grid),
-                               dim3(g.threads), g.lds, st);
+            // allow fewer than 4): measured best for this kernel at C2 / C3 / C5
+            rc = launch_stream_pass(a, map->device, nib ? p.nib_bytes : p.bytes, p.width, ch, nib, bs,
+                                    nstripes, st);
             if (rc) return rc;
             continue;
         }
@@ -800,17 +838,7 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         int rc;
         if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs) &&
             (p.row0 != 0 || stream_copy_offsets(a, bs))) {
-            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4, 1);
-            if (rc) return rc;
-            const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
-                                                : (p.width == 4 && g.ntiles <= 64ull * g.grid ? 2 : 1);
-            rc = geometry(map->device, p.bytes, bs, nstripes, g, 1, 1024, 4, gm);
-            if (rc) return rc;
-            a.ntiles = g.ntiles;
-            a.tiles_per_stripe = g.tiles_per_stripe;
-            a.tile_order = g_tune.stream_order;
-            rc = launch_stream(a, p.width, 1, g_tune.stream_pf != 0, false, dim3(g.grid),
-                               dim3(g.threads), g.lds, st);
+            rc = launch_stream_pass(a, map->device, p.bytes, p.width, 1, false, bs, nstripes, st);
             if (rc) return rc;
             continue;
         }
@@ -1176,6 +1204,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_nib = std::max(0, std::min(value, 2));
     } else if (k == "stream_pf") {
         g_tune.stream_pf = value != 0;
+    } else if (k == "tiles_per_slot") {
+        g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
     } else if (k == "scatter_lanes") {
         g_tune.scatter_lanes = std::max(0, std::min(value, 2));
     } else {

@@ -456,3 +456,34 @@ def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
     for s in range(S):
         assert got[0][s, :size].tobytes() == objs[s]
         assert (got[0][s, size:] == 0xA5).all()
+
+
+@pytest.mark.parametrize("size", [10 << 20, (10 << 20) + 7])
+def test_frame_paths_split_into_launches(F, size):
+    """Copy-through encode and decode-join passes split into several launches (knob
+    tiles_per_slot 1: at most one 4 KiB tile per resident workgroup per launch, so 9 stripes of
+    1 MiB payloads take 3 launches per pass) give the same fragments and objects as one launch."""
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    k, m, S = 10, 4, 9
+    objs = _objects(S, size, 4242 + size)
+    frags, joined = [], []
+    try:
+        for tps in (0, 1):
+            _lib.check(_lib.dev().ecamd_tune(b"tiles_per_slot", tps), "tune")
+            fb = F.FrameBatch(be, k, m, size, S, checksum=ec_api.CHKSUM_CRC32)
+            fb.encode(_upload_objects(objs, fb.obj_stride))
+            frags.append(fb.fragments())
+            stride = (size + 16 + 15) // 16 * 16
+            d = DeviceBuffer(S * stride)
+            d.upload(np.full(S * stride, 0xA5, dtype=np.uint8))
+            fb.decode([0, 3, 10], d, obj_stride=stride)
+            joined.append(d.download().reshape(S, stride))
+    finally:
+        _lib.dev().ecamd_tune(b"tiles_per_slot", 0)
+    assert np.array_equal(frags[0], frags[1])
+    assert np.array_equal(joined[0], joined[1])
+    for s in range(S):
+        assert joined[1][s, :size].tobytes() == objs[s]
+        assert (joined[1][s, size:] == 0xA5).all()

@@ -116,11 +116,22 @@ def test_batched_encode_matches_oracle(k, m, bs, S):
         assert (out[s, k:] == orc.encode(k, m, data)).all()
 
 
+@pytest.mark.parametrize("tiles_per_slot", [0, 1])
 @pytest.mark.parametrize("k,m,bs,S,missing", [
     (10, 4, 1 << 20, 16, [0, 1, 2, 3]), (10, 4, 1 << 20, 16, [0, 5, 10, 13]),
     (20, 8, 1 << 22, 4, list(range(8))), (20, 8, 1 << 20, 4, [0, 2, 4, 6, 20, 22, 24, 26]),
-    (4, 2, 65536, 128, [1, 3])])
-def test_roundtrip_encode_erase_decode(k, m, bs, S, missing):
+    (4, 2, 65536, 128, [1, 3]), (10, 4, (1 << 20) + 40, 7, [2, 11])])
+def test_roundtrip_encode_erase_decode(k, m, bs, S, missing, tiles_per_slot):
+    """tiles_per_slot 1: every pass split into launches of at most one tile per resident
+    workgroup (a few launches each here), as long batches are split by default."""
+    _lib.check(_lib.dev().ecamd_tune(b"tiles_per_slot", tiles_per_slot), "tune")
+    try:
+        _roundtrip(k, m, bs, S, missing)
+    finally:
+        _lib.dev().ecamd_tune(b"tiles_per_slot", 0)
+
+
+def _roundtrip(k, m, bs, S, missing):
     lay = D.Layout.alloc(k + m, bs, S)
     lay.fill_splitmix(nfrags=k, stripe0=5)
     D.rs_encode(k, m, lay)
@@ -137,11 +148,56 @@ def test_roundtrip_encode_erase_decode(k, m, bs, S, missing):
         assert (lay.download_stripes()[:, d] == ref[:, d]).all()
 
 
+def test_long_batch_split_into_launches():
+    """A batch of more than 64 tiles per resident workgroup runs as several stream launches
+    (ecamd_device.hip launch_stream_pass): k=4 m=2, 64 KiB+16 fragments (17 tiles each, the last
+    partial), 5000 stripes = 85000 tiles, so at least two launches on a 256-CU MI355X.  Encode
+    checked against the oracle on stripes around every possible split, strided decode and the
+    stripe-list decode_multi (4000 stripes in one erasure group: split too) on the whole batch."""
+    k, m, bs, S = 4, 2, 65536 + 16, 5000
+    lay = D.Layout.alloc(k + m, bs, S)
+    lay.fill_splitmix(nfrags=k, stripe0=3)
+    D.rs_encode(k, m, lay)
+    ref = lay.download_stripes()
+    rng = np.random.default_rng(7)
+    check = {0, 1, S - 2, S - 1} | set(rng.integers(0, S, 12).tolist())
+    for cus in (128, 256, 304):  # the split point for other CU counts, 4 workgroups per CU
+        b = 64 * cus * 4 // 17
+        check |= {b - 1, b, b + 1}
+    for s in sorted(x for x in check if 0 <= x < S):
+        data = stripe_fragments(3 + s, k, bs)
+        assert (ref[s, :k] == data).all()
+        assert (ref[s, k:] == orc.encode(k, m, data)).all(), s
+    host = ref.copy()
+    host[:, [0, 4]] = 0x5A
+    lay.upload_stripes(host)
+    D.rs_decode(k, m, [0, 4], lay)
+    assert (lay.download_stripes() == ref).all()
+    pats = [[0, 5] if s % 5 == 0 else [1] for s in range(S)]
+    for s, pat in enumerate(pats):
+        host[s] = ref[s]
+        host[s, pat] = 0xA5
+    lay.upload_stripes(host)
+    D.rs_decode_multi(k, m, pats, lay)
+    assert (lay.download_stripes() == ref).all()
+    lay.buf.free()
+
+
+@pytest.mark.parametrize("tiles_per_slot", [0, 1])
 @pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 64), (4, 2, 4096, 200), (20, 8, 8192, 40)])
-def test_decode_multi_heterogeneous(k, m, bs, S):
+def test_decode_multi_heterogeneous(k, m, bs, S, tiles_per_slot):
     """Every stripe lost its own set of fragments (including none, all-parity and
     m-missing cases); one call rebuilds them all, each equal to the oracle's decode of that
-    stripe on the same (inconsistent, garbage-filled) buffers."""
+    stripe on the same (inconsistent, garbage-filled) buffers.  tiles_per_slot 1: the stripe-list
+    launches split into several."""
+    _lib.check(_lib.dev().ecamd_tune(b"tiles_per_slot", tiles_per_slot), "tune")
+    try:
+        _decode_multi_case(k, m, bs, S)
+    finally:
+        _lib.dev().ecamd_tune(b"tiles_per_slot", 0)
+
+
+def _decode_multi_case(k, m, bs, S):
     rng = np.random.default_rng(k * 100 + S)
     lay = D.Layout.alloc(k + m, bs, S)
     lay.fill_splitmix(nfrags=k, stripe0=9)

@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pre", type=int, default=2, help="launches of the kernel before the warm-up")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--per-pass", type=int, default=1,
+                    help="dispatches of the dominant kernel per encode / decode pass (a long pass "
+                         "runs as several launches, ecamd_device.hip launch_stream_pass)")
     ap.add_argument("--stripes", type=int, default=256)
     ap.add_argument("--bench", default="", help="bench JSON log of the profiled command")
     ap.add_argument("--command", default="")
@@ -93,15 +96,20 @@ def main():
     for name, lst in by.items():
         d = stats([x[1] for x in lst])
         if args.kernel and args.kernel in name:
-            lo = args.pre + 2 * args.warmup
-            timed = lst[lo:lo + 2 * args.steps]
+            P = args.per_pass
+            lo = (args.pre + 2 * args.warmup) * P
+            timed = lst[lo:lo + 2 * args.steps * P]
             timed_ids = {x[0] for x in timed}
             t = stats([x[1] for x in timed])
+            passes = [sum(x[1] for x in timed[i:i + P]) for i in range(0, len(timed), P)]
             d.update({"timed_calls": t["calls"], "timed_avg_ns": t["avg_ns"],
                       "timed_min_ns": t["min_ns"], "timed_max_ns": t["max_ns"],
                       "timed_median_ns": t["median_ns"],
+                      "dispatches_per_pass": P,
+                      "timed_pass_avg_ns": round(statistics.mean(passes), 1) if passes else None,
                       "first_dispatch_ns": lst[0][1],
-                      "note": f"timed = dispatches {lo}..{lo + 2 * args.steps - 1} of this kernel"})
+                      "note": f"timed = dispatches {lo}..{lo + 2 * args.steps * P - 1} of this kernel "
+                              f"({P} per pass)"})
         out["kernels"][name] = d
 
     # labelled windows (e.g. the steady-state launches of each C5 operation)
@@ -147,8 +155,8 @@ def main():
                 # PMC runs are separate processes: use the same position-based timed window
                 vals.sort()
                 if args.kernel and args.kernel in kern:
-                    lo = args.pre + 2 * args.warmup
-                    sel = [v for _, v in vals[lo:lo + 2 * args.steps]] or [v for _, v in vals]
+                    lo = (args.pre + 2 * args.warmup) * args.per_pass
+                    sel = [v for _, v in vals[lo:lo + 2 * args.steps * args.per_pass]] or [v for _, v in vals]
                 else:
                     sel = [v for _, v in vals]
                 d[cname] = statistics.mean(sel)
