@@ -192,6 +192,8 @@ struct Tuning {
     Knob tiles_per_slot{0};   // stream passes: most tiles per resident workgroup in one launch
                               //   (longer batches run as several launches; 0: 32 for 4-output
                               //   passes, else 64; tools/slot_sweep.py)
+    Knob xor_tiles_per_slot{64};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
+                                  //   64: (3,3) x 1024 stripes +7%, 10 -> 4 +1%, tools/xor_slot_sweep.py)
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
                             //   peers (0), for every destination incl. local ones (1, exercises the
                             //   fork / join on one-GPU boxes), or none: all on the caller's stream (2)
@@ -413,21 +415,20 @@ int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3
 // faster than one), 64 for the others (C2 loses 1.5% at 32: its launches are short) -- each
 // starting its workgroups in step again; 4-output launches of at most 64 tiles per slot take
 // twice the resident workgroups (C3 +1.2-2.7%; C2 -7% and C5 -2-4% that way, so only there).
-int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch, bool nib,
-                       int64_t bs, int nstripes, hipStream_t st)
+// The stripe ranges of a strided pass split into launches of at most `limit` tiles per resident
+// workgroup (`slots` of them), as even as the stripes allow; launch(args, stripes) per range, the
+// args' bases (or stripe list) moved to the range's first stripe.
+template <class Launch>
+int for_each_launch(const ApplyArgs& a, int nstripes, uint64_t tiles_per_stripe, uint64_t slots,
+                    uint64_t limit, Launch&& launch)
 {
-    const int knob = g_tune.tiles_per_slot;
-    const uint64_t kTilesPerSlot = knob > 0 ? static_cast<uint64_t>(knob) : (width == 4 ? 32 : 64);
-    Geometry g;
-    int rc = geometry(dev, lds_bytes, bs, nstripes, g, ch, 1024, 4, 1);
-    if (rc) return rc;
-    int per = nstripes;  // stripes per launch, as even as the split allows
-    if (g.ntiles > kTilesPerSlot * g.grid) {
-        const uint64_t launches = (g.ntiles + kTilesPerSlot * g.grid - 1) / (kTilesPerSlot * g.grid);
+    const uint64_t ntiles = tiles_per_stripe * static_cast<uint64_t>(nstripes);
+    int per = nstripes;
+    if (limit && ntiles > limit * slots) {
+        const uint64_t launches = (ntiles + limit * slots - 1) / (limit * slots);
         per = static_cast<int>((static_cast<uint64_t>(nstripes) + launches - 1) / launches);
     }
     for (int s0 = 0; s0 < nstripes; s0 += per) {
-        const int n = std::min(per, nstripes - s0);
         ApplyArgs c = a;
         if (a.stripe_list) {
             c.stripe_list = a.stripe_list + s0;  // stripe indices stay absolute
@@ -436,21 +437,32 @@ int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch
             c.out_base = a.out_base + s0 * a.out_stride;
             if (a.copy_records) c.copy_base = a.copy_base + s0 * a.copy_stride;
         }
-        rc = geometry(dev, lds_bytes, bs, n, g, ch, 1024, 4, 1);
-        if (rc) return rc;
-        const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
-                                            : (width == 4 && g.ntiles <= 64ull * g.grid ? 2 : 1);
-        if (gm != 1) {
-            rc = geometry(dev, lds_bytes, bs, n, g, ch, 1024, 4, gm);
-            if (rc) return rc;
-        }
-        c.ntiles = g.ntiles;
-        c.tiles_per_stripe = g.tiles_per_stripe;
-        c.tile_order = g_tune.stream_order;
-        rc = launch_stream(c, width, ch, g_tune.stream_pf != 0, nib, dim3(g.grid), dim3(g.threads), g.lds, st);
+        const int rc = launch(c, std::min(per, nstripes - s0));
         if (rc) return rc;
     }
     return 0;
+}
+
+int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch, bool nib,
+                       int64_t bs, int nstripes, hipStream_t st)
+{
+    const int knob = g_tune.tiles_per_slot;
+    const uint64_t limit = knob > 0 ? static_cast<uint64_t>(knob) : (width == 4 ? 32 : 64);
+    Geometry g;
+    int rc = geometry(dev, lds_bytes, bs, nstripes, g, ch, 1024, 4, 1);
+    if (rc) return rc;
+    return for_each_launch(a, nstripes, g.tiles_per_stripe, g.grid, limit, [&](ApplyArgs& c, int n) {
+        Geometry h;
+        int r = geometry(dev, lds_bytes, bs, n, h, ch, 1024, 4, 1);
+        if (r) return r;
+        const int gm = g_tune.grid_mult > 0 ? g_tune.grid_mult
+                                            : (width == 4 && h.ntiles <= 64ull * h.grid ? 2 : 1);
+        if (gm != 1 && (r = geometry(dev, lds_bytes, bs, n, h, ch, 1024, 4, gm))) return r;
+        c.ntiles = h.ntiles;
+        c.tiles_per_stripe = h.tiles_per_stripe;
+        c.tile_order = g_tune.stream_order;
+        return launch_stream(c, width, ch, g_tune.stream_pf != 0, nib, dim3(h.grid), dim3(h.threads), h.lds, st);
+    });
 }
 
 template <int W>
@@ -646,17 +658,27 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
             if (!PTRS && g_tune.stream && stream_offsets(a, bs)) {
-                // geometry: 256 threads, xor_wgs (default 2) workgroups per CU
+                // geometry: 256 threads, xor_wgs (default 2) workgroups per CU; long passes as
+                // several launches (xor_tiles_per_slot, as launch_stream_pass)
                 const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : 2;
-                g.grid = static_cast<int>(std::min<int64_t>(g.ntiles, static_cast<int64_t>(cu_count(dev)) * wgs));
-                const dim3 grid(std::max(g.grid, 1)), block(g.threads);
-                switch ((a.ncols + 3) / 4) {
-                case 1: hipLaunchKernelGGL((xor_stream_kernel<1>), grid, block, 0, st, a); break;
-                case 2: hipLaunchKernelGGL((xor_stream_kernel<2>), grid, block, 0, st, a); break;
-                case 3: hipLaunchKernelGGL((xor_stream_kernel<3>), grid, block, 0, st, a); break;
-                case 4: hipLaunchKernelGGL((xor_stream_kernel<4>), grid, block, 0, st, a); break;
-                default: hipLaunchKernelGGL((xor_stream_kernel<8>), grid, block, 0, st, a); break;
-                }
+                const int64_t slots = static_cast<int64_t>(cu_count(dev)) * wgs;
+                const int knob = g_tune.xor_tiles_per_slot;
+                rc = for_each_launch(a, nstripes, g.tiles_per_stripe, static_cast<uint64_t>(slots),
+                                     static_cast<uint64_t>(std::max(knob, 0)), [&](ApplyArgs& c, int n) {
+                    c.ntiles = g.tiles_per_stripe * static_cast<uint32_t>(n);
+                    const dim3 grid(static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(c.ntiles, slots)))),
+                        block(g.threads);
+                    switch ((c.ncols + 3) / 4) {
+                    case 1: hipLaunchKernelGGL((xor_stream_kernel<1>), grid, block, 0, st, c); break;
+                    case 2: hipLaunchKernelGGL((xor_stream_kernel<2>), grid, block, 0, st, c); break;
+                    case 3: hipLaunchKernelGGL((xor_stream_kernel<3>), grid, block, 0, st, c); break;
+                    case 4: hipLaunchKernelGGL((xor_stream_kernel<4>), grid, block, 0, st, c); break;
+                    default: hipLaunchKernelGGL((xor_stream_kernel<8>), grid, block, 0, st, c); break;
+                    }
+                    HIP_TRY(hipGetLastError());
+                    return 0;
+                });
+                if (rc) return rc;
             } else {
                 if (a.stripe_list)  // only the stream kernel reads a stripe list
                     return fail(ECAMD_EINVAL, "stripe list on a non-stream xor launch");
@@ -1206,6 +1228,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_pf = value != 0;
     } else if (k == "tiles_per_slot") {
         g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
+    } else if (k == "xor_tiles_per_slot") {
+        g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 64;
     } else if (k == "scatter_lanes") {
         g_tune.scatter_lanes = std::max(0, std::min(value, 2));
     } else {

@@ -121,3 +121,34 @@ def test_xor_batch_rejects_bad_codes_and_patterns(D):
         D.xor_encode(3, 4, 3, lay)  # not a flat_xor_hd code
     with pytest.raises(ECAmdError):
         D.xor_decode(3, 3, 3, [0, 1, 2, 3], lay)  # beyond what hd = 3 recovers
+
+
+def test_xor_batch_split_into_launches(D):
+    """Flat-XOR passes split into several launches (knob xor_tiles_per_slot 1: at most one 4 KiB
+    tile per resident workgroup per launch -- 40 stripes of 17 tiles take 2 launches on a 256-CU
+    MI355X): encode and the stripe-list decode_multi, every stripe against the oracle."""
+    from liberasurecode_amd import _lib
+    k, m, hd, bs, S = 10, 6, 4, 65536 + 6, 40
+    oc = XO.XorCode(k, m, hd)
+    _lib.check(_lib.dev().ecamd_tune(b"xor_tiles_per_slot", 1), "tune")
+    try:
+        host, lay = _batch(D, k, m, bs, S, 99)
+        D.xor_encode(k, m, hd, lay)
+        got = lay.download_stripes()
+        for s in range(S):
+            want = [x.copy() for x in host[s]]
+            for j in range(k, k + m):
+                want[j][:] = 0
+            oc.encode(want)
+            assert all((got[s, i] == want[i]).all() for i in range(k + m)), s
+        pats = _recoverable(k, m, hd, 123, 2)
+        per = [pats[0] if s % 8 else pats[1] for s in range(S)]  # 35 stripes in one list: split
+        host, lay = _batch(D, k, m, bs, S, 100)
+        D.xor_decode_multi(k, m, hd, per, lay, decode_parity=True)
+        got = lay.download_stripes()
+        for s in range(S):
+            want = _zeroed(host[s], per[s])
+            assert oc.decode(want, per[s], 1) == 0
+            assert all((got[s, i] == want[i]).all() for i in range(k + m)), (s, per[s])
+    finally:
+        _lib.dev().ecamd_tune(b"xor_tiles_per_slot", 64)
