@@ -192,6 +192,8 @@ struct Tuning {
     Knob tiles_per_slot{0};   // stream passes: most tiles per resident workgroup in one launch
                               //   (longer batches run as several launches; 0: 32 for 4-output
                               //   passes, else 64; tools/slot_sweep.py)
+    Knob bs_tiles_per_slot{8};    // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
+                                  //   8: C5 x 64 / 128 stripes +2-4%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{64};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
                                   //   64: (3,3) x 1024 stripes +7%, 10 -> 4 +1%, tools/xor_slot_sweep.py)
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
@@ -528,9 +530,26 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     for (int r = 0; r < nrows; r++) b.out_off[r] = a.out_off32[r];
     // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
     // one 4-wave workgroup per wave per SIMD the kernel is built for (2 for 5..8 outputs)
-    const int grid = static_cast<int>(std::min<int64_t>(
-        b.ntiles, static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows)));
-    *rc = bitslice_launch(fn, b, grid, st);
+    const int64_t slots = static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows);
+    // long passes as several launches (bs_tiles_per_slot; as launch_stream_pass)
+    const uint64_t limit = static_cast<uint64_t>(std::max(0, static_cast<int>(g_tune.bs_tiles_per_slot)));
+    int per = nstripes;
+    if (limit && b.ntiles > limit * slots) {
+        const uint64_t launches = (b.ntiles + limit * slots - 1) / (limit * slots);
+        per = static_cast<int>((static_cast<uint64_t>(nstripes) + launches - 1) / launches);
+    }
+    for (int s0 = 0; s0 < nstripes && *rc == 0; s0 += per) {
+        BsArgs c = b;
+        const int n = std::min(per, nstripes - s0);
+        if (b.stripe_list) {
+            c.stripe_list = b.stripe_list + s0;
+        } else {
+            c.in_base = b.in_base + s0 * b.in_stride;
+            c.out_base = b.out_base + s0 * b.out_stride;
+        }
+        c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
+        *rc = bitslice_launch(fn, c, static_cast<int>(std::min<int64_t>(c.ntiles, slots)), st);
+    }
     return *rc ? 0 : bs / kBsTile * kBsTile;
 }
 
@@ -1228,6 +1247,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_pf = value != 0;
     } else if (k == "tiles_per_slot") {
         g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
+    } else if (k == "bs_tiles_per_slot") {
+        g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 8;
     } else if (k == "xor_tiles_per_slot") {
         g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 64;
     } else if (k == "scatter_lanes") {

@@ -104,12 +104,21 @@ def test_knob_off_gives_the_same_bytes(sync_compile):
     assert (a == want).all() and (lay.download_stripes() == want).all()
 
 
+@pytest.mark.parametrize("bs_tps", [8, 1])
 @pytest.mark.parametrize("k,m,lost", [(20, 8, None), (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]), (3, 5, None),
                                       (1, 8, None)])
-def test_many_tiles_per_workgroup(sync_compile, k, m, lost):
+def test_many_tiles_per_workgroup(sync_compile, k, m, lost, bs_tps):
     """ntiles >> workgroups (2 per CU): the same bytes as the LDS-table kernels, which the tests
     above pin to the oracle.  k = 1 and 3 take the shallower ring (prefetch stays within one tile
-    ahead)."""
+    ahead).  bs_tps 1: the pass split into launches of one tile per workgroup (6 here)."""
+    sync_compile.ecamd_tune(b"bs_tiles_per_slot", bs_tps)
+    try:
+        _many_tiles(sync_compile, k, m, lost)
+    finally:
+        sync_compile.ecamd_tune(b"bs_tiles_per_slot", 8)
+
+
+def _many_tiles(sync_compile, k, m, lost):
     bs, S = 1 << 20, 48
     lay = D.Layout.alloc(k + m, bs, S)
     lay.fill_splitmix(nfrags=k if lost is None else k + m, stripe0=11)
@@ -178,7 +187,7 @@ def test_entries_bounded_and_evicted_kernels_reload(sync_compile):
 def test_ring4_many_tiles(sync_compile, k, m, lost):
     """The 4-deep LDS ring (prefetch three inputs ahead, across tile boundaries)."""
     sync_compile.ecamd_tune(b"bitslice_depth", 4)
-    test_many_tiles_per_workgroup(sync_compile, k, m, lost)
+    _many_tiles(sync_compile, k, m, lost)
 
 
 @pytest.mark.parametrize("k,m,bs,rows", [(10, 4, 65536 + 100, 4), (6, 3, 49152, 3)])
