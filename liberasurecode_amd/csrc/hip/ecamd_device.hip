@@ -192,8 +192,8 @@ struct Tuning {
     Knob tiles_per_slot{0};   // stream passes: most tiles per resident workgroup in one launch
                               //   (longer batches run as several launches; 0: 32 for 4-output
                               //   passes, else 64; tools/slot_sweep.py)
-    Knob bs_tiles_per_slot{8};    // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
-                                  //   8: C5 x 64 / 128 stripes +2-4%, tools/bs_slot_sweep.py)
+    Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
+                                  //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{64};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
                                   //   64: (3,3) x 1024 stripes +7%, 10 -> 4 +1%, tools/xor_slot_sweep.py)
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
@@ -1248,7 +1248,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "tiles_per_slot") {
         g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
     } else if (k == "bs_tiles_per_slot") {
-        g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 8;
+        g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {
         g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 64;
     } else if (k == "scatter_lanes") {

@@ -104,7 +104,7 @@ def test_knob_off_gives_the_same_bytes(sync_compile):
     assert (a == want).all() and (lay.download_stripes() == want).all()
 
 
-@pytest.mark.parametrize("bs_tps", [8, 1])
+@pytest.mark.parametrize("bs_tps", [16, 1])
 @pytest.mark.parametrize("k,m,lost", [(20, 8, None), (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]), (3, 5, None),
                                       (1, 8, None)])
 def test_many_tiles_per_workgroup(sync_compile, k, m, lost, bs_tps):
@@ -115,7 +115,7 @@ def test_many_tiles_per_workgroup(sync_compile, k, m, lost, bs_tps):
     try:
         _many_tiles(sync_compile, k, m, lost)
     finally:
-        sync_compile.ecamd_tune(b"bs_tiles_per_slot", 8)
+        sync_compile.ecamd_tune(b"bs_tiles_per_slot", 16)
 
 
 def _many_tiles(sync_compile, k, m, lost):

@@ -57,7 +57,7 @@ def main():
             print(json.dumps({"S": S, "bs_tiles_per_slot": lim, "op": op, "ms": round(med, 4),
                               "frac": round(algo / (med * 1e-3) / 8e12, 4)}), flush=True)
         lay.buf.free()
-    d.ecamd_tune(b"bs_tiles_per_slot", 8)  # the library default
+    d.ecamd_tune(b"bs_tiles_per_slot", 16)  # the library default
     d.ecamd_tune(b"bitslice", 1)
 
 
