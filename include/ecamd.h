@@ -38,9 +38,11 @@ int ecamd_device_count(void);
 int ecamd_get_device(int *dev);
 int ecamd_set_device(int dev);
 const char *ecamd_last_error(void);
-/* Launch-geometry knobs for sweeps ("threads", "wgs_per_cu", "nt", ...; every setting produces
- * bit-identical results, only the launch shape changes); 0 restores the default.  Safe to call
- * while other threads launch: each launch reads each knob once. */
+/* Launch-geometry knobs for sweeps ("threads", "wgs_per_cu", "nt", "grid_mult", "tiles_per_slot",
+ * "xor_tiles_per_slot", "bs_tiles_per_slot", "scatter_lanes", ...; every setting produces
+ * bit-identical results, only the launch shape changes); 0 restores the default (for
+ * xor_ / bs_tiles_per_slot 0 means one launch per pass, a negative value the default).  Safe to
+ * call while other threads launch: each launch reads each knob once. */
 int ecamd_tune(const char *key, int value);
 
 /* Bitsliced 8-output passes (hip/ecamd_jit.hip): 1 if run-time compilation (hiprtc) is usable;

@@ -47,3 +47,21 @@ def test_single_rank_dry_run():
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1 and line["stripes_per_rank"] == [256]
+
+
+@pytest.mark.parametrize("k,width,F,S,cus,want", [
+    (10, 4, 1 << 20, 256, 256, 2),     # C3: 65536 tiles, 32 per slot x 1024 slots -> 2 launches
+    (10, 4, 1 << 20, 128, 256, 1),
+    (10, 4, 1 << 20, 2048, 256, 16),   # strong scaling at one GPU
+    (10, 4, (1 << 20) + 6, 256, 256, 3),  # a partial tile per fragment
+    (4, 2, 64 << 10, 4096, 256, 1),    # C2: 64 per slot
+    (4, 2, 64 << 10, 8192, 256, 2),
+    (20, 8, 4 << 20, 32, 256, 1),      # C5: the bitsliced kernel
+])
+def test_bench_dispatches_per_pass(k, width, F, S, cus, want):
+    """bench.py's count of stream-kernel launches per pass mirrors launch_stream_pass
+    (ecamd_device.hip): at most 32 (4-output) / 64 tiles of 256 lanes x 16 B per resident
+    workgroup (4 per CU) per launch."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.dispatches_per_pass(k, width, F, S, cus) == want
