@@ -56,6 +56,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle", type=int, default=60,
+                    help="untimed steps before the warm-up steps (clock ramp-up; reported)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=0,
                     help="stripes per GPU (weak) or in total (strong); 0 = the config's")
@@ -470,6 +472,14 @@ def main():
         if i is not None:
             ev[i][2].record(stream)
 
+    # Settle: the GPU leaves its idle clocks only after tens of ms of sustained load (C3 at warm-up
+    # 2 / 5 / 20 / 80 steps: 0.70 / 0.72 / 0.739 / 0.741 of 8 TB/s, profiles/r02_warmup_sweep.log),
+    # so a fixed number of untimed steps runs before the W warm-up steps; reported in the line.
+    settle_t0 = time.perf_counter()
+    for _ in range(args.settle):
+        step()
+    stream.synchronize()
+    settle_ms = (time.perf_counter() - settle_t0) * 1e3
     for _ in range(args.warmup):
         step()
     stream.synchronize()
@@ -552,6 +562,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"steps": args.settle, "ms": round(settle_ms, 1),
+                       "note": "untimed steps before the warm-up: the GPU's clocks ramp under sustained load"},
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": args.scaling,

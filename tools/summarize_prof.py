@@ -3,10 +3,12 @@
 
 Per kernel: launch count and duration statistics from the kernel trace (per-dispatch start / end
 timestamps), plus -- for the bench's dominant kernel -- the same statistics over the TIMED steps
-only: the bench launches it `--pre` times before the warm-up (2: an encode and a decode, which
-also compile any bitsliced kernel the config needs), twice per warm-up step, twice per timed step,
+only: the bench launches it `--pre` times before the settle steps (2: an encode and a decode, which
+also compile any bitsliced kernel the config needs), twice per settle step (`--settle`, bench.py's
+untimed clock ramp-up), twice per warm-up step, twice per timed step,
 then for the untimed mixed-pattern decodes; the timed launches are dispatches
-[pre + 2*warmup, pre + 2*warmup + 2*steps) of that kernel in dispatch order.  bench.py reads
+[pre + 2*(settle + warmup), pre + 2*(settle + warmup) + 2*steps) of that kernel in dispatch order
+(times --per-pass when a pass is several launches).  bench.py reads
 "timed_avg_ns" to put the trace-derived roofline fraction beside its HIP-event one.
 
 HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and
@@ -66,6 +68,7 @@ def main():
     ap.add_argument("round")
     ap.add_argument("--kernel", default="", help="dominant kernel (name prefix)")
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle", type=int, default=60, help="bench.py's untimed settle steps")
     ap.add_argument("--pre", type=int, default=2, help="launches of the kernel before the warm-up")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--per-pass", type=int, default=1,
@@ -97,7 +100,7 @@ def main():
         d = stats([x[1] for x in lst])
         if args.kernel and args.kernel in name:
             P = args.per_pass
-            lo = (args.pre + 2 * args.warmup) * P
+            lo = (args.pre + 2 * (args.settle + args.warmup)) * P
             timed = lst[lo:lo + 2 * args.steps * P]
             timed_ids = {x[0] for x in timed}
             t = stats([x[1] for x in timed])
@@ -155,7 +158,7 @@ def main():
                 # PMC runs are separate processes: use the same position-based timed window
                 vals.sort()
                 if args.kernel and args.kernel in kern:
-                    lo = (args.pre + 2 * args.warmup) * args.per_pass
+                    lo = (args.pre + 2 * (args.settle + args.warmup)) * args.per_pass
                     sel = [v for _, v in vals[lo:lo + 2 * args.steps * args.per_pass]] or [v for _, v in vals]
                 else:
                     sel = [v for _, v in vals]
