@@ -114,7 +114,6 @@ int ensure_device(int* dev_out)
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4, MB>),               \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5, MB>)
         const void* fk[] = {KF_(2, 1), KF_(4, 1), KF_(8, 1), KF_(2, 4), KF_(4, 4), KF_(8, 4),
-                            KF_(2, 5), KF_(4, 5), KF_(8, 5),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<1>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
@@ -167,7 +166,6 @@ struct Tuning {
     Knob frame_crc_wgs{0};    //   512-thread workgroups per CU (0 = 2)
     Knob frame_crc_units{0};  //   work units (stripe ranges) per CU to aim for (0 = 4)
     Knob frame_crc_mb{0};     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
-    Knob frame_crc_pair{1};   //   fused framed encode: tile pairs (one shift map per two tiles)
     Knob frame_unfused{0};  // framed encode: 1 = always split then encode (A/B against copy-through)
     Knob crc_gap_bits{8};   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     Knob crc_span_kib{128}; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
@@ -234,7 +232,6 @@ int dev_tune(const char* key)
     if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
     if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
-    if (k == "frame_crc_pair") return g_tune.frame_crc_pair;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
 }
@@ -1002,8 +999,7 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     if (k > 4 * kStreamGroups || !stream_offsets(a, bs) || !stream_copy_offsets(a, bs)) return ECAMD_EINVAL;
     const int kg = (k + 3) / 4;
     const int ns = 4 * kg + p.width;
-    if (mb != 1 && mb != 4 && mb != 5) return ECAMD_EINVAL;
-    if (mb == 5 && ((bs / kTile) / q) % 2) return ECAMD_EINVAL;  // tile pairs: an even range
+    if (mb != 1 && mb != 4) return ECAMD_EINVAL;
     const size_t lds = fused_crc_lds(k, m, mb);
     if (lds != p.bytes + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4) return ECAMD_EINVAL;
     if (lds > static_cast<size_t>(kLdsBytes)) return ECAMD_EINVAL;
@@ -1025,11 +1021,11 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     default: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 5, MB>), grid, block, lds, st, a, c); break;       \
     }
     if (p.width == 2) {
-        if (mb == 5) { ECAMD_FUSED(2, 5) } else if (mb == 4) { ECAMD_FUSED(2, 4) } else { ECAMD_FUSED(2, 1) }
+        if (mb == 4) { ECAMD_FUSED(2, 4) } else { ECAMD_FUSED(2, 1) }
     } else if (p.width == 4) {
-        if (mb == 5) { ECAMD_FUSED(4, 5) } else if (mb == 4) { ECAMD_FUSED(4, 4) } else { ECAMD_FUSED(4, 1) }
+        if (mb == 4) { ECAMD_FUSED(4, 4) } else { ECAMD_FUSED(4, 1) }
     } else {
-        if (mb == 5) { ECAMD_FUSED(8, 5) } else if (mb == 4) { ECAMD_FUSED(8, 4) } else { ECAMD_FUSED(8, 1) }
+        if (mb == 4) { ECAMD_FUSED(8, 4) } else { ECAMD_FUSED(8, 1) }
     }
 #undef ECAMD_FUSED
     HIP_TRY(hipGetLastError());
@@ -1213,8 +1209,6 @@ int ecamd_tune(const char* key, int value)
         g_tune.crc_pos = value;  // 0 off, anything else on
     } else if (k == "frame_crc_wgs") {
         g_tune.frame_crc_wgs = std::max(0, std::min(value, 4));
-    } else if (k == "frame_crc_pair") {
-        g_tune.frame_crc_pair = value;  // 0 off, anything else on
     } else if (k == "frame_crc_mb") {
         g_tune.frame_crc_mb = value;
     } else if (k == "frame_crc_units") {

@@ -341,11 +341,6 @@ int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64
     // fused kernel, where the LDS also serves the codec; MB = 1 when the larger image does not fit
     int mb = dev_tune("frame_crc_mb") == 1 ? 1 : 4;
     if (mb == 4 && fused_crc_lds(c.k, c.m, 4) > static_cast<size_t>(kLdsBytes)) mb = 1;
-    // tile pairs (one A^2T shift per two tiles: 20 instead of 24 lookups per piece) when the range
-    // has an even number of tiles and two workgroups per CU still fit the larger image
-    if (mb == 4 && dev_tune("frame_crc_pair") != 0 && (tiles / q) % 2 == 0 &&
-        2 * fused_crc_lds(c.k, c.m, 5) <= static_cast<size_t>(kLdsBytes))
-        mb = 5;
     if ((rc = fused_image(dev, legacy, mb, &img))) return rc;
     rc = rs_encode_copy_crc(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
                             partial, q, stream, mb);

@@ -32,35 +32,11 @@ using crcdev::piece_r0;
 
 constexpr int kMap4 = 128;  // one G=4 field-table map (8 x 16 words)
 
-// The CRC tables a tile's state steps read (all in LDS): piece tables r0 and the one-tile shift
-// A^T; with tile pairs also the piece tables one tile further back (A^T r0) and A^2T.
-struct CrcTabs {
-    const uint32_t* piece;
-    const uint32_t* gap;
-    const uint32_t* piece_back;
-    const uint32_t* gap2;
-};
-
-// One 16-byte piece into its fragment's lane state.  PH < 0: s = A^T s ^ r0(x), one step per tile.
-// Tile pairs (PH 0, 1: the two tiles x0, x1 of a pair): s = A^2T s ^ A^T r0(x0) ^ r0(x1), the state
-// shifted by both tiles at the first one (linearity), so the second only adds its r0 -- one shift
-// map per two tiles: 20 instead of 24 LDS lookups per piece on average, no extra registers.
-template <int PH, int MB>
-__device__ __forceinline__ void crc_step(const CrcTabs& c, uint32_t& s, v4u x)
-{
-    if constexpr (PH < 0)
-        s = lmap<4>(c.gap, s) ^ piece_r0<MB>(c.piece, x);
-    else if constexpr (PH == 0)
-        s = lmap<4>(c.gap2, s) ^ piece_r0<MB>(c.piece_back, x);
-    else
-        s ^= piece_r0<MB>(c.piece, x);
-}
-
 // MB: byte tables for the first MB dwords of a piece, nibble tables for the rest (crcdev).
-template <int W, int G, int KG, int MB, int PH>
-__device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* lds, const CrcTabs& c,
-                                            const StreamTile& t, uint32_t (&acc)[8][W / 2],
-                                            uint32_t (&st)[4 * KG + W])
+template <int W, int G, int KG, int MB>
+__device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* lds, const uint32_t* ctab,
+                                            const uint32_t* gap, const StreamTile& t,
+                                            uint32_t (&acc)[8][W / 2], uint32_t (&st)[4 * KG + W])
 {
     v4u x[4];
 #pragma unroll
@@ -74,70 +50,36 @@ __device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* l
         const int j = 4 * G + i;
         if (j < a.ncols) {  // wave-uniform
             __builtin_amdgcn_raw_buffer_store_b128(x[i], t.rcopy, a.copy_off32[j] + t.off, 0, 2);
-            crc_step<PH, MB>(c, st[j], x[i]);
+            st[j] = lmap<4>(gap, st[j]) ^ piece_r0<MB>(ctab, x[i]);
         }
     }
     if (4 * G + 0 < a.ncols) mac_chunk_imm<W, 4 * G + 0>(lds, x[0], acc);
     if (4 * G + 1 < a.ncols) mac_chunk_imm<W, 4 * G + 1>(lds, x[1], acc);
     if (4 * G + 2 < a.ncols) mac_chunk_imm<W, 4 * G + 2>(lds, x[2], acc);
     if (4 * G + 3 < a.ncols) mac_chunk_imm<W, 4 * G + 3>(lds, x[3], acc);
-    if constexpr (G + 1 < KG) fused_group<W, G + 1, KG, MB, PH>(a, lds, c, t, acc, st);
-}
-
-// One tile of every fragment: codec + copy-through + the CRC steps of all its pieces.
-template <int W, int KG, int MB, int PH>
-__device__ __forceinline__ void fused_tile(const ApplyArgs& a, const uint8_t* lds, const CrcTabs& c,
-                                           const StreamTile& t, __amdgpu_buffer_rsrc_t rout,
-                                           uint32_t (&st)[4 * KG + W])
-{
-    constexpr int D = W / 2;
-    uint32_t acc[8][D];
-#pragma unroll
-    for (int w = 0; w < 8; w++)
-#pragma unroll
-        for (int d = 0; d < D; d++) acc[w][d] = 0u;
-    fused_group<W, 0, KG, MB, PH>(a, lds, c, t, acc, st);
-#pragma unroll
-    for (int o = 0; o < W; o++) {
-        if (o >= a.nrows) break;
-        v4u v;
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-            const uint32_t A = acc[2 * d][o >> 1], B = acc[2 * d + 1][o >> 1];
-            v[d] = (o & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(v, rout, a.out_off32[o] + t.off, 0, 2);
-        crc_step<PH, MB>(c, st[4 * KG + o], v);
-    }
+    if constexpr (G + 1 < KG) fused_group<W, G + 1, KG, MB>(a, lds, ctab, gap, t, acc, st);
 }
 
 }  // namespace
 
-// MB 1 / 4: byte tables for the first MB dwords of a piece; MB 5: all-byte tables and tile pairs.
 template <int W, int KG, int MB>
-__global__ void __launch_bounds__(512, 4) gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c)
+__global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c)
 {
-    constexpr bool PAIR = MB == 5;
-    constexpr int PMB = PAIR ? 4 : MB;
-    constexpr int kPieceWords = crcdev::piece_words(PMB);
+    constexpr int kPieceWords = crcdev::piece_words(MB);
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int D = W / 2;
     constexpr int EB = 2 * W;
     constexpr int NS = 4 * KG + W;  // state slots: inputs 0 .. 4KG-1, outputs 4KG .. 4KG+W-1
     const int tbytes = a.ncols * 512 * EB;
     for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
         *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
     uint32_t* ctab = reinterpret_cast<uint32_t*>(lds + tbytes);
-    // pieces | gap | 6 levels | A^1024 [| pieces one tile back | A^2T]
-    constexpr int cwords = kPieceWords + 8 * kMap4 + (PAIR ? kPieceWords + kMap4 : 0);
+    constexpr int cwords = kPieceWords + 8 * kMap4;  // pieces | gap | 6 levels | A^1024
     for (int i = threadIdx.x; i < cwords; i += blockDim.x) ctab[i] = c.img[i];
     uint32_t* xch = ctab + cwords;  // [wave][NS] lane-0 states of each wave
     __syncthreads();
-    CrcTabs tabs;
-    tabs.piece = ctab;
-    tabs.gap = ctab + kPieceWords;
-    tabs.piece_back = ctab + kPieceWords + 8 * kMap4;
-    tabs.gap2 = tabs.piece_back + kPieceWords;
-    const uint32_t* level = tabs.gap + kMap4;
+    const uint32_t* gap = ctab + kPieceWords;
+    const uint32_t* level = gap + kMap4;
     const uint32_t* a1024 = level + 6 * kMap4;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
     const int cstride = static_cast<int>(blockDim.x) * 16;
@@ -161,18 +103,25 @@ __global__ void __launch_bounds__(512, 4) gf16_frame_crc_kernel(const ApplyArgs 
         uint32_t st[NS];
 #pragma unroll
         for (int f = 0; f < NS; f++) st[f] = 0u;
-        const int t0 = static_cast<int>(r) * c.per, t1 = static_cast<int>(r + 1) * c.per;
-        if constexpr (PAIR) {  // the host only picks MB 5 for an even `per`
-            for (int t = t0; t < t1; t += 2) {
-                tile.off = t * cstride + static_cast<int>(threadIdx.x) * 16;
-                fused_tile<W, KG, PMB, 0>(a, lds, tabs, tile, rout, st);
-                tile.off += cstride;
-                fused_tile<W, KG, PMB, 1>(a, lds, tabs, tile, rout, st);
-            }
-        } else {
-            for (int t = t0; t < t1; t++) {
-                tile.off = t * cstride + static_cast<int>(threadIdx.x) * 16;
-                fused_tile<W, KG, PMB, -1>(a, lds, tabs, tile, rout, st);
+        for (int t = static_cast<int>(r) * c.per; t < static_cast<int>(r + 1) * c.per; t++) {
+            tile.off = t * cstride + static_cast<int>(threadIdx.x) * 16;
+            uint32_t acc[8][D];
+#pragma unroll
+            for (int w = 0; w < 8; w++)
+#pragma unroll
+                for (int d = 0; d < D; d++) acc[w][d] = 0u;
+            fused_group<W, 0, KG, MB>(a, lds, ctab, gap, tile, acc, st);
+#pragma unroll
+            for (int o = 0; o < W; o++) {
+                if (o >= a.nrows) break;
+                v4u v;
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    const uint32_t A = acc[2 * d][o >> 1], B = acc[2 * d + 1][o >> 1];
+                    v[d] = (o & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(v, rout, a.out_off32[o] + tile.off, 0, 2);
+                st[4 * KG + o] = lmap<4>(gap, st[4 * KG + o]) ^ piece_r0<MB>(ctab, v);
             }
         }
         // lanes of a wave -> the wave's 1 KiB segment end (the crc_partial_kernel butterfly)
@@ -209,7 +158,6 @@ __global__ void __launch_bounds__(512, 4) gf16_frame_crc_kernel(const ApplyArgs 
     template __global__ void gf16_frame_crc_kernel<W, 5, MB>(const ApplyArgs, const FusedCrcArgs);
 ECAMD_FUSED_INST(2, 1) ECAMD_FUSED_INST(4, 1) ECAMD_FUSED_INST(8, 1)
 ECAMD_FUSED_INST(2, 4) ECAMD_FUSED_INST(4, 4) ECAMD_FUSED_INST(8, 4)
-ECAMD_FUSED_INST(2, 5) ECAMD_FUSED_INST(4, 5) ECAMD_FUSED_INST(8, 5)
 #undef ECAMD_FUSED_INST
 
 }  // namespace ecamd

@@ -62,11 +62,6 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
                        const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb = 1);
 size_t fused_crc_lds(int k, int m, int mb);  // LDS bytes of the fused framed encode
 // fused image words with byte tables for the first mb dwords of a piece, nibble tables after
-// mb 1 / 4: byte tables for the first mb dwords of a piece; 5: all-byte plus the tile-pair tables
-// (pieces one tile back, A^2T) of gf16_frame_crc_kernel<W, KG, 5>
-constexpr int crc_fused_words(int mb = 1)
-{
-    return mb == 5 ? crc_fused_words(4) + 4 * 1024 + 128 : mb * 1024 + (4 - mb) * 128 + 8 * 128;
-}
+constexpr int crc_fused_words(int mb = 1) { return mb * 1024 + (4 - mb) * 128 + 8 * 128; }
 
 }  // namespace ecamd

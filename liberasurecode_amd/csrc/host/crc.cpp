@@ -91,16 +91,6 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
 
 std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb)
 {
-    if (mb == 5) {  // all-byte image + tile pairs: the piece tables shifted one tile back, A^2T
-        std::vector<uint32_t> w = build_fused_crc_image(m, tile_bytes, 4);
-        const size_t pw = 4 * 4 * 256;
-        const auto back = zero_shift(m, tile_bytes);  // r0 of a piece one tile before the next
-        for (size_t i = 0; i < pw; i++) w.push_back(back.apply(w[i]));
-        const size_t at = w.size();
-        w.resize(at + 128, 0);
-        field_tables(zero_shift(m, 2 * tile_bytes), 4, w.data() + at);
-        return w;
-    }
     // piece tables first: byte tables for the first mb dwords (B = 4 + mb; 8 = all four)
     const CrcImage pieces = build_crc_image(m, mb == 4 ? 8 : 4 + mb, 4, 4, false);
     size_t pw = static_cast<size_t>(mb) * 4 * 256 + static_cast<size_t>(4 - mb) * 8 * 16;

@@ -31,8 +31,6 @@ def main():
     ap.add_argument("--stripes", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fused-sweep", action="store_true")
-    ap.add_argument("--pair-sweep", action="store_true",
-                    help="fused CRC encode with and without tile pairs (frame_crc_pair), interleaved")
     ap.add_argument("--align", type=int, default=128, help="payload alignment of the fragment batch")
     ap.add_argument("--no-crc-sweep", action="store_true")
     ap.add_argument("--grid-mult", type=int, default=0, help="grid_mult tuning (0 = library default)")
@@ -81,21 +79,6 @@ def main():
                           "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms / 1e6, 1)}),
               flush=True)
     d.ecamd_tune(b"frame_unfused", 0)
-    if args.pair_sweep:  # fused CRC encode: one state shift per tile vs per two tiles
-        fb.checksum = frame.CHKSUM_CRC32
-        res = {0: [], 1: []}
-        for _ in range(5):
-            for pair in (0, 1):
-                d.ecamd_tune(b"frame_crc_pair", pair)
-                res[pair].append(timed(lambda: fb.encode(obj, stream=st), st, args.reps))
-        d.ecamd_tune(b"frame_crc_pair", 1)
-        for pair, ms in res.items():
-            ms.sort()
-            print(json.dumps({"op": "frame_encode_fused_crc", "pair": pair, "ms_median": round(ms[len(ms) // 2], 4),
-                              "ms_all": [round(x, 4) for x in ms],
-                              "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms[len(ms) // 2] / 1e6, 1)}),
-                  flush=True)
-        return
     if args.fused_sweep:  # fused CRC encode geometry: workgroups per CU x work units per CU
         fb.checksum = frame.CHKSUM_CRC32
         for mb, wgs, units in [(b, w, u) for _ in range(2) for b in (1, 4) for w in (2, 3)
