@@ -269,6 +269,18 @@ def profile_summary(cfg):
     return None, None
 
 
+def _profile_world(command):
+    """--gpus N of the profiled command line (1 when absent)."""
+    parts = command.split()
+    for i, p in enumerate(parts[:-1]):
+        if p == "--gpus":
+            try:
+                return int(parts[i + 1])
+            except ValueError:
+                return None
+    return 1
+
+
 def kernel_entry(summ, kernel):
     for name, d in (summ or {}).get("kernels", {}).items():
         if kernel in name:
@@ -411,7 +423,13 @@ def main():
         os.environ.setdefault("ECAMD_DIST_BACKEND", "gloo")
     from liberasurecode_amd.shard import Coordinator, split_range, stripe_range
 
-    co = Coordinator()  # one process per GPU; RCCL only for the barrier and time reductions
+    # one process per GPU; RCCL only for the barrier and time reductions.  Device identities are
+    # all-gathered over gloo first; ranks that landed on one GPU fail here, named (shard.py)
+    try:
+        co = Coordinator()
+    except Exception as e:
+        sys.stderr.write(f"bench.py: coordinator setup failed: {e}\n")
+        sys.exit(2)
     world, rank = co.world, co.rank
     ranks_seen = int(co.reduce([1.0], op="sum")[0])
     if ranks_seen != world:
@@ -438,7 +456,9 @@ def main():
                               "scaling": args.scaling, "total_stripes": total_stripes,
                               "stripes_per_rank": [int(x) for x in co.reduce(
                                   [float(S) if r == rank else 0.0 for r in range(world)], "sum")],
-                              "covered_once": True}), flush=True)
+                              "covered_once": True, "coord_backend": co.coord_backend,
+                              "devices": co.devices, "shared_devices": co.shared_devices}),
+                  flush=True)
         else:
             co.reduce([float(S) if r == rank else 0.0 for r in range(world)], "sum")
         co.close()
@@ -520,31 +540,45 @@ def main():
     kernel = ("ecamd_bs_kernel" if bitsliced else f"gf16_hybrid_kernel<{(k + 3) // 4}>" if width == 8 else
               f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>")
 
+    # The survey's second decode pattern per config, outside the timed steps:
+    # erasures mixing data and parity.  Every rank decodes its own shard at once (as in the timed
+    # steps), so at N > 1 the figure is per GPU under the same concurrent load.
+    mixed = MIXED_PATTERNS.get(args.config)
+    mixed_gibs = None
+    per_rank_mixed = None
+    if mixed is not None:
+        D.rs_decode(k, m, mixed, lay, stream=stream)
+        stream.synchronize()
+        co.barrier()
+        a, b = D.Event(), D.Event()
+        a.record(stream)
+        for _ in range(5):
+            D.rs_decode(k, m, mixed, lay, stream=stream)
+        b.record(stream)
+        stream.synchronize()
+        mixed_gibs = obj_bytes / GIB / (a.elapsed_ms(b) / 5 / 1e3)
+        per_rank_mixed = co.reduce([mixed_gibs if r == rank else 0.0 for r in range(world)], "sum")
+    co.barrier()
+
     out = None
     if rank == 0:
         copy_gbs = measured_copy_peak(D, stream)
-        # The survey's second decode pattern per config, outside the timed steps:
-        # erasures mixing data and parity (fewer full dot products than all-data erasures).
-        mixed = MIXED_PATTERNS.get(args.config)
-        mixed_gibs = None
-        if mixed is not None:
-            a, b = D.Event(), D.Event()
-            D.rs_decode(k, m, mixed, lay, stream=stream)
-            a.record(stream)
-            for _ in range(5):
-                D.rs_decode(k, m, mixed, lay, stream=stream)
-            b.record(stream)
-            mixed_gibs = round(obj_bytes / GIB / (a.elapsed_ms(b) / 5 / 1e3), 3)
-
         summ, summ_src = profile_summary(args.config)
+        # the committed trace describes ONE command (bench.py --gpus 1, its config and stripes):
+        # quote it only for a run of that shape
+        prof_world = _profile_world((summ or {}).get("command", ""))
+        prof_stripes = (summ or {}).get("stripes_per_gpu", S_cfg)
+        trace_match = (summ is not None and summ.get("config") == args.config and
+                       prof_world == world and prof_stripes == S and args.scaling == "weak")
         kd = kernel_entry(summ, kernel) or {}
         traffic = kd.get("hbm_bytes_per_launch")
-        prof_stripes = (summ or {}).get("stripes_per_gpu", S_cfg)
         if traffic is not None and S != prof_stripes:
             traffic = int(traffic * S / prof_stripes)  # profile ran at its own S
-        trace = None
+        trace = None if trace_match else {
+            "omitted": f"{summ_src} profiles config={(summ or {}).get('config')} "
+                       f"gpus={prof_world} stripes={prof_stripes}, not this run"}
         timed_ns = kd.get("timed_avg_ns")
-        if timed_ns:
+        if timed_ns and trace_match:
             t_pass = kd.get("dispatches_per_pass", 1)
             t_algo = algo_bytes * per_pass // t_pass * prof_stripes // S
             trace = {"source": summ_src, "timed_launches": kd.get("timed_calls"),
@@ -580,7 +614,13 @@ def main():
             "encode_gibs_per_gpu": round(enc_gibs, 3),
             "decode_gibs_per_gpu": round(dec_gibs, 3),
             "decode_mixed_pattern": mixed,
-            "decode_mixed_gibs_per_gpu": mixed_gibs,
+            "decode_mixed_gibs_per_gpu": (round(sum(per_rank_mixed) / world, 3)
+                                          if per_rank_mixed else None),
+            "per_rank_decode_mixed_gibs": ([round(x, 2) for x in per_rank_mixed]
+                                           if per_rank_mixed else None),
+            "coord_backend": co.coord_backend,
+            "devices": co.devices,
+            "shared_devices": co.shared_devices,
             "roofline": {"bound": "hbm", "kernel": kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -53,6 +53,8 @@ int ecamd_tune(const char *key, int value);
 int ecamd_bitslice_available(void);
 int ecamd_bitslice_wait(void);
 int ecamd_bitslice_entries(void);
+/* Bitsliced kernel launches this process has enqueued (tests pin which kernel ran). */
+long long ecamd_bitslice_launches(void);
 
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
 typedef struct ecamd_map ecamd_map;

@@ -82,7 +82,9 @@ int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int *r
  * every one of ndev visible devices, or the comma-separated subset named by spec (the
  * ECAMD_PERCALL_DEVICES environment variable; NULL or "" = all; out-of-range or repeated ids are
  * dropped, and a spec naming none of them means all).  Writes up to max ids to devs, returns the
- * count.  Call n of a process goes to devs[n % count]. */
+ * count.  Call n of a process goes to devs[n % count] -- except with the spec "current", where
+ * every call runs on the caller's current device (one process per GPU: liberasurecode_amd/shard.py
+ * sets it for its ranks). */
 int ecamd_percall_device_plan(int ndev, const char *spec, int *devs, int max);
 
 /* Bitsliced GF(2^16) maps (host/bitslice.hpp): the XOR network built for an R x K matrix

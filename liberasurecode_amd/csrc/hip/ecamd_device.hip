@@ -167,6 +167,8 @@ struct Tuning {
     Knob frame_crc_units{0};  //   work units (stripe ranges) per CU to aim for (0 = 4)
     Knob frame_crc_mb{0};     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
     Knob frame_unfused{0};  // framed encode: 1 = always split then encode (A/B against copy-through)
+    Knob frame_copy_stream{1};  // object <-> payload copies: streaming 32-bit-offset kernels (0: the
+                                //   first-version per-16-byte kernels, A/B and fallback)
     Knob crc_gap_bits{8};   // CRC32 kernel at crc_bits 4: field width of the gap / butterfly maps
     Knob crc_span_kib{128}; // CRC32 kernel: KiB of payload per wave (span), multiple of 4
     Knob crc_pos{1};        // CRC32 kernel: position-specific piece tables (one gap step per 4 pieces)
@@ -229,6 +231,7 @@ int dev_tune(const char* key)
     if (k == "crc_span_kib") return g_tune.crc_span_kib;
     if (k == "frame_crc_fused") return g_tune.frame_crc_fused;
     if (k == "frame_copy_padded") return g_tune.frame_copy_padded;
+    if (k == "frame_copy_stream") return g_tune.frame_copy_stream;
     if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
     if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
@@ -256,7 +259,8 @@ struct ecamd_map {
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
                                 std::shared_ptr<void>& hold);
-int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st);
+int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
+                    const std::shared_ptr<void>& hold);
 }  // namespace ecamd
 
 namespace {
@@ -548,7 +552,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
             c.out_base = b.out_base + s0 * b.out_stride;
         }
         c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
-        *rc = bitslice_launch(fn, c, static_cast<int>(std::min<int64_t>(c.ntiles, slots)), st);
+        *rc = bitslice_launch(fn, c, static_cast<int>(std::min<int64_t>(c.ntiles, slots)), st, hold);
     }
     return *rc ? 0 : bs / kBsTile * kBsTile;
 }
@@ -1215,6 +1219,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_units = std::max(0, std::min(value, 64));
     } else if (k == "frame_copy_padded") {
         g_tune.frame_copy_padded = value;  // 0 off, anything else on
+    } else if (k == "frame_copy_stream") {
+        g_tune.frame_copy_stream = value;
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_unfused") {

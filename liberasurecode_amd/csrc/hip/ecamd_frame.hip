@@ -241,6 +241,101 @@ __global__ void frame_split_kernel(const SplitArgs a)
     }
 }
 
+// Streaming forms of the two copies for objects / stripes whose offsets fit 32 bits: a tile is
+// kCopyU x 256 lanes x 16 B of one data fragment of one stripe (t -> stripe, fragment, tile: 32-bit
+// index math once per tile), loads and stores are buffer ops on one resource per stripe with
+// 32-bit offsets, and the unaligned side of the copy (object offset j*bs when bs % 16 != 0) takes
+// unaligned 16-byte buffer accesses -- as the copy-through codec launch does -- instead of bytes.
+// Only the chunk that straddles two payloads or the object's end goes byte by byte.
+constexpr int kCopyU = 4;
+
+__global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs a)
+{
+    const uint32_t per_frag = static_cast<uint32_t>((a.bs + 15) / 16);  // payload chunks
+    const uint32_t tpf = (per_frag + 256 * kCopyU - 1) / (256 * kCopyU);
+    const uint32_t ntiles = tpf * static_cast<uint32_t>(a.k) * static_cast<uint32_t>(a.nstripes);
+    const int bs = static_cast<int>(a.bs);
+    const int size = static_cast<int>(a.size);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sj = t / tpf;
+        const uint32_t tc = t - sj * tpf;
+        const uint32_t s = sj / static_cast<uint32_t>(a.k);
+        const int j = static_cast<int>(sj - s * static_cast<uint32_t>(a.k));
+        const auto robj = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(a.obj) + static_cast<int64_t>(s) * a.obj_stride, 0, size, 0x00020000);
+        uint8_t* pay = a.frags + static_cast<int64_t>(s) * a.stripe_stride + j * a.frag_stride + kHeaderBytes;
+        const auto rpay = __builtin_amdgcn_make_buffer_rsrc(pay, 0, static_cast<int>(per_frag * 16), 0x00020000);
+        u32x4 v[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const int src = j * bs + c * 16;
+            // object bytes left for this chunk: fast when all 16 are inside the object and payload
+            const bool full = c * 16 + 16 <= bs && src + 16 <= size;
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, full ? src : static_cast<int>(0x80000000u), 0, 2);
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            if (c >= static_cast<int>(per_frag)) continue;
+            const int src = j * bs + c * 16;
+            if (!(c * 16 + 16 <= bs && src + 16 <= size)) {  // ragged end: bytes, zero padded
+                int n = size - src;
+                n = n < 0 ? 0 : n;
+                n = n > bs - c * 16 ? bs - c * 16 : n;
+                const uint8_t* p = a.obj + static_cast<int64_t>(s) * a.obj_stride + src;
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int i = 0; i < (n < 16 ? n : 16); ++i) w[i >> 2] |= static_cast<uint32_t>(p[i]) << (8 * (i & 3));
+                v[u] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v[u], rpay, c * 16, 0, 2);
+        }
+    }
+}
+
+// fragments_to_string, streaming: the mirror of the split -- chunk c of payload j (an aligned
+// 16-byte load) lands at object offset j*bs + 16c (an unaligned store when bs % 16 != 0; aligned
+// loads + unaligned stores measured faster than the reverse for Swift's bs = 104858); the
+// payload's last partial chunk and anything reaching past the object's end go byte by byte, so
+// nothing is written outside [0, size).
+__global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
+{
+    const int bs = static_cast<int>(a.bs);
+    const int size = static_cast<int>(a.size);
+    const uint32_t per_frag = static_cast<uint32_t>((bs + 15) / 16);
+    const uint32_t tpf = (per_frag + 256 * kCopyU - 1) / (256 * kCopyU);
+    const uint32_t ntiles = tpf * static_cast<uint32_t>(k) * static_cast<uint32_t>(a.nstripes);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t sj = t / tpf;
+        const uint32_t tc = t - sj * tpf;
+        const uint32_t s = sj / static_cast<uint32_t>(k);
+        const int j = static_cast<int>(sj - s * static_cast<uint32_t>(k));
+        const uint8_t* pay = a.frags + static_cast<int64_t>(s) * a.stripe_stride + j * a.frag_stride + kHeaderBytes;
+        const auto rpay = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay), 0, bs, 0x00020000);
+        uint8_t* ob = a.obj + static_cast<int64_t>(s) * a.obj_stride;
+        const auto robj = __builtin_amdgcn_make_buffer_rsrc(ob, 0, size, 0x00020000);
+        u32x4 v[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const bool full = c * 16 + 16 <= bs && j * bs + c * 16 + 16 <= size;
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, full ? c * 16 : static_cast<int>(0x80000000u), 0, 2);
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            if (c >= static_cast<int>(per_frag)) continue;
+            const int dst = j * bs + c * 16;
+            if (c * 16 + 16 <= bs && dst + 16 <= size) {
+                __builtin_amdgcn_raw_buffer_store_b128(v[u], robj, dst, 0, 2);
+                continue;
+            }
+            const int n = min(bs - c * 16, size - dst);  // the payload's tail / the object's end
+            for (int i = 0; i < n; ++i) ob[dst + i] = pay[c * 16 + i];
+        }
+    }
+}
+
 // fragments_to_string: object bytes [0, size) = data payloads 0..k-1 concatenated.
 __global__ void frame_join_kernel(const JoinArgs a)
 {

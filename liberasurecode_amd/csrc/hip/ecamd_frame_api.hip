@@ -240,6 +240,23 @@ int grid_for(int dev, int64_t work)
         1, std::min<int64_t>((work + 255) / 256, static_cast<int64_t>(dev_cu_count(dev)) * 16)));
 }
 
+// The streaming split / join kernels address a stripe's payloads and an object with 32-bit
+// buffer offsets.
+bool copy_fits32(int k, int64_t frag_stride, int64_t bs, int64_t obj_size)
+{
+    const int64_t lim = (int64_t{1} << 31) - 4096;
+    return k > 0 && bs > 0 && obj_size < lim && bs + 16 < lim &&
+           (k - 1) * frag_stride + kHeaderBytes + bs + 16 < lim && k * bs < lim;
+}
+
+// Tiles of kCopyU x 256 chunks per (stripe, data fragment); 8 resident 256-thread workgroups per CU.
+int copy_grid(int dev, int64_t chunks_per_frag, int k, int nstripes)
+{
+    const int64_t tiles = (chunks_per_frag + 1023) / 1024 * k * static_cast<int64_t>(nstripes);
+    return static_cast<int>(std::max<int64_t>(
+        1, std::min<int64_t>(tiles, static_cast<int64_t>(dev_cu_count(dev)) * 8)));
+}
+
 // XOR plan of a reference operation applied in place on the payloads of every stripe.
 int xor_plan_apply(const Code& c, int op, const int* missing, int arg, uint8_t* payload0,
                    int64_t ss, int64_t fs, int64_t bs, int nstripes, void* stream,
@@ -437,8 +454,12 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
     }
     SplitArgs sa{static_cast<const uint8_t*>(d_obj), obj_stride, static_cast<int64_t>(obj_size),
                  frags, stripe_stride, frag_stride, bs, k, nstripes, aligned ? 1 : 0};
-    hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),
-                       dim3(256), 0, st, sa);
+    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0)
+        hipLaunchKernelGGL(frame_split_stream_kernel,
+                           dim3(copy_grid(dev, (bs + 15) / 16, k, nstripes)), dim3(256), 0, st, sa);
+    else
+        hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),
+                           dim3(256), 0, st, sa);
     HIP_TRY(hipGetLastError());
     if (backend == kBackendRs) {
         rc = ecamd_rs_encode(k, m, p0, stripe_stride, frag_stride, bs, nstripes, stream);
@@ -502,9 +523,13 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     JoinArgs ja{frags, stripe_stride, frag_stride, bs, static_cast<uint8_t*>(d_obj), obj_stride,
                 static_cast<int64_t>(obj_size), nstripes,
                 (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
-    hipLaunchKernelGGL(frame_join_kernel,
-                       dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),
-                       dim3(256), 0, static_cast<hipStream_t>(stream), ja);
+    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0)
+        hipLaunchKernelGGL(frame_join_stream_kernel, dim3(copy_grid(dev, (bs + 15) / 16, k, nstripes)),
+                           dim3(256), 0, static_cast<hipStream_t>(stream), ja, k);
+    else
+        hipLaunchKernelGGL(frame_join_kernel,
+                           dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),
+                           dim3(256), 0, static_cast<hipStream_t>(stream), ja);
     HIP_TRY(hipGetLastError());
     return 0;
 }

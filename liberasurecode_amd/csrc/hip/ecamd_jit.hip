@@ -26,6 +26,7 @@
 #include <cstring>
 #include <ctime>
 #include <fstream>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -135,6 +136,31 @@ uint64_t fnv1a(const std::string& s)
     return h;
 }
 
+// The code object's target: the device's architecture name without feature flags ("gfx950"), so
+// the cache key and the compile follow the GPU rather than the build (kept per device).
+std::string device_arch(int dev)
+{
+    static std::mutex mu;
+    static std::map<int, std::string> names;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = names.find(dev);
+    if (it != names.end()) return it->second;
+    std::string arch = "gfx950";
+    hipDeviceProp_t p{};
+    if (hipGetDeviceProperties(&p, dev) == hipSuccess && p.gcnArchName[0]) {
+        arch = p.gcnArchName;
+        arch = arch.substr(0, arch.find(':'));
+    }
+    (void)hipGetLastError();
+    return names[dev] = arch;
+}
+
+bool file_exists(const std::string& path)
+{
+    struct stat st {};
+    return stat(path.c_str(), &st) == 0;
+}
+
 bool read_file(const std::string& path, std::string& out)
 {
     std::ifstream f(path, std::ios::binary);
@@ -150,35 +176,43 @@ struct BsEntry {
     int R = 0, K = 0;
     int depth = 0;        // bitslice_source: 0 register loads, 2 / 4 LDS ring
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
+    std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
     pid_t pid = -1;       // compiler child while running
+    time_t started = 0;   // when the child was spawned
     int state = 0;        // 0 compiling, 2 waiting for a compiler slot, 1 code object ready, -1 failed
     std::string code;
     std::map<int, hipFunction_t> fn;  // per device; nullptr: unusable there
     std::vector<std::pair<int, hipModule_t>> modules;  // (device, module), spilled ones included
     uint64_t last_use = 0;
+    // The last launch of this entry's kernels on each (device, stream): an event recorded after it
+    // (bitslice_launch), so unloading waits for exactly those launches, not for whole devices.
+    std::mutex ev_mu;
+    std::map<std::pair<int, hipStream_t>, hipEvent_t> last_launch;
 
     // Reached only for an entry evicted from the cache (the cache itself is never destroyed, so
     // nothing here runs at process exit) once its last holder -- a launch in progress keeps one --
-    // has let go: no launch of its functions can still be enqueued; wait for those in flight on
-    // each device the modules live on, then unload them.
+    // has let go, and never under g_jit_mu: no launch of its functions can still be enqueued; wait
+    // for the recorded ones, then unload the modules.
     ~BsEntry()
     {
         int cur = -1;
         (void)hipGetDevice(&cur);
-        std::vector<int> synced;
+        for (const auto& kv : last_launch) {
+            if (hipSetDevice(kv.first.first) != hipSuccess) continue;
+            (void)hipEventSynchronize(kv.second);
+            (void)hipEventDestroy(kv.second);
+        }
         for (const auto& dm : modules) {
             if (hipSetDevice(dm.first) != hipSuccess) continue;
-            if (std::find(synced.begin(), synced.end(), dm.first) == synced.end()) {
-                (void)hipDeviceSynchronize();
-                synced.push_back(dm.first);
-            }
             (void)hipModuleUnload(dm.second);
         }
         if (cur >= 0) (void)hipSetDevice(cur);
         (void)hipGetLastError();
     }
 };
+
+std::atomic<long long> g_bs_launches{0};  // bitsliced kernel launches enqueued by this process
 
 // Matrices with a bitsliced kernel (or one on the way), the least recently used evicted past the
 // "bitslice_entries" knob (256); heap objects never destroyed, so no HIP call runs during static
@@ -234,7 +268,7 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
-                  static_cast<unsigned long long>(fnv1a(generator_fingerprint() + req)));
+                  static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
     const std::string dir = cache_dir();
     if (dir.empty()) {  // no usable cache directory: the LDS tables serve this matrix
         e.state = -1;
@@ -267,10 +301,11 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     posix_spawn_file_actions_init(&fa);
     posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);  // keep our stdout clean
     posix_spawn_file_actions_addclosefrom_np(&fa, 3);  // no GPU / socket descriptors in the child
-    const char* argv[] = {helper.c_str(), req_path.c_str(), e.co_path.c_str(), nullptr};
+    const char* argv[] = {helper.c_str(), req_path.c_str(), e.co_path.c_str(), e.arch.c_str(), nullptr};
     pid_t pid = -1;
     if (posix_spawn(&pid, helper.c_str(), &fa, nullptr, const_cast<char* const*>(argv), environ) == 0) {
         e.pid = pid;
+        e.started = time(nullptr);
         e.state = 0;
         g_running.push_back(ep);
         static std::once_flag once;
@@ -279,24 +314,44 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     posix_spawn_file_actions_destroy(&fa);
 }
 
-// Advance an entry: reap its compiler child (block when `wait`), or start a queued compile when a
-// slot is free (or at once when `wait`).  Caller holds the lock.
-void poll_compile(const std::shared_ptr<BsEntry>& ep, bool wait)
+// A compile whose child cannot be waited for (reaped by the host process: SIGCHLD ignored, or a
+// waitpid(-1) elsewhere) counts as running while its pid exists, for at most this long.
+constexpr int kOrphanSeconds = 300;
+
+// Advance an entry without blocking: reap its compiler child, or start a queued compile when a
+// slot is free (or at once when `force`).  Caller holds the lock.
+void poll_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
     BsEntry& e = *ep;
-    if (e.state == 2) start_compile(ep, wait);
+    if (e.state == 2) start_compile(ep, force);
     if (e.state != 0) return;
     int status = 0;
     pid_t r;
     do {
-        r = waitpid(e.pid, &status, wait ? 0 : WNOHANG);
+        r = waitpid(e.pid, &status, WNOHANG);
     } while (r < 0 && errno == EINTR);
     if (r == 0) return;  // still running
+    if (r < 0 && errno == ECHILD && !file_exists(e.co_path) && kill(e.pid, 0) == 0 &&
+        time(nullptr) - e.started < kOrphanSeconds)
+        return;  // not ours to reap any more, but still there: keep waiting for its code object
     e.pid = -1;
     g_running.erase(std::remove(g_running.begin(), g_running.end(), ep), g_running.end());
-    // a child reaped elsewhere (r < 0), or another process compiling the same request, may still
-    // have produced the code object
+    // a child reaped elsewhere, or another process compiling the same request, may still have
+    // produced the code object
     e.state = read_file(e.co_path, e.code) ? 1 : -1;
+}
+
+// Block until the entry's compile (started now if queued) has finished, polling with the lock
+// released so other threads' launches never wait behind a compile.  `lk` holds g_jit_mu.
+void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntry>& ep)
+{
+    poll_compile(ep, true);
+    while (ep->state == 0) {
+        lk.unlock();
+        usleep(2000);
+        lk.lock();
+        poll_compile(ep, true);
+    }
 }
 
 }  // namespace
@@ -311,7 +366,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     depth = bitslice_depth(depth, K);
     std::vector<int> key = {R, K, depth};
     key.insert(key.end(), coeff.begin(), coeff.end());
-    std::lock_guard<std::mutex> lk(g_jit_mu);
+    std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
+    std::unique_lock<std::mutex> lk(g_jit_mu);
     for (size_t i = 0; i < g_running.size();) {  // reap finished compilers, freeing their slots
         const auto ep = g_running[i];
         poll_compile(ep, false);
@@ -324,6 +380,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
             if (it->second->state != 0 && (victim == g_jit.end() || it->second->last_use < victim->second->last_use))
                 victim = it;
         if (victim == g_jit.end()) break;  // all compiling: let the map grow until they finish
+        evicted.push_back(std::move(victim->second));
         g_jit.erase(victim);
     }
     auto& slot = g_jit[key];
@@ -333,6 +390,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->R = R;
         slot->K = K;
         slot->depth = depth;
+        slot->arch = device_arch(dev);
         // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
         slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R) > 2 ? 2 : 0);
         start_compile(slot, wait);
@@ -344,8 +402,12 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     for (;;) {
         auto it = e.fn.find(dev);
         if (it != e.fn.end()) return it->second;
-        poll_compile(ep, wait);
+        if (wait)
+            wait_compile(lk, ep);
+        else
+            poll_compile(ep, false);
         if (e.state == 0 || e.state == 2) return nullptr;
+        if ((it = e.fn.find(dev)) != e.fn.end()) return it->second;  // loaded while unlocked
         hipFunction_t fn = nullptr;
         int spill = 0;
         if (e.state == 1) {
@@ -375,7 +437,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     }
 }
 
-int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st)
+int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
+                    const std::shared_ptr<void>& hold)
 {
     BsArgs a = args;
     void* params[] = {&a};
@@ -383,6 +446,17 @@ int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t 
                                                params, nullptr);
     if (e != hipSuccess)
         return dev_fail(ECAMD_EHIP, "hipModuleLaunchKernel(bitslice): %s", hipGetErrorString(e));
+    g_bs_launches.fetch_add(1, std::memory_order_relaxed);
+    auto* entry = static_cast<BsEntry*>(hold.get());
+    if (entry) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> lk(entry->ev_mu);
+        hipEvent_t& ev = entry->last_launch[{dev, st}];
+        if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+        if (ev) (void)hipEventRecord(ev, st);
+        (void)hipGetLastError();
+    }
     return 0;
 }
 
@@ -390,13 +464,20 @@ int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t 
 
 extern "C" int ecamd_bitslice_wait(void)
 {
-    std::lock_guard<std::mutex> lk(ecamd::g_jit_mu);
+    std::unique_lock<std::mutex> lk(ecamd::g_jit_mu);
+    std::vector<std::shared_ptr<ecamd::BsEntry>> all;
+    for (auto& kv : ecamd::g_jit) all.push_back(kv.second);
     int failed = 0;
-    for (auto& kv : ecamd::g_jit) {
-        ecamd::poll_compile(kv.second, true);  // starts queued compiles too
-        if (kv.second->state != 1) failed++;
+    for (const auto& ep : all) {
+        ecamd::wait_compile(lk, ep);  // starts queued compiles too
+        if (ep->state != 1) failed++;
     }
     return failed;
+}
+
+extern "C" long long ecamd_bitslice_launches(void)
+{
+    return ecamd::g_bs_launches.load(std::memory_order_relaxed);
 }
 
 extern "C" int ecamd_bitslice_entries(void)

@@ -126,14 +126,16 @@ std::vector<std::vector<Staging*>> g_pool;  // by device
 
 struct DevicePlan {
     std::vector<int> devs;
+    bool current = false;  // ECAMD_PERCALL_DEVICES=current: the caller's current device
     std::atomic<unsigned> next{0};
     DevicePlan()
     {
         const int n = ecamd_device_count();
         if (n <= 0) return;
+        const char* spec = std::getenv("ECAMD_PERCALL_DEVICES");
+        current = spec && std::strcmp(spec, "current") == 0;
         devs.resize(static_cast<size_t>(n));
-        devs.resize(static_cast<size_t>(
-            ecamd_percall_device_plan(n, std::getenv("ECAMD_PERCALL_DEVICES"), devs.data(), n)));
+        devs.resize(static_cast<size_t>(ecamd_percall_device_plan(n, spec, devs.data(), n)));
     }
 };
 
@@ -141,6 +143,8 @@ int pick_device()
 {
     static DevicePlan plan;  // thread-safe one-time initialisation
     if (plan.devs.empty()) return -1;
+    int cur = -1;
+    if (plan.current && ecamd_get_device(&cur) == 0 && cur >= 0) return cur;
     return plan.devs[plan.next.fetch_add(1, std::memory_order_relaxed) % plan.devs.size()];
 }
 

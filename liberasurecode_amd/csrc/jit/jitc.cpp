@@ -7,10 +7,13 @@
 // and with ECAMD_JIT_KEEP_SOURCE=1 the generated source lands beside the code object as
 // <out minus .co>.hip for inspection.  This program never touches the GPU.
 //
-//   ecamd_jitc <request> <out.co>      request: bitslice_request() text; exit 0 on success
+//   ecamd_jitc <request> <out.co> [arch]   request: bitslice_request() text; arch: the target GPU
+//                                          (the parent passes its device's, default gfx950);
+//                                          exit 0 on success
 #include <hip/hiprtc.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -37,10 +40,16 @@ bool write_whole(const std::string& path, const std::string& bytes)
 
 int main(int argc, char** argv)
 {
-    if (argc != 3) {
-        std::fprintf(stderr, "usage: %s <request> <out.co>\n", argv[0]);
+    if (argc != 3 && argc != 4) {
+        std::fprintf(stderr, "usage: %s <request> <out.co> [arch]\n", argv[0]);
         return 2;
     }
+    std::string arch = argc == 4 && argv[3][0] ? argv[3] : "gfx950";
+    for (char ch : arch)
+        if (!std::isalnum(static_cast<unsigned char>(ch))) {
+            std::fprintf(stderr, "ecamd_jitc: bad arch %s\n", argv[3]);
+            return 2;
+        }
     std::ifstream in(argv[1]);
     std::stringstream ss;
     ss << in.rdbuf();
@@ -63,7 +72,8 @@ int main(int argc, char** argv)
     hiprtcProgram prog = nullptr;
     if (hiprtcCreateProgram(&prog, src.c_str(), "ecamd_bitslice.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return 1;
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const std::string arch_opt = "--offload-arch=" + arch;
+    const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17"};
     if (hiprtcCompileProgram(prog, 3, opts) != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);

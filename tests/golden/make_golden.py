@@ -215,6 +215,23 @@ def rs_cases(lib):
     reconstruct_case(10, 4, 4096, [0, 5], 3, False)
     reconstruct_case(20, 8, 1 << 22, list(range(8)), 3, False)
 
+    # Round 3: every pattern the bench times, pinned at full size, and shapes that take the
+    # bitsliced 8-output kernel (>= 5 outputs, whole 16 KiB tiles, k <= 32) -- appended, so the
+    # stripe ids of the cases above stay the same
+    decode_case(10, 4, 1 << 20, [0, 5, 10, 13], False)                  # C3 mixed
+    decode_case(20, 8, 1 << 22, [0, 2, 4, 6, 20, 22, 24, 26], False)    # C5 mixed
+    decode_case(20, 8, 1 << 22, list(range(8)), True)                   # C5, inconsistent inputs
+    decode_case(20, 8, 3 * 16384 + 2, [1, 3, 5, 7, 9, 21, 23, 25], True)  # tiles + ragged tail
+    decode_case(12, 6, 65536, [1, 3, 5, 13, 15, 17], False)
+    decode_case(24, 8, 65536, [0, 1, 2, 3, 24, 25, 26, 27], True)
+    decode_case(10, 6, 65536, [0, 1, 2, 3, 4], False)                     # 5 outputs
+    for k, m, bs in [(20, 8, 3 * 16384 + 2), (12, 6, 65536), (24, 8, 65536), (32, 8, 32768),
+                     (10, 5, 65536)]:
+        encode_case(k, m, bs)
+    for d in (0, 6, 20, 26):
+        reconstruct_case(20, 8, 1 << 22, [0, 2, 4, 6, 20, 22, 24, 26], d, False)
+    reconstruct_case(10, 4, 1 << 20, [0, 5, 10, 13], 5, False)
+
     # decoding-matrix inverses for listed patterns
     for k, m, miss in [(10, 4, [0, 1, 2, 3]), (10, 4, [0, 5, 10, 13]), (20, 8, list(range(8))),
                        (4, 2, [1, 5]), (12, 6, [0, 2, 4, 13, 15, 17])]:
@@ -332,11 +349,14 @@ def xor_cases(lib, bs=48):
 
 
 def main():
+    import sys
     rs = load_rs()
     data = rs_cases(rs)
     with open(os.path.join(HERE, "rs_vand.json"), "w") as f:
         json.dump(data, f, separators=(",", ":"))
     print("rs_vand.json:", {k: len(v) for k, v in data.items()})
+    if "--rs-only" in sys.argv:
+        return
     xd = xor_cases(load_xor())
     with open(os.path.join(HERE, "xor_codes.json"), "w") as f:
         json.dump(xd, f, separators=(",", ":"))

@@ -80,3 +80,18 @@ def test_no_gpu_fails_loudly():
         assert "PTR" in r.stdout
     else:
         assert "NULL" in r.stdout and "no HIP device" in r.stderr
+
+
+@pytest.mark.parametrize("header,lib", [("ecamd.h", "libecamd.so"), ("ecamd_host.h", "libecamd_host.so"),
+                                        ("ecamd_probe.h", "libecamd_probe.so")])
+def test_extension_exports_only_its_c_abi(header, lib):
+    """The device / host extension libraries export their C ABI and nothing else: the C++
+    internals, kernel stubs and helpers stay local (version script abi/ecamd.map)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(LIB, lib)], capture_output=True,
+                         text=True, check=True).stdout
+    names = sorted(l.split()[-1] for l in out.splitlines() if l.split()[-2] in "TtWwDdBbRrVv")
+    stray = [n for n in names if not n.startswith("ecamd_") and not n.startswith("_end")
+             and n not in ("_edata", "__bss_start", "_fini", "_init")]
+    assert not stray, stray[:20]
+    assert set(n for n in names if n.startswith("ecamd_")) <= set(declared(header)) | set(
+        declared("ecamd_host.h")), "exported but undeclared"

@@ -65,3 +65,47 @@ def test_bench_dispatches_per_pass(k, width, F, S, cus, want):
     sys.path.insert(0, ROOT)
     import bench
     assert bench.dispatches_per_pass(k, width, F, S, cus) == want
+
+
+def test_ranks_sharing_a_gpu_fail_loudly():
+    """Two ranks on one GPU while the host shows a GPU per rank: the device check (identities
+    all-gathered over gloo before any RCCL collective) stops the job and names the ranks."""
+    r = run_bench("--gpus", "2", "--dry-run",
+                  env={"ECAMD_FAKE_DEVICES": "0,0", "ECAMD_FAKE_DEVICE_COUNT": "8"})
+    assert r.returncode != 0
+    assert "ranks 0, 1 on GPU" in r.stderr and "8 GPUs for 2 ranks" in r.stderr
+
+
+def test_distinct_devices_reported():
+    r = run_bench("--gpus", "2", "--dry-run",
+                  env={"ECAMD_FAKE_DEVICES": "0,1", "ECAMD_FAKE_DEVICE_COUNT": "8"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["coord_backend"] == "gloo" and not line["shared_devices"]
+    assert [d["device"] for d in line["devices"]] == [0, 1]
+    assert len({d["pci"] for d in line["devices"]}) == 2
+
+
+def _ident(dev, count, host=1, bus=None):
+    return {"host": host, "device": dev, "pci_domain": 0, "pci_bus": 0x40 + dev if bus is None else bus,
+            "pci_device": 0, "device_count": count, "local_rank": 0}
+
+
+def test_check_devices_rules():
+    sys.path.insert(0, ROOT)
+    from liberasurecode_amd.shard import DeviceCollision, check_devices
+    # one GPU each: fine on either backend
+    assert check_devices([_ident(d, 8) for d in range(8)], "nccl") is False
+    # same PCI address under different indices (e.g. two HIP_VISIBLE_DEVICES views) is a collision
+    with pytest.raises(DeviceCollision, match="ranks 0, 1"):
+        check_devices([_ident(0, 8, bus=0x40), _ident(1, 8, bus=0x40)], "nccl")
+    # fewer GPUs than ranks: a gloo rehearsal is allowed and reported, RCCL is refused
+    assert check_devices([_ident(0, 1), _ident(0, 1)], "gloo") is True
+    with pytest.raises(DeviceCollision, match="RCCL needs one GPU per rank"):
+        check_devices([_ident(0, 1), _ident(0, 1)], "nccl")
+    # the same device index on two hosts is two GPUs
+    assert check_devices([_ident(0, 1, host=1), _ident(0, 1, host=2)], "nccl") is False
+    # unknown PCI address: fall back to the device index
+    assert check_devices([_ident(0, 8, bus=-1), _ident(1, 8, bus=-1)], "nccl") is False
+    with pytest.raises(DeviceCollision, match="index 3"):
+        check_devices([_ident(3, 8, bus=-1), _ident(3, 8, bus=-1)], "gloo")

@@ -487,3 +487,69 @@ def test_frame_paths_split_into_launches(F, size):
     for s in range(S):
         assert joined[1][s, :size].tobytes() == objs[s]
         assert (joined[1][s, size:] == 0xA5).all()
+
+
+COPY_SIZES = [1, 15, 16, 17, 100, 4 * 16 + 3, 777777, 10 * 104858, 10 * 104858 - 3, (1 << 20) * 10 + 6,
+              (1 << 20) * 10]
+
+
+@pytest.mark.parametrize("name,k,m,hd", [("rs", 10, 4, 0), ("rs", 4, 2, 0), ("xor", 10, 6, 4),
+                                         ("xor", 3, 3, 3), ("rs", 20, 8, 0)])
+@pytest.mark.parametrize("missing", [[], "parity"])
+def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
+    """Decode with every data fragment present (src/erasurecode.c:597-607: fragments_to_string
+    only) runs the streaming join: payload chunks read at unaligned offsets j*bs when bs % 16 != 0,
+    the straddling chunks byte by byte.  Objects equal the originals, guard bytes after each
+    object stay intact, and the first-version join (knob frame_copy_stream 0) agrees."""
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    be = _backend(name)
+    lost = list(range(k, k + min(m, 2))) if missing == "parity" else []
+    S = 3
+    for size in COPY_SIZES:
+        if k == 20 and size > (1 << 20):
+            continue
+        objs = _objects(S, size, k * 7 + size)
+        fb = F.FrameBatch(be, k, m, size, S, hd=hd or 3)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        stride = (size + 16 + 15) // 16 * 16 + 32
+        got = []
+        try:
+            for knob in (1, 0):
+                _lib.check(_lib.dev().ecamd_tune(b"frame_copy_stream", knob), "tune")
+                d = DeviceBuffer(S * stride)
+                d.upload(np.full(S * stride, 0xA5, dtype=np.uint8))
+                fb.decode(lost, d, obj_stride=stride)
+                got.append(d.download().reshape(S, stride))
+        finally:
+            _lib.dev().ecamd_tune(b"frame_copy_stream", 1)
+        assert np.array_equal(got[0], got[1]), size
+        for s in range(S):
+            assert got[0][s, :size].tobytes() == objs[s], (size, s)
+            assert (got[0][s, size:] == 0xA5).all(), (size, s)
+
+
+@pytest.mark.parametrize("name,k,m,hd", [("xor", 10, 6, 4), ("xor", 3, 3, 3), ("rs", 10, 4, 0)])
+def test_frame_split_stream_matches_first_version(F, name, k, m, hd):
+    """prepare_fragments_for_encode on the streaming split kernel (XOR framed encode always; RS
+    with the copy-through launch off): fragments byte-equal to the first-version split kernel and
+    to the restated framing, for sizes with bs % 16 != 0 and tiny objects."""
+    from liberasurecode_amd import _lib
+    be = _backend(name)
+    S = 3
+    for size in COPY_SIZES:
+        objs = _objects(S, size, k * 11 + size)
+        out = []
+        try:
+            _lib.check(_lib.dev().ecamd_tune(b"frame_unfused", 1), "tune")
+            for knob in (1, 0):
+                _lib.check(_lib.dev().ecamd_tune(b"frame_copy_stream", knob), "tune")
+                fb = F.FrameBatch(be, k, m, size, S, hd=hd or 3, checksum=ec_api.CHKSUM_CRC32)
+                fb.encode(_upload_objects(objs, fb.obj_stride))
+                out.append(fb.fragments())
+        finally:
+            _lib.dev().ecamd_tune(b"frame_copy_stream", 1)
+            _lib.dev().ecamd_tune(b"frame_unfused", 0)
+        assert np.array_equal(out[0], out[1]), size
+        want = expected_stripe(be, k, m, hd, objs[2], ec_api.CHKSUM_CRC32)
+        assert all(out[0][2, i].tobytes() == want[i] for i in range(k + m)), size

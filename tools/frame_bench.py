@@ -26,6 +26,21 @@ def timed(fn, stream, reps):
     return a.elapsed_ms(b) / reps
 
 
+def systematic(d, st, fb, out, S, size, tag, reps, copy_gbs):
+    """Decode with every data fragment present (src/erasurecode.c:597-607): fragments_to_string
+    only -- a copy of S*size object bytes out of the payloads (read + write = 2x the bytes)."""
+    for lost in ([], [fb.k, fb.k + 1]):
+        for knob in (1, 0):
+            d.ecamd_tune(b"frame_copy_stream", knob)
+            ms = timed(lambda: fb.decode(lost, out, stream=st), st, reps)
+            gbs = 2 * S * size / ms / 1e6
+            print(json.dumps({"op": "frame_decode_systematic_" + tag, "lost": lost, "copy_stream": knob,
+                              "ms": round(ms, 4), "GiBps_object": round(S * size / (ms / 1e3) / 2**30, 1),
+                              "copy_GBps": round(gbs, 1), "frac_of_copy_probe": round(gbs / copy_gbs, 4),
+                              "frac_of_8TBps": round(gbs / 8000, 4)}), flush=True)
+    d.ecamd_tune(b"frame_copy_stream", 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=256)
@@ -39,6 +54,9 @@ def main():
     d = _lib.dev()
     d.ecamd_tune(b"grid_mult", args.grid_mult)
     st = D.Stream()
+    import bench
+    copy_gbs = bench.measured_copy_peak(D, st)
+    print(json.dumps({"copy_probe_GBps": round(copy_gbs, 1)}), flush=True)
     fb = frame.FrameBatch(frame.RS_VAND, k, m, size, S, align=args.align)
     print(json.dumps({"align": args.align, "frag_stride": fb.frag_stride, "head": fb.head}), flush=True)
     obj = D.DeviceBuffer(fb.obj_stride * S)
@@ -108,6 +126,8 @@ def main():
                               "ms": round(ms, 3), "GiBps_object": round(S2 * size2 / (ms / 1e3) / 2**30, 1)}),
                   flush=True)
         out2 = D.DeviceBuffer(fb2.obj_stride * S2)
+        fb2.encode(obj2, stream=st)
+        systematic(d, st, fb2, out2, S2, size2, tag, args.reps, copy_gbs)
         for padded in (1, 0):
             d.ecamd_tune(b"frame_copy_padded", padded)
             ms = timed(lambda: fb2.decode([0, 1, 2, 3], out2, stream=st), st, args.reps)
@@ -118,6 +138,9 @@ def main():
         obj2.free()
         fb2.buf.free()
     out = D.DeviceBuffer(fb.obj_stride * S)
+    fb.checksum = frame.CHKSUM_NONE
+    fb.encode(obj, stream=st)
+    systematic(d, st, fb, out, S, size, "c3", args.reps, copy_gbs)
     ms = timed(lambda: fb.decode([0, 1, 2, 3], out, stream=st), st, args.reps)
     print(json.dumps({"op": "frame_decode_4data", "ms": round(ms, 3),
                       "GiBps_object": round(obj_bytes / (ms / 1e3) / 2**30, 1)}), flush=True)

@@ -1,45 +1,104 @@
 #!/usr/bin/env python3
-"""Per-call latency of the drop-in API (liberasurecode_encode / _decode through
-liberasurecode.so.1 -> liberasurecode_rs_vand.so.1 -> GPU), one thread, RS(10,4), object sizes
-4 KiB .. 16 MiB; median of N calls.  Prints one JSON line per size."""
-import ctypes as C
+"""Per-call latency of the drop-in API, one thread, RS(10,4): liberasurecode_encode / _decode
+(4 data fragments lost) through this repo's liberasurecode.so.1, with
+
+  own: this repo's codec liberasurecode_rs_vand.so.1 -> libecamd -> the MI355X, and
+  ref: the REFERENCE codec (oracle/_ref/liberasurecode_rs_vand.so.1, compiled from /root/reference
+       sources) first on LD_LIBRARY_PATH, run in a child process -- the CPU codec the drop-in
+       replaces, behind the same frontend, on the same host,
+
+object sizes 4 KiB .. 16 MiB, median / p10 / p90 of N calls, and the crossover: the largest size
+at which the CPU codec is still faster per call.  One JSON line per (codec, checksum, size), then
+a summary line.  (The reference frontend itself is unbuildable here -- DESIGN.md §2.)"""
+import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-import ec_api  # noqa: E402
+SIZES = [4096, 16384, 65536, 262144, 1 << 20, 4 << 20, 16 << 20]
+
+
+def pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+
+def measure(codec, reps):
+    import ec_api
+    out = []
+    for ct in (ec_api.CHKSUM_NONE, ec_api.CHKSUM_CRC32):
+        desc = ec_api.create(ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND, 10, 4, ct=ct)
+        assert desc > 0, desc
+        for size in SIZES:
+            data = os.urandom(size)
+            n = reps if size <= (4 << 20) else max(8, reps // 3)
+            enc, dec = [], []
+            for it in range(n + 3):
+                t0 = time.perf_counter()
+                rc, d, p, flen = ec_api.encode(desc, data)
+                t1 = time.perf_counter()
+                assert rc == 0
+                frags = ec_api.fragments(d, 10, flen) + ec_api.fragments(p, 4, flen)
+                ec_api.lib().liberasurecode_encode_cleanup(desc, d, p)
+                avail = frags[4:]
+                t1b = time.perf_counter()
+                rc, got = ec_api.decode(desc, avail, flen)
+                t2 = time.perf_counter()
+                assert rc == 0 and got == data
+                if it >= 3:  # first calls: pool / map set-up
+                    enc.append(t1 - t0)
+                    dec.append(t2 - t1b)  # includes the ctypes copy-out of the decoded object
+            rec = {"codec": codec, "ct": ct, "size": size, "calls": n}
+            for name, xs in (("encode", enc), ("decode_4lost", dec)):
+                med = statistics.median(xs)
+                rec[f"{name}_us"] = round(med * 1e6, 1)
+                rec[f"{name}_p10_us"] = round(pct(xs, 0.1) * 1e6, 1)
+                rec[f"{name}_p90_us"] = round(pct(xs, 0.9) * 1e6, 1)
+                rec[f"{name}_GiBps"] = round(size / med / 2**30, 3)
+            out.append(rec)
+            print(json.dumps(rec), flush=True)
+        ec_api.lib().liberasurecode_instance_destroy(desc)
+    return out
+
+
+def crossover(own, ref, op):
+    """Largest size where the reference CPU codec is faster per call (None: never)."""
+    best = None
+    for ct in sorted({r["ct"] for r in own}):
+        o = {r["size"]: r[f"{op}_us"] for r in own if r["ct"] == ct}
+        f = {r["size"]: r[f"{op}_us"] for r in ref if r["ct"] == ct}
+        slower = [s for s in SIZES if s in o and s in f and f[s] < o[s]]
+        best = max(slower) if slower and (best is None or max(slower) > best) else best
+    return best
 
 
 def main():
-    desc = ec_api.create(ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND, 10, 4, ct=ec_api.CHKSUM_CRC32)
-    assert desc > 0, desc
-    for size in [4096, 65536, 1 << 20, 4 << 20, 16 << 20]:
-        data = os.urandom(size)
-        enc, dec = [], []
-        for it in range(30):
-            t0 = time.perf_counter()
-            rc, d, p, flen = ec_api.encode(desc, data)
-            t1 = time.perf_counter()
-            assert rc == 0
-            frags = ec_api.fragments(d, 10, flen) + ec_api.fragments(p, 4, flen)
-            ec_api.lib().liberasurecode_encode_cleanup(desc, d, p)
-            avail = frags[4:]
-            t1b = time.perf_counter()
-            rc, out = ec_api.decode(desc, avail, flen)
-            t2 = time.perf_counter()
-            assert rc == 0 and out == data
-            if it >= 5:
-                enc.append(t1 - t0)
-                dec.append(t2 - t1b)  # includes the ctypes copy-out of the decoded object
-        me, md = statistics.median(enc), statistics.median(dec)
-        print(json.dumps({"size": size, "encode_us": round(me * 1e6, 1),
-                          "decode_4lost_us": round(md * 1e6, 1),
-                          "encode_GiBps": round(size / me / 2**30, 2),
-                          "decode_GiBps": round(size / md / 2**30, 2)}), flush=True)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=25)
+    ap.add_argument("--codec", default="both", choices=["both", "own", "ref"])
+    args = ap.parse_args()
+    if args.codec in ("own", "ref"):
+        measure(args.codec, args.reps)
+        return
+    ref_dir = os.path.join(ROOT, "oracle", "_ref")
+    env = dict(os.environ, LD_LIBRARY_PATH=ref_dir + (":" + os.environ["LD_LIBRARY_PATH"]
+                                                      if os.environ.get("LD_LIBRARY_PATH") else ""))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--codec", "ref", "--reps",
+                        str(args.reps)], env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ref = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    for x in ref:
+        print(json.dumps(x), flush=True)
+    own = measure("own", args.reps)
+    print(json.dumps({"summary": "per-call crossover (1 thread, RS 10+4): largest object size where "
+                                 "the reference CPU codec is faster than the GPU drop-in",
+                      "encode_crossover_bytes": crossover(own, ref, "encode"),
+                      "decode_crossover_bytes": crossover(own, ref, "decode_4lost")}), flush=True)
 
 
 if __name__ == "__main__":
