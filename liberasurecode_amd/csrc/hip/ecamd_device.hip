@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <atomic>
 #include <condition_variable>
 #include <cstdarg>
@@ -174,8 +175,8 @@ struct Tuning {
     Knob crc_pos{1};        // CRC32 kernel: position-specific piece tables (one gap step per 4 pieces)
     Knob stream{1};         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
     Knob stream_ch{1};      //   16-byte chunks per lane (1, 2; W = 8 always 1)
-    Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = 2: 8 waves/CU
-                            // measured best, tools/xor_sweep.py)
+    Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = by shape, see
+                            // launch_xor)
     Knob grid_mult{0};      // stream launches: workgroups per resident slot (0: 2 for 4-output
                             //   passes of at most 64 tiles per slot, else 1; tools/grid_sweep.py,
                             //   tools/c3_size_sweep.py)
@@ -196,8 +197,9 @@ struct Tuning {
                               //   passes, else 64; tools/slot_sweep.py)
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
-    Knob xor_tiles_per_slot{64};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
-                                  //   64: (3,3) x 1024 stripes +7%, 10 -> 4 +1%, tools/xor_slot_sweep.py)
+    Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
+                                  //   32 measured best with the 12-wave geometry, (3,3,3) C1 +2%,
+                                  //   tools/xor_geom_sweep.py; 64 before)
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
                             //   peers (0), for every destination incl. local ones (1, exercises the
                             //   fork / join on one-GPU boxes), or none: all on the caller's stream (2)
@@ -258,7 +260,7 @@ struct ecamd_map {
 
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold);
+                                std::shared_ptr<void>& hold, bool copy = false);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
                     const std::shared_ptr<void>& hold);
 }  // namespace ecamd
@@ -497,28 +499,40 @@ int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, siz
 // passes use -- on the whole 16 KiB tiles of every fragment; returns the bytes it covered (0: not
 // taken -- shape, knob, or the kernel is still compiling); the LDS-table passes of those rows then
 // run on the rest of each fragment only.
+// Copy-through (copy_off non-null: the framed encode / decode-join of map_apply_copy): input j is
+// also stored at copy_base + s*copy_stride + copy_off[j] (< 0: not copied) as it is loaded, and
+// when base.limited (objects shorter than the k payloads) only the whole tiles below base.min_len
+// are taken -- the LDS-table passes run the rest byte-exactly.
 int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyArgs& base,
                         const int64_t* in_off, const int64_t* out_off, int64_t bs, int nstripes,
-                        hipStream_t st, int* rc)
+                        hipStream_t st, int* rc, const int64_t* copy_off = nullptr)
 {
     *rc = 0;
     const int mode = g_tune.bitslice;
     const int K = map->K;
-    if (!mode || nrows < g_tune.bitslice_min_rows || nrows > kBsMaxR || K > kBsMaxK || base.copy_records || base.limited ||
-        bs < kBsTile)
+    if (!mode || nrows < g_tune.bitslice_min_rows || nrows > kBsMaxR || K > kBsMaxK || bs < kBsTile)
         return 0;
+    if (!copy_off && (base.copy_records || base.limited)) return 0;
+    if (copy_off && bitslice_depth(g_tune.bitslice_depth, K) != 0) return 0;  // ring form: no copy-through
+    const int64_t cover = (base.limited ? std::min<int64_t>(bs, base.min_len) : bs) / kBsTile * kBsTile;
+    if (cover < kBsTile) return 0;
     ApplyArgs a = base;
     a.ncols = K;
     a.nrows = nrows;
     for (int j = 0; j < K; j++) a.in_off[j] = in_off[j];
     for (int r = 0; r < nrows; r++) a.out_off[r] = out_off[row0 + r];
     if (!stream_offsets(a, bs)) return 0;
+    if (copy_off) {
+        for (int j = 0; j < K; j++) a.copy_off[j] = copy_off[j];
+        if (!stream_copy_offsets(a, bs)) return 0;
+    }
     std::vector<int> sub(static_cast<size_t>(nrows) * K);
     for (int r = 0; r < nrows; r++)
         for (int j = 0; j < K; j++)
             sub[static_cast<size_t>(r) * K + j] = map->coeff[static_cast<size_t>(row0 + r) * K + j];
     std::shared_ptr<void> hold;  // the kernel's module stays loaded until the launch is enqueued
-    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, g_tune.bitslice_depth, mode == 2, hold);
+    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, g_tune.bitslice_depth, mode == 2, hold,
+                                         copy_off != nullptr);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -528,10 +542,29 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     b.stripe_list = a.stripe_list;
     b.in_records = a.in_records;
     b.out_records = a.out_records;
-    b.tiles_per_stripe = static_cast<uint32_t>(bs / kBsTile);
+    b.tiles_per_stripe = static_cast<uint32_t>(cover / kBsTile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     for (int j = 0; j < K; j++) b.in_off[j] = a.in_off32[j];
     for (int r = 0; r < nrows; r++) b.out_off[r] = a.out_off32[r];
+    if (copy_off) {  // offsets as idx * step (the kernel keeps 8 scalar registers, not 32)
+        int64_t step = 0;
+        for (int j = 0; j < K; j++)
+            if (copy_off[j] > 0) step = std::gcd(step, copy_off[j]);
+        if (step == 0) step = 1;
+        for (int j = 0; j < K; j++) {
+            if (copy_off[j] < 0) {
+                b.copy_idx[j] = 0xff;
+                continue;
+            }
+            const int64_t idx = copy_off[j] / step;
+            if (idx > 254) return 0;
+            b.copy_idx[j] = static_cast<uint8_t>(idx);
+        }
+        b.copy_base = a.copy_base;
+        b.copy_stride = a.copy_stride;
+        b.copy_records = a.copy_records;
+        b.copy_step = static_cast<uint32_t>(step);
+    }
     // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
     // one 4-wave workgroup per wave per SIMD the kernel is built for (2 for 5..8 outputs)
     const int64_t slots = static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows);
@@ -550,11 +583,12 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         } else {
             c.in_base = b.in_base + s0 * b.in_stride;
             c.out_base = b.out_base + s0 * b.out_stride;
+            if (c.copy_records) c.copy_base = b.copy_base + s0 * b.copy_stride;
         }
         c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
         *rc = bitslice_launch(fn, c, static_cast<int>(std::min<int64_t>(c.ntiles, slots)), st, hold);
     }
-    return *rc ? 0 : bs / kBsTile * kBsTile;
+    return *rc ? 0 : cover;
 }
 
 template <bool PTRS>
@@ -681,9 +715,12 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
             if (!PTRS && g_tune.stream && stream_offsets(a, bs)) {
-                // geometry: 256 threads, xor_wgs (default 2) workgroups per CU; long passes as
-                // several launches (xor_tiles_per_slot, as launch_stream_pass)
-                const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : 2;
+                // geometry: 256 threads, xor_wgs workgroups per CU -- by default 3 (12 waves) for
+                // passes of more than 4 inputs into 3+ outputs, else 2 (tools/xor_geom_sweep.py,
+                // profiles/r03_xor_geom.log: (10,6,4) encode 0.712 -> 0.756 of 8 TB/s, (3,3,3)
+                // best at 2); long passes as several launches (xor_tiles_per_slot, as
+                // launch_stream_pass)
+                const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : (a.ncols > 4 && a.nrows >= 3 ? 3 : 2);
                 const int64_t slots = static_cast<int64_t>(cu_count(dev)) * wgs;
                 const int knob = g_tune.xor_tiles_per_slot;
                 rc = for_each_launch(a, nstripes, g.tiles_per_stripe, static_cast<uint64_t>(slots),
@@ -850,7 +887,39 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
 {
     const ecamd_map* map = e.map.get();
     hipStream_t st = static_cast<hipStream_t>(stream);
+    auto len_of = [&](const std::vector<int64_t>* v, int i) { return v ? (*v)[static_cast<size_t>(i)] : bs; };
+    // Row groups of 5..8 outputs first take the bitsliced kernel over the whole 16 KiB tiles that
+    // every input / copy / output fully holds (the first group copying the inputs through); the
+    // LDS-table passes of those rows then run on the rest of each fragment only.
+    std::vector<int64_t> bs_done(static_cast<size_t>((map->R + 7) / 8), 0);
+    {
+        ApplyArgs b{};
+        b.in_base = in_base;
+        b.in_stride = in_stride;
+        b.out_base = out_base;
+        b.out_stride = out_stride;
+        b.copy_base = copy_base;
+        b.copy_stride = copy_stride;
+        b.min_len = bs;
+        for (int j = 0; j < map->K; j++) {
+            b.min_len = std::min(b.min_len, len_of(in_len, j));
+            if (copy_off[static_cast<size_t>(j)] >= 0) b.min_len = std::min(b.min_len, len_of(copy_len, j));
+        }
+        for (int r = 0; r < map->R; r++) b.min_len = std::min(b.min_len, len_of(out_len, r));
+        b.limited = b.min_len < bs ? 1 : 0;
+        for (int g = 0; g * 8 < map->R && g_tune.stream; g++) {
+            int brc = 0;
+            b.copy_records = g == 0 ? 1 : 0;  // (recomputed from copy_off inside)
+            bs_done[static_cast<size_t>(g)] =
+                launch_bitslice(map, g * 8, std::min(8, map->R - g * 8), b, in_off.data(), out_off.data(), bs,
+                                nstripes, st, &brc, g == 0 ? copy_off.data() : nullptr);
+            if (brc) return brc;
+        }
+    }
     for (const auto& p : map->passes) {
+        const int64_t done = bs_done[static_cast<size_t>(p.row0 / 8)];
+        if (done >= bs) continue;
+        const int64_t pbs = bs - done;  // this pass runs bytes [done, bs) of every fragment
         ApplyArgs a{};
         a.tables = map->d_tables + p.offset;
         a.in_base = in_base;
@@ -859,34 +928,36 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         a.out_stride = out_stride;
         a.copy_base = copy_base;
         a.copy_stride = copy_stride;
-        a.bs = bs;
+        a.bs = pbs;
         a.ncols = p.ncols;
         a.nrows = std::min(p.width, map->R - p.row0);
         a.accumulate = p.col0 > 0;
+        auto rest = [&](int64_t len) { return static_cast<int32_t>(std::max<int64_t>(0, std::min(pbs, len - done))); };
         for (int j = 0; j < p.ncols; j++) {
-            a.in_off[j] = in_off[p.col0 + j];
-            a.copy_off[j] = copy_off[p.col0 + j];
-            a.in_len32[j] = static_cast<int32_t>(in_len ? (*in_len)[p.col0 + j] : bs);
-            a.copy_len32[j] = static_cast<int32_t>(copy_len ? (*copy_len)[p.col0 + j] : bs);
+            a.in_off[j] = in_off[p.col0 + j] + done;
+            a.copy_off[j] = copy_off[p.col0 + j] < 0 ? -1 : copy_off[p.col0 + j] + done;
+            a.in_len32[j] = rest(len_of(in_len, p.col0 + j));
+            a.copy_len32[j] = rest(len_of(copy_len, p.col0 + j));
         }
         for (int r = 0; r < a.nrows; r++)
-            a.out_len32[r] = static_cast<int32_t>(out_len ? (*out_len)[p.row0 + r] : bs);
-        a.min_len = bs;
+            a.out_len32[r] = rest(len_of(out_len, p.row0 + r));
+        a.min_len = pbs;
         for (int j = 0; j < p.ncols; j++) {
             a.min_len = std::min<int64_t>(a.min_len, a.in_len32[j]);
             if (a.copy_off[j] >= 0) a.min_len = std::min<int64_t>(a.min_len, a.copy_len32[j]);
         }
         for (int r = 0; r < a.nrows; r++) a.min_len = std::min<int64_t>(a.min_len, a.out_len32[r]);
-        a.limited = a.min_len < bs ? 1 : 0;
-        for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
+        a.limited = a.min_len < pbs ? 1 : 0;
+        for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r] + done;
         Geometry g;
         int rc;
-        if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, bs) &&
-            (p.row0 != 0 || stream_copy_offsets(a, bs))) {
-            rc = launch_stream_pass(a, map->device, p.bytes, p.width, 1, false, bs, nstripes, st);
+        if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, pbs) &&
+            (p.row0 != 0 || stream_copy_offsets(a, pbs))) {
+            rc = launch_stream_pass(a, map->device, p.bytes, p.width, 1, false, pbs, nstripes, st);
             if (rc) return rc;
             continue;
         }
+        if (done > 0) return fail(ECAMD_EINVAL, "copy-through tail needs 32-bit stream offsets");
         rc = geometry(map->device, p.bytes, bs, nstripes, g);
         if (rc) return rc;
         a.ntiles = g.ntiles;
@@ -1256,7 +1327,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_tiles_per_slot") {
         g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {
-        g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 64;
+        g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 32;
     } else if (k == "scatter_lanes") {
         g_tune.scatter_lanes = std::max(0, std::min(value, 2));
     } else {

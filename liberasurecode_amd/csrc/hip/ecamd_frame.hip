@@ -249,6 +249,12 @@ __global__ void frame_split_kernel(const SplitArgs a)
 // Only the chunk that straddles two payloads or the object's end goes byte by byte.
 constexpr int kCopyU = 4;
 
+__device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int dw, int by);
+
+// prepare_fragments_for_encode, streaming: chunk c of payload j = object bytes [j*bs + 16c, +16),
+// realigned in registers from the two aligned object chunks under it when j*bs % 16 != 0 (aligned
+// loads and stores on both sides); the payload's last chunk, anything reaching past the object's
+// end (zero padded) and a window whose second chunk would reach past the object go byte by byte.
 __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs a)
 {
     const uint32_t per_frag = static_cast<uint32_t>((a.bs + 15) / 16);  // payload chunks
@@ -261,48 +267,78 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         const uint32_t tc = t - sj * tpf;
         const uint32_t s = sj / static_cast<uint32_t>(a.k);
         const int j = static_cast<int>(sj - s * static_cast<uint32_t>(a.k));
+        const int lo = j * bs;
+        const int delta = lo & 15, dw = delta >> 2, by = delta & 3;
         const auto robj = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t*>(a.obj) + static_cast<int64_t>(s) * a.obj_stride, 0, size, 0x00020000);
         uint8_t* pay = a.frags + static_cast<int64_t>(s) * a.stripe_stride + j * a.frag_stride + kHeaderBytes;
         const auto rpay = __builtin_amdgcn_make_buffer_rsrc(pay, 0, static_cast<int>(per_frag * 16), 0x00020000);
-        u32x4 v[kCopyU];
+        u32x4 v0[kCopyU], v1[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
             const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
-            const int src = j * bs + c * 16;
-            // object bytes left for this chunk: fast when all 16 are inside the object and payload
-            const bool full = c * 16 + 16 <= bs && src + 16 <= size;
-            v[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, full ? src : static_cast<int>(0x80000000u), 0, 2);
+            const int src = lo + c * 16;
+            const int q = src >> 4;
+            const bool fast = c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
+            v0[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
+            v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                robj, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
             const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
             if (c >= static_cast<int>(per_frag)) continue;
-            const int src = j * bs + c * 16;
-            if (!(c * 16 + 16 <= bs && src + 16 <= size)) {  // ragged end: bytes, zero padded
+            const int src = lo + c * 16;
+            const int q = src >> 4;
+            u32x4 v;
+            if (c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size)) {
+                v = delta ? window16(v0[u], v1[u], dw, by) : v0[u];
+            } else {  // ragged end: bytes, zero padded
                 int n = size - src;
                 n = n < 0 ? 0 : n;
                 n = n > bs - c * 16 ? bs - c * 16 : n;
                 const uint8_t* p = a.obj + static_cast<int64_t>(s) * a.obj_stride + src;
                 uint32_t w[4] = {0, 0, 0, 0};
                 for (int i = 0; i < (n < 16 ? n : 16); ++i) w[i >> 2] |= static_cast<uint32_t>(p[i]) << (8 * (i & 3));
-                v[u] = u32x4{w[0], w[1], w[2], w[3]};
+                v = u32x4{w[0], w[1], w[2], w[3]};
             }
-            __builtin_amdgcn_raw_buffer_store_b128(v[u], rpay, c * 16, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rpay, c * 16, 0, 2);
         }
     }
 }
 
-// fragments_to_string, streaming: the mirror of the split -- chunk c of payload j (an aligned
-// 16-byte load) lands at object offset j*bs + 16c (an unaligned store when bs % 16 != 0; aligned
-// loads + unaligned stores measured faster than the reverse for Swift's bs = 104858); the
-// payload's last partial chunk and anything reaching past the object's end go byte by byte, so
-// nothing is written outside [0, size).
+// Bytes [d, d + 16) of the 32-byte pair (lo, hi), d = 4 * dw + by wave-uniform: v_alignbyte on
+// the dword pairs (realigns an unaligned 16-byte window from two aligned loads).
+__device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int dw, int by)
+{
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    u32x4 o;
+    switch (dw) {  // wave-uniform
+    case 0: o = u32x4{w[0], w[1], w[2], w[3]}; break;
+    case 1: o = u32x4{w[1], w[2], w[3], w[4]}; break;
+    case 2: o = u32x4{w[2], w[3], w[4], w[5]}; break;
+    default: o = u32x4{w[3], w[4], w[5], w[6]}; break;
+    }
+    if (by) {
+        const uint32_t n = dw == 0 ? w[4] : dw == 1 ? w[5] : dw == 2 ? w[6] : w[7];
+        o = u32x4{__builtin_amdgcn_alignbyte(o.y, o.x, by), __builtin_amdgcn_alignbyte(o.z, o.y, by),
+                  __builtin_amdgcn_alignbyte(o.w, o.z, by), __builtin_amdgcn_alignbyte(n, o.w, by)};
+    }
+    return o;
+}
+
+// fragments_to_string, streaming: payload j fills object bytes [lo, hi) = [j*bs, min((j+1)*bs,
+// size)); its lanes write the object's aligned 16-byte chunks [floor(lo/16), ceil(hi/16)).  A chunk
+// wholly inside [lo, hi) is an aligned store of bytes [p, p + 16) of the payload (p = 16ch - lo),
+// realigned in registers from the two aligned payload chunks under it when bs % 16 != 0 (Swift's
+// 1 MiB segments at k = 10: bs = 104858) -- aligned loads and stores on both sides.  The partial
+// chunks at either end of the range (shared with the neighbouring payload) and a window whose
+// second chunk would reach past the payload go byte by byte; nothing is written outside [0, size).
 __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
 {
     const int bs = static_cast<int>(a.bs);
     const int size = static_cast<int>(a.size);
-    const uint32_t per_frag = static_cast<uint32_t>((bs + 15) / 16);
+    const uint32_t per_frag = static_cast<uint32_t>(bs / 16 + 2);
     const uint32_t tpf = (per_frag + 256 * kCopyU - 1) / (256 * kCopyU);
     const uint32_t ntiles = tpf * static_cast<uint32_t>(k) * static_cast<uint32_t>(a.nstripes);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -310,28 +346,39 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         const uint32_t tc = t - sj * tpf;
         const uint32_t s = sj / static_cast<uint32_t>(k);
         const int j = static_cast<int>(sj - s * static_cast<uint32_t>(k));
+        const int lo = j * bs;
+        const int hi = lo + bs < size ? lo + bs : size;
+        if (hi <= lo) continue;  // payload past the object's end (wave-uniform)
+        const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
+        const int delta = (16 - (lo & 15)) & 15;  // p mod 16 for every chunk of this payload
+        const int dw = delta >> 2, by = delta & 3;
         const uint8_t* pay = a.frags + static_cast<int64_t>(s) * a.stripe_stride + j * a.frag_stride + kHeaderBytes;
         const auto rpay = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay), 0, bs, 0x00020000);
         uint8_t* ob = a.obj + static_cast<int64_t>(s) * a.obj_stride;
         const auto robj = __builtin_amdgcn_make_buffer_rsrc(ob, 0, size, 0x00020000);
-        u32x4 v[kCopyU];
+        u32x4 v0[kCopyU], v1[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
-            const bool full = c * 16 + 16 <= bs && j * bs + c * 16 + 16 <= size;
-            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, full ? c * 16 : static_cast<int>(0x80000000u), 0, 2);
+            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
+            const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi &&
+                              (delta == 0 || (q << 4) + 32 <= bs);
+            v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
+            v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                rpay, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
-            if (c >= static_cast<int>(per_frag)) continue;
-            const int dst = j * bs + c * 16;
-            if (c * 16 + 16 <= bs && dst + 16 <= size) {
-                __builtin_amdgcn_raw_buffer_store_b128(v[u], robj, dst, 0, 2);
+            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            if (ch >= c1) continue;
+            const int A = ch << 4;
+            const int q = (A - lo) >> 4;
+            if (A >= lo && A + 16 <= hi && (delta == 0 || (q << 4) + 32 <= bs)) {
+                __builtin_amdgcn_raw_buffer_store_b128(delta ? window16(v0[u], v1[u], dw, by) : v0[u], robj, A, 0, 2);
                 continue;
             }
-            const int n = min(bs - c * 16, size - dst);  // the payload's tail / the object's end
-            for (int i = 0; i < n; ++i) ob[dst + i] = pay[c * 16 + i];
+            const int b0 = A > lo ? A : lo, b1 = A + 16 < hi ? A + 16 : hi;
+            for (int b = b0; b < b1; ++b) ob[b] = pay[b - lo];
         }
     }
 }

@@ -524,7 +524,7 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
                 static_cast<int64_t>(obj_size), nstripes,
                 (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
     if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0)
-        hipLaunchKernelGGL(frame_join_stream_kernel, dim3(copy_grid(dev, (bs + 15) / 16, k, nstripes)),
+        hipLaunchKernelGGL(frame_join_stream_kernel, dim3(copy_grid(dev, bs / 16 + 2, k, nstripes)),
                            dim3(256), 0, static_cast<hipStream_t>(stream), ja, k);
     else
         hipLaunchKernelGGL(frame_join_kernel,

@@ -175,6 +175,7 @@ struct BsEntry {
     std::vector<int> coeff;
     int R = 0, K = 0;
     int depth = 0;        // bitslice_source: 0 register loads, 2 / 4 LDS ring
+    bool copy = false;    // copy-through variant (framed paths)
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -242,7 +243,9 @@ const std::string& generator_fingerprint()
     static std::once_flag once;
     std::call_once(once, [] {
         const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0);
-        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + kBsNetworkVersion;
+        BitsliceStyle copy;
+        copy.copy_through = true;
+        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -265,7 +268,7 @@ void stop_children_at_exit()
 void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
     BsEntry& e = *ep;
-    const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth);
+    const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
@@ -360,11 +363,11 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
 // bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
 // keeps the kernel's module loaded until the caller has enqueued its launch.
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold)
+                                std::shared_ptr<void>& hold, bool copy)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
-    depth = bitslice_depth(depth, K);
-    std::vector<int> key = {R, K, depth};
+    depth = copy ? 0 : bitslice_depth(depth, K);
+    std::vector<int> key = {R, K, depth, copy ? 1 : 0};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
     std::unique_lock<std::mutex> lk(g_jit_mu);
@@ -390,6 +393,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->R = R;
         slot->K = K;
         slot->depth = depth;
+        slot->copy = copy;
         slot->arch = device_arch(dev);
         // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
         slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R) > 2 ? 2 : 0);

@@ -174,6 +174,11 @@ struct ecamd_bs_args {
     u32 tiles_per_stripe;
     i32 in_off[32];
     i32 out_off[8];
+    u8* copy_base;
+    i64 copy_stride;
+    u32 copy_records;
+    u32 copy_step;
+    u8 copy_idx[32];
 };
 __device__ __forceinline__ u32 x3(u32 a, u32 b, u32 c)
 {
@@ -310,7 +315,17 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
              "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
              "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
-             "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n";
+             "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n"
+             ;
+        if (style.copy_through) {
+            // straight-line copy stores (a branch per input breaks the register allocation of the
+            // network): a skipped input gets an out-of-range offset, which the buffer unit drops
+            s << "        const __amdgpu_buffer_rsrc_t rcopy = __builtin_amdgcn_make_buffer_rsrc(\n"
+                 "            (void*)(a.copy_base + (i64)s * a.copy_stride), 0, (int)a.copy_records, 0x00020000);\n";
+            for (int j = 0; j < net.K; j++)
+                s << "        const i32 cofs" << j << " = a.copy_idx[" << j << "] == 0xff ? (i32)0x80000000u : (i32)(a.copy_idx["
+                  << j << "] * a.copy_step);\n";
+        }
         acc_init();
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n"
@@ -318,7 +333,12 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
               << "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
               << "] + off + c * 4096, 0, 2);\n"
               << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
-              << "            }\n";
+              << (style.copy_through ? "                __builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" + std::to_string(j) +
+                                                 " + off + c * 4096, 0, 2);  // copy-through\n"
+                                           : std::string())
+              << "            }\n"
+              << (style.copy_through ? "            __builtin_amdgcn_sched_barrier(0);  // stores leave before the network\n"
+                                     : "");
             network(j);
             s << "        }\n";
         }
@@ -404,23 +424,28 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     return s.str();
 }
 
-std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth)
+std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy)
 {
     std::ostringstream s;
-    s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
+    if (copy)
+        s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " 1\n";
+    else
+        s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
     for (size_t i = 0; i < coeff.size(); i++) s << coeff[i] << ((i + 1) % static_cast<size_t>(K) ? " " : "\n");
     return s.str();
 }
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth)
+                            int& depth, bool* copy)
 {
     std::istringstream s(text);
     std::string magic;
-    int version = 0;
-    if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version != 1) return false;
+    int version = 0, cp = 0;
+    if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || (version != 1 && version != 2)) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
+    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 1 || depth != 0)) return false;  // copy: register loads
+    if (copy) *copy = cp != 0;
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)
         if (!(s >> c) || c < 0 || c > 0xffff) return false;

@@ -54,6 +54,7 @@ void bitslice_eval(const BitsliceNet& net, const uint16_t* in /* K x 32 */, uint
 struct BitsliceStyle {
     bool lazy_temps = true;
     bool input_barrier = false;
+    bool copy_through = false;  // framed paths: every input also stored to its copy slot (BsArgs)
 };
 std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
 int bitslice_depth(int depth, int K);
@@ -62,9 +63,9 @@ int bitslice_depth(int depth, int K);
 int bitslice_waves_per_simd(int R);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
-std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth);
+std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth);
+                            int& depth, bool* copy = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)
@@ -82,6 +83,14 @@ struct BsArgs {
     uint32_t tiles_per_stripe;
     int32_t in_off[kBsMaxK];
     int32_t out_off[kBsMaxR];
+    // copy-through (framed encode / decode-join, register loads only): input j is also stored at
+    // copy_base + s*copy_stride + copy_idx[j]*copy_step (copy_idx 0xff: not copied; packed bytes,
+    // not 32-bit offsets, to keep the kernel's scalar registers free); copy_records 0 = off
+    uint8_t* copy_base;
+    int64_t copy_stride;
+    uint32_t copy_records;
+    uint32_t copy_step;
+    uint8_t copy_idx[kBsMaxK];
 };
 
 }  // namespace ecamd

@@ -55,11 +55,13 @@ int main(int argc, char** argv)
     ss << in.rdbuf();
     std::vector<int> coeff;
     int R = 0, K = 0, cap = 0, depth = 0;
-    if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth)) {
+    bool copy = false;
+    if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
-    ecamd::BitsliceStyle style;  // experiments only: the parent's cache key does not see these
+    ecamd::BitsliceStyle style;  // lazy / barrier: experiments only, the parent's cache key does not see them
+    style.copy_through = copy;
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
     std::remove(argv[1]);

@@ -151,4 +151,4 @@ def test_xor_batch_split_into_launches(D):
             assert oc.decode(want, per[s], 1) == 0
             assert all((got[s, i] == want[i]).all() for i in range(k + m)), (s, per[s])
     finally:
-        _lib.dev().ecamd_tune(b"xor_tiles_per_slot", 64)
+        _lib.dev().ecamd_tune(b"xor_tiles_per_slot", -1)

@@ -81,7 +81,7 @@ def main():
                 print(json.dumps(r), flush=True)
         lay.buf.free()
     d.ecamd_tune(b"xor_wgs", 0)
-    d.ecamd_tune(b"xor_tiles_per_slot", 64)
+    d.ecamd_tune(b"xor_tiles_per_slot", -1)
 
 
 if __name__ == "__main__":

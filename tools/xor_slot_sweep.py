@@ -60,7 +60,7 @@ def main():
             print(json.dumps({"shape": f"{k}to{m}", "S": S, "xor_tiles_per_slot": lim, "ms": round(med, 4),
                               "TBps": round(algo / med / 1e9, 3)}), flush=True)
         lay.buf.free()
-    d.ecamd_tune(b"xor_tiles_per_slot", 64)  # the library default
+    d.ecamd_tune(b"xor_tiles_per_slot", -1)  # the library default
 
 
 if __name__ == "__main__":
