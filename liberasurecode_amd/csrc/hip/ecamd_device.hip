@@ -109,18 +109,25 @@ int ensure_device(int* dev_out)
 #undef KP_
         for (const void* k : pk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
+#define KFN_(W, MB) reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 1, MB, true>),     \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 2, MB, true>),         \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 3, MB, true>),         \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4, MB, true>),         \
+               reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5, MB, true>)
 #define KF_(W, MB) reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 1, MB>),           \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 2, MB>),               \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 3, MB>),               \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 4, MB>),               \
                reinterpret_cast<const void*>(&gf16_frame_crc_kernel<W, 5, MB>)
         const void* fk[] = {KF_(2, 1), KF_(4, 1), KF_(8, 1), KF_(2, 4), KF_(4, 4), KF_(8, 4),
+                            KFN_(2, 4), KFN_(4, 4), KFN_(8, 4), KFN_(2, 1), KFN_(4, 1), KFN_(8, 1),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<1>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<4>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>)};
 #undef KF_
+#undef KFN_
         for (const void* k : fk)
             HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes));
         for (const void* k : sk)
@@ -154,6 +161,8 @@ struct Knob {
     }
 };
 
+constexpr int kFrameCrcNibDefault = 0;
+
 struct Tuning {
     Knob threads{0};     // threads per workgroup of the gf16 kernel
     Knob wgs_per_cu{0};  // resident workgroups per CU the grid is sized for
@@ -167,6 +176,8 @@ struct Tuning {
     Knob frame_crc_wgs{0};    //   512-thread workgroups per CU (0 = 2)
     Knob frame_crc_units{0};  //   work units (stripe ranges) per CU to aim for (0 = 4)
     Knob frame_crc_mb{0};     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
+    Knob frame_crc_nib{kFrameCrcNibDefault};  //   1: the codec on nibble tables (conflict-free LDS;
+                                              //   tools/frame_bench.py --fused-sweep); < 0: default
     Knob frame_unfused{0};  // framed encode: 1 = always split then encode (A/B against copy-through)
     Knob frame_copy_stream{1};  // object <-> payload copies: streaming 32-bit-offset kernels (0: the
                                 //   first-version per-16-byte kernels, A/B and fallback)
@@ -237,6 +248,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_wgs") return g_tune.frame_crc_wgs;
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
     if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
+    if (k == "frame_crc_nib") return g_tune.frame_crc_nib;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
 }
@@ -1026,11 +1038,11 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
 
 // LDS bytes of gf16_frame_crc_kernel for an RS(k, m) encode: the pass's split tables, the CRC image
 // (byte tables for the first mb piece dwords) and the waves' state exchange.
-size_t fused_crc_lds(int k, int m, int mb)
+size_t fused_crc_lds(int k, int m, int mb, bool nib)
 {
     const int w = m <= 2 ? 2 : (m <= 4 ? 4 : 8);
     const int ns = 4 * ((k + 3) / 4) + w;
-    return static_cast<size_t>(k) * 512 * 2 * w + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4;
+    return static_cast<size_t>(k) * (nib ? 64 : 512) * 2 * w + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4;
 }
 
 // rs_encode_copy with the payload CRC32 folded in (gf16_frame_crc_kernel): r0 of range r of
@@ -1038,7 +1050,7 @@ size_t fused_crc_lds(int k, int m, int mb)
 // launching when the shape does not fit the fused kernel (the caller then runs the split path).
 int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                        int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb)
+                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb, bool nib)
 {
     constexpr int kThreads = 512;
     constexpr int64_t kTile = kThreads * 16;
@@ -1056,7 +1068,7 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
         if (e->outputs[r] != k + r) return ECAMD_EINVAL;
     const auto& p = map->passes[0];
     ApplyArgs a{};
-    a.tables = map->d_tables + p.offset;
+    a.tables = map->d_tables + (nib ? p.nib_offset : p.offset);
     a.in_base = static_cast<const uint8_t*>(obj);
     a.in_stride = obj_stride;
     a.out_base = static_cast<uint8_t*>(payload0);
@@ -1075,8 +1087,10 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     const int kg = (k + 3) / 4;
     const int ns = 4 * kg + p.width;
     if (mb != 1 && mb != 4) return ECAMD_EINVAL;
-    const size_t lds = fused_crc_lds(k, m, mb);
-    if (lds != p.bytes + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4) return ECAMD_EINVAL;
+    if (nib && (!map->d_tables || p.nib_bytes == 0)) return ECAMD_EINVAL;
+    const size_t lds = fused_crc_lds(k, m, mb, nib);
+    if (lds != (nib ? p.nib_bytes : p.bytes) + (static_cast<size_t>(crc_fused_words(mb)) + 8 * ns) * 4)
+        return ECAMD_EINVAL;
     if (lds > static_cast<size_t>(kLdsBytes)) return ECAMD_EINVAL;
     a.tiles_per_stripe = static_cast<uint32_t>(bs / kTile);
     a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
@@ -1087,21 +1101,28 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     const dim3 grid(static_cast<unsigned>(std::min<int64_t>(units, static_cast<int64_t>(cu_count(map->device)) * wgs)));
     const dim3 block(kThreads);
     hipStream_t st = static_cast<hipStream_t>(stream);
-#define ECAMD_FUSED(W, MB)                                                                                  \
-    switch (kg) {                                                                                           \
-    case 1: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 1, MB>), grid, block, lds, st, a, c); break;        \
-    case 2: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 2, MB>), grid, block, lds, st, a, c); break;        \
-    case 3: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 3, MB>), grid, block, lds, st, a, c); break;        \
-    case 4: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 4, MB>), grid, block, lds, st, a, c); break;        \
-    default: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 5, MB>), grid, block, lds, st, a, c); break;       \
+#define ECAMD_FUSED(W, MB, NIB)                                                                                  \
+    switch (kg) {                                                                                                \
+    case 1: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 1, MB, NIB>), grid, block, lds, st, a, c); break;        \
+    case 2: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 2, MB, NIB>), grid, block, lds, st, a, c); break;        \
+    case 3: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 3, MB, NIB>), grid, block, lds, st, a, c); break;        \
+    case 4: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 4, MB, NIB>), grid, block, lds, st, a, c); break;        \
+    default: hipLaunchKernelGGL((gf16_frame_crc_kernel<W, 5, MB, NIB>), grid, block, lds, st, a, c); break;       \
+    }
+#define ECAMD_FUSED_W(W)                                    \
+    if (nib) {                                              \
+        if (mb == 4) { ECAMD_FUSED(W, 4, true) } else { ECAMD_FUSED(W, 1, true) }    \
+    } else {                                                \
+        if (mb == 4) { ECAMD_FUSED(W, 4, false) } else { ECAMD_FUSED(W, 1, false) }  \
     }
     if (p.width == 2) {
-        if (mb == 4) { ECAMD_FUSED(2, 4) } else { ECAMD_FUSED(2, 1) }
+        ECAMD_FUSED_W(2)
     } else if (p.width == 4) {
-        if (mb == 4) { ECAMD_FUSED(4, 4) } else { ECAMD_FUSED(4, 1) }
+        ECAMD_FUSED_W(4)
     } else {
-        if (mb == 4) { ECAMD_FUSED(8, 4) } else { ECAMD_FUSED(8, 1) }
+        ECAMD_FUSED_W(8)
     }
+#undef ECAMD_FUSED_W
 #undef ECAMD_FUSED
     HIP_TRY(hipGetLastError());
     return 0;
@@ -1283,9 +1304,11 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "crc_pos") {
         g_tune.crc_pos = value;  // 0 off, anything else on
     } else if (k == "frame_crc_wgs") {
-        g_tune.frame_crc_wgs = std::max(0, std::min(value, 4));
+        g_tune.frame_crc_wgs = std::max(0, std::min(value, 8));
     } else if (k == "frame_crc_mb") {
         g_tune.frame_crc_mb = value;
+    } else if (k == "frame_crc_nib") {
+        g_tune.frame_crc_nib = value < 0 ? kFrameCrcNibDefault : (value != 0);
     } else if (k == "frame_crc_units") {
         g_tune.frame_crc_units = std::max(0, std::min(value, 64));
     } else if (k == "frame_copy_padded") {

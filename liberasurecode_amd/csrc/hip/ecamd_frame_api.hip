@@ -356,11 +356,13 @@ int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64
     const uint32_t* img = nullptr;
     // all-byte piece tables (16 KiB) measured 4% faster than byte + nibble (MB = 1, 5.5 KiB) in the
     // fused kernel, where the LDS also serves the codec; MB = 1 when the larger image does not fit
+    // codec on nibble tables (knob frame_crc_nib): conflict-free lookups and an image 1/8 the size
+    const bool nib = dev_tune("frame_crc_nib") != 0;
     int mb = dev_tune("frame_crc_mb") == 1 ? 1 : 4;
-    if (mb == 4 && fused_crc_lds(c.k, c.m, 4) > static_cast<size_t>(kLdsBytes)) mb = 1;
+    if (mb == 4 && fused_crc_lds(c.k, c.m, 4, nib) > static_cast<size_t>(kLdsBytes)) mb = 1;
     if ((rc = fused_image(dev, legacy, mb, &img))) return rc;
     rc = rs_encode_copy_crc(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                            partial, q, stream, mb);
+                            partial, q, stream, mb, nib);
     if (rc) return rc;
     const int J = static_cast<int>(bs / q / 1024);  // KiB per range
     const DevImage* di = nullptr;

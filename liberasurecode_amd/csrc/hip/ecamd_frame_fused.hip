@@ -33,7 +33,9 @@ using crcdev::piece_r0;
 constexpr int kMap4 = 128;  // one G=4 field-table map (8 x 16 words)
 
 // MB: byte tables for the first MB dwords of a piece, nibble tables for the rest (crcdev).
-template <int W, int G, int KG, int MB>
+// NIB: the codec's own lookups on nibble tables (conflict-free, 1/8 of the LDS image) instead of
+// byte tables -- the LDS array, not instruction issue, bounds this kernel.
+template <int W, int G, int KG, int MB, bool NIB>
 __device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* lds, const uint32_t* ctab,
                                             const uint32_t* gap, const StreamTile& t,
                                             uint32_t (&acc)[8][W / 2], uint32_t (&st)[4 * KG + W])
@@ -53,16 +55,23 @@ __device__ __forceinline__ void fused_group(const ApplyArgs& a, const uint8_t* l
             st[j] = lmap<4>(gap, st[j]) ^ piece_r0<MB>(ctab, x[i]);
         }
     }
-    if (4 * G + 0 < a.ncols) mac_chunk_imm<W, 4 * G + 0>(lds, x[0], acc);
-    if (4 * G + 1 < a.ncols) mac_chunk_imm<W, 4 * G + 1>(lds, x[1], acc);
-    if (4 * G + 2 < a.ncols) mac_chunk_imm<W, 4 * G + 2>(lds, x[2], acc);
-    if (4 * G + 3 < a.ncols) mac_chunk_imm<W, 4 * G + 3>(lds, x[3], acc);
-    if constexpr (G + 1 < KG) fused_group<W, G + 1, KG, MB>(a, lds, ctab, gap, t, acc, st);
+    if constexpr (NIB) {
+        if (4 * G + 0 < a.ncols) mac_chunk_nib_imm<W, 4 * G + 0>(lds, x[0], acc);
+        if (4 * G + 1 < a.ncols) mac_chunk_nib_imm<W, 4 * G + 1>(lds, x[1], acc);
+        if (4 * G + 2 < a.ncols) mac_chunk_nib_imm<W, 4 * G + 2>(lds, x[2], acc);
+        if (4 * G + 3 < a.ncols) mac_chunk_nib_imm<W, 4 * G + 3>(lds, x[3], acc);
+    } else {
+        if (4 * G + 0 < a.ncols) mac_chunk_imm<W, 4 * G + 0>(lds, x[0], acc);
+        if (4 * G + 1 < a.ncols) mac_chunk_imm<W, 4 * G + 1>(lds, x[1], acc);
+        if (4 * G + 2 < a.ncols) mac_chunk_imm<W, 4 * G + 2>(lds, x[2], acc);
+        if (4 * G + 3 < a.ncols) mac_chunk_imm<W, 4 * G + 3>(lds, x[3], acc);
+    }
+    if constexpr (G + 1 < KG) fused_group<W, G + 1, KG, MB, NIB>(a, lds, ctab, gap, t, acc, st);
 }
 
 }  // namespace
 
-template <int W, int KG, int MB>
+template <int W, int KG, int MB, bool NIB>
 __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c)
 {
     constexpr int kPieceWords = crcdev::piece_words(MB);
@@ -70,7 +79,7 @@ __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, 
     constexpr int D = W / 2;
     constexpr int EB = 2 * W;
     constexpr int NS = 4 * KG + W;  // state slots: inputs 0 .. 4KG-1, outputs 4KG .. 4KG+W-1
-    const int tbytes = a.ncols * 512 * EB;
+    const int tbytes = a.ncols * (NIB ? 64 : 512) * EB;
     for (int o = threadIdx.x * 16; o < tbytes; o += blockDim.x * 16)
         *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(a.tables + o);
     uint32_t* ctab = reinterpret_cast<uint32_t*>(lds + tbytes);
@@ -110,7 +119,7 @@ __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, 
             for (int w = 0; w < 8; w++)
 #pragma unroll
                 for (int d = 0; d < D; d++) acc[w][d] = 0u;
-            fused_group<W, 0, KG, MB>(a, lds, ctab, gap, tile, acc, st);
+            fused_group<W, 0, KG, MB, NIB>(a, lds, ctab, gap, tile, acc, st);
 #pragma unroll
             for (int o = 0; o < W; o++) {
                 if (o >= a.nrows) break;
@@ -150,14 +159,16 @@ __global__ void __launch_bounds__(512) gf16_frame_crc_kernel(const ApplyArgs a, 
     }
 }
 
-#define ECAMD_FUSED_INST(W, MB)                                                                   \
-    template __global__ void gf16_frame_crc_kernel<W, 1, MB>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 2, MB>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 3, MB>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 4, MB>(const ApplyArgs, const FusedCrcArgs); \
-    template __global__ void gf16_frame_crc_kernel<W, 5, MB>(const ApplyArgs, const FusedCrcArgs);
-ECAMD_FUSED_INST(2, 1) ECAMD_FUSED_INST(4, 1) ECAMD_FUSED_INST(8, 1)
-ECAMD_FUSED_INST(2, 4) ECAMD_FUSED_INST(4, 4) ECAMD_FUSED_INST(8, 4)
+#define ECAMD_FUSED_INST(W, MB, NIB)                                                                   \
+    template __global__ void gf16_frame_crc_kernel<W, 1, MB, NIB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 2, MB, NIB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 3, MB, NIB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 4, MB, NIB>(const ApplyArgs, const FusedCrcArgs); \
+    template __global__ void gf16_frame_crc_kernel<W, 5, MB, NIB>(const ApplyArgs, const FusedCrcArgs);
+ECAMD_FUSED_INST(2, 1, false) ECAMD_FUSED_INST(4, 1, false) ECAMD_FUSED_INST(8, 1, false)
+ECAMD_FUSED_INST(2, 4, false) ECAMD_FUSED_INST(4, 4, false) ECAMD_FUSED_INST(8, 4, false)
+ECAMD_FUSED_INST(2, 4, true) ECAMD_FUSED_INST(4, 4, true) ECAMD_FUSED_INST(8, 4, true)
+ECAMD_FUSED_INST(2, 1, true) ECAMD_FUSED_INST(4, 1, true) ECAMD_FUSED_INST(8, 1, true)
 #undef ECAMD_FUSED_INST
 
 }  // namespace ecamd

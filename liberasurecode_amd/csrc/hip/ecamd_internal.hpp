@@ -59,8 +59,9 @@ int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64
 // nothing launched, when the shape does not fit (bs % 8192, q must divide bs/8192, one map pass).
 int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                        int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb = 1);
-size_t fused_crc_lds(int k, int m, int mb);  // LDS bytes of the fused framed encode
+                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb = 1,
+                       bool nib = false);
+size_t fused_crc_lds(int k, int m, int mb, bool nib = false);  // LDS bytes of the fused framed encode
 // fused image words with byte tables for the first mb dwords of a piece, nibble tables after
 constexpr int crc_fused_words(int mb = 1) { return mb * 1024 + (4 - mb) * 128 + 8 * 128; }
 

@@ -70,7 +70,7 @@ __global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
 template <int KG>
 __global__ void gf16_hybrid_kernel(const ApplyArgs a);
 struct FusedCrcArgs;
-template <int W, int KG, int MB>
+template <int W, int KG, int MB, bool NIB = false>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);

@@ -375,9 +375,10 @@ def test_percall_crc_handoff(F, bs, legacy):
 
 
 @pytest.mark.parametrize("k,m,bs,S", [(10, 4, 1 << 20, 3), (4, 2, 8192, 7), (6, 3, 3 * 8192, 5),
-                                      (8, 4, 64 * 8192, 2), (3, 2, 40 * 8192, 9), (12, 6, 16384, 4)])
+                                      (8, 4, 64 * 8192, 2), (3, 2, 40 * 8192, 9), (12, 6, 16384, 4),
+                                      (20, 8, 4 * 8192, 3)])
 @pytest.mark.parametrize("legacy", [False, True])
-@pytest.mark.parametrize("mb", [1, 4])
+@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1"])
 def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkeypatch):
     """CHKSUM_CRC32 framed encode of objects that fill the payloads: the fused launch (codec +
     copy-through + payload checksums folded per range) against the copy-through encode + separate
@@ -389,7 +390,8 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     size = k * bs
     objs = _objects(S, size, k * 7 + m + bs)
     out = []
-    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", mb), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, mb)), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_nib", 1 if mb in ("nib", "nib1") else 0), "tune")
     try:
         for fused in (1, 0):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_fused", fused), "tune")
@@ -399,6 +401,7 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     finally:
         _lib.dev().ecamd_tune(b"frame_crc_fused", 1)
         _lib.dev().ecamd_tune(b"frame_crc_mb", 0)
+        _lib.dev().ecamd_tune(b"frame_crc_nib", -1)  # the library default
     assert np.array_equal(out[0], out[1])
     if bs <= (1 << 16):
         want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)

@@ -44,3 +44,11 @@ def test_round_robin_balance():
     devs = plan(8, None)
     calls = [devs[n % len(devs)] for n in range(80)]
     assert all(calls.count(d) == 10 for d in devs)
+
+
+def test_current_spec_plans_every_device():
+    """ECAMD_PERCALL_DEVICES=current: the plan keeps every device (the pool may serve any of
+    them) and each call runs on the caller's current device (hostio.cpp pick_device) -- what
+    liberasurecode_amd/shard.py sets for its one-process-per-GPU ranks."""
+    assert plan(8, "current") == list(range(8))
+

@@ -97,18 +97,26 @@ def main():
                           "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms / 1e6, 1)}),
               flush=True)
     d.ecamd_tune(b"frame_unfused", 0)
-    if args.fused_sweep:  # fused CRC encode geometry: workgroups per CU x work units per CU
+    if args.fused_sweep:  # fused CRC encode: codec tables (byte / nibble) x workgroups per CU x units per CU
         fb.checksum = frame.CHKSUM_CRC32
-        for mb, wgs, units in [(b, w, u) for _ in range(2) for b in (1, 4) for w in (2, 3)
-                               for u in (2, 4)]:
-            if True:
+        variants = [(4, 0, 2, 4), (1, 0, 2, 4), (4, 1, 2, 4), (4, 1, 3, 4), (4, 1, 4, 4), (4, 1, 3, 8),
+                    (4, 1, 4, 8), (1, 1, 2, 4), (1, 1, 3, 4), (1, 1, 4, 8)]
+        res = {v: [] for v in variants}
+        for _ in range(3):
+            for mb, nib, wgs, units in variants:
                 d.ecamd_tune(b"frame_crc_mb", mb)
+                d.ecamd_tune(b"frame_crc_nib", nib)
                 d.ecamd_tune(b"frame_crc_wgs", wgs)
                 d.ecamd_tune(b"frame_crc_units", units)
-                ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
-                print(json.dumps({"op": "frame_encode_fused_crc", "mb": mb, "wgs": wgs, "units_per_cu": units,
-                                  "ms": round(ms, 3)}), flush=True)
+                res[(mb, nib, wgs, units)].append(timed(lambda: fb.encode(obj, stream=st), st, args.reps))
+        import statistics
+        for (mb, nib, wgs, units), ts in res.items():
+            ms = statistics.median(ts)
+            print(json.dumps({"op": "frame_encode_fused_crc", "mb": mb, "codec_nib": nib, "wgs": wgs,
+                              "units_per_cu": units, "ms": round(ms, 4),
+                              "frac": round((obj_bytes + payload_bytes) / ms / 1e6 / 8000, 4)}), flush=True)
         d.ecamd_tune(b"frame_crc_mb", 0)
+        d.ecamd_tune(b"frame_crc_nib", -1)
         d.ecamd_tune(b"frame_crc_wgs", 0)
         d.ecamd_tune(b"frame_crc_units", 0)
     # objects that do not fill the payloads: Swift's default 1 MiB EC segments (bs = 104858) and a
