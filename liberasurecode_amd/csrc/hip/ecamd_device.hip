@@ -162,6 +162,7 @@ struct Knob {
 };
 
 constexpr int kFrameCrcNibDefault = 0;
+constexpr int kFrameCrcBsDefault = 1;
 
 struct Tuning {
     Knob threads{0};     // threads per workgroup of the gf16 kernel
@@ -176,6 +177,11 @@ struct Tuning {
     Knob frame_crc_wgs{0};    //   512-thread workgroups per CU (0 = 2)
     Knob frame_crc_units{0};  //   work units (stripe ranges) per CU to aim for (0 = 4)
     Knob frame_crc_mb{0};     //   piece dwords on byte tables (1, 2 or 4; 0 = 1), 4-output passes
+    Knob frame_crc_bs{kFrameCrcBsDefault};  //   1: the bitsliced kernel's crc variant for maps of
+                                            //   <= 4 outputs (< 0: default)
+    Knob frame_crc_bs_wgs{0}; //   its grid in 256-thread workgroups per CU (0: one per work unit)
+    Knob frame_crc_pos{2};    //   its CRC position table sets (1, 2, 4: one gap step per that many pieces;
+                              //   2 measured best, profiles/r03_fused_sweep_pos.log)
     Knob frame_crc_nib{kFrameCrcNibDefault};  //   1: the codec on nibble tables (conflict-free LDS;
                                               //   tools/frame_bench.py --fused-sweep); < 0: default
     Knob frame_unfused{0};  // framed encode: 1 = always split then encode (A/B against copy-through)
@@ -249,6 +255,8 @@ int dev_tune(const char* key)
     if (k == "frame_crc_units") return g_tune.frame_crc_units;
     if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
     if (k == "frame_crc_nib") return g_tune.frame_crc_nib;
+    if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
+    if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
 }
@@ -272,7 +280,7 @@ struct ecamd_map {
 
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy = false);
+                                std::shared_ptr<void>& hold, bool copy = false, int crc = 0);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
                     const std::shared_ptr<void>& hold);
 }  // namespace ecamd
@@ -1128,6 +1136,72 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     return 0;
 }
 
+int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                          int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos)
+{
+    const int mode = g_tune.bitslice;
+    if (!mode || m > 4 || k > kBsMaxK || bs % kBsTile || nstripes <= 0 || q <= 0 || (bs / kBsTile) % q)
+        return ECAMD_EINVAL;
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
+    if (rc) return rc;
+    if (!e->map || !copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)) return ECAMD_EINVAL;
+    for (int j = 0; j < k; j++)
+        if (e->inputs[j] != j) return ECAMD_EINVAL;
+    for (int r = 0; r < m; r++)
+        if (e->outputs[r] != k + r) return ECAMD_EINVAL;
+    const ecamd_map* map = e->map.get();
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(obj);
+    a.in_stride = obj_stride;
+    a.out_base = static_cast<uint8_t*>(payload0);
+    a.out_stride = stripe_stride;
+    a.copy_base = static_cast<uint8_t*>(payload0);
+    a.copy_stride = stripe_stride;
+    a.ncols = k;
+    a.nrows = m;
+    for (int j = 0; j < k; j++) {
+        a.in_off[j] = j * bs;
+        a.copy_off[j] = j * frag_stride;
+    }
+    for (int r = 0; r < m; r++) a.out_off[r] = (k + r) * frag_stride;
+    if (!stream_offsets(a, bs) || !stream_copy_offsets(a, bs) || k > 254) return ECAMD_EINVAL;
+    std::shared_ptr<void> hold;
+    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
+    if (!fn) return ECAMD_EINVAL;
+    BsArgs b{};
+    b.in_base = a.in_base;
+    b.out_base = a.out_base;
+    b.in_stride = a.in_stride;
+    b.out_stride = a.out_stride;
+    b.in_records = a.in_records;
+    b.out_records = a.out_records;
+    b.tiles_per_stripe = static_cast<uint32_t>(bs / kBsTile);
+    b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
+    for (int j = 0; j < k; j++) {
+        b.in_off[j] = a.in_off32[j];
+        b.copy_idx[j] = static_cast<uint8_t>(j);
+    }
+    for (int r = 0; r < m; r++) b.out_off[r] = a.out_off32[r];
+    b.copy_base = a.copy_base;
+    b.copy_stride = a.copy_stride;
+    b.copy_records = a.copy_records;
+    b.copy_step = static_cast<uint32_t>(frag_stride);
+    b.crc_img = d_img;
+    b.crc_partial = d_partial;
+    b.crc_q = q;
+    b.crc_per = static_cast<int32_t>(bs / kBsTile / q);
+    b.crc_nfrag = k + m;
+    const int64_t units = static_cast<int64_t>(nstripes) * q;
+    // one work unit per workgroup by default: the dispatcher hands the next unit to whichever CU
+    // frees a slot, which balances units better than a grid-stride loop over resident workgroups
+    const int wgs = static_cast<int>(g_tune.frame_crc_bs_wgs);
+    const int grid = static_cast<int>(
+        wgs > 0 ? std::min<int64_t>(units, static_cast<int64_t>(cu_count(map->device)) * wgs) : units);
+    return bitslice_launch(fn, b, grid, static_cast<hipStream_t>(stream), hold);
+}
+
 int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
                    int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
                    void* stream, int64_t obj_size)
@@ -1307,6 +1381,12 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_wgs = std::max(0, std::min(value, 8));
     } else if (k == "frame_crc_mb") {
         g_tune.frame_crc_mb = value;
+    } else if (k == "frame_crc_bs") {
+        g_tune.frame_crc_bs = value < 0 ? kFrameCrcBsDefault : value;
+    } else if (k == "frame_crc_pos") {
+        g_tune.frame_crc_pos = value >= 4 ? 4 : value >= 2 ? 2 : 1;
+    } else if (k == "frame_crc_bs_wgs") {
+        g_tune.frame_crc_bs_wgs = std::max(0, std::min(value, 8));
     } else if (k == "frame_crc_nib") {
         g_tune.frame_crc_nib = value < 0 ? kFrameCrcNibDefault : (value != 0);
     } else if (k == "frame_crc_units") {

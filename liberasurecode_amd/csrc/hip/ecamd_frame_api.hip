@@ -320,13 +320,16 @@ int xor_batch_check(const Code& c, const void* base, int64_t ss, int64_t fs, int
 
 std::map<std::pair<int, int>, uint32_t*> g_fused_images;  // (dev, legacy + 2 * mb) -> device image
 
-int fused_image(int dev, bool legacy, int mb, const uint32_t** out)
+int fused_image(int dev, bool legacy, int mb, const uint32_t** out, int tile = 8192, int npos = 0)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_pair(dev, (legacy ? 1 : 0) + 2 * mb);
+    auto key = std::make_pair(dev, (legacy ? 1 : 0) + 2 * mb + 16 * npos + 256 * tile);
     auto it = g_fused_images.find(key);
     if (it == g_fused_images.end()) {
-        const std::vector<uint32_t> w = build_fused_crc_image(CrcMachine(legacy), 8192, mb);
+        // npos > 0: the bitsliced crc variant's image (position sets of byte tables, step = tile)
+        const std::vector<uint32_t> w =
+            npos ? build_fused_crc_image_pos(CrcMachine(legacy), static_cast<uint64_t>(tile), npos)
+                 : build_fused_crc_image(CrcMachine(legacy), static_cast<uint64_t>(tile), mb);
         uint32_t* d = nullptr;
         HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
         HIP_TRY(hipMemcpy(d, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -340,33 +343,25 @@ int fused_image(int dev, bool legacy, int mb, const uint32_t** out)
 // payload checksums (q ranges per payload), then crc_finalize_kernel over the ranges and the
 // headers.  ECAMD_EINVAL (nothing launched) when the shape does not fit: the caller runs the
 // copy-through encode + separate CRC pass instead.
-int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64_t obj_stride,
-                     uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs,
-                     int nstripes, void* stream)
+// Ranges per payload for the fused CRC kernels: enough work units (stripes x ranges) to fill the
+// chip, each a long sequential run of whole tiles.
+int fused_ranges(int dev, int64_t tiles, int nstripes, int default_per_cu)
 {
-    if (dev_tune("frame_crc_fused") == 0 || bs % 8192 || nstripes <= 0) return ECAMD_EINVAL;
-    const int64_t tiles = bs / 8192;
-    int q = 1;  // ranges per payload: enough work units to fill the chip, each a long sequential run
-    const int64_t per_cu = dev_tune("frame_crc_units") > 0 ? dev_tune("frame_crc_units") : 4;
+    int q = 1;
+    const int64_t per_cu = dev_tune("frame_crc_units") > 0 ? dev_tune("frame_crc_units") : default_per_cu;
     while (tiles % (2 * q) == 0 && static_cast<int64_t>(nstripes) * q < per_cu * dev_cu_count(dev)) q *= 2;
+    return q;
+}
+
+// crc_finalize_kernel over the q ranges of every payload of the batch and the 80-byte headers.
+int finalize_ranges(int dev, const Code& c, bool legacy, uint64_t obj_size, uint8_t* frags, int64_t ss,
+                    int64_t fs, int64_t bs, int nstripes, const uint32_t* partial, int q, void* stream)
+{
     const int nf = c.k + c.m;
-    uint32_t* partial = nullptr;
-    int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * q, &partial);
-    if (rc) return rc;
-    const uint32_t* img = nullptr;
-    // all-byte piece tables (16 KiB) measured 4% faster than byte + nibble (MB = 1, 5.5 KiB) in the
-    // fused kernel, where the LDS also serves the codec; MB = 1 when the larger image does not fit
-    // codec on nibble tables (knob frame_crc_nib): conflict-free lookups and an image 1/8 the size
-    const bool nib = dev_tune("frame_crc_nib") != 0;
-    int mb = dev_tune("frame_crc_mb") == 1 ? 1 : 4;
-    if (mb == 4 && fused_crc_lds(c.k, c.m, 4, nib) > static_cast<size_t>(kLdsBytes)) mb = 1;
-    if ((rc = fused_image(dev, legacy, mb, &img))) return rc;
-    rc = rs_encode_copy_crc(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                            partial, q, stream, mb, nib);
-    if (rc) return rc;
     const int J = static_cast<int>(bs / q / 1024);  // KiB per range
     const DevImage* di = nullptr;
-    if ((rc = image(dev, legacy, 5, J, 8, false, &di))) return rc;
+    int rc = image(dev, legacy, 5, J, 8, false, &di);
+    if (rc) return rc;
     CrcArgs a{};
     a.base = frags;
     a.stripe_stride = ss;
@@ -387,6 +382,56 @@ int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64
                        header_args(c, kChksumCrc32, bs, obj_size, 0));
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+// The same framed encode on the bitsliced kernel's crc variant (no codec tables: the LDS serves
+// only the CRC lookups) for maps of up to 4 outputs over whole 16 KiB tiles.  ECAMD_EINVAL when it
+// does not apply or its kernel is still compiling (knob bitslice 1): the caller runs the LDS-table
+// fused kernel instead.
+int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, int64_t obj_stride,
+                         uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs,
+                         int nstripes, void* stream)
+{
+    if (dev_tune("frame_crc_bs") == 0 || c.m > 4 || bs % 16384 || nstripes <= 0) return ECAMD_EINVAL;
+    // one 16 KiB tile per work unit at C3 (64 units per CU, one per workgroup): the dispatcher
+    // balances them (32 / 16 per CU measured 3 / 6% slower, profiles/r03_fused_sweep_pos.log)
+    const int q = fused_ranges(dev, bs / 16384, nstripes, 64);
+    uint32_t* partial = nullptr;
+    int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * (c.k + c.m) * q, &partial);
+    if (rc) return rc;
+    const uint32_t* img = nullptr;
+    const int npos = dev_tune("frame_crc_pos");
+    if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos))) return rc;
+    rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                               partial, q, stream, npos);
+    if (rc) return rc;
+    return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
+}
+
+int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64_t obj_stride,
+                     uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs,
+                     int nstripes, void* stream)
+{
+    if (dev_tune("frame_crc_fused") == 0 || bs % 8192 || nstripes <= 0) return ECAMD_EINVAL;
+    int rc = encode_crc_bitsliced(dev, c, legacy, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, stream);
+    if (rc != ECAMD_EINVAL) return rc;
+    const int q = fused_ranges(dev, bs / 8192, nstripes, 4);
+    const int nf = c.k + c.m;
+    uint32_t* partial = nullptr;
+    rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * q, &partial);
+    if (rc) return rc;
+    const uint32_t* img = nullptr;
+    // all-byte piece tables (16 KiB) measured 4% faster than byte + nibble (MB = 1, 5.5 KiB) in the
+    // fused kernel, where the LDS also serves the codec; MB = 1 when the larger image does not fit
+    // codec on nibble tables (knob frame_crc_nib): conflict-free lookups and an image 1/8 the size
+    const bool nib = dev_tune("frame_crc_nib") != 0;
+    int mb = dev_tune("frame_crc_mb") == 1 ? 1 : 4;
+    if (mb == 4 && fused_crc_lds(c.k, c.m, 4, nib) > static_cast<size_t>(kLdsBytes)) mb = 1;
+    if ((rc = fused_image(dev, legacy, mb, &img))) return rc;
+    rc = rs_encode_copy_crc(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                            partial, q, stream, mb, nib);
+    if (rc) return rc;
+    return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
 }
 
 }  // namespace

@@ -62,6 +62,12 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
                        const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int mb = 1,
                        bool nib = false);
 size_t fused_crc_lds(int k, int m, int mb, bool nib = false);  // LDS bytes of the fused framed encode
+// The same on the bitsliced kernel's crc variant (up to 4 outputs, 16 KiB tiles, q ranges of
+// 16 KiB tiles per payload; d_img: the CRC image built for a 4096-byte chain step).  ECAMD_EINVAL,
+// nothing launched, when it does not apply or the kernel is not compiled yet.
+int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                          int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos = 1);
 // fused image words with byte tables for the first mb dwords of a piece, nibble tables after
 constexpr int crc_fused_words(int mb = 1) { return mb * 1024 + (4 - mb) * 128 + 8 * 128; }
 

@@ -176,6 +176,7 @@ struct BsEntry {
     int R = 0, K = 0;
     int depth = 0;        // bitslice_source: 0 register loads, 2 / 4 LDS ring
     bool copy = false;    // copy-through variant (framed paths)
+    int crc = 0;          // copy-through + payload CRC32 variant: position table sets (1, 2, 4), 0 = none
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -243,9 +244,11 @@ const std::string& generator_fingerprint()
     static std::once_flag once;
     std::call_once(once, [] {
         const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0);
-        BitsliceStyle copy;
+        BitsliceStyle copy, crc;
         copy.copy_through = true;
-        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) + kBsNetworkVersion;
+        crc.copy_through = crc.crc = true;
+        fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
+             bitslice_source(tiny, 0, crc) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -268,7 +271,8 @@ void stop_children_at_exit()
 void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
     BsEntry& e = *ep;
-    const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy);
+    const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
+                                             e.crc > 0 ? e.crc : 1);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
@@ -363,11 +367,13 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
 // bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
 // keeps the kernel's module loaded until the caller has enqueued its launch.
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy)
+                                std::shared_ptr<void>& hold, bool copy, int crc)
 {
-    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
+    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty() || (crc && R > 4)) return nullptr;
+    if (crc) crc = crc >= 4 ? 4 : crc >= 2 ? 2 : 1;
+    copy = copy || crc;
     depth = copy ? 0 : bitslice_depth(depth, K);
-    std::vector<int> key = {R, K, depth, copy ? 1 : 0};
+    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1)};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
     std::unique_lock<std::mutex> lk(g_jit_mu);
@@ -394,9 +400,10 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->K = K;
         slot->depth = depth;
         slot->copy = copy;
+        slot->crc = crc;
         slot->arch = device_arch(dev);
         // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
-        slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R) > 2 ? 2 : 0);
+        slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 ? 2 : 0);
         start_compile(slot, wait);
     }
     const std::shared_ptr<BsEntry> ep = slot;

@@ -179,6 +179,11 @@ struct ecamd_bs_args {
     u32 copy_records;
     u32 copy_step;
     u8 copy_idx[32];
+    const u32* crc_img;
+    u32* crc_partial;
+    i32 crc_q;
+    i32 crc_per;
+    i32 crc_nfrag;
 };
 __device__ __forceinline__ u32 x3(u32 a, u32 b, u32 c)
 {
@@ -214,9 +219,47 @@ __device__ __forceinline__ void tr16(u32 (&A)[16])
 }
 )HIP";
 
+// The crc variant's device helpers -- the same algebra as hip/ecamd_crc_dev.hpp (GF(2)-linear maps
+// of the 32-bit CRC state through field tables in LDS), restated for the stand-alone hiprtc source.
+const char* kPreludeCrc = R"HIP(
+template <int K>
+__device__ __forceinline__ u32 bx4(u32 v)  // 4 * byte K of v, one SDWA op
+{
+    u32 r;
+    if constexpr (K == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(v));
+    else if constexpr (K == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(v));
+    else if constexpr (K == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(v));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(v));
+    return r;
+}
+__device__ __forceinline__ u32 tab_at(const u32* t, u32 byteoff) { return *(const u32*)((const char*)t + byteoff); }
+// nibble fields: table 2b for the low nibble of byte b, 2b+1 for the high one (16 words each)
+__device__ __forceinline__ u32 lmap4(const u32* t, u32 x)
+{
+    const u32 lo = x & 0x0f0f0f0fu, hi = (x >> 4) & 0x0f0f0f0fu;
+    const u32 a = x3(tab_at(t, bx4<0>(lo)), tab_at(t + 16, bx4<0>(hi)), tab_at(t + 32, bx4<1>(lo)));
+    const u32 b = x3(tab_at(t + 48, bx4<1>(hi)), tab_at(t + 64, bx4<2>(lo)), tab_at(t + 80, bx4<2>(hi)));
+    return x3(a, b, tab_at(t + 96, bx4<3>(lo)) ^ tab_at(t + 112, bx4<3>(hi)));
+}
+// byte fields: table b for byte b (256 words each)
+__device__ __forceinline__ u32 lmap8(const u32* t, u32 x)
+{
+    return x3(tab_at(t, bx4<0>(x)), tab_at(t + 256, bx4<1>(x)), tab_at(t + 512, bx4<2>(x))) ^ tab_at(t + 768, bx4<3>(x));
+}
+// r0 of a 16-byte piece: dword w through the byte tables at tab + 1024 w
+__device__ __forceinline__ u32 piece_r0(const u32* t, u32 a, u32 b, u32 c, u32 d)
+{
+    return x3(lmap8(t, a), lmap8(t + 1024, b), lmap8(t + 2048, c)) ^ lmap8(t + 3072, d);
+}
+)HIP";
+
 }  // namespace
 
-int bitslice_waves_per_simd(int R) { return R <= 4 ? 4 : 2; }
+int bitslice_waves_per_simd(int R, bool crc) { return R <= 4 ? (crc ? 3 : 4) : 2; }
 
 int bitslice_depth(int depth, int K)
 {
@@ -234,7 +277,8 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
       << " inputs, " << net.xor_ops() << " network ops per tile, "
       << (D ? "LDS ring of " + std::to_string(D) + " inputs per wave" : std::string("register loads")) << "\n";
     s << kPrelude;
-    const int wpe = bitslice_waves_per_simd(net.R);
+    if (style.crc) s << kPreludeCrc;
+    const int wpe = bitslice_waves_per_simd(net.R, style.crc);
     s << "extern \"C\" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
       << wpe << ")))\n"
          "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
@@ -305,6 +349,97 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "            }\n"
              "        }\n";
     };
+    if (style.crc) {
+        // Work unit u = (stripe, range of crc_per consecutive tiles).  Lane l's pieces of one fragment
+        // sit at tile*16384 + c*4096 + l*16, c = 0..3: consecutive pieces are 4096 bytes apart across
+        // tile boundaries too, so each lane state steps s = A^4096 s ^ r0(piece) (gap map).  At the
+        // end of the unit a 6-level shuffle butterfly folds each wave (1 KiB segments of every 4 KiB
+        // block), the 4 waves meet in LDS and Horner with A^1024 gives r0 of the range.
+        const int NS = net.K + net.R;
+        const int NP = style.crc_pos >= 4 ? 4 : style.crc_pos >= 2 ? 2 : 1;
+        const int words = bs_crc_words(NP);
+        // the CRC of 4 pieces x0..x3 (4096 bytes apart) of fragment f: NP pieces per gap step, piece c
+        // through position set c % NP
+        auto crc4 = [&](const std::string& f, const char* x) {
+            for (int c0 = 0; c0 < 4; c0 += NP) {
+                s << "                st[" << f << "] = lmap4(gap, st[" << f << "])";
+                for (int c = c0; c < c0 + NP; c++)
+                    s << " ^ piece_r0(ctab + " << (c % NP) * 4096 << ", " << x << c << "[0], " << x << c << "[1], "
+                      << x << c << "[2], " << x << c << "[3])";
+                s << ";\n";
+            }
+        };
+        s << "    __shared__ u32 ctab[" << words << "];\n"
+          << "    __shared__ u32 xch[4 * " << NS << "];\n"
+          << "    for (int i = threadIdx.x; i < " << words << "; i += 256) ctab[i] = a.crc_img[i];\n"
+          << "    __syncthreads();\n"
+          << "    const u32* gap = ctab + " << NP * 4096 << ";\n"
+             "    const u32* level = gap + 128;\n"
+             "    const u32* a1024 = level + 6 * 128;\n"
+             "    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;\n"
+             "    const u32 units = a.ntiles / a.tiles_per_stripe * (u32)a.crc_q;\n"
+             "    for (u32 u = blockIdx.x; u < units; u += gridDim.x) {\n"
+             "        const u32 s = u / (u32)a.crc_q;\n"
+             "        const u32 rg = u - s * (u32)a.crc_q;\n"
+             "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
+             "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n"
+             "        const __amdgpu_buffer_rsrc_t rcopy = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.copy_base + (i64)s * a.copy_stride), 0, (int)a.copy_records, 0x00020000);\n";
+        for (int j = 0; j < net.K; j++)
+            s << "        const i32 cofs" << j << " = a.copy_idx[" << j << "] == 0xff ? (i32)0x80000000u : (i32)(a.copy_idx["
+              << j << "] * a.copy_step);\n";
+        s << "        u32 st[" << NS << "];\n"
+          << "#pragma unroll\n        for (int f = 0; f < " << NS << "; f++) st[f] = 0u;\n"
+          << "        for (i32 t = (i32)rg * a.crc_per; t < (i32)(rg + 1) * a.crc_per; t++) {\n"
+          << "        const i32 off = t * " << kBsTile << " + (i32)threadIdx.x * 16;\n";
+        acc_init();
+        for (int j = 0; j < net.K; j++) {
+            s << "        {  // input " << j << "\n            u32 P[16];\n";
+            for (int c = 0; c < 4; c++)
+                s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                  << "] + off + " << c * 4096 << ", 0, 2);\n";
+            for (int c = 0; c < 4; c++)
+                s << "            __builtin_amdgcn_raw_buffer_store_b128(xq" << c << ", rcopy, cofs" << j << " + off + "
+                  << c * 4096 << ", 0, 2);  // copy-through\n";
+            crc4(std::to_string(j), "xq");
+            for (int c = 0; c < 4; c++)
+                s << "            P[" << 4 * c << "] = xq" << c << "[0]; P[" << 4 * c + 1 << "] = xq" << c << "[1]; P["
+                  << 4 * c + 2 << "] = xq" << c << "[2]; P[" << 4 * c + 3 << "] = xq" << c << "[3];\n";
+            s << "            __builtin_amdgcn_sched_barrier(0);\n";
+            network(j);
+            s << "        }\n";
+        }
+        for (int r = 0; r < net.R; r++) {
+            s << "        {  // output " << r << "\n            tr16(acc[" << r << "]);\n";
+            for (int c = 0; c < 4; c++)
+                s << "            const v4u vq" << c << " = {acc[" << r << "][" << 4 * c << "], acc[" << r << "][" << 4 * c + 1
+                  << "], acc[" << r << "][" << 4 * c + 2 << "], acc[" << r << "][" << 4 * c + 3 << "]};\n"
+                  << "            __builtin_amdgcn_raw_buffer_store_b128(vq" << c << ", rout, a.out_off[" << r << "] + off + "
+                  << c * 4096 << ", 0, 2);\n";
+            crc4(std::to_string(net.K + r), "vq");
+            s << "        }\n";
+        }
+        s << "        }\n";  // tiles of the unit
+        s << "#pragma unroll\n"
+             "        for (int f = 0; f < " << NS << "; f++) {\n"
+             "            u32 x = st[f];\n"
+             "#pragma unroll\n"
+             "            for (int l = 0; l < 6; l++) x = lmap4(level + 128 * l, x) ^ __shfl_down(x, 1 << l, 64);\n"
+             "            if (lane == 0) xch[wave * " << NS << " + f] = x;\n"
+             "        }\n"
+             "        __syncthreads();\n"
+             "        if ((int)threadIdx.x < " << NS << ") {\n"
+             "            const int f = threadIdx.x;\n"
+             "            u32 v = 0u;\n"
+             "            for (int w = 0; w < 4; w++) v = lmap4(a1024, v) ^ xch[w * " << NS << " + f];\n"
+             "            a.crc_partial[((i64)s * a.crc_nfrag + f) * a.crc_q + rg] = v;\n"
+             "        }\n"
+             "        __syncthreads();\n"
+             "    }\n}\n";
+        return s.str();
+    }
     if (!D) {
         s << "    for (u32 t = blockIdx.x; t < a.ntiles; t += gridDim.x) {\n"
              "        const u32 sl = t / a.tiles_per_stripe;\n"
@@ -424,11 +559,15 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     return s.str();
 }
 
-std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy)
+std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
+                             bool crc, int crc_pos)
 {
     std::ostringstream s;
-    if (copy)
-        s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " 1\n";
+    // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position sets
+    const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
+    if (copy || crc)
+        s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " "
+          << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2)) << "\n";
     else
         s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
     for (size_t i = 0; i < coeff.size(); i++) s << coeff[i] << ((i + 1) % static_cast<size_t>(K) ? " " : "\n");
@@ -436,7 +575,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 }
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth, bool* copy)
+                            int& depth, bool* copy, bool* crc, int* crc_pos)
 {
     std::istringstream s(text);
     std::string magic;
@@ -444,8 +583,12 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || (version != 1 && version != 2)) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 1 || depth != 0)) return false;  // copy: register loads
-    if (copy) *copy = cp != 0;
+    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 11 || depth != 0)) return false;  // copy: register loads
+    if ((cp & 2) && (!(cp & 1) || R > 4)) return false;  // crc implies copy; up to 4 outputs
+    if ((cp >> 2) && !(cp & 2)) return false;
+    if (copy) *copy = (cp & 1) != 0;
+    if (crc) *crc = (cp & 2) != 0;
+    if (crc_pos) *crc_pos = 1 << (cp >> 2);
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)
         if (!(s >> c) || c < 0 || c > 0xffff) return false;

@@ -55,17 +55,31 @@ struct BitsliceStyle {
     bool lazy_temps = true;
     bool input_barrier = false;
     bool copy_through = false;  // framed paths: every input also stored to its copy slot (BsArgs)
+    // framed encode with CRC32 (implies copy_through): the kernel also folds every input and output
+    // 16-byte piece into per-lane CRC states (LDS tables, the codec itself needs none) over work
+    // units of consecutive tiles and writes r0 of each unit's range (BsArgs crc_*)
+    bool crc = false;
+    // crc variant: position table sets (1, 2 or 4): a lane's 4 pieces per fragment and tile are
+    // folded in groups of crc_pos with per-position tables, one gap step per group
+    int crc_pos = 1;
 };
+// LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
+// piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
+// levels + A^1024
+constexpr int bs_crc_words(int npos) { return npos * 4 * 1024 + 8 * 128; }
+constexpr int kBsCrcStep = 4096;  // bytes between a lane's consecutive pieces of one fragment
 std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
 int bitslice_depth(int depth, int K);
 // Waves per SIMD the kernel of an R-output map is built for: 2 (16 R accumulators + the network
-// in <= 256 VGPRs) for 5..8 outputs, 4 (<= 128 VGPRs) for up to 4.
-int bitslice_waves_per_simd(int R);
+// in <= 256 VGPRs) for 5..8 outputs, 4 (<= 128 VGPRs) for up to 4; the crc variant (up to 4
+// outputs) 3 (its K + R CRC states need more than 128).
+int bitslice_waves_per_simd(int R, bool crc = false);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
-std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false);
+std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
+                             bool crc = false, int crc_pos = 1);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth, bool* copy = nullptr);
+                            int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)
@@ -91,6 +105,13 @@ struct BsArgs {
     uint32_t copy_records;
     uint32_t copy_step;
     uint8_t copy_idx[kBsMaxK];
+    // crc variant: unit u = (stripe u / crc_q, range u % crc_q of crc_per tiles); r0 of the range
+    // of fragment f (inputs 0..K-1, then the outputs) lands in crc_partial[(s*crc_nfrag + f)*crc_q + r]
+    const uint32_t* crc_img;  // kBsCrcWords
+    uint32_t* crc_partial;
+    int32_t crc_q;
+    int32_t crc_per;
+    int32_t crc_nfrag;
 };
 
 }  // namespace ecamd

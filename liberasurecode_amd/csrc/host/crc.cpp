@@ -89,6 +89,25 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
     return img;
 }
 
+std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos)
+{
+    // npos sets of all-byte piece tables, set u shifted to the group's last piece
+    // (A^(step*(npos-1-u)) folded in), then the gap map A^(step*npos) and the 6 butterfly levels
+    // and A^1024 of build_fused_crc_image
+    const CrcImage pieces = build_crc_image(m, 8, 4, 4, false);
+    const size_t pw = 4 * 4 * 256;
+    std::vector<uint32_t> w(static_cast<size_t>(npos) * pw + 8 * 128, 0);
+    for (int u = 0; u < npos; u++) {
+        const Mat32 sh = zero_shift(m, step * static_cast<uint64_t>(npos - 1 - u));
+        for (size_t i = 0; i < pw; i++) w[u * pw + i] = sh.apply(pieces.words[i]);
+    }
+    uint32_t* maps = w.data() + static_cast<size_t>(npos) * pw;
+    field_tables(zero_shift(m, step * static_cast<uint64_t>(npos)), 4, maps);
+    for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), 4, maps + 128 * (1 + t));
+    field_tables(zero_shift(m, 1024), 4, maps + 128 * 7);
+    return w;
+}
+
 std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb)
 {
     // piece tables first: byte tables for the first mb dwords (B = 4 + mb; 8 = all four)

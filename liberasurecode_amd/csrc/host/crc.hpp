@@ -81,5 +81,8 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos = fa
 // tables for dword 0 and nibble tables for dwords 1-3, then four G = 4 maps: A^tile_bytes (the
 // step between a lane's pieces), A^(16*2^t) for t < 6 (in-wave butterfly), A^1024 (across waves).
 std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb = 1);
+// The bitsliced crc variant's image: npos position sets of byte piece tables (pieces `step` bytes
+// apart, each set shifted to the group's last piece) + gap A^(step*npos) + butterfly levels + A^1024.
+std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos);
 
 }  // namespace ecamd

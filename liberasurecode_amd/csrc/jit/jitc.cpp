@@ -55,13 +55,16 @@ int main(int argc, char** argv)
     ss << in.rdbuf();
     std::vector<int> coeff;
     int R = 0, K = 0, cap = 0, depth = 0;
-    bool copy = false;
-    if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy)) {
+    bool copy = false, crc = false;
+    int crc_pos = 1;
+    if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy, &crc, &crc_pos)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
     ecamd::BitsliceStyle style;  // lazy / barrier: experiments only, the parent's cache key does not see them
     style.copy_through = copy;
+    style.crc = crc;
+    style.crc_pos = crc_pos;
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
     std::remove(argv[1]);

@@ -378,7 +378,7 @@ def test_percall_crc_handoff(F, bs, legacy):
                                       (8, 4, 64 * 8192, 2), (3, 2, 40 * 8192, 9), (12, 6, 16384, 4),
                                       (20, 8, 4 * 8192, 3)])
 @pytest.mark.parametrize("legacy", [False, True])
-@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1"])
+@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4"])
 def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkeypatch):
     """CHKSUM_CRC32 framed encode of objects that fill the payloads: the fused launch (codec +
     copy-through + payload checksums folded per range) against the copy-through encode + separate
@@ -390,18 +390,30 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     size = k * bs
     objs = _objects(S, size, k * 7 + m + bs)
     out = []
-    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, mb)), "tune")
+    bsv = str(mb).startswith("bs")
+    if bsv and (m > 4 or bs % 16384):
+        pytest.skip("the bitsliced crc variant takes up to 4 outputs over whole 16 KiB tiles")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, 4 if bsv else mb)), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4}.get(mb, 1)), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_nib", 1 if mb in ("nib", "nib1") else 0), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_bs", 1 if bsv else 0), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2 if bsv else 1), "tune")
     try:
         for fused in (1, 0):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_fused", fused), "tune")
+            n0 = _bs_launches()
             fb = F.FrameBatch(be, k, m, size, S)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
+            if fused and bsv:
+                assert _bs_launches() > n0, "the bitsliced crc variant did not run"
     finally:
         _lib.dev().ecamd_tune(b"frame_crc_fused", 1)
         _lib.dev().ecamd_tune(b"frame_crc_mb", 0)
         _lib.dev().ecamd_tune(b"frame_crc_nib", -1)  # the library default
+        _lib.dev().ecamd_tune(b"frame_crc_bs", -1)
+        _lib.dev().ecamd_tune(b"frame_crc_pos", 1)
+        _lib.dev().ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
     if bs <= (1 << 16):
         want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)

@@ -15,6 +15,13 @@ from liberasurecode_amd import _lib, frame  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
 
+def bs_launches(d):
+    import ctypes
+    f = d.ecamd_bitslice_launches
+    f.restype = ctypes.c_longlong
+    return f()
+
+
 def timed(fn, stream, reps):
     a, b = D.Event(), D.Event()
     fn()
@@ -53,6 +60,7 @@ def main():
     S, k, m, size = args.stripes, 10, 4, 10 * 1048576
     d = _lib.dev()
     d.ecamd_tune(b"grid_mult", args.grid_mult)
+    d.ecamd_tune(b"bitslice", 2)  # run-time compiled kernels ready before any timing (steady state)
     st = D.Stream()
     import bench
     copy_gbs = bench.measured_copy_peak(D, st)
@@ -91,30 +99,45 @@ def main():
                         (1, frame.CHKSUM_CRC32)):
         fb.checksum = ct
         d.ecamd_tune(b"frame_unfused", unfused)
+        n0 = bs_launches(d)
         ms = timed(lambda: fb.encode(obj, stream=st), st, args.reps)
         print(json.dumps({"op": "frame_encode", "unfused": unfused, "checksum": ct, "ms": round(ms, 3),
+                          "bitsliced_launches": bs_launches(d) - n0,
                           "GiBps_object": round(obj_bytes / (ms / 1e3) / 2**30, 1),
                           "min_traffic_GBps": round((obj_bytes + payload_bytes) / ms / 1e6, 1)}),
               flush=True)
     d.ecamd_tune(b"frame_unfused", 0)
     if args.fused_sweep:  # fused CRC encode: codec tables (byte / nibble) x workgroups per CU x units per CU
         fb.checksum = frame.CHKSUM_CRC32
-        variants = [(4, 0, 2, 4), (1, 0, 2, 4), (4, 1, 2, 4), (4, 1, 3, 4), (4, 1, 4, 4), (4, 1, 3, 8),
-                    (4, 1, 4, 8), (1, 1, 2, 4), (1, 1, 3, 4), (1, 1, 4, 8)]
+        # (bitsliced crc variant, its position sets, workgroups per CU (0: one per unit), units per CU);
+        # bitsliced 0 = the LDS-table fused kernel (byte tables, 2 workgroups per CU)
+        variants = [(0, 1, 2, 4), (1, 1, 0, 32), (1, 1, 0, 64), (1, 2, 0, 64), (1, 4, 0, 64), (1, 2, 0, 32),
+                    (1, 4, 0, 32)]
+        d.ecamd_tune(b"bitslice", 2)
+        for bsv, pos, wgs, units in variants:  # compile the crc variants outside the timing
+            d.ecamd_tune(b"frame_crc_bs", bsv)
+            d.ecamd_tune(b"frame_crc_pos", pos)
+            fb.encode(obj, stream=st)
+        st.synchronize()
         res = {v: [] for v in variants}
         for _ in range(3):
-            for mb, nib, wgs, units in variants:
-                d.ecamd_tune(b"frame_crc_mb", mb)
-                d.ecamd_tune(b"frame_crc_nib", nib)
-                d.ecamd_tune(b"frame_crc_wgs", wgs)
+            for bsv, pos, wgs, units in variants:
+                d.ecamd_tune(b"frame_crc_bs", bsv)
+                d.ecamd_tune(b"frame_crc_pos", pos)
+                d.ecamd_tune(b"frame_crc_wgs", wgs if not bsv else 0)
+                d.ecamd_tune(b"frame_crc_bs_wgs", wgs)
                 d.ecamd_tune(b"frame_crc_units", units)
-                res[(mb, nib, wgs, units)].append(timed(lambda: fb.encode(obj, stream=st), st, args.reps))
+                res[(bsv, pos, wgs, units)].append(timed(lambda: fb.encode(obj, stream=st), st, args.reps))
         import statistics
-        for (mb, nib, wgs, units), ts in res.items():
+        for (bsv, pos, wgs, units), ts in res.items():
             ms = statistics.median(ts)
-            print(json.dumps({"op": "frame_encode_fused_crc", "mb": mb, "codec_nib": nib, "wgs": wgs,
+            print(json.dumps({"op": "frame_encode_fused_crc", "bitsliced_crc": bsv, "crc_pos": pos, "wgs": wgs,
                               "units_per_cu": units, "ms": round(ms, 4),
                               "frac": round((obj_bytes + payload_bytes) / ms / 1e6 / 8000, 4)}), flush=True)
+        d.ecamd_tune(b"frame_crc_pos", 1)
+        d.ecamd_tune(b"frame_crc_bs", -1)
+        d.ecamd_tune(b"frame_crc_bs_wgs", 0)
+        d.ecamd_tune(b"bitslice", 1)
         d.ecamd_tune(b"frame_crc_mb", 0)
         d.ecamd_tune(b"frame_crc_nib", -1)
         d.ecamd_tune(b"frame_crc_wgs", 0)
