@@ -212,6 +212,10 @@ struct Tuning {
     Knob tiles_per_slot{0};   // stream passes: most tiles per resident workgroup in one launch
                               //   (longer batches run as several launches; 0: 32 for 4-output
                               //   passes, else 64; tools/slot_sweep.py)
+    Knob bs_grid{1};              // ecamd_bs_kernel: 1 = one workgroup per tile, the dispatcher balancing
+                                  //   them (C5 encode 0.705 -> 0.748, rebuild-8 0.688 -> 0.738 of 8 TB/s,
+                                  //   tools/c5_grid_ab.py); 0 = grid-stride over the resident slots
+    Knob xor_grid{1};             // xor_stream_kernel: 1 = one workgroup per tile, 0 = resident slots
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
@@ -606,7 +610,9 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
             if (c.copy_records) c.copy_base = b.copy_base + s0 * b.copy_stride;
         }
         c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
-        *rc = bitslice_launch(fn, c, static_cast<int>(std::min<int64_t>(c.ntiles, slots)), st, hold);
+        // bs_grid 1: one workgroup per tile (the dispatcher balances the tiles); 0: the resident slots
+        const int64_t grid = g_tune.bs_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots);
+        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold);
     }
     return *rc ? 0 : cover;
 }
@@ -735,18 +741,20 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
             if (!PTRS && g_tune.stream && stream_offsets(a, bs)) {
-                // geometry: 256 threads, xor_wgs workgroups per CU -- by default 3 (12 waves) for
-                // passes of more than 4 inputs into 3+ outputs, else 2 (tools/xor_geom_sweep.py,
-                // profiles/r03_xor_geom.log: (10,6,4) encode 0.712 -> 0.756 of 8 TB/s, (3,3,3)
-                // best at 2); long passes as several launches (xor_tiles_per_slot, as
-                // launch_stream_pass)
+                // geometry: 256 threads, one workgroup per 4 KiB tile (xor_grid; the dispatcher
+                // hands each freed slot the next tile: (10,6,4) encode 0.753 -> 0.790 of 8 TB/s,
+                // (3,3,3) 0.717 -> 0.743, profiles/r03_xor_grid.log); long passes as several
+                // launches of xor_tiles_per_slot tiles per slot (as launch_stream_pass), slots =
+                // xor_wgs per CU -- by default 3 for passes of more than 4 inputs into 3+ outputs,
+                // else 2 (tools/xor_geom_sweep.py, profiles/r03_xor_geom.log)
                 const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : (a.ncols > 4 && a.nrows >= 3 ? 3 : 2);
                 const int64_t slots = static_cast<int64_t>(cu_count(dev)) * wgs;
                 const int knob = g_tune.xor_tiles_per_slot;
                 rc = for_each_launch(a, nstripes, g.tiles_per_stripe, static_cast<uint64_t>(slots),
                                      static_cast<uint64_t>(std::max(knob, 0)), [&](ApplyArgs& c, int n) {
                     c.ntiles = g.tiles_per_stripe * static_cast<uint32_t>(n);
-                    const dim3 grid(static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(c.ntiles, slots)))),
+                    const dim3 grid(static_cast<int>(std::max<int64_t>(
+                        1, g_tune.xor_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots)))),
                         block(g.threads);
                     switch ((c.ncols + 3) / 4) {
                     case 1: hipLaunchKernelGGL((xor_stream_kernel<1>), grid, block, 0, st, c); break;
@@ -1427,6 +1435,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream_pf = value != 0;
     } else if (k == "tiles_per_slot") {
         g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
+    } else if (k == "bs_grid") {
+        g_tune.bs_grid = value < 0 ? 1 : value != 0;
+    } else if (k == "xor_grid") {
+        g_tune.xor_grid = value != 0;  // < 0: the default (1)
     } else if (k == "bs_tiles_per_slot") {
         g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--wgs", default="2,3,4")
     ap.add_argument("--slots", default="64,32,0")
+    ap.add_argument("--grid", default="0", help="xor_grid values (1: one workgroup per tile)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "xor_geom_sweep.jsonl"))
     args = ap.parse_args()
     d = _lib.dev()
@@ -44,13 +45,15 @@ def main():
                 fn0 = lambda: D.xor_decode(k, m, hd, lost, lay, stream=st)  # noqa: E731
                 algo = None
             variants = {}
-            for w in [int(x) for x in args.wgs.split(",")]:
-                for t in [int(x) for x in args.slots.split(",")]:
-                    def fn(w=w, t=t):
-                        d.ecamd_tune(b"xor_wgs", w)
-                        d.ecamd_tune(b"xor_tiles_per_slot", t)
-                        fn0()
-                    variants[f"w{w}_t{t}"] = fn
+            for gr in [int(x) for x in args.grid.split(",")]:
+                for w in [int(x) for x in args.wgs.split(",")]:
+                    for t in [int(x) for x in args.slots.split(",")]:
+                        def fn(w=w, t=t, gr=gr):
+                            d.ecamd_tune(b"xor_grid", gr)
+                            d.ecamd_tune(b"xor_wgs", w)
+                            d.ecamd_tune(b"xor_tiles_per_slot", t)
+                            fn0()
+                        variants[f"g{gr}_w{w}_t{t}"] = fn
             ref = None
             for n, fn in variants.items():
                 fn()
@@ -81,6 +84,7 @@ def main():
                 print(json.dumps(r), flush=True)
         lay.buf.free()
     d.ecamd_tune(b"xor_wgs", 0)
+    d.ecamd_tune(b"xor_grid", 1)
     d.ecamd_tune(b"xor_tiles_per_slot", -1)
 
 
