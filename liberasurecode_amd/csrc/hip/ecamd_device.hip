@@ -206,6 +206,11 @@ struct Tuning {
                             //   LDS ring 2 / 4 deep; tools/c5_prof.py C5_MODES A/B
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
+    Knob stream_chunk{-1};  //   > 0: grid of one workgroup per `stream_chunk` consecutive tiles (the
+                            //   dispatcher balancing them, as bs_grid), 0: grid-stride over the
+                            //   slots; -1 (default): 2 when the tables are at most 8 KiB (C2 encode
+                            //   0.783 -> 0.803 of 8 TB/s), else 0 -- a workgroup per range reloads
+                            //   the tables (C3's 40 KiB: 0.739 -> 0.64-0.69, tools/stream_chunk_ab.py)
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     Knob stream_pf{0};      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
@@ -215,6 +220,7 @@ struct Tuning {
     Knob bs_grid{1};              // ecamd_bs_kernel: 1 = one workgroup per tile, the dispatcher balancing
                                   //   them (C5 encode 0.705 -> 0.748, rebuild-8 0.688 -> 0.738 of 8 TB/s,
                                   //   tools/c5_grid_ab.py); 0 = grid-stride over the resident slots
+    Knob frame_copy_grid{0};      // framed split / join stream kernels: 1 = one workgroup per tile
     Knob xor_grid{1};             // xor_stream_kernel: 1 = one workgroup per tile, 0 = resident slots
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
@@ -248,6 +254,7 @@ int dev_tune(const char* key)
     const std::string k(key);
     if (k == "crc_bits") return g_tune.crc_bits;
     if (k == "crc_wgs") return g_tune.crc_wgs;
+    if (k == "frame_copy_grid") return g_tune.frame_copy_grid;
     if (k == "frame_unfused") return g_tune.frame_unfused;
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     if (k == "crc_pos") return g_tune.crc_pos;
@@ -493,7 +500,14 @@ int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch
         c.ntiles = h.ntiles;
         c.tiles_per_stripe = h.tiles_per_stripe;
         c.tile_order = g_tune.stream_order;
-        return launch_stream(c, width, ch, g_tune.stream_pf != 0, nib, dim3(h.grid), dim3(h.threads), h.lds, st);
+        int grid = h.grid;
+        const int chunk = g_tune.stream_chunk >= 0 ? g_tune.stream_chunk : (h.lds <= 8192 ? 2 : 0);
+        if (chunk > 0) {  // contiguous ranges of `chunk` tiles, one per workgroup
+            const uint64_t per = static_cast<uint64_t>(chunk);
+            grid = static_cast<int>(std::min<uint64_t>((h.ntiles + per - 1) / per, 1u << 30));
+            c.tile_order = 1;
+        }
+        return launch_stream(c, width, ch, g_tune.stream_pf != 0, nib, dim3(grid), dim3(h.threads), h.lds, st);
     });
 }
 
@@ -1378,7 +1392,7 @@ int ecamd_tune(const char* key, int value)
         // 4 nibble tables, 8 byte tables, 5..7 byte tables for the first bits-4 dwords of a piece
         g_tune.crc_bits = (value >= 4 && value <= 8) ? value : 5;  // 0 restores the default (5)
     } else if (k == "crc_wgs") {
-        g_tune.crc_wgs = std::max(0, std::min(value, 4));
+        g_tune.crc_wgs = std::max(0, std::min(value, 1 << 16));  // > resident: one workgroup per 8 spans
     } else if (k == "crc_gap_bits") {
         g_tune.crc_gap_bits = value == 4 ? 4 : 8;  // 0 restores the default (8)
     } else if (k == "crc_span_kib") {
@@ -1427,6 +1441,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.bitslice_depth = value >= 4 ? 4 : value >= 2 ? 2 : 0;
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
+    } else if (k == "stream_chunk") {
+        g_tune.stream_chunk = std::max(-1, std::min(value, 1 << 16));  // -1: by table size
     } else if (k == "stream_order") {
         g_tune.stream_order = std::max(0, std::min(value, 3));
     } else if (k == "stream_nib") {
@@ -1437,6 +1453,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
     } else if (k == "bs_grid") {
         g_tune.bs_grid = value < 0 ? 1 : value != 0;
+    } else if (k == "frame_copy_grid") {
+        g_tune.frame_copy_grid = value > 0;
     } else if (k == "xor_grid") {
         g_tune.xor_grid = value != 0;  // < 0: the default (1)
     } else if (k == "bs_tiles_per_slot") {

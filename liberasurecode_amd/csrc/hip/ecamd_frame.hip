@@ -328,15 +328,19 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 }
 
 // fragments_to_string, streaming: payload j fills object bytes [lo, hi) = [j*bs, min((j+1)*bs,
-// size)); its lanes write the object's aligned 16-byte chunks [floor(lo/16), ceil(hi/16)).  A chunk
-// wholly inside [lo, hi) is an aligned store of bytes [p, p + 16) of the payload (p = 16ch - lo),
-// realigned in registers from the two aligned payload chunks under it when bs % 16 != 0 (Swift's
-// 1 MiB segments at k = 10: bs = 104858) -- aligned loads and stores on both sides.  The partial
-// chunks at either end of the range (shared with the neighbouring payload) and a window whose
-// second chunk would reach past the payload go byte by byte; nothing is written outside [0, size).
+// size)).  Every aligned 16-byte object chunk has ONE owner: payload j writes chunks
+// [floor(lo/16), e) with e = floor(hi/16) below the object's end (a chunk straddling payloads j and
+// j+1 belongs to j+1) and ceil(size/16) for the last payload.  A chunk wholly inside [lo, hi) is an
+// aligned store of payload bytes [p, p + 16) (p = 16ch - lo), realigned in registers from the two
+// aligned payload chunks under it when bs % 16 != 0 (Swift's 1 MiB segments at k = 10: bs = 104858);
+// the payload rows are read up to their 16-byte-rounded length, which the fragment layout reserves.
+// The straddling chunk is one lane's store too: the last 16 payload bytes of j-1, realigned, joined
+// with the first bytes of j.  Only the object's final partial chunk goes byte by byte, so nothing
+// is written outside [0, size).  Needs bs >= 32 (the host falls back to frame_join_kernel).
 __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
 {
     const int bs = static_cast<int>(a.bs);
+    const int bs16 = (bs + 15) & ~15;
     const int size = static_cast<int>(a.size);
     const uint32_t per_frag = static_cast<uint32_t>(bs / 16 + 2);
     const uint32_t tpf = (per_frag + 256 * kCopyU - 1) / (256 * kCopyU);
@@ -349,11 +353,11 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         const int lo = j * bs;
         const int hi = lo + bs < size ? lo + bs : size;
         if (hi <= lo) continue;  // payload past the object's end (wave-uniform)
-        const int c0 = lo >> 4, c1 = (hi + 15) >> 4;
+        const int c0 = lo >> 4, c1 = hi < size ? hi >> 4 : (size + 15) >> 4;
         const int delta = (16 - (lo & 15)) & 15;  // p mod 16 for every chunk of this payload
         const int dw = delta >> 2, by = delta & 3;
         const uint8_t* pay = a.frags + static_cast<int64_t>(s) * a.stripe_stride + j * a.frag_stride + kHeaderBytes;
-        const auto rpay = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay), 0, bs, 0x00020000);
+        const auto rpay = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay), 0, bs16, 0x00020000);
         uint8_t* ob = a.obj + static_cast<int64_t>(s) * a.obj_stride;
         const auto robj = __builtin_amdgcn_make_buffer_rsrc(ob, 0, size, 0x00020000);
         u32x4 v0[kCopyU], v1[kCopyU];
@@ -361,8 +365,7 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         for (int u = 0; u < kCopyU; ++u) {
             const int ch = c0 + static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
             const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
-            const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi &&
-                              (delta == 0 || (q << 4) + 32 <= bs);
+            const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi;
             v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
             v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
                 rpay, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
@@ -372,13 +375,28 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
             const int ch = c0 + static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
             if (ch >= c1) continue;
             const int A = ch << 4;
-            const int q = (A - lo) >> 4;
-            if (A >= lo && A + 16 <= hi && (delta == 0 || (q << 4) + 32 <= bs)) {
+            if (A >= lo && A + 16 <= hi) {
                 __builtin_amdgcn_raw_buffer_store_b128(delta ? window16(v0[u], v1[u], dw, by) : v0[u], robj, A, 0, 2);
                 continue;
             }
-            const int b0 = A > lo ? A : lo, b1 = A + 16 < hi ? A + 16 : hi;
-            for (int b = b0; b < b1; ++b) ob[b] = pay[b - lo];
+            if (A < lo && A + 16 <= hi) continue;  // the straddling chunk: below
+            // the object's final partial chunk (bytes before lo, if any, from payload j-1)
+            const int b1 = A + 16 < hi ? A + 16 : hi;
+            for (int b = A; b < b1; ++b) ob[b] = b < lo ? pay[b - lo - a.frag_stride + bs] : pay[b - lo];
+        }
+        // chunk c0 straddles payloads j-1 and j: lane 0 of the payload's first tile
+        if (tc == 0 && (lo & 15) && (c0 << 4) + 16 <= hi && threadIdx.x == 0) {
+            const int d = lo - (c0 << 4);  // bytes from payload j-1
+            const auto rprev = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay - a.frag_stride), 0,
+                                                                 bs16, 0x00020000);
+            const int a0 = (bs - 16) & ~15, e = bs & 15;
+            const u32x4 l0 = __builtin_amdgcn_raw_buffer_load_b128(rprev, a0, 0, 2);
+            const u32x4 l1 = __builtin_amdgcn_raw_buffer_load_b128(rprev, e ? a0 + 16 : static_cast<int>(0x80000000u),
+                                                                   0, 2);
+            const u32x4 tail = e ? window16(l0, l1, e >> 2, e & 3) : l0;  // payload j-1 bytes [bs-16, bs)
+            const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(rpay, 0, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(window16(tail, head, (16 - d) >> 2, (16 - d) & 3), robj, c0 << 4,
+                                                   0, 2);
         }
     }
 }

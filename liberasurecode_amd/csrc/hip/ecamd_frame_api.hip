@@ -178,8 +178,10 @@ int run_crc(int dev, bool legacy, bool with_crc, const uint8_t* base, int64_t ss
         if (rc) return rc;
         int wpc = dev_tune("crc_wgs");
         // Measured on MI355X (C3 payloads, 3.5 GiB): B=8 at 2 workgroups/CU 6.35 TB/s, 3: 5.94,
-        // 4 (LDS-capped to 3): 5.95; B=4 at 4: 5.36 ("Framing").
-        if (wpc <= 0) wpc = B == 8 ? 2 : 4;
+        // 4 (LDS-capped to 3): 5.95; B=4 at 4: 5.36 ("Framing"); the default B=5 with
+        // position tables at 8 (twice the resident grid): 0.703 -> 0.724 of 8 TB/s against 4
+        // (tools/crc_grid_sweep.py, profiles/r03_crc_grid_sweep.log)
+        if (wpc <= 0) wpc = B == 8 ? 2 : 8;
         const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(
                                                       static_cast<int64_t>(dev_cu_count(dev)) * wpc,
                                                       (waves + 7) / 8));
@@ -249,12 +251,13 @@ bool copy_fits32(int k, int64_t frag_stride, int64_t bs, int64_t obj_size)
            (k - 1) * frag_stride + kHeaderBytes + bs + 16 < lim && k * bs < lim;
 }
 
-// Tiles of kCopyU x 256 chunks per (stripe, data fragment); 8 resident 256-thread workgroups per CU.
+// Tiles of kCopyU x 256 chunks per (stripe, data fragment); 8 resident 256-thread workgroups per CU
+// (grid-stride), or one workgroup per tile (knob frame_copy_grid).
 int copy_grid(int dev, int64_t chunks_per_frag, int k, int nstripes)
 {
     const int64_t tiles = (chunks_per_frag + 1023) / 1024 * k * static_cast<int64_t>(nstripes);
-    return static_cast<int>(std::max<int64_t>(
-        1, std::min<int64_t>(tiles, static_cast<int64_t>(dev_cu_count(dev)) * 8)));
+    const int64_t cap = dev_tune("frame_copy_grid") ? (int64_t{1} << 30) : static_cast<int64_t>(dev_cu_count(dev)) * 8;
+    return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(tiles, cap)));
 }
 
 // XOR plan of a reference operation applied in place on the payloads of every stripe.
@@ -570,7 +573,8 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     JoinArgs ja{frags, stripe_stride, frag_stride, bs, static_cast<uint8_t*>(d_obj), obj_stride,
                 static_cast<int64_t>(obj_size), nstripes,
                 (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
-    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0)
+    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && bs >= 32 &&
+        dev_tune("frame_copy_stream") != 0)
         hipLaunchKernelGGL(frame_join_stream_kernel, dim3(copy_grid(dev, bs / 16 + 2, k, nstripes)),
                            dim3(256), 0, static_cast<hipStream_t>(stream), ja, k);
     else

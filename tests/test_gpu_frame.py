@@ -391,8 +391,9 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     objs = _objects(S, size, k * 7 + m + bs)
     out = []
     bsv = str(mb).startswith("bs")
-    if bsv and (m > 4 or bs % 16384):
-        pytest.skip("the bitsliced crc variant takes up to 4 outputs over whole 16 KiB tiles")
+    # the bitsliced crc variant takes up to 4 outputs over whole 16 KiB tiles; other shapes fall
+    # back (LDS-table fused kernel, or for 5-8 outputs the bitsliced copy-through + split CRC pass)
+    bs_fits = m <= 4 and bs % 16384 == 0
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, 4 if bsv else mb)), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4}.get(mb, 1)), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_nib", 1 if mb in ("nib", "nib1") else 0), "tune")
@@ -405,8 +406,10 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
             fb = F.FrameBatch(be, k, m, size, S)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
-            if fused and bsv:
+            if fused and bsv and bs_fits:
                 assert _bs_launches() > n0, "the bitsliced crc variant did not run"
+            elif fused and bsv and m <= 4:
+                assert _bs_launches() == n0, "a bitsliced kernel ran on a shape it does not take"
     finally:
         _lib.dev().ecamd_tune(b"frame_crc_fused", 1)
         _lib.dev().ecamd_tune(b"frame_crc_mb", 0)
@@ -504,8 +507,8 @@ def test_frame_paths_split_into_launches(F, size):
         assert (joined[1][s, size:] == 0xA5).all()
 
 
-COPY_SIZES = [1, 15, 16, 17, 100, 4 * 16 + 3, 777777, 10 * 104858, 10 * 104858 - 3, (1 << 20) * 10 + 6,
-              (1 << 20) * 10]
+COPY_SIZES = [1, 15, 16, 17, 100, 4 * 16 + 3, 339, 407, 777777, 10 * 104858, 10 * 104858 - 3, 1048581,
+              (1 << 20) * 10 + 6, (1 << 20) * 10]
 
 
 @pytest.mark.parametrize("name,k,m,hd", [("rs", 10, 4, 0), ("rs", 4, 2, 0), ("xor", 10, 6, 4),
@@ -514,8 +517,9 @@ COPY_SIZES = [1, 15, 16, 17, 100, 4 * 16 + 3, 777777, 10 * 104858, 10 * 104858 -
 def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
     """Decode with every data fragment present (src/erasurecode.c:597-607: fragments_to_string
     only) runs the streaming join: payload chunks read at unaligned offsets j*bs when bs % 16 != 0,
-    the straddling chunks byte by byte.  Objects equal the originals, guard bytes after each
-    object stay intact, and the first-version join (knob frame_copy_stream 0) agrees."""
+    each chunk straddling two payloads one lane's merged store, the object's last partial chunk
+    byte by byte.  Objects equal the originals, guard bytes after each object stay intact, and the
+    one-workgroup-per-tile grid and the first-version join (knob frame_copy_stream 0) agree."""
     from liberasurecode_amd import _lib
     from liberasurecode_amd.device import DeviceBuffer
     be = _backend(name)
@@ -530,15 +534,18 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
         stride = (size + 16 + 15) // 16 * 16 + 32
         got = []
         try:
-            for knob in (1, 0):
+            for knob, grid in ((1, 0), (1, 1), (0, 0)):
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_stream", knob), "tune")
+                _lib.check(_lib.dev().ecamd_tune(b"frame_copy_grid", grid), "tune")
                 d = DeviceBuffer(S * stride)
                 d.upload(np.full(S * stride, 0xA5, dtype=np.uint8))
                 fb.decode(lost, d, obj_stride=stride)
                 got.append(d.download().reshape(S, stride))
         finally:
             _lib.dev().ecamd_tune(b"frame_copy_stream", 1)
+            _lib.dev().ecamd_tune(b"frame_copy_grid", 0)
         assert np.array_equal(got[0], got[1]), size
+        assert np.array_equal(got[0], got[2]), size
         for s in range(S):
             assert got[0][s, :size].tobytes() == objs[s], (size, s)
             assert (got[0][s, size:] == 0xA5).all(), (size, s)

@@ -38,15 +38,18 @@ def systematic(d, st, fb, out, S, size, tag, reps, copy_gbs):
     """Decode with every data fragment present (src/erasurecode.c:597-607): fragments_to_string
     only -- a copy of S*size object bytes out of the payloads (read + write = 2x the bytes)."""
     for lost in ([], [fb.k, fb.k + 1]):
-        for knob in (1, 0):
+        for knob, grid in ((1, 0), (1, 1), (0, 0)):
             d.ecamd_tune(b"frame_copy_stream", knob)
-            ms = timed(lambda: fb.decode(lost, out, stream=st), st, reps)
+            d.ecamd_tune(b"frame_copy_grid", grid)
+            ms = timed(lambda: fb.decode(lost, out, stream=st), st, reps, warm=3)
             gbs = 2 * S * size / ms / 1e6
             print(json.dumps({"op": "frame_decode_systematic_" + tag, "lost": lost, "copy_stream": knob,
+                              "copy_grid": grid,
                               "ms": round(ms, 4), "GiBps_object": round(S * size / (ms / 1e3) / 2**30, 1),
                               "copy_GBps": round(gbs, 1), "frac_of_copy_probe": round(gbs / copy_gbs, 4),
                               "frac_of_8TBps": round(gbs / 8000, 4)}), flush=True)
     d.ecamd_tune(b"frame_copy_stream", 1)
+    d.ecamd_tune(b"frame_copy_grid", 0)
 
 
 def main():
