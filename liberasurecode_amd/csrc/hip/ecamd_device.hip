@@ -220,7 +220,10 @@ struct Tuning {
     Knob bs_grid{1};              // ecamd_bs_kernel: 1 = one workgroup per tile, the dispatcher balancing
                                   //   them (C5 encode 0.705 -> 0.748, rebuild-8 0.688 -> 0.738 of 8 TB/s,
                                   //   tools/c5_grid_ab.py); 0 = grid-stride over the resident slots
-    Knob frame_copy_grid{0};      // framed split / join stream kernels: 1 = one workgroup per tile
+    Knob frame_crc_lane{0};       // bitsliced crc variant (<= 4 outputs): lane-shift fold (A/B)
+    Knob frame_copy_grid{1};      // framed split / join stream kernels: 1 = one workgroup per tile
+                                  //   (systematic join, Swift 1 MiB segments 0.83 -> 0.91 of the copy
+                                  //   probe, C3 0.97 -> 1.02; tools/frame_bench.py), 0 = 8 per CU
     Knob xor_grid{1};             // xor_stream_kernel: 1 = one workgroup per tile, 0 = resident slots
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
@@ -255,6 +258,7 @@ int dev_tune(const char* key)
     if (k == "crc_bits") return g_tune.crc_bits;
     if (k == "crc_wgs") return g_tune.crc_wgs;
     if (k == "frame_copy_grid") return g_tune.frame_copy_grid;
+    if (k == "frame_crc_lane") return g_tune.frame_crc_lane;
     if (k == "frame_unfused") return g_tune.frame_unfused;
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     if (k == "crc_pos") return g_tune.crc_pos;
@@ -1163,7 +1167,9 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
                           const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos)
 {
     const int mode = g_tune.bitslice;
-    if (!mode || m > 4 || k > kBsMaxK || bs % kBsTile || nstripes <= 0 || q <= 0 || (bs / kBsTile) % q)
+    // more than 4 outputs: the kernel folds every tile on its own (bitslice.cpp fold_each), q = tiles
+    if (!mode || m > kBsMaxR || k > kBsMaxK || bs % kBsTile || nstripes <= 0 || q <= 0 || (bs / kBsTile) % q ||
+        (m > 4 && q != bs / kBsTile))
         return ECAMD_EINVAL;
     std::shared_ptr<RsEntry> e;
     int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
@@ -1190,7 +1196,8 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     for (int r = 0; r < m; r++) a.out_off[r] = (k + r) * frag_stride;
     if (!stream_offsets(a, bs) || !stream_copy_offsets(a, bs) || k > 254) return ECAMD_EINVAL;
     std::shared_ptr<void> hold;
-    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
+    const int crc = crc_pos | (g_tune.frame_crc_lane ? 8 : 0);  // + 8: lane-shift fold (always for m > 4)
+    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1406,7 +1413,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "frame_crc_bs") {
         g_tune.frame_crc_bs = value < 0 ? kFrameCrcBsDefault : value;
     } else if (k == "frame_crc_pos") {
-        g_tune.frame_crc_pos = value >= 4 ? 4 : value >= 2 ? 2 : 1;
+        g_tune.frame_crc_pos = value <= 0 ? 2 : value >= 4 ? 4 : value >= 2 ? 2 : 1;  // <= 0: the default
     } else if (k == "frame_crc_bs_wgs") {
         g_tune.frame_crc_bs_wgs = std::max(0, std::min(value, 8));
     } else if (k == "frame_crc_nib") {
@@ -1453,8 +1460,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.tiles_per_slot = value >= 1 && value <= (1 << 20) ? value : 0;  // 0 restores the default
     } else if (k == "bs_grid") {
         g_tune.bs_grid = value < 0 ? 1 : value != 0;
+    } else if (k == "frame_crc_lane") {
+        g_tune.frame_crc_lane = value > 0;
     } else if (k == "frame_copy_grid") {
-        g_tune.frame_copy_grid = value > 0;
+        g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
     } else if (k == "xor_grid") {
         g_tune.xor_grid = value != 0;  // < 0: the default (1)
     } else if (k == "bs_tiles_per_slot") {

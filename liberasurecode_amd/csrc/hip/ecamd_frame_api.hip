@@ -395,10 +395,11 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
                          uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs,
                          int nstripes, void* stream)
 {
-    if (dev_tune("frame_crc_bs") == 0 || c.m > 4 || bs % 16384 || nstripes <= 0) return ECAMD_EINVAL;
+    if (dev_tune("frame_crc_bs") == 0 || c.m > 8 || bs % 16384 || nstripes <= 0) return ECAMD_EINVAL;
     // one 16 KiB tile per work unit at C3 (64 units per CU, one per workgroup): the dispatcher
-    // balances them (32 / 16 per CU measured 3 / 6% slower, profiles/r03_fused_sweep_pos.log)
-    const int q = fused_ranges(dev, bs / 16384, nstripes, 64);
+    // balances them (32 / 16 per CU measured 3 / 6% slower, profiles/r03_fused_sweep_pos.log);
+    // maps of 5-8 outputs fold every tile on its own (one range per tile)
+    const int q = c.m > 4 ? static_cast<int>(bs / 16384) : fused_ranges(dev, bs / 16384, nstripes, 64);
     uint32_t* partial = nullptr;
     int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * (c.k + c.m) * q, &partial);
     if (rc) return rc;

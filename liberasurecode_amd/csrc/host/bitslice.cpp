@@ -250,6 +250,24 @@ __device__ __forceinline__ u32 lmap8(const u32* t, u32 x)
 {
     return x3(tab_at(t, bx4<0>(x)), tab_at(t + 256, bx4<1>(x)), tab_at(t + 512, bx4<2>(x))) ^ tab_at(t + 768, bx4<3>(x));
 }
+// v through this lane's map A^(16 (63 - lane)): 8 nibble fields, lane-interleaved tables (word
+// (t * 16 + n) * 64 + lane: conflict-free), lofs = 4 * lane
+__device__ __forceinline__ u32 lane_shift(const u32* t, u32 v, u32 lofs)
+{
+    const u32 a = x3(tab_at(t, ((v & 15u) << 8) + lofs), tab_at(t + 1024, (((v >> 4) & 15u) << 8) + lofs),
+                     tab_at(t + 2048, (((v >> 8) & 15u) << 8) + lofs));
+    const u32 b = x3(tab_at(t + 3072, (((v >> 12) & 15u) << 8) + lofs), tab_at(t + 4096, (((v >> 16) & 15u) << 8) + lofs),
+                     tab_at(t + 5120, (((v >> 20) & 15u) << 8) + lofs));
+    return x3(a, b, tab_at(t + 6144, (((v >> 24) & 15u) << 8) + lofs) ^ tab_at(t + 7168, ((v >> 28) << 8) + lofs));
+}
+// lane F of `held` := lane 0 of v (v_readlane into an SGPR, v_writelane back)
+template <int F>
+__device__ __forceinline__ u32 put_lane(u32 held, u32 v)
+{
+    const u32 w = __builtin_amdgcn_readlane(v, 0);
+    asm("v_writelane_b32 %0, %1, %2" : "+v"(held) : "s"(w), "i"(F));
+    return held;
+}
 // r0 of a 16-byte piece: dword w through the byte tables at tab + 1024 w
 __device__ __forceinline__ u32 piece_r0(const u32* t, u32 a, u32 b, u32 c, u32 d)
 {
@@ -355,29 +373,49 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         // tile boundaries too, so each lane state steps s = A^4096 s ^ r0(piece) (gap map).  At the
         // end of the unit a 6-level shuffle butterfly folds each wave (1 KiB segments of every 4 KiB
         // block), the 4 waves meet in LDS and Horner with A^1024 gives r0 of the range.
+        // More than 4 outputs (fold_each): the network leaves no registers for a state per fragment,
+        // so a unit is one tile and each fragment's 4 pieces are folded (butterfly, wave value into
+        // LDS) right after they are checksummed; only the 4-wave combine waits for the tile's end.
+        const bool fold_each = net.R > 4;
+        const bool lane_fold = fold_each || style.crc_lane;
         const int NS = net.K + net.R;
         const int NP = style.crc_pos >= 4 ? 4 : style.crc_pos >= 2 ? 2 : 1;
         const int words = bs_crc_words(NP);
         // the CRC of 4 pieces x0..x3 (4096 bytes apart) of fragment f: NP pieces per gap step, piece c
         // through position set c % NP
         auto crc4 = [&](const std::string& f, const char* x) {
+            const std::string sv = fold_each ? std::string("cs") : "st[" + f + "]";
+            if (fold_each) s << "            u32 cs;\n";
             for (int c0 = 0; c0 < 4; c0 += NP) {
-                s << "                st[" << f << "] = lmap4(gap, st[" << f << "])";
+                if (fold_each && c0 == 0)
+                    s << "            cs = 0u";  // a fresh state: no gap step before the first pieces
+                else
+                    s << "            " << sv << " = lmap4(gap, " << sv << ")";
                 for (int c = c0; c < c0 + NP; c++)
                     s << " ^ piece_r0(ctab + " << (c % NP) * 4096 << ", " << x << c << "[0], " << x << c << "[1], "
                       << x << c << "[2], " << x << c << "[3])";
                 s << ";\n";
             }
+            if (fold_each)  // each lane's state shifted to the segment end, then an XOR reduction
+                s << "            cs = lane_shift(lanes, cs, lofs);\n"
+                     "#pragma unroll\n"
+                     "            for (int l = 0; l < 6; l++) cs ^= __shfl_xor(cs, 1 << l, 64);\n"
+                     // lane f of `held` keeps fragment f's wave value: no branch inside the network code
+                     "            held = put_lane<" << f << ">(held, cs);\n";
         };
-        s << "    __shared__ u32 ctab[" << words << "];\n"
+        const int lds_words = words + (lane_fold ? kBsCrcLaneWords : 0);
+        s << "    __shared__ u32 ctab[" << lds_words << "];\n"
           << "    __shared__ u32 xch[4 * " << NS << "];\n"
-          << "    for (int i = threadIdx.x; i < " << words << "; i += 256) ctab[i] = a.crc_img[i];\n"
+          << "    for (int i = threadIdx.x; i < " << lds_words << "; i += 256) ctab[i] = a.crc_img[i];\n"
           << "    __syncthreads();\n"
           << "    const u32* gap = ctab + " << NP * 4096 << ";\n"
              "    const u32* level = gap + 128;\n"
              "    const u32* a1024 = level + 6 * 128;\n"
-             "    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;\n"
-             "    const u32 units = a.ntiles / a.tiles_per_stripe * (u32)a.crc_q;\n"
+             "    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;\n";
+        if (lane_fold)
+            s << "    const u32* lanes = ctab + " << words << ";\n"
+                 "    const u32 lofs = (u32)lane * 4u;\n";
+        s << "    const u32 units = a.ntiles / a.tiles_per_stripe * (u32)a.crc_q;\n"
              "    for (u32 u = blockIdx.x; u < units; u += gridDim.x) {\n"
              "        const u32 s = u / (u32)a.crc_q;\n"
              "        const u32 rg = u - s * (u32)a.crc_q;\n"
@@ -390,9 +428,11 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         for (int j = 0; j < net.K; j++)
             s << "        const i32 cofs" << j << " = a.copy_idx[" << j << "] == 0xff ? (i32)0x80000000u : (i32)(a.copy_idx["
               << j << "] * a.copy_step);\n";
-        s << "        u32 st[" << NS << "];\n"
-          << "#pragma unroll\n        for (int f = 0; f < " << NS << "; f++) st[f] = 0u;\n"
-          << "        for (i32 t = (i32)rg * a.crc_per; t < (i32)(rg + 1) * a.crc_per; t++) {\n"
+        if (!fold_each)
+            s << "        u32 st[" << NS << "];\n"
+              << "#pragma unroll\n        for (int f = 0; f < " << NS << "; f++) st[f] = 0u;\n";
+        if (fold_each) s << "        u32 held = 0u;\n";
+        s << "        for (i32 t = (i32)rg * a.crc_per; t < (i32)(rg + 1) * a.crc_per; t++) {\n"
           << "        const i32 off = t * " << kBsTile << " + (i32)threadIdx.x * 16;\n";
         acc_init();
         for (int j = 0; j < net.K; j++) {
@@ -421,15 +461,26 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             crc4(std::to_string(net.K + r), "vq");
             s << "        }\n";
         }
-        s << "        }\n";  // tiles of the unit
-        s << "#pragma unroll\n"
-             "        for (int f = 0; f < " << NS << "; f++) {\n"
-             "            u32 x = st[f];\n"
-             "#pragma unroll\n"
-             "            for (int l = 0; l < 6; l++) x = lmap4(level + 128 * l, x) ^ __shfl_down(x, 1 << l, 64);\n"
-             "            if (lane == 0) xch[wave * " << NS << " + f] = x;\n"
-             "        }\n"
-             "        __syncthreads();\n"
+        s << "        }\n";  // tiles of the unit (one when fold_each: the host sets crc_per = 1)
+        if (fold_each)
+            s << "        if (lane < " << NS << ") xch[wave * " << NS << " + lane] = held;\n";
+        else if (lane_fold)
+            s << "#pragma unroll\n"
+                 "        for (int f = 0; f < " << NS << "; f++) {\n"
+                 "            u32 x = lane_shift(lanes, st[f], lofs);\n"
+                 "#pragma unroll\n"
+                 "            for (int l = 0; l < 6; l++) x ^= __shfl_xor(x, 1 << l, 64);\n"
+                 "            if (lane == 0) xch[wave * " << NS << " + f] = x;\n"
+                 "        }\n";
+        else
+            s << "#pragma unroll\n"
+                 "        for (int f = 0; f < " << NS << "; f++) {\n"
+                 "            u32 x = st[f];\n"
+                 "#pragma unroll\n"
+                 "            for (int l = 0; l < 6; l++) x = lmap4(level + 128 * l, x) ^ __shfl_down(x, 1 << l, 64);\n"
+                 "            if (lane == 0) xch[wave * " << NS << " + f] = x;\n"
+                 "        }\n";
+        s << "        __syncthreads();\n"
              "        if ((int)threadIdx.x < " << NS << ") {\n"
              "            const int f = threadIdx.x;\n"
              "            u32 v = 0u;\n"
@@ -560,14 +611,15 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 }
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
-                             bool crc, int crc_pos)
+                             bool crc, int crc_pos, bool crc_lane)
 {
     std::ostringstream s;
-    // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position sets
+    // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
+    // sets, bit 4 lane-shift fold
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     if (copy || crc)
         s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " "
-          << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2)) << "\n";
+          << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0)) << "\n";
     else
         s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
     for (size_t i = 0; i < coeff.size(); i++) s << coeff[i] << ((i + 1) % static_cast<size_t>(K) ? " " : "\n");
@@ -575,7 +627,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 }
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth, bool* copy, bool* crc, int* crc_pos)
+                            int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane)
 {
     std::istringstream s(text);
     std::string magic;
@@ -583,12 +635,14 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || (version != 1 && version != 2)) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 11 || depth != 0)) return false;  // copy: register loads
-    if ((cp & 2) && (!(cp & 1) || R > 4)) return false;  // crc implies copy; up to 4 outputs
+    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 27 || (cp & 12) == 12 || depth != 0))
+        return false;  // copy: register loads
+    if ((cp & 2) && !(cp & 1)) return false;  // crc implies copy
     if ((cp >> 2) && !(cp & 2)) return false;
     if (copy) *copy = (cp & 1) != 0;
     if (crc) *crc = (cp & 2) != 0;
-    if (crc_pos) *crc_pos = 1 << (cp >> 2);
+    if (crc_pos) *crc_pos = 1 << ((cp >> 2) & 3);
+    if (crc_lane) *crc_lane = (cp & 16) != 0;
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)
         if (!(s >> c) || c < 0 || c > 0xffff) return false;

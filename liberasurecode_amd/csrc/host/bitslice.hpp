@@ -62,12 +62,16 @@ struct BitsliceStyle {
     // crc variant: position table sets (1, 2 or 4): a lane's 4 pieces per fragment and tile are
     // folded in groups of crc_pos with per-position tables, one gap step per group
     int crc_pos = 1;
+    // crc variant: fold each wave's lane states with lane-shift tables (one map per lane, 32 KiB
+    // more LDS) and an XOR reduction instead of the 6-level butterfly; always on for 5-8 outputs
+    bool crc_lane = false;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
 // levels + A^1024
 constexpr int bs_crc_words(int npos) { return npos * 4 * 1024 + 8 * 128; }
 constexpr int kBsCrcStep = 4096;  // bytes between a lane's consecutive pieces of one fragment
+constexpr int kBsCrcLaneWords = 8 * 16 * 64;  // lane-shift tables after bs_crc_words (fold-each form)
 std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
 int bitslice_depth(int depth, int K);
 // Waves per SIMD the kernel of an R-output map is built for: 2 (16 R accumulators + the network
@@ -77,9 +81,10 @@ int bitslice_waves_per_simd(int R, bool crc = false);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
-                             bool crc = false, int crc_pos = 1);
+                             bool crc = false, int crc_pos = 1, bool crc_lane = false);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr);
+                            int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
+                            bool* crc_lane = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

@@ -93,7 +93,7 @@ std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t st
 {
     // npos sets of all-byte piece tables, set u shifted to the group's last piece
     // (A^(step*(npos-1-u)) folded in), then the gap map A^(step*npos) and the 6 butterfly levels
-    // and A^1024 of build_fused_crc_image
+    // and A^1024 of build_fused_crc_image, then the lane-shift tables
     const CrcImage pieces = build_crc_image(m, 8, 4, 4, false);
     const size_t pw = 4 * 4 * 256;
     std::vector<uint32_t> w(static_cast<size_t>(npos) * pw + 8 * 128, 0);
@@ -105,6 +105,16 @@ std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t st
     field_tables(zero_shift(m, step * static_cast<uint64_t>(npos)), 4, maps);
     for (int t = 0; t < 6; t++) field_tables(zero_shift(m, 16ull << t), 4, maps + 128 * (1 + t));
     field_tables(zero_shift(m, 1024), 4, maps + 128 * 7);
+    // lane-shift tables (the fold-each kernel of maps of 5-8 outputs): lane l's map A^(16 (63 - l))
+    // as 8 nibble tables, word ((t * 16 + n) * 64 + l), so the 32 lanes of a bank group read 32
+    // distinct banks
+    w.resize(w.size() + 8 * 16 * 64, 0);
+    uint32_t* lanes = w.data() + static_cast<size_t>(npos) * pw + 8 * 128;
+    uint32_t tab[128];
+    for (int l = 0; l < 64; l++) {
+        field_tables(zero_shift(m, 16ull * static_cast<uint64_t>(63 - l)), 4, tab);
+        for (int i = 0; i < 128; i++) lanes[static_cast<size_t>(i) * 64 + l] = tab[i];
+    }
     return w;
 }
 

@@ -378,7 +378,7 @@ def test_percall_crc_handoff(F, bs, legacy):
                                       (8, 4, 64 * 8192, 2), (3, 2, 40 * 8192, 9), (12, 6, 16384, 4),
                                       (20, 8, 4 * 8192, 3)])
 @pytest.mark.parametrize("legacy", [False, True])
-@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4"])
+@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4", "bsl"])
 def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkeypatch):
     """CHKSUM_CRC32 framed encode of objects that fill the payloads: the fused launch (codec +
     copy-through + payload checksums folded per range) against the copy-through encode + separate
@@ -391,11 +391,12 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     objs = _objects(S, size, k * 7 + m + bs)
     out = []
     bsv = str(mb).startswith("bs")
-    # the bitsliced crc variant takes up to 4 outputs over whole 16 KiB tiles; other shapes fall
-    # back (LDS-table fused kernel, or for 5-8 outputs the bitsliced copy-through + split CRC pass)
-    bs_fits = m <= 4 and bs % 16384 == 0
+    # the bitsliced crc variant takes whole 16 KiB tiles (5-8 outputs: its fold-each form); other
+    # payload sizes fall back to the LDS-table fused kernel or the copy-through encode + CRC pass
+    bs_fits = m <= 8 and bs % 16384 == 0
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, 4 if bsv else mb)), "tune")
-    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4}.get(mb, 1)), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4, "bsl": 2}.get(mb, 1)), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_lane", 1 if mb == "bsl" else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_nib", 1 if mb in ("nib", "nib1") else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_bs", 1 if bsv else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2 if bsv else 1), "tune")
@@ -415,7 +416,8 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
         _lib.dev().ecamd_tune(b"frame_crc_mb", 0)
         _lib.dev().ecamd_tune(b"frame_crc_nib", -1)  # the library default
         _lib.dev().ecamd_tune(b"frame_crc_bs", -1)
-        _lib.dev().ecamd_tune(b"frame_crc_pos", 1)
+        _lib.dev().ecamd_tune(b"frame_crc_pos", -1)
+        _lib.dev().ecamd_tune(b"frame_crc_lane", 0)
         _lib.dev().ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
     if bs <= (1 << 16):
@@ -543,7 +545,7 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
                 got.append(d.download().reshape(S, stride))
         finally:
             _lib.dev().ecamd_tune(b"frame_copy_stream", 1)
-            _lib.dev().ecamd_tune(b"frame_copy_grid", 0)
+            _lib.dev().ecamd_tune(b"frame_copy_grid", 1)
         assert np.array_equal(got[0], got[1]), size
         assert np.array_equal(got[0], got[2]), size
         for s in range(S):

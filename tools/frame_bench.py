@@ -49,7 +49,7 @@ def systematic(d, st, fb, out, S, size, tag, reps, copy_gbs):
                               "copy_GBps": round(gbs, 1), "frac_of_copy_probe": round(gbs / copy_gbs, 4),
                               "frac_of_8TBps": round(gbs / 8000, 4)}), flush=True)
     d.ecamd_tune(b"frame_copy_stream", 1)
-    d.ecamd_tune(b"frame_copy_grid", 0)
+    d.ecamd_tune(b"frame_copy_grid", 1)
 
 
 def main():
@@ -115,30 +115,35 @@ def main():
         fb.checksum = frame.CHKSUM_CRC32
         # (bitsliced crc variant, its position sets, workgroups per CU (0: one per unit), units per CU);
         # bitsliced 0 = the LDS-table fused kernel (byte tables, 2 workgroups per CU)
-        variants = [(0, 1, 2, 4), (1, 1, 0, 32), (1, 1, 0, 64), (1, 2, 0, 64), (1, 4, 0, 64), (1, 2, 0, 32),
-                    (1, 4, 0, 32)]
+        # (..., lane-shift fold)
+        variants = [(0, 1, 2, 4, 0), (1, 2, 0, 64, 0), (1, 2, 0, 64, 1), (1, 1, 0, 64, 0), (1, 1, 0, 64, 1),
+                    (1, 2, 0, 32, 1)]
         d.ecamd_tune(b"bitslice", 2)
-        for bsv, pos, wgs, units in variants:  # compile the crc variants outside the timing
+        for bsv, pos, wgs, units, lane in variants:  # compile the crc variants outside the timing
             d.ecamd_tune(b"frame_crc_bs", bsv)
             d.ecamd_tune(b"frame_crc_pos", pos)
+            d.ecamd_tune(b"frame_crc_lane", lane)
             fb.encode(obj, stream=st)
         st.synchronize()
         res = {v: [] for v in variants}
         for _ in range(3):
-            for bsv, pos, wgs, units in variants:
+            for bsv, pos, wgs, units, lane in variants:
                 d.ecamd_tune(b"frame_crc_bs", bsv)
                 d.ecamd_tune(b"frame_crc_pos", pos)
+                d.ecamd_tune(b"frame_crc_lane", lane)
                 d.ecamd_tune(b"frame_crc_wgs", wgs if not bsv else 0)
                 d.ecamd_tune(b"frame_crc_bs_wgs", wgs)
                 d.ecamd_tune(b"frame_crc_units", units)
-                res[(bsv, pos, wgs, units)].append(timed(lambda: fb.encode(obj, stream=st), st, args.reps))
+                res[(bsv, pos, wgs, units, lane)].append(timed(lambda: fb.encode(obj, stream=st), st, args.reps, warm=5))
         import statistics
-        for (bsv, pos, wgs, units), ts in res.items():
+        for (bsv, pos, wgs, units, lane), ts in res.items():
             ms = statistics.median(ts)
-            print(json.dumps({"op": "frame_encode_fused_crc", "bitsliced_crc": bsv, "crc_pos": pos, "wgs": wgs,
+            print(json.dumps({"op": "frame_encode_fused_crc", "bitsliced_crc": bsv, "crc_pos": pos, "lane_fold": lane,
+                              "wgs": wgs,
                               "units_per_cu": units, "ms": round(ms, 4),
                               "frac": round((obj_bytes + payload_bytes) / ms / 1e6 / 8000, 4)}), flush=True)
-        d.ecamd_tune(b"frame_crc_pos", 1)
+        d.ecamd_tune(b"frame_crc_pos", -1)
+        d.ecamd_tune(b"frame_crc_lane", 0)
         d.ecamd_tune(b"frame_crc_bs", -1)
         d.ecamd_tune(b"frame_crc_bs_wgs", 0)
         d.ecamd_tune(b"bitslice", 1)

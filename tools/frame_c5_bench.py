@@ -50,11 +50,37 @@ def main(rounds=5, reps=5):
                 b.record(st)
                 st.synchronize()
                 times[(name, mode)].append(a.elapsed_ms(b) / reps)
+    # CHKSUM_CRC32: the bitsliced crc variant (fold-each form for 8 outputs) against the bitsliced
+    # copy-through encode + the split CRC pass (knob frame_crc_bs 0); fragments checked equal
+    d.ecamd_tune(b"bitslice", 2)
+    fc = frame.FrameBatch(frame.RS_VAND, k, m, size, S, checksum=frame.CHKSUM_CRC32)
+    frags = []
+    for knob in (1, 0):
+        d.ecamd_tune(b"frame_crc_bs", knob)
+        fc.encode(obj, stream=st)
+        st.synchronize()
+        frags.append(fc.fragments())
+    assert (frags[0] == frags[1]).all(), "fused and split CRC framing differ"
+    del frags
+    for _ in range(rounds):
+        for knob in (1, 0):
+            d.ecamd_tune(b"frame_crc_bs", knob)
+            for _ in range(3):
+                fc.encode(obj, stream=st)
+            a.record(st)
+            for _ in range(reps):
+                fc.encode(obj, stream=st)
+            b.record(st)
+            st.synchronize()
+            times.setdefault(("encode_crc32", 3 if knob else 4), []).append(a.elapsed_ms(b) / reps)
+    ops["encode_crc32"] = (None, S * (k + k + m) * F)
+    d.ecamd_tune(b"frame_crc_bs", -1)
     d.ecamd_tune(b"bitslice", 1)
+    kernel = {2: "bitsliced", 0: "lds_tables", 3: "bitsliced_crc_variant", 4: "bitsliced_then_split_crc"}
     for (name, mode), ts in times.items():
         med = statistics.median(ts)
         algo = ops[name][1]
-        print(json.dumps({"op": "frame_c5_" + name, "kernel": "bitsliced" if mode == 2 else "lds_tables",
+        print(json.dumps({"op": "frame_c5_" + name, "kernel": kernel[mode],
                           "ms": round(med, 4), "algorithmic_bytes": algo,
                           "frac": round(algo / med / 1e6 / 8000, 4),
                           "GiBps_object": round(S * size / (med / 1e3) / 2**30, 1)}), flush=True)
