@@ -180,8 +180,10 @@ struct Tuning {
     Knob frame_crc_bs{kFrameCrcBsDefault};  //   1: the bitsliced kernel's crc variant for maps of
                                             //   <= 4 outputs (< 0: default)
     Knob frame_crc_bs_wgs{0}; //   its grid in 256-thread workgroups per CU (0: one per work unit)
-    Knob frame_crc_pos{2};    //   its CRC position table sets (1, 2, 4: one gap step per that many pieces;
-                              //   2 measured best, profiles/r03_fused_sweep_pos.log)
+    Knob frame_crc_pos{0};    //   its CRC position table sets (1, 2, 4: one gap step per that many pieces;
+                              //   0 = by shape: 1 with the lane-shift fold of <= 4 outputs (its 32 KiB
+                              //   of lane tables leave room for 1 set at 3 workgroups per CU), else 2
+                              //   (profiles/r03_fused_sweep_pos.log, r03_fused_sweep_lane.log)
     Knob frame_crc_nib{kFrameCrcNibDefault};  //   1: the codec on nibble tables (conflict-free LDS;
                                               //   tools/frame_bench.py --fused-sweep); < 0: default
     Knob frame_unfused{0};  // framed encode: 1 = always split then encode (A/B against copy-through)
@@ -220,7 +222,9 @@ struct Tuning {
     Knob bs_grid{1};              // ecamd_bs_kernel: 1 = one workgroup per tile, the dispatcher balancing
                                   //   them (C5 encode 0.705 -> 0.748, rebuild-8 0.688 -> 0.738 of 8 TB/s,
                                   //   tools/c5_grid_ab.py); 0 = grid-stride over the resident slots
-    Knob frame_crc_lane{0};       // bitsliced crc variant (<= 4 outputs): lane-shift fold (A/B)
+    Knob frame_crc_lane{1};       // bitsliced crc variant (<= 4 outputs): lane-shift fold with 1
+                                  //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
+                                  //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_copy_grid{1};      // framed split / join stream kernels: 1 = one workgroup per tile
                                   //   (systematic join, Swift 1 MiB segments 0.83 -> 0.91 of the copy
                                   //   probe, C3 0.97 -> 1.02; tools/frame_bench.py), 0 = 8 per CU
@@ -1196,8 +1200,8 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     for (int r = 0; r < m; r++) a.out_off[r] = (k + r) * frag_stride;
     if (!stream_offsets(a, bs) || !stream_copy_offsets(a, bs) || k > 254) return ECAMD_EINVAL;
     std::shared_ptr<void> hold;
-    const int crc = crc_pos | (g_tune.frame_crc_lane ? 8 : 0);  // + 8: lane-shift fold (always for m > 4)
-    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc);
+    // crc_pos: position sets (1, 2, 4) + 8 for the lane-shift fold (which 5-8 outputs always take)
+    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1413,7 +1417,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "frame_crc_bs") {
         g_tune.frame_crc_bs = value < 0 ? kFrameCrcBsDefault : value;
     } else if (k == "frame_crc_pos") {
-        g_tune.frame_crc_pos = value <= 0 ? 2 : value >= 4 ? 4 : value >= 2 ? 2 : 1;  // <= 0: the default
+        g_tune.frame_crc_pos = value <= 0 ? 0 : value >= 4 ? 4 : value >= 2 ? 2 : 1;  // <= 0: by shape
     } else if (k == "frame_crc_bs_wgs") {
         g_tune.frame_crc_bs_wgs = std::max(0, std::min(value, 8));
     } else if (k == "frame_crc_nib") {
@@ -1461,7 +1465,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_grid") {
         g_tune.bs_grid = value < 0 ? 1 : value != 0;
     } else if (k == "frame_crc_lane") {
-        g_tune.frame_crc_lane = value > 0;
+        g_tune.frame_crc_lane = value != 0;  // < 0: the default (1)
     } else if (k == "frame_copy_grid") {
         g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
     } else if (k == "xor_grid") {

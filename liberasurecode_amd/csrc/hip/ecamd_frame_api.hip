@@ -404,10 +404,13 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
     int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * (c.k + c.m) * q, &partial);
     if (rc) return rc;
     const uint32_t* img = nullptr;
-    const int npos = dev_tune("frame_crc_pos");
+    // maps of 5-8 outputs always fold with the lane-shift tables (bitslice.cpp fold_each)
+    const bool lane = c.m > 4 || dev_tune("frame_crc_lane") != 0;
+    int npos = dev_tune("frame_crc_pos");
+    if (npos <= 0) npos = lane && c.m <= 4 ? 1 : 2;
     if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos))) return rc;
     rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                               partial, q, stream, npos);
+                               partial, q, stream, npos | (lane ? 8 : 0));
     if (rc) return rc;
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
 }

@@ -395,7 +395,7 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     # payload sizes fall back to the LDS-table fused kernel or the copy-through encode + CRC pass
     bs_fits = m <= 8 and bs % 16384 == 0
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, 4 if bsv else mb)), "tune")
-    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4, "bsl": 2}.get(mb, 1)), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4, "bsl": 0}.get(mb, 1)), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_lane", 1 if mb == "bsl" else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_nib", 1 if mb in ("nib", "nib1") else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_bs", 1 if bsv else 0), "tune")
@@ -417,7 +417,7 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
         _lib.dev().ecamd_tune(b"frame_crc_nib", -1)  # the library default
         _lib.dev().ecamd_tune(b"frame_crc_bs", -1)
         _lib.dev().ecamd_tune(b"frame_crc_pos", -1)
-        _lib.dev().ecamd_tune(b"frame_crc_lane", 0)
+        _lib.dev().ecamd_tune(b"frame_crc_lane", -1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
     if bs <= (1 << 16):

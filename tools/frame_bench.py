@@ -143,7 +143,7 @@ def main():
                               "units_per_cu": units, "ms": round(ms, 4),
                               "frac": round((obj_bytes + payload_bytes) / ms / 1e6 / 8000, 4)}), flush=True)
         d.ecamd_tune(b"frame_crc_pos", -1)
-        d.ecamd_tune(b"frame_crc_lane", 0)
+        d.ecamd_tune(b"frame_crc_lane", -1)
         d.ecamd_tune(b"frame_crc_bs", -1)
         d.ecamd_tune(b"frame_crc_bs_wgs", 0)
         d.ecamd_tune(b"bitslice", 1)
