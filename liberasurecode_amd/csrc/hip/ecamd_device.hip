@@ -125,7 +125,14 @@ int ensure_device(int* dev_out)
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<2>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<3>),
                             reinterpret_cast<const void*>(&gf16_hybrid_kernel<4>),
-                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>)};
+                            reinterpret_cast<const void*>(&gf16_hybrid_kernel<5>),
+#define KR_(W) reinterpret_cast<const void*>(&gf16_realign_kernel<W, 1>),                        \
+               reinterpret_cast<const void*>(&gf16_realign_kernel<W, 2>),                        \
+               reinterpret_cast<const void*>(&gf16_realign_kernel<W, 3>),                        \
+               reinterpret_cast<const void*>(&gf16_realign_kernel<W, 4>),                        \
+               reinterpret_cast<const void*>(&gf16_realign_kernel<W, 5>)
+                            KR_(2), KR_(4)};
+#undef KR_
 #undef KF_
 #undef KFN_
         for (const void* k : fk)
@@ -208,6 +215,10 @@ struct Tuning {
                             //   LDS ring 2 / 4 deep; tools/c5_prof.py C5_MODES A/B
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
+    Knob stream_realign{0}; //   copy-through inputs at offsets that are not multiples of 16: 1 = aligned
+                            //   loads realigned in registers (gf16_realign_kernel), 0 = unaligned 16-byte
+                            //   loads -- measured faster (Swift segments 1.366 vs 1.444 ms, C3 + 10 B
+                            //   1.226 vs 1.281 ms, tools/realign_ab.py, profiles/r03_realign_ab.log)
     Knob stream_chunk{-1};  //   > 0: grid of one workgroup per `stream_chunk` consecutive tiles (the
                             //   dispatcher balancing them, as bs_grid), 0: grid-stride over the
                             //   slots; -1 (default): 2 when the tables are at most 8 KiB (C2 encode
@@ -420,6 +431,27 @@ int launch_stream_w(const ApplyArgs& a, dim3 grid, dim3 block, size_t lds, hipSt
 int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3 grid, dim3 block,
                   size_t lds, hipStream_t st)
 {
+    bool unaligned = false;  // inputs at offsets that are not multiples of 16 (objects, j*bs)
+    for (int j = 0; j < a.ncols; j++) unaligned = unaligned || (a.in_off32[j] & 15) != 0;
+    if (unaligned && width <= 4 && ch == 1 && !nib && g_tune.stream_realign) {
+        // aligned loads realigned in registers (ecamd_stream.hpp, RA)
+#define RA_(W)                                                                                    \
+    switch ((a.ncols + 3) / 4) {                                                                  \
+    case 1: hipLaunchKernelGGL((gf16_realign_kernel<W, 1>), grid, block, lds, st, a); break;      \
+    case 2: hipLaunchKernelGGL((gf16_realign_kernel<W, 2>), grid, block, lds, st, a); break;      \
+    case 3: hipLaunchKernelGGL((gf16_realign_kernel<W, 3>), grid, block, lds, st, a); break;      \
+    case 4: hipLaunchKernelGGL((gf16_realign_kernel<W, 4>), grid, block, lds, st, a); break;      \
+    default: hipLaunchKernelGGL((gf16_realign_kernel<W, 5>), grid, block, lds, st, a); break;     \
+    }
+        if (width == 2) {
+            RA_(2)
+        } else {
+            RA_(4)
+        }
+#undef RA_
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     if (width == 8 && !nib && g_tune.stream_hybrid) {  // LDS + L1 lookups (gf16_hybrid_kernel)
         switch ((a.ncols + 3) / 4) {
         case 1: hipLaunchKernelGGL((gf16_hybrid_kernel<1>), grid, block, lds, st, a); break;
@@ -1452,6 +1484,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.bitslice_depth = value >= 4 ? 4 : value >= 2 ? 2 : 0;
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
+    } else if (k == "stream_realign") {
+        g_tune.stream_realign = value > 0;  // < 0: the default (0)
     } else if (k == "stream_chunk") {
         g_tune.stream_chunk = std::max(-1, std::min(value, 1 << 16));  // -1: by table size
     } else if (k == "stream_order") {

@@ -69,6 +69,8 @@ template <int W, int KG>
 __global__ void gf16_ptrs_stream_kernel(const ApplyArgs a);
 template <int KG>
 __global__ void gf16_hybrid_kernel(const ApplyArgs a);
+template <int W, int KG>
+__global__ void gf16_realign_kernel(const ApplyArgs a);
 struct FusedCrcArgs;
 template <int W, int KG, int MB, bool NIB = false>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);

@@ -167,9 +167,58 @@ __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds
     }
 }
 
-template <int W, int CH, int G, int KG>
+// Bytes [d, d + 16) of the 32-byte pair (lo, hi), d wave-uniform (a scalar branch picks the
+// dword shift, v_alignbyte the byte shift).
+__device__ __forceinline__ v4u realign16(const v4u& lo, const v4u& hi, int d)
+{
+    const uint32_t w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    v4u o;
+    uint32_t n;
+    switch (d >> 2) {
+    case 0: o = v4u{w[0], w[1], w[2], w[3]}; n = w[4]; break;
+    case 1: o = v4u{w[1], w[2], w[3], w[4]}; n = w[5]; break;
+    case 2: o = v4u{w[2], w[3], w[4], w[5]}; n = w[6]; break;
+    default: o = v4u{w[3], w[4], w[5], w[6]}; n = w[7]; break;
+    }
+    const int by = d & 3;
+    if (by)
+        o = v4u{__builtin_amdgcn_alignbyte(o[1], o[0], by), __builtin_amdgcn_alignbyte(o[2], o[1], by),
+                __builtin_amdgcn_alignbyte(o[3], o[2], by), __builtin_amdgcn_alignbyte(n, o[3], by)};
+    return o;
+}
+
+// RA (realign): inputs at offsets that are not multiples of 16 (copy-through encode straight from
+// objects whose chunks start at j*bs, e.g. Swift's bs = 104858) are read as the two aligned
+// 16-byte chunks under each lane's window and realigned in registers: aligned loads instead of
+// unaligned ones that straddle two chunks (the launcher sends the last 16 bytes of a fragment
+// down the byte-exact tail path, so the second chunk never leaves the input).
+template <int W, int CH, int G, int KG, bool RA = false>
 __device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile& t, v4u (&x)[4][CH])
 {
+    if constexpr (RA) {
+        v4u y[4][CH];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int j = 4 * G + i;
+            const int base = (j < a.ncols) ? (a.in_off32[j] & ~15) + t.off : static_cast<int>(0x80000000u);
+#pragma unroll
+            for (int c = 0; c < CH; c++) {
+                x[i][c] = __builtin_amdgcn_raw_buffer_load_b128(t.rin, base + c * t.cstride, 0, 2);
+                y[i][c] = __builtin_amdgcn_raw_buffer_load_b128(
+                    t.rin, (j < a.ncols && (a.in_off32[j] & 15)) ? base + c * t.cstride + 16
+                                                                 : static_cast<int>(0x80000000u), 0, 2);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int j = 4 * G + i;
+            const int d = j < a.ncols ? a.in_off32[j] & 15 : 0;  // wave-uniform
+            if (d)
+#pragma unroll
+                for (int c = 0; c < CH; c++) x[i][c] = realign16(x[i][c], y[i][c], d);
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int j = 4 * G + i;
@@ -182,12 +231,12 @@ __device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile&
 
 // Group G's lookups; with PF the loads of group G+1 are issued before them (in flight during the
 // lookups), without PF after them (each wave: load, wait, look up -- latency hidden by occupancy).
-template <int W, int CH, int G, int KG, bool PF, int TM>
+template <int W, int CH, int G, int KG, bool PF, int TM, bool RA = false>
 __device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* lds, const StreamTile& t,
                                              v4u (&cur)[4][CH], uint32_t (&acc)[CH][8][W / 2])
 {
     v4u nxt[4][CH];
-    if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG>(a, t, nxt);
+    if constexpr (PF && G + 1 < KG) load_group<W, CH, G + 1, KG, RA>(a, t, nxt);
     if constexpr (TM == 2 && CH == 1) {
         // input 0's hi table via L1 (12.5% of the lookups; taking 3/16 -- input 2's hi for words
         // 0..3, or input 0's lo for words 0..3 -- measured 12% slower than none: a 40 KiB table
@@ -210,18 +259,18 @@ __device__ __forceinline__ void stream_group(const ApplyArgs& a, const uint8_t* 
         input_mac<W, CH, 4 * G + 3, TM>(a, lds, t, cur[3], acc);
     }
     if constexpr (G + 1 < KG) {
-        if constexpr (!PF) load_group<W, CH, G + 1, KG>(a, t, nxt);
+        if constexpr (!PF) load_group<W, CH, G + 1, KG, RA>(a, t, nxt);
 #pragma unroll
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int c = 0; c < CH; c++) cur[i][c] = nxt[i][c];
-        stream_group<W, CH, G + 1, KG, PF, TM>(a, lds, t, cur, acc);
+        stream_group<W, CH, G + 1, KG, PF, TM, RA>(a, lds, t, cur, acc);
     }
 }
 
 }  // namespace
 
-template <int W, int KG, int CH, bool PF, bool NIB, int TM>
+template <int W, int KG, int CH, bool PF, bool NIB, int TM, bool RA = false>
 __device__ __forceinline__ void gf16_stream_body(const ApplyArgs& a)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -252,7 +301,9 @@ __device__ __forceinline__ void gf16_stream_body(const ApplyArgs& a)
         // last, partial tile of each fragment -- and, for objects shorter than the k payloads
         // (ApplyArgs::limited), every tile reaching past the shortest input's end: the byte-exact
         // per-chunk path reads zeros there
-        if (toff + span > a.bs || (a.limited && toff + span > a.min_len)) {
+        // (RA: also the tile holding a fragment's last 16 bytes, whose second aligned chunk would
+        // reach past the input)
+        if (toff + span + (RA ? 16 : 0) > a.bs || (a.limited && toff + span + (RA ? 16 : 0) > a.min_len)) {
 #pragma unroll
             for (int c = 0; c < CH; c++) {
                 const int64_t o = toff + c * cstride + static_cast<int64_t>(threadIdx.x) * 16;
@@ -290,8 +341,8 @@ __device__ __forceinline__ void gf16_stream_body(const ApplyArgs& a)
 #pragma unroll
                 for (int d = 0; d < D; d++) acc[c][w][d] = 0u;
         v4u cur[4][CH];
-        load_group<W, CH, 0, KG>(a, tile, cur);
-        stream_group<W, CH, 0, KG, PF, TM>(a, lds, tile, cur, acc);
+        load_group<W, CH, 0, KG, RA>(a, tile, cur);
+        stream_group<W, CH, 0, KG, PF, TM, RA>(a, lds, tile, cur, acc);
 
 #pragma unroll
         for (int r = 0; r < W; r++) {
@@ -317,6 +368,13 @@ template <int W, int KG, int CH, bool PF, bool NIB>
 __global__ void __launch_bounds__(1024) gf16_stream_kernel(const ApplyArgs a)
 {
     gf16_stream_body<W, KG, CH, PF, NIB, NIB ? 1 : 0>(a);
+}
+
+// Copy-through passes whose inputs start at offsets that are not multiples of 16 (RA above).
+template <int W, int KG>
+__global__ void __launch_bounds__(1024) gf16_realign_kernel(const ApplyArgs a)
+{
+    gf16_stream_body<W, KG, 1, false, false, 0, true>(a);
 }
 
 // 8-output passes with the hybrid LDS + L1 lookups (TM = 2), e.g. C5's 20 -> 8.
@@ -421,6 +479,12 @@ __global__ void __launch_bounds__(1024) gf16_ptrs_stream_kernel(const ApplyArgs 
     template __global__ void ecamd::gf16_hybrid_kernel<3>(const ecamd::ApplyArgs); \
     template __global__ void ecamd::gf16_hybrid_kernel<4>(const ecamd::ApplyArgs); \
     template __global__ void ecamd::gf16_hybrid_kernel<5>(const ecamd::ApplyArgs);
+#define ECAMD_REALIGN_KG(W)                                                               \
+    template __global__ void ecamd::gf16_realign_kernel<W, 1>(const ecamd::ApplyArgs);    \
+    template __global__ void ecamd::gf16_realign_kernel<W, 2>(const ecamd::ApplyArgs);    \
+    template __global__ void ecamd::gf16_realign_kernel<W, 3>(const ecamd::ApplyArgs);    \
+    template __global__ void ecamd::gf16_realign_kernel<W, 4>(const ecamd::ApplyArgs);    \
+    template __global__ void ecamd::gf16_realign_kernel<W, 5>(const ecamd::ApplyArgs);
 #define ECAMD_PTRS_KG(W)                                                                  \
     template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 1>(const ecamd::ApplyArgs);      \
     template __global__ void ecamd::gf16_ptrs_stream_kernel<W, 2>(const ecamd::ApplyArgs);      \

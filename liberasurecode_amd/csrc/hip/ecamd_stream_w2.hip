@@ -7,3 +7,4 @@ ECAMD_STREAM_KG(2, 1, false, true)
 ECAMD_STREAM_KG(2, 2, true, false)
 ECAMD_STREAM_KG(2, 2, false, false)
 ECAMD_PTRS_KG(2)
+ECAMD_REALIGN_KG(2)

@@ -7,3 +7,4 @@ ECAMD_STREAM_KG(4, 1, false, true)
 ECAMD_STREAM_KG(4, 2, true, false)
 ECAMD_STREAM_KG(4, 2, false, false)
 ECAMD_PTRS_KG(4)
+ECAMD_REALIGN_KG(4)

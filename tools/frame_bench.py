@@ -153,7 +153,10 @@ def main():
         d.ecamd_tune(b"frame_crc_units", 0)
     # objects that do not fill the payloads: Swift's default 1 MiB EC segments (bs = 104858) and a
     # C3 object 6 bytes short -- copy-through with zero padding vs split + encode
-    for size2, S2, tag in (((1 << 20), 2560, "swift_1MiB_segment"), (k * (1 << 20) - 6, S, "c3_minus_6B")):
+    # (and two shapes that isolate its costs: aligned payloads that fill exactly, with a partial last
+    # 4 KiB tile -- bs = 104864 -- and with none -- bs = 26 x 4096)
+    for size2, S2, tag in (((1 << 20), 2560, "swift_1MiB_segment"), (k * (1 << 20) - 6, S, "c3_minus_6B"),
+                           (k * 104864, 2560, "swift_aligned_fill"), (k * 26 * 4096, 2560, "swift_tile_multiple")):
         fb2 = frame.FrameBatch(6, k, m, size2, S2, align=args.align)
         obj2 = D.DeviceBuffer(fb2.obj_stride * S2)
         _lib.check(d.ecamd_fill_splitmix(obj2.ptr, fb2.obj_stride, 0, 1, size2, S2, 0, 0xB0B, st.handle), "fill")
@@ -161,7 +164,7 @@ def main():
                            (0, frame.CHKSUM_CRC32)):
             fb2.checksum = ct
             d.ecamd_tune(b"frame_copy_padded", padded)
-            ms = timed(lambda: fb2.encode(obj2, stream=st), st, args.reps)
+            ms = timed(lambda: fb2.encode(obj2, stream=st), st, args.reps, warm=3)
             print(json.dumps({"op": "frame_encode_" + tag, "copy_padded": padded, "checksum": ct,
                               "ms": round(ms, 3), "GiBps_object": round(S2 * size2 / (ms / 1e3) / 2**30, 1)}),
                   flush=True)
