@@ -87,6 +87,14 @@ int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int *r
  * sets it for its ranks). */
 int ecamd_percall_device_plan(int ndev, const char *spec, int *devs, int max);
 
+/* Host copies of one per-call request (host/copy_pool.cpp): dst[i] <- src[i], len[i] bytes, i < n,
+ * regions not overlapping.  Batches of 1 MiB or more are split into 256 KiB pieces shared by the
+ * caller and ECAMD_COPY_THREADS helper threads (default 4, 0 = off; one request uses them at a
+ * time, a caller that finds them busy copies alone).  Complete on return; 0, or ECAMD_EINVAL
+ * (-22) for null arrays.  Used by the per-call staging (pack / unpack) and by liberasurecode.so.1
+ * for its object <-> fragment copies. */
+int ecamd_host_copy(int n, void *const *dst, const void *const *src, const int64_t *len);
+
 /* Bitsliced GF(2^16) maps (host/bitslice.hpp): the XOR network built for an R x K matrix
  * (R <= 8, K <= 32, at most `cap` shared temporaries per input) evaluated on 32 words per input
  * (in: K x 32, out: R x 32; *ops = VALU ops of the network per tile), and the HIP source of the

@@ -80,6 +80,24 @@ char* new_fragment(int payload, bool zero_payload = true)
     return f;
 }
 
+// ECAMD_FRONTEND_ZERO_ALL=1 zeroes every buffer in full as the reference does, for A/B runs of
+// the host passes skipped below (tools/e2e_bench.py); the bytes returned are the same either way.
+bool zero_all()
+{
+    static const bool on = [] {
+        const char* f = getenv("ECAMD_FRONTEND_ZERO_ALL");
+        return f && f[0] == '1';
+    }();
+    return on;
+}
+
+// Zero [0, n) of p except [lo, hi), the part the caller fills next.
+void zero_outside(char* p, size_t n, size_t lo, size_t hi)
+{
+    if (lo > 0) std::memset(p, 0, lo);
+    if (hi < n) std::memset(p + hi, 0, n - hi);
+}
+
 int frag_idx(char* f) { return has_magic(f) ? static_cast<int>(hdr(f)->meta.idx) : -1; }
 int frag_size(char* f) { return has_magic(f) ? static_cast<int>(hdr(f)->meta.size) : -1; }
 int frag_orig_size(char* f) { return has_magic(f) ? static_cast<int>(hdr(f)->meta.orig_data_size) : -1; }
@@ -129,6 +147,7 @@ struct CodecHooks {
     void (*crc_disarm)(void) = nullptr;
     void (*exec_reset)(void) = nullptr;                          // ecamd_percall_reset / _status
     int (*exec_status)(void) = nullptr;
+    int (*copy)(int, void* const*, const void* const*, const int64_t*) = nullptr;  // ecamd_host_copy
     bool crc() const { return crc_arm && crc_lookup && crc_disarm; }
     bool ours() const { return exec_reset && exec_status; }
 };
@@ -143,6 +162,8 @@ CodecHooks resolve_hooks(void* so)
     h.crc_disarm = reinterpret_cast<void (*)(void)>(dlsym(so, "ecamd_percall_crc_disarm"));
     h.exec_reset = reinterpret_cast<void (*)(void)>(dlsym(so, "ecamd_percall_reset"));
     h.exec_status = reinterpret_cast<int (*)(void)>(dlsym(so, "ecamd_percall_status"));
+    h.copy = reinterpret_cast<int (*)(int, void* const*, const void* const*, const int64_t*)>(
+        dlsym(so, "ecamd_host_copy"));
     dlerror();
     return h;
 }
@@ -495,8 +516,29 @@ void stamp(ec_backend* be, char* f, int idx, uint64_t orig, int bs, ec_checksum_
                                           : zcrc(&h->meta, sizeof(fragment_metadata_t));
 }
 
+// A batch of host copies: through this repo's helper threads when the codec library offers them
+// (ecamd_host_copy, include/ecamd_host.h), else one memcpy after the other.
+struct CopyBatch {
+    std::vector<void*> dst;
+    std::vector<const void*> src;
+    std::vector<int64_t> len;
+    void add(void* d, const void* s, int64_t n)
+    {
+        if (n <= 0) return;
+        dst.push_back(d);
+        src.push_back(s);
+        len.push_back(n);
+    }
+    void run(const CodecHooks* h)
+    {
+        const int n = static_cast<int>(dst.size());
+        if (h && h->copy && h->copy(n, dst.data(), src.data(), len.data()) == 0) return;
+        for (int i = 0; i < n; i++) std::memcpy(dst[i], src[i], static_cast<size_t>(len[i]));
+    }
+};
+
 // fragments_to_string (erasurecode_preprocessing.c:269-370): concatenate data payloads.
-int assemble(int k, char** frags, int n, char** out, uint64_t* out_len)
+int assemble(int k, char** frags, int n, char** out, uint64_t* out_len, const CodecHooks* h)
 {
     *out = nullptr;
     if (n < k) return -1;
@@ -520,16 +562,28 @@ int assemble(int k, char** frags, int n, char** out, uint64_t* out_len)
         }
     }
     if (have != k) return -1;
-    char* s = static_cast<char*>(aligned_zero(static_cast<size_t>(orig > 0 ? orig : 0)));
+    // get_aligned_buffer16 zeroes the whole object before the payloads are copied over it; only
+    // what the payloads do not cover (short fragments) is zeroed here, the result is the same
+    const size_t len = static_cast<size_t>(orig > 0 ? orig : 0);
+    char* s = nullptr;
+    if (zero_all()) {
+        s = static_cast<char*>(aligned_zero(len));
+    } else if (posix_memalign(reinterpret_cast<void**>(&s), 16, len ? len : 1) != 0) {
+        s = nullptr;
+    }
     if (!s) return -ENOMEM;
     *out_len = static_cast<uint64_t>(orig);
     int off = 0, left = orig;
+    CopyBatch cb;
     for (int i = 0; i < k && left > 0; i++) {
         int take = std::min(frag_size(data[i]), left);
-        std::memcpy(s + off, payload(data[i]), static_cast<size_t>(take));
+        if (take <= 0) continue;  // a corrupt (negative or zero) size copies nothing
+        cb.add(s + off, payload(data[i]), take);
         left -= take;
         off += take;
     }
+    cb.run(h);
+    if (left > 0) std::memset(s + off, 0, static_cast<size_t>(left));
     *out = s;
     return 0;
 }
@@ -819,8 +873,13 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
             const int off = static_cast<int>(be->common.ops->get_encode_offset(be->desc.backend_desc, meta));
             int left = total;
             const char* src = orig_data;
+            // This repo's codecs write every parity byte, so in front of them only the bytes the
+            // object copy does not cover are zeroed (the reference zeroes every fragment first:
+            // 14 MiB of memset per 10 MiB object at k=10 m=4); a foreign codec gets zeroed buffers.
+            const bool lean = hooks_of(be).ours() && !zero_all();
+            CopyBatch cb;
             for (int i = 0; i < k + m && ret == 0; i++) {
-                char* f = new_fragment(bs + meta);
+                char* f = new_fragment(bs + meta, !lean);
                 if (!f) {
                     ret = -ENOMEM;
                     break;
@@ -828,13 +887,19 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
                 if (i < k) {
                     data[i] = f;
                     const int take = left > bs ? bs : left;
-                    if (left > 0) std::memcpy(payload(f) + off, src, static_cast<size_t>(take));
+                    if (lean) {
+                        const size_t lo = static_cast<size_t>(off);
+                        zero_outside(payload(f), static_cast<size_t>(bs + meta), lo,
+                                     lo + static_cast<size_t>(take > 0 ? take : 0));
+                    }
+                    if (left > 0) cb.add(payload(f) + off, src, take);
                     src += take;
                     left -= take;
                 } else {
                     parity[i - k] = f;
                 }
             }
+            if (ret == 0) cb.run(&hooks_of(be));  // object -> data payloads
             CrcArm arm(be, be->args.uargs.ct == CHKSUM_CRC32);  // through the stamping below
             if (ret == 0) {
                 std::vector<char*> dp(k), pp(m);
@@ -901,7 +966,7 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
             return -EBADHEADER;
         }
     if (be->common.ops->is_systematic &&
-        assemble(k, available_fragments, num_fragments, out_data, out_data_len) == 0)
+        assemble(k, available_fragments, num_fragments, out_data, out_data_len, &hooks_of(be)) == 0)
         return 0;  // every data fragment present: no backend work
 
     std::vector<char*> data(k), parity(m), owned;
@@ -935,7 +1000,7 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
             hdr(f)->magic = LIBERASURECODE_FRAG_HEADER_MAGIC;  // init_fragment_header
             stamp(be, f, missing[j], static_cast<uint64_t>(orig), bs, be->args.uargs.ct, false);
         }
-        ret = assemble(k, data.data(), k, out_data, out_data_len);
+        ret = assemble(k, data.data(), k, out_data, out_data_len, &hooks_of(be));
         if (ret < 0) LOGE("Could not convert decoded fragments to a string!");
     }
     free_owned(owned);

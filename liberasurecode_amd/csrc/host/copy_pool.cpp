@@ -1,0 +1,152 @@
+// copy_pool.cpp -- host copies of one per-call request spread over a few helper threads.
+//
+// A drop-in call (liberasurecode_encode / _decode, the per-call codec) moves every byte of the
+// object through host memory three times: object -> fragments (frontend), fragments -> pinned
+// staging (pack), staging -> fragments (unpack), and the reverse for decode.  One core copies
+// ~10 GB/s, so a single caller -- a Swift proxy worker is one thread -- is bound by its own
+// memcpy, not by PCIe.  ecamd_host_copy splits a batch of copies into pieces that the caller and
+// ECAMD_COPY_THREADS helpers (default 4, 0 = off) take from a shared counter.  One request uses
+// the helpers at a time; a caller that finds them busy copies alone, so many concurrent callers
+// keep their own cores and are never queued behind each other.  After fork() the child copies
+// alone (the helpers live in the parent only).
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "ecamd.h"
+#include "ecamd_host.h"
+
+namespace {
+
+constexpr int64_t kPiece = 256 << 10;     // bytes per piece handed to one thread
+constexpr int64_t kParallelMin = 1 << 20;  // smaller batches are copied by the caller alone
+
+struct Piece {
+    char* dst;
+    const char* src;
+    int64_t len;
+};
+
+struct Pool {
+    std::mutex busy;  // held by the one request using the helpers
+    std::mutex mu;
+    std::condition_variable wake, idle;
+    std::vector<Piece> job;
+    std::atomic<int64_t> next{0};
+    int64_t gen = 0;
+    int working = 0;  // helpers inside the current generation
+    int threads = 0;
+    std::atomic<pid_t> owner{0};  // process that started the helpers
+    std::atomic<bool> started{false};
+};
+
+Pool& pool()
+{
+    static Pool* p = new Pool();  // never destroyed: helpers may outlive static destructors
+    return *p;
+}
+
+int configured_threads()
+{
+    const char* s = std::getenv("ECAMD_COPY_THREADS");
+    if (!s || !*s) return 4;
+    return std::max(0, std::min(64, std::atoi(s)));
+}
+
+void drain(Pool& p)
+{
+    const int64_t n = static_cast<int64_t>(p.job.size());
+    for (int64_t i = p.next.fetch_add(1); i < n; i = p.next.fetch_add(1))
+        std::memcpy(p.job[i].dst, p.job[i].src, static_cast<size_t>(p.job[i].len));
+}
+
+void helper(Pool* p)
+{
+    int64_t seen = 0;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(p->mu);
+            p->wake.wait(lk, [&] { return p->gen != seen; });
+            seen = p->gen;
+            p->working++;
+        }
+        drain(*p);
+        {
+            std::lock_guard<std::mutex> lk(p->mu);
+            if (--p->working == 0) p->idle.notify_all();
+        }
+    }
+}
+
+// Starts the helpers once per process; false when there are none (disabled, forked child, or a
+// thread could not be created).
+bool ensure_started(Pool& p)
+{
+    // a forked child must not touch the mutexes: a parent thread may have held them at fork()
+    if (p.started.load() && p.owner.load() != getpid()) return false;
+    std::lock_guard<std::mutex> lk(p.mu);
+    if (p.started.load()) return p.threads > 0;
+    p.owner.store(getpid());
+    p.started.store(true);
+    const int want = configured_threads();
+    for (int i = 0; i < want; i++) {
+        try {
+            std::thread(helper, &p).detach();
+            p.threads++;
+        } catch (...) {
+            break;
+        }
+    }
+    return p.threads > 0;
+}
+
+void copy_serial(int n, void* const* dst, const void* const* src, const int64_t* len)
+{
+    for (int i = 0; i < n; i++)
+        if (len[i] > 0) std::memcpy(dst[i], src[i], static_cast<size_t>(len[i]));
+}
+
+}  // namespace
+
+extern "C" int ecamd_host_copy(int n, void* const* dst, const void* const* src, const int64_t* len)
+{
+    if (n <= 0) return 0;
+    if (!dst || !src || !len) return ECAMD_EINVAL;
+    int64_t total = 0;
+    for (int i = 0; i < n; i++) total += std::max<int64_t>(0, len[i]);
+    Pool& p = pool();
+    if (total < kParallelMin || !ensure_started(p) || !p.busy.try_lock()) {
+        copy_serial(n, dst, src, len);
+        return 0;
+    }
+    {
+        std::unique_lock<std::mutex> lk(p.mu);
+        // helpers still finishing the previous generation hold no piece of it any more (the
+        // counter ran out), but wait for them so the job vector can be rebuilt safely
+        p.idle.wait(lk, [&] { return p.working == 0; });
+        p.job.clear();
+        for (int i = 0; i < n; i++)
+            for (int64_t off = 0; off < len[i]; off += kPiece)
+                p.job.push_back({static_cast<char*>(dst[i]) + off,
+                                 static_cast<const char*>(src[i]) + off,
+                                 std::min(kPiece, len[i] - off)});
+        p.next.store(0);
+        p.gen++;
+    }
+    p.wake.notify_all();
+    drain(p);
+    {
+        std::unique_lock<std::mutex> lk(p.mu);
+        p.idle.wait(lk, [&] { return p.working == 0; });
+    }
+    p.busy.unlock();
+    return 0;
+}

@@ -243,14 +243,21 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     std::vector<uint32_t> crc(want_crc ? nfr : 0, 0u);
     const int64_t nchunks = (bs + chunk - 1) / chunk;
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
+    std::vector<void*> cdst(static_cast<size_t>(nfr));
+    std::vector<const void*> csrc(static_cast<size_t>(nfr));
+    std::vector<int64_t> clen(static_cast<size_t>(nfr));
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
         int r = ecamd_stream_synchronize(st->slot[s].stream);
         if (r) return r;
         const int64_t off = pending[s] * chunk;
         const int64_t n = std::min(chunk, bs - off);
-        for (int o = 0; o < R; o++)
-            std::memcpy(out[o] + off, st->slot[s].h_pin + (K + o) * chunk, static_cast<size_t>(n));
+        for (int o = 0; o < R; o++) {
+            cdst[o] = out[o] + off;
+            csrc[o] = st->slot[s].h_pin + (K + o) * chunk;
+            clen[o] = n;
+        }
+        ecamd_host_copy(R, cdst.data(), csrc.data(), clen.data());  // unpack (copy_pool.cpp)
         if (want_crc) {  // chunks drain in order, so the running CRCs extend by this chunk
             const auto* cc = reinterpret_cast<const uint32_t*>(st->slot[s].h_pin + crc_off);
             for (int f = 0; f < nfr; f++) crc[f] = crc_combine(t_crc.legacy, crc[f], cc[f], n);
@@ -264,8 +271,12 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         if ((rc = drain(s))) break;
         const int64_t off = c * chunk;
         const int64_t n = std::min(chunk, bs - off);
-        for (int j = 0; j < K; j++)
-            std::memcpy(sl.h_pin + j * chunk, in[j] + off, static_cast<size_t>(n));
+        for (int j = 0; j < K; j++) {
+            cdst[j] = sl.h_pin + j * chunk;
+            csrc[j] = in[j] + off;
+            clen[j] = n;
+        }
+        ecamd_host_copy(K, cdst.data(), csrc.data(), clen.data());  // pack
         // One DMA each way per chunk (the slabs are [K inputs | R outputs] x chunk, contiguous):
         // for small fragments the per-call cost is API latency, not bytes.  A short last chunk
         // also moves the stale tail of each slot, which the kernel and the unpack never read.

@@ -314,3 +314,25 @@ def test_xor_too_many_failures(hd):
     for j in range(9):  # one fragment left: the pre-check refuses
         assert E.reconstruct(desc, frags[9:], flen, j)[0] == -E.EINSUFFFRAGS
     E.lib().liberasurecode_instance_destroy(desc)
+
+
+@pytest.mark.parametrize("zero_all", ["0", "1"])
+def test_frontend_on_dirty_heap(zero_all):
+    """The frontend zeroes only what this repo's codec does not overwrite (frontend.cpp: lean
+    encode buffers, assemble): with glibc handing out garbage-filled memory every fragment and
+    every decoded object must still equal the reference framing's (zero padding, zero tail).
+    ECAMD_FRONTEND_ZERO_ALL=1 is the reference's full zeroing, the A/B switch."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MALLOC_PERTURB_="165", MALLOC_MMAP_THRESHOLD_="33554432",
+               ECAMD_FRONTEND_ZERO_ALL=zero_all)
+    r = subprocess.run([sys.executable, os.path.join(here, "perturbed_heap_run.py")],
+                       capture_output=True, text=True, timeout=300, env=env,
+                       cwd=os.path.dirname(here))
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["perturbed"], "glibc did not perturb the heap: the test proves nothing"
+    assert res["cases"] >= 150
+    assert res["failures"] == []

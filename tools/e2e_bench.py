@@ -110,8 +110,18 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--objects", type=int, default=64)
+    ap.add_argument("--per-call-only", action="store_true",
+                    help="only the per-call API leg (A/B runs of frontend switches)")
     args = ap.parse_args()
     k, m, F = 10, 4, 1 << 20
+    if args.per_call_only:
+        pc = per_call(k, m, F, args.threads, args.objects)
+        print(json.dumps({"per_call_api_encode_gibs": round(pc["encode"], 2),
+                          "per_call_api_decode_gibs": round(pc["decode"], 2),
+                          "threads": args.threads, "objects": args.objects,
+                          "frontend_zero_all": os.environ.get("ECAMD_FRONTEND_ZERO_ALL", "0"),
+                          "copy_threads": os.environ.get("ECAMD_COPY_THREADS", "4")}))
+        return
     enc, dec = pipeline(k, m, F, args.stripes, args.batch, [0, 1, 2, 3])
     pc = per_call(k, m, F, args.threads, args.objects)
     print(json.dumps({"e2e_pipeline_encode_gibs": round(enc, 2),
