@@ -873,13 +873,16 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
             const int off = static_cast<int>(be->common.ops->get_encode_offset(be->desc.backend_desc, meta));
             int left = total;
             const char* src = orig_data;
-            // This repo's codecs write every parity byte, so in front of them only the bytes the
-            // object copy does not cover are zeroed (the reference zeroes every fragment first:
-            // 14 MiB of memset per 10 MiB object at k=10 m=4); a foreign codec gets zeroed buffers.
+            // In front of this repo's codecs only the data bytes the object copy does not cover are
+            // zeroed (the reference zeroes every fragment first: 14 MiB of memset per 10 MiB object
+            // at k=10 m=4).  Parity stays zeroed for flat_xor_hd, whose encode XORs into the parity
+            // buffers as the reference's does (xor_code.c:141-191); this repo's rs_vand writes every
+            // parity byte.  A foreign codec gets zeroed buffers throughout.
             const bool lean = hooks_of(be).ours() && !zero_all();
+            const bool lean_parity = lean && be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND;
             CopyBatch cb;
             for (int i = 0; i < k + m && ret == 0; i++) {
-                char* f = new_fragment(bs + meta, !lean);
+                char* f = new_fragment(bs + meta, !(i < k ? lean : lean_parity));
                 if (!f) {
                     ret = -ENOMEM;
                     break;
