@@ -16,6 +16,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(HERE))
 import ec_api as E  # noqa: E402
 from test_gpu_frontend import expected, make  # noqa: E402
 
