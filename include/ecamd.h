@@ -232,6 +232,8 @@ int ecamd_synchronize(void);
 int ecamd_stream_create(void **stream);
 int ecamd_stream_destroy(void *stream);
 int ecamd_stream_synchronize(void *stream);
+/* 0 when all work on stream is complete, 1 while some is pending, ECAMD_EHIP on error. */
+int ecamd_stream_query(void *stream);
 /* HIP events for timing work on a stream (elapsed_ms waits for `stop`). */
 int ecamd_event_create(void **ev);
 int ecamd_event_destroy(void *ev);

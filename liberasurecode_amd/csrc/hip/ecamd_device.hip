@@ -2010,6 +2010,14 @@ int ecamd_stream_synchronize(void* stream)
     return 0;
 }
 
+int ecamd_stream_query(void* stream)
+{
+    const hipError_t e = hipStreamQuery(static_cast<hipStream_t>(stream));
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorNotReady) return 1;
+    return ECAMD_EHIP;
+}
+
 int ecamd_event_create(void** ev)
 {
     hipEvent_t e;

@@ -9,6 +9,7 @@
 // are cached by content, so callers may free() and rebuild matrices at will.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -74,6 +75,32 @@ uint32_t crc_combine(bool legacy, uint32_t a, uint32_t b, int64_t len_b)
 }
 
 constexpr int64_t kChunkTarget = 8 << 20;  // bytes of all fragments per chunk (both directions)
+
+// Small calls are latency-bound (two DMAs, a launch and their completions: ~35 us at 4 KiB).  For
+// a chunk of at most kSpinBytes of fragments the caller polls the stream for up to
+// ECAMD_PERCALL_SPIN_US microseconds before it blocks in hipStreamSynchronize (0 = always block).
+constexpr int64_t kSpinBytes = 1 << 20;
+
+int spin_us()
+{
+    static const int us = [] {
+        const char* s = std::getenv("ECAMD_PERCALL_SPIN_US");
+        return s && *s ? std::max(0, std::atoi(s)) : 0;
+    }();
+    return us;
+}
+
+int wait_stream(void* stream, bool small)
+{
+    if (small && spin_us() > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us());
+        do {
+            const int q = ecamd_stream_query(stream);
+            if (q <= 0) return q;
+        } while (std::chrono::steady_clock::now() < until);
+    }
+    return ecamd_stream_synchronize(stream);
+}
 
 struct MapHolder {
     ecamd_map* map = nullptr;
@@ -248,7 +275,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     std::vector<int64_t> clen(static_cast<size_t>(nfr));
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
-        int r = ecamd_stream_synchronize(st->slot[s].stream);
+        int r = wait_stream(st->slot[s].stream, chunk * nfr <= kSpinBytes);
         if (r) return r;
         const int64_t off = pending[s] * chunk;
         const int64_t n = std::min(chunk, bs - off);

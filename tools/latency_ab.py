@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""A/B of per-call latency settings (round 3): tools/latency_bench.py --codec own in child processes,
+interleaved rounds --
+  round2        ECAMD_FRONTEND_ZERO_ALL=1 ECAMD_COPY_THREADS=0 ECAMD_PERCALL_SPIN_US=0 (round-2 host path)
+  default       lean zeroing, 4 copy helpers, blocking waits
+  spin          default + poll the stream up to 200 us before blocking (chunks <= 1 MiB)
+One JSON line per (setting, round, checksum, size) with the median encode / decode latency."""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SETTINGS = {"round2": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0", "ECAMD_PERCALL_SPIN_US": "0"},
+            "default": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "0"},
+            "spin": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "200"}}
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    for rnd in range(rounds):
+        for name, env in SETTINGS.items():
+            r = subprocess.run([sys.executable, os.path.join(HERE, "latency_bench.py"), "--codec", "own",
+                                "--reps", "25"], capture_output=True, text=True, timeout=600,
+                               env=dict(os.environ, **env))
+            if r.returncode != 0:
+                sys.stderr.write(r.stderr[-2000:])
+                raise SystemExit(r.returncode)
+            for line in r.stdout.splitlines():
+                if line.startswith("{"):
+                    rec = json.loads(line)
+                    print(json.dumps({"setting": name, "round": rnd, "ct": rec["ct"], "size": rec["size"],
+                                      "encode_us": rec["encode_us"], "decode_4lost_us": rec["decode_4lost_us"],
+                                      "encode_p90_us": rec["encode_p90_us"],
+                                      "decode_4lost_p90_us": rec["decode_4lost_p90_us"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
