@@ -74,7 +74,16 @@ uint32_t crc_combine(bool legacy, uint32_t a, uint32_t b, int64_t len_b)
     return m.apply(a) ^ b;
 }
 
-constexpr int64_t kChunkTarget = 8 << 20;  // bytes of all fragments per chunk (both directions)
+// bytes of all fragments per chunk (both directions); ECAMD_PERCALL_CHUNK_KIB overrides (A/B runs)
+int64_t chunk_target()
+{
+    static const int64_t bytes = [] {
+        const char* s = std::getenv("ECAMD_PERCALL_CHUNK_KIB");
+        const long v = s && *s ? std::atol(s) : 0;
+        return v >= 64 ? static_cast<int64_t>(v) << 10 : int64_t(8) << 20;
+    }();
+    return bytes;
+}
 
 // Small calls are latency-bound (two DMAs, a launch and their completions: ~35 us at 4 KiB).  For
 // a chunk of at most kSpinBytes of fragments the caller polls the stream for up to
@@ -257,7 +266,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     const int64_t nfr = K + R;
     // The chunk is also the fragment pitch in the slab: a multiple of 128 puts every fragment
     // on a cache line (16-byte-aligned pitches cost the codec 13-19%).
-    int64_t chunk = std::max<int64_t>(128, (kChunkTarget / nfr) / 128 * 128);
+    int64_t chunk = std::max<int64_t>(128, (chunk_target() / nfr) / 128 * 128);
     const int64_t padded = (bs + 127) / 128 * 128;
     chunk = std::min(chunk, padded);
     int rc = 0;

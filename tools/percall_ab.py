@@ -6,6 +6,7 @@ interleaved rounds, 1 and 8 caller threads, three settings --
   lean          ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=0  (only uncovered bytes zeroed)
   lean+helpers  ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=4  (default: copies of a call shared
                 with the helper threads of host/copy_pool.cpp)
+  ... chunk N   the same with ECAMD_PERCALL_CHUNK_KIB (staging chunk, default 8 MiB of fragments)
 One JSON line per run."""
 import json
 import os
@@ -15,7 +16,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SETTINGS = {"ref-zeroing": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0"},
             "lean": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "0"},
-            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4"}}
+            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4"},
+            "lean+helpers chunk 2 MiB": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                                         "ECAMD_PERCALL_CHUNK_KIB": "2048"},
+            "lean+helpers chunk 4 MiB": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                                         "ECAMD_PERCALL_CHUNK_KIB": "4096"}}
 
 
 def run(setting, threads, objects):
