@@ -17,9 +17,11 @@ SETTINGS = {"round2": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0"
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     for rnd in range(rounds):
-        for name, env in SETTINGS.items():
+        names = list(SETTINGS)
+        for name in names[rnd % len(names):] + names[:rnd % len(names)]:  # rotated every round
+            env = SETTINGS[name]
             r = subprocess.run([sys.executable, os.path.join(HERE, "latency_bench.py"), "--codec", "own",
                                 "--reps", "25"], capture_output=True, text=True, timeout=600,
                                env=dict(os.environ, **env))

@@ -6,7 +6,8 @@ interleaved rounds, 1 and 8 caller threads, three settings --
   lean          ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=0  (only uncovered bytes zeroed)
   lean+helpers  ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=4  (default: copies of a call shared
                 with the helper threads of host/copy_pool.cpp)
-  ... chunk N   the same with ECAMD_PERCALL_CHUNK_KIB (staging chunk, default 8 MiB of fragments)
+(the staging chunk, ECAMD_PERCALL_CHUNK_KIB, measured at 2 and 4 MiB against the default 8 MiB in round 3:
+no gain, profiles/r03_percall_ab1.log).  The order of the settings rotates every round.
 One JSON line per run."""
 import json
 import os
@@ -16,11 +17,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SETTINGS = {"ref-zeroing": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0"},
             "lean": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "0"},
-            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4"},
-            "lean+helpers chunk 2 MiB": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                                         "ECAMD_PERCALL_CHUNK_KIB": "2048"},
-            "lean+helpers chunk 4 MiB": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                                         "ECAMD_PERCALL_CHUNK_KIB": "4096"}}
+            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4"}}
 
 
 def run(setting, threads, objects):
@@ -40,7 +37,8 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     for rnd in range(rounds):
         for threads, objects in ((1, 48), (8, 256)):
-            for setting in SETTINGS:
+            names = list(SETTINGS)
+            for setting in names[rnd % len(names):] + names[:rnd % len(names)]:
                 res = run(setting, threads, objects)
                 res["round"] = rnd
                 print(json.dumps(res), flush=True)
