@@ -85,10 +85,12 @@ int64_t chunk_target()
     return bytes;
 }
 
-// Small calls are latency-bound (two DMAs, a launch and their completions: ~35 us at 4 KiB).  For
-// a chunk of at most kSpinBytes of fragments the caller polls the stream for up to
-// ECAMD_PERCALL_SPIN_US microseconds before it blocks in hipStreamSynchronize (0 = always block).
-constexpr int64_t kSpinBytes = 1 << 20;
+// Waiting for a chunk: with ECAMD_PERCALL_SPIN_US > 0 the caller polls the stream for up to that
+// many microseconds before it blocks in hipStreamSynchronize.  Only chunks of at least
+// kSpinMinBytes of fragments poll: for 4-16 KiB calls polling measured 1-6 us SLOWER than
+// blocking, while 4-16 MiB objects gained 15% with it (tools/latency_ab.py,
+// profiles/r03_latency_ab2.log).
+constexpr int64_t kSpinMinBytes = 64 << 10;
 
 int spin_us()
 {
@@ -99,9 +101,9 @@ int spin_us()
     return us;
 }
 
-int wait_stream(void* stream, bool small)
+int wait_stream(void* stream, bool poll)
 {
-    if (small && spin_us() > 0) {
+    if (poll && spin_us() > 0) {
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us());
         do {
             const int q = ecamd_stream_query(stream);
@@ -284,7 +286,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     std::vector<int64_t> clen(static_cast<size_t>(nfr));
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
-        int r = wait_stream(st->slot[s].stream, chunk * nfr <= kSpinBytes);
+        int r = wait_stream(st->slot[s].stream, chunk * nfr >= kSpinMinBytes);
         if (r) return r;
         const int64_t off = pending[s] * chunk;
         const int64_t n = std::min(chunk, bs - off);

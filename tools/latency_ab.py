@@ -3,7 +3,8 @@
 interleaved rounds --
   round2        ECAMD_FRONTEND_ZERO_ALL=1 ECAMD_COPY_THREADS=0 ECAMD_PERCALL_SPIN_US=0 (round-2 host path)
   default       lean zeroing, 4 copy helpers, blocking waits
-  spin          default + poll the stream up to 200 us before blocking (chunks <= 1 MiB)
+  spin          default + poll the stream up to 1000 us before blocking (chunks >= 64 KiB of fragments;
+                round 3's first form polled 200 us for chunks <= 1 MiB, profiles/r03_latency_ab2.log)
 One JSON line per (setting, round, checksum, size) with the median encode / decode latency."""
 import json
 import os
@@ -13,7 +14,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SETTINGS = {"round2": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0", "ECAMD_PERCALL_SPIN_US": "0"},
             "default": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "0"},
-            "spin": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "200"}}
+            "spin": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "1000"}}
 
 
 def main():
