@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """A/B of per-call latency settings (round 3): tools/latency_bench.py --codec own in child processes,
 interleaved rounds --
-  round2        ECAMD_FRONTEND_ZERO_ALL=1 ECAMD_COPY_THREADS=0 ECAMD_PERCALL_SPIN_US=0 (round-2 host path)
-  default       lean zeroing, 4 copy helpers, blocking waits
-  spin          default + poll the stream up to 1000 us before blocking (chunks >= 64 KiB of fragments;
-                round 3's first form polled 200 us for chunks <= 1 MiB, profiles/r03_latency_ab2.log)
+  round2        ECAMD_FRONTEND_ZERO_ALL=1 ECAMD_COPY_THREADS=0 ECAMD_FRONTEND_POOL_MIB=0 (round-2 host path)
+  no-pool       lean zeroing, 4 copy helpers, no recycled buffers
+  default       lean zeroing, 4 copy helpers, recycled fragment / object buffers
+(earlier forms of this tool compared polling the staging streams, ECAMD_PERCALL_SPIN_US:
+profiles/r03_latency_ab2.log, r03_latency_ab3.log)
 One JSON line per (setting, round, checksum, size) with the median encode / decode latency."""
 import json
 import os
@@ -12,9 +13,9 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SETTINGS = {"round2": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0", "ECAMD_PERCALL_SPIN_US": "0"},
-            "default": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "0"},
-            "spin": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_PERCALL_SPIN_US": "1000"}}
+SETTINGS = {"round2": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0", "ECAMD_FRONTEND_POOL_MIB": "0"},
+            "no-pool": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_FRONTEND_POOL_MIB": "0"},
+            "default": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_FRONTEND_POOL_MIB": "256"}}
 
 
 def main():

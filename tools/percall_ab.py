@@ -6,7 +6,8 @@ interleaved rounds, 1 and 8 caller threads, three settings --
   lean          ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=0  (only uncovered bytes zeroed)
   lean+helpers  ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=4  (default: copies of a call shared
                 with the helper threads of host/copy_pool.cpp)
-  lean+helpers+spin  ... and ECAMD_PERCALL_SPIN_US=1000 (poll the staging streams before blocking)
+  lean+helpers+pool  ... and the frontend's recycled fragment / object buffers (ECAMD_FRONTEND_POOL_MIB,
+                default 256; the others run with 0)
 (the staging chunk, ECAMD_PERCALL_CHUNK_KIB, measured at 2 and 4 MiB against the default 8 MiB in round 3:
 no gain, profiles/r03_percall_ab1.log).  The order of the settings rotates every round.
 One JSON line per run."""
@@ -16,11 +17,13 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SETTINGS = {"ref-zeroing": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0"},
-            "lean": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "0"},
-            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4"},
-            "lean+helpers+spin": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                                  "ECAMD_PERCALL_SPIN_US": "1000"}}
+SETTINGS = {"ref-zeroing": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0",
+                            "ECAMD_FRONTEND_POOL_MIB": "0"},
+            "lean": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "0", "ECAMD_FRONTEND_POOL_MIB": "0"},
+            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                             "ECAMD_FRONTEND_POOL_MIB": "0"},
+            "lean+helpers+pool": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                                  "ECAMD_FRONTEND_POOL_MIB": "256"}}
 
 
 def run(setting, threads, objects):
