@@ -288,7 +288,7 @@ def kernel_entry(summ, kernel):
     return None
 
 
-def c5_rebuild(D, stream, reps=20, warm=25):
+def c5_rebuild(D, stream, reps=30, warm=120):
     """BASELINE configs[4]: k=20 m=8, 4 MiB fragments, 8 fragments lost, 32 stripes in HBM.
     'reconstruct with 8 missing' two ways: one pass that rebuilds all 8 (ecamd_rs_decode with
     rebuild_parity: the k inputs are read once, inverse / composite rows from one host-side
@@ -309,7 +309,9 @@ def c5_rebuild(D, stream, reps=20, warm=25):
     a, b = D.Event(), D.Event()
 
     def timed(fn):
-        # steady state: the clock settles over the first few launches of a new kernel mix
+        # steady state: the clock settles over the first launches of a new kernel mix, and it has
+        # dropped while the compiles above kept the GPU idle -- 120 launches are ~80 ms of load,
+        # the settle the main steps use
         for _ in range(warm):
             fn()
         a.record(stream)
