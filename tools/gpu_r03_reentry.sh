@@ -3,11 +3,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1 || { echo "SMOKE FAILED"; tail -20 gpurun_out/r03_smoke.log; exit 1; }
-tail -1 gpurun_out/r03_smoke.log
-timeout -k 10 300 python bench.py > gpurun_out/r03_bench_reentry.log 2>&1 || { echo "BENCH FAILED"; tail -20 gpurun_out/r03_bench_reentry.log; exit 1; }
-tail -1 gpurun_out/r03_bench_reentry.log
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03_gpu_tests_reentry.log 2>&1
+timeout -k 10 400 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke2.log 2>&1 || { echo "SMOKE FAILED"; tail -20 gpurun_out/r03_smoke2.log; exit 1; }
+tail -1 gpurun_out/r03_smoke2.log
+timeout -k 10 300 python bench.py > gpurun_out/r03_bench_reentry2.log 2>&1 || { echo "BENCH FAILED"; tail -20 gpurun_out/r03_bench_reentry2.log; exit 1; }
+tail -1 gpurun_out/r03_bench_reentry2.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03_gpu_tests_reentry2.log 2>&1
 rc=$?
-echo "PYTEST_RC=$rc"; tail -15 gpurun_out/r03_gpu_tests_reentry.log
+echo "PYTEST_RC=$rc"; tail -15 gpurun_out/r03_gpu_tests_reentry2.log
 exit $rc
