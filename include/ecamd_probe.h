@@ -34,7 +34,8 @@ int ecamd_probe_mix(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d
  * (mode 0), from global memory through the vector L1 (1) or half each (2); grid = CUs x wgs_per_cu
  * workgroups of 256 lanes, iters x 4 lookups per lane. */
 int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void *d_table, void *stream);
-/* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup) and the
+/* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup, 2 grid-stride
+ * with each tile's fragment order rotated by the tile index) and the
  * chunk layout (wave_contig 1: a wave's ch chunks are 1 KiB apart, contiguous) as parameters. */
 int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int order,
                            int wave_contig, void *d_base, int64_t blocksize, int K, int R,

@@ -12,7 +12,8 @@ struct MixArgs {
     int K, R;
     uint32_t ntiles;
     uint32_t tiles_per_stripe;
-    int order;        // 0: grid-stride tile order, 1: contiguous tile range per workgroup
+    int order;        // 0: grid-stride tile order, 1: contiguous tile range per workgroup,
+                      // 2: grid-stride with the fragment order rotated per tile
     int wave_contig;  // 1: a wave's CH chunks are contiguous (1 KiB apart)
     int frag[64];     // fragment slot of read i (0..K-1) and of write r (K+r): which slots are read
                       //   and which written (identity: reads first, then writes)

@@ -142,7 +142,7 @@ int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
     const int64_t sstride = bs * (K + R);
     if (K < 1 || R < 0 || K + R > 64 || bs % span || !aligned16(base) || sstride >= (1ll << 31) || nstripes < 1)
         return fail(-22, "mix probe: bad shape");
-    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0, order != 0,
+    MixArgs a{static_cast<uint8_t*>(base), sstride, static_cast<int>(bs), K, R, 0, 0, order,
               wave_contig != 0, {}};
     for (int i = 0; i < K + R; i++) {
         a.frag[i] = frag ? frag[i] : i;

@@ -111,11 +111,17 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
     const int lane_off = a.wave_contig
                              ? static_cast<int>(threadIdx.x / 64) * 1024 * CH + static_cast<int>(threadIdx.x % 64) * 16
                              : static_cast<int>(threadIdx.x) * 16;
+    // order 2: grid-stride, but tile t reads its K fragments starting at fragment t % K and writes
+    // its R outputs starting at t % R (rotated), so neighbouring tiles hit different fragments at once
+    const bool contig = a.order == 1;
     const uint32_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
-    const uint32_t t0 = a.order ? blockIdx.x * per : blockIdx.x;
-    const uint32_t t1 = a.order ? min(a.ntiles, t0 + per) : a.ntiles;
-    const uint32_t dt = a.order ? 1u : gridDim.x;
+    const uint32_t t0 = contig ? blockIdx.x * per : blockIdx.x;
+    const uint32_t t1 = contig ? min(a.ntiles, t0 + per) : a.ntiles;
+    const uint32_t dt = contig ? 1u : gridDim.x;
     for (uint32_t t = t0; t < t1; t += dt) {
+        const int rk = a.order == 2 ? static_cast<int>(t % static_cast<uint32_t>(a.K)) : 0;
+        const int rr = a.order == 2 && a.R > 0 ? static_cast<int>(t % static_cast<uint32_t>(a.R)) : 0;
+        auto rd = [&](int i) { return a.frag[i + rk < a.K ? i + rk : i + rk - a.K]; };
         const uint32_t s = t / a.tiles_per_stripe;
         const int off = static_cast<int>(t - s * a.tiles_per_stripe) * static_cast<int>(blockDim.x) * 16 * CH +
                         lane_off;
@@ -131,7 +137,7 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
 #pragma unroll
             for (int c = 0; c < CH; c++)
                 cur[i][c] = (i < a.K) ? __builtin_amdgcn_raw_buffer_load_b128(
-                                            rsrc, a.frag[i] * a.frag_stride + off + c * cstride, 0, LP)
+                                            rsrc, rd(i) * a.frag_stride + off + c * cstride, 0, LP)
                                       : v4{0u, 0u, 0u, 0u};
         for (int j0 = 0; j0 < a.K; j0 += 4) {
 #pragma unroll
@@ -140,7 +146,7 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
                 for (int c = 0; c < CH; c++)
                     nxt[i][c] = (j0 + 4 + i < a.K)
                                     ? __builtin_amdgcn_raw_buffer_load_b128(
-                                          rsrc, a.frag[j0 + 4 + i] * a.frag_stride + off + c * cstride, 0, LP)
+                                          rsrc, rd(j0 + 4 + i) * a.frag_stride + off + c * cstride, 0, LP)
                                     : v4{0u, 0u, 0u, 0u};
 #pragma unroll
             for (int i = 0; i < 4; i++)
@@ -153,9 +159,10 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
         for (int r = 0; r < a.R; r++)
 #pragma unroll
             for (int c = 0; c < CH; c++)
-                __builtin_amdgcn_raw_buffer_store_b128(acc[c] + static_cast<unsigned>(r), rsrc,
-                                                       a.frag[a.K + r] * a.frag_stride + off + c * cstride,
-                                                       0, SP);
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    acc[c] + static_cast<unsigned>(r), rsrc,
+                    a.frag[a.K + (r + rr < a.R ? r + rr : r + rr - a.R)] * a.frag_stride + off + c * cstride, 0,
+                    SP);
     }
 }
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B at C3 (k=10 m=4, 1 MiB, 256 stripes): the LDS-table stream kernel (default for <= 4 outputs)
 against the bitsliced kernel built for 4 waves per SIMD (knob bitslice_min_rows 4), encode and
-decode of data {0,1,2,3}, interleaved rounds after a clock-settling warm-up, steady launches (HIP
+decode of data {0,1,2,3} and of the mixed {0,5,10,13}, interleaved rounds after a clock-settling warm-up, steady launches (HIP
 events). The bitsliced kernel runs both launch shapes (knob bs_grid: 1 = one workgroup per tile,
 0 = grid-stride over the resident slots)."""
 import json
@@ -17,6 +17,7 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 K, M, F, S = 10, 4, 1 << 20, 256
 LOST = [0, 1, 2, 3]
+MIXED = [0, 5, 10, 13]  # SURVEY §8d's second C3 pattern: data and parity lost, writes interleaved
 
 
 def main(rounds=3, n=30, skip=10):
@@ -28,15 +29,18 @@ def main(rounds=3, n=30, skip=10):
     d.ecamd_tune(b"bitslice_min_rows", 4)
     D.rs_encode(K, M, lay, stream=st)
     D.rs_decode(K, M, LOST, lay, stream=st)
+    D.rs_decode(K, M, MIXED, lay, stream=st)
     ref = lay.download_stripes()
     d.ecamd_tune(b"bitslice_min_rows", 0)
     D.rs_encode(K, M, lay, stream=st)
     D.rs_decode(K, M, LOST, lay, stream=st)
+    D.rs_decode(K, M, MIXED, lay, stream=st)
     assert (lay.download_stripes() == ref).all()
     d.ecamd_tune(b"bitslice_min_rows", 4)
     d.ecamd_tune(b"bs_grid", 0)
     D.rs_encode(K, M, lay, stream=st)
     D.rs_decode(K, M, LOST, lay, stream=st)
+    D.rs_decode(K, M, MIXED, lay, stream=st)
     assert (lay.download_stripes() == ref).all()
     d.ecamd_tune(b"bs_grid", 1)
     for _ in range(60):  # settle the clocks
@@ -48,7 +52,8 @@ def main(rounds=3, n=30, skip=10):
             d.ecamd_tune(b"bitslice_min_rows", rows)
             d.ecamd_tune(b"bs_grid", grid)
             for op, fn in (("encode", lambda: D.rs_encode(K, M, lay, stream=st)),
-                           ("decode", lambda: D.rs_decode(K, M, LOST, lay, stream=st))):
+                           ("decode", lambda: D.rs_decode(K, M, LOST, lay, stream=st)),
+                           ("decode_mixed", lambda: D.rs_decode(K, M, MIXED, lay, stream=st))):
                 ev = [D.Event() for _ in range(n + 1)]
                 ev[0].record(st)
                 for i in range(n):
