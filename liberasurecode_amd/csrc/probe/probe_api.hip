@@ -136,7 +136,8 @@ int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
     int dev = 0;
     int rc = ensure_device(&dev);
     if (rc) return rc;
-    if (ch != 1 && ch != 2) return fail(-22, "mix probe: ch must be 1 or 2");
+    if (ch != 1 && ch != 2 && ch != 4) return fail(-22, "mix probe: ch must be 1, 2 or 4");
+    if (ch == 4 && threads > 256) return fail(-22, "mix probe: ch 4 runs at most 256 threads");
     if (threads < 64 || threads > 1024 || threads % 64) return fail(-22, "mix probe: threads");
     const int64_t span = static_cast<int64_t>(threads) * 16 * ch;
     const int64_t sstride = bs * (K + R);
@@ -158,8 +159,10 @@ int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
     if (!launched && lp == LP && sp == SP) {                                                      \
         if (ch == 1)                                                                              \
             hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 1>), dim3(grid), dim3(threads), 0, st, a); \
-        else                                                                                      \
+        else if (ch == 2)                                                                         \
             hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 2>), dim3(grid), dim3(threads), 0, st, a); \
+        else                                                                                      \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 4>), dim3(grid), dim3(threads), 0, st, a); \
         launched = true;                                                                          \
     }
     ECAMD_MIX_POLICIES(ECAMD_MIX)

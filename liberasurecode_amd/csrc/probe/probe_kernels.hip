@@ -101,7 +101,7 @@ template __global__ void bw_probe_kernel<8>(uint8_t*, const uint8_t*, int64_t, i
 // (SP) as the aux immediate (gfx950 cpol: 1 = sc0, 2 = nt, 16 = sc1).  CH chunks of 16 B per lane
 // per fragment, the chunks of one lane blockDim*16 bytes apart.
 template <int LP, int SP, int CH>
-__global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
+__global__ void __launch_bounds__(CH == 4 ? 256 : 1024) mix_probe_kernel(MixArgs a)
 {
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
     // wave_contig: each wave covers CH KiB of a fragment contiguously (chunks 1 KiB apart);
@@ -168,7 +168,8 @@ __global__ void __launch_bounds__(1024) mix_probe_kernel(MixArgs a)
 
 #define ECAMD_MIX(LP, SP) \
     template __global__ void mix_probe_kernel<LP, SP, 1>(MixArgs); \
-    template __global__ void mix_probe_kernel<LP, SP, 2>(MixArgs);
+    template __global__ void mix_probe_kernel<LP, SP, 2>(MixArgs); \
+    template __global__ void mix_probe_kernel<LP, SP, 4>(MixArgs);
 ECAMD_MIX_POLICIES(ECAMD_MIX)
 #undef ECAMD_MIX
 

@@ -35,8 +35,9 @@ if len(sys.argv) > 1 and sys.argv[1] == "slots":  # which slots of a C3 stripe a
     ORDERS = (0,)
 if len(sys.argv) > 1 and sys.argv[1] == "geom":  # tile widths, C3 contiguous and mixed writes
     SHAPES = [("c3", 10, 4, 1 << 20, 256, None), ("c3_mixed", 10, 4, 1 << 20, 256, slots([0, 5, 10, 13]))]
-    GEOMS = [("tile4k", 256, 0, 1), ("tile8k", 256, 0, 2), ("tile16k", 1024, 0, 1), ("tile1k_1wave", 64, 0, 1),
-             ("tile2k_1wave", 64, 0, 2), ("tile2k_2wave", 128, 0, 1), ("tile4k_2wave", 128, 0, 2)]
+    GEOMS = [("tile4k", 256, 0, 1), ("tile1k_1wave", 64, 0, 1), ("tile16k_4wave_ch4", 256, 0, 4),
+             ("tile4k_1wave_ch4", 64, 0, 4), ("tile8k_2wave_ch4", 128, 0, 4), ("tile2k_1wave", 64, 0, 2),
+             ("stride16k_4wave_ch4_x2", 256, 8, 4)]
     ORDERS = (0,)
 
 
