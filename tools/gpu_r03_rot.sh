@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-3: tile-width probe of the C3 contiguous and mixed write patterns (tools/rot_probe.py geom).
+# Round-3: launch shape of the stream kernel for the C3 mixed decode (tools/mixed_shape_ab.py).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python3 tools/rot_probe.py geom > gpurun_out/r03_geom_probe3.log 2>&1 || { echo PROBE_FAILED; tail -20 gpurun_out/r03_geom_probe3.log; exit 1; }
-cat gpurun_out/r03_geom_probe3.log
+timeout -k 10 500 python3 tools/mixed_shape_ab.py > gpurun_out/r03_mixed_shape_ab.log 2>&1 || { echo AB_FAILED; tail -20 gpurun_out/r03_mixed_shape_ab.log; exit 1; }
+cat gpurun_out/r03_mixed_shape_ab.log
