@@ -236,6 +236,7 @@ struct Tuning {
     Knob frame_crc_lane{1};       // bitsliced crc variant (<= 4 outputs): lane-shift fold with 1
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
+    Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
     Knob frame_copy_grid{1};      // framed split / join stream kernels: 1 = one workgroup per tile
                                   //   (systematic join, Swift 1 MiB segments 0.83 -> 0.91 of the copy
                                   //   probe, C3 0.97 -> 1.02; tools/frame_bench.py), 0 = 8 per CU
@@ -274,6 +275,7 @@ int dev_tune(const char* key)
     if (k == "crc_wgs") return g_tune.crc_wgs;
     if (k == "frame_copy_grid") return g_tune.frame_copy_grid;
     if (k == "frame_crc_lane") return g_tune.frame_crc_lane;
+    if (k == "frame_crc_bs_nib") return g_tune.frame_crc_bs_nib;
     if (k == "frame_unfused") return g_tune.frame_unfused;
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     if (k == "crc_pos") return g_tune.crc_pos;
@@ -1233,6 +1235,7 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     if (!stream_offsets(a, bs) || !stream_copy_offsets(a, bs) || k > 254) return ECAMD_EINVAL;
     std::shared_ptr<void> hold;
     // crc_pos: position sets (1, 2, 4) + 8 for the lane-shift fold (which 5-8 outputs always take)
+    // + 16 for nibble piece tables
     hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
@@ -1500,6 +1503,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_grid = value < 0 ? 1 : value != 0;
     } else if (k == "frame_crc_lane") {
         g_tune.frame_crc_lane = value != 0;  // < 0: the default (1)
+    } else if (k == "frame_crc_bs_nib") {
+        g_tune.frame_crc_bs_nib = value > 0;  // <= 0: the default (byte tables)
     } else if (k == "frame_copy_grid") {
         g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
     } else if (k == "xor_grid") {

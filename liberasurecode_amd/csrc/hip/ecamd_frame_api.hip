@@ -323,15 +323,16 @@ int xor_batch_check(const Code& c, const void* base, int64_t ss, int64_t fs, int
 
 std::map<std::pair<int, int>, uint32_t*> g_fused_images;  // (dev, legacy + 2 * mb) -> device image
 
-int fused_image(int dev, bool legacy, int mb, const uint32_t** out, int tile = 8192, int npos = 0)
+int fused_image(int dev, bool legacy, int mb, const uint32_t** out, int tile = 8192, int npos = 0,
+                bool nib = false)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_pair(dev, (legacy ? 1 : 0) + 2 * mb + 16 * npos + 256 * tile);
+    auto key = std::make_pair(dev, (legacy ? 1 : 0) + 2 * mb + 16 * npos + 128 * (nib ? 1 : 0) + 256 * tile);
     auto it = g_fused_images.find(key);
     if (it == g_fused_images.end()) {
-        // npos > 0: the bitsliced crc variant's image (position sets of byte tables, step = tile)
+        // npos > 0: the bitsliced crc variant's image (position sets of byte or nibble tables, step = tile)
         const std::vector<uint32_t> w =
-            npos ? build_fused_crc_image_pos(CrcMachine(legacy), static_cast<uint64_t>(tile), npos)
+            npos ? build_fused_crc_image_pos(CrcMachine(legacy), static_cast<uint64_t>(tile), npos, nib)
                  : build_fused_crc_image(CrcMachine(legacy), static_cast<uint64_t>(tile), mb);
         uint32_t* d = nullptr;
         HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
@@ -408,9 +409,10 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
     const bool lane = c.m > 4 || dev_tune("frame_crc_lane") != 0;
     int npos = dev_tune("frame_crc_pos");
     if (npos <= 0) npos = lane && c.m <= 4 ? 1 : 2;
-    if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos))) return rc;
+    const bool nib = dev_tune("frame_crc_bs_nib") > 0;
+    if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos, nib))) return rc;
     rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                               partial, q, stream, npos | (lane ? 8 : 0));
+                               partial, q, stream, npos | (lane ? 8 : 0) | (nib ? 16 : 0));
     if (rc) return rc;
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
 }

@@ -177,7 +177,7 @@ struct BsEntry {
     int depth = 0;        // bitslice_source: 0 register loads, 2 / 4 LDS ring
     bool copy = false;    // copy-through variant (framed paths)
     int crc = 0;          // copy-through + payload CRC32 variant: position table sets (1, 2, 4), 0 = none;
-                          //   + 8: lane-shift fold
+                          //   + 8: lane-shift fold, + 16: nibble piece tables
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -246,14 +246,16 @@ const std::string& generator_fingerprint()
     std::call_once(once, [] {
         const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0);
         const BitsliceNet tiny5 = bitslice_network({3, 5, 7, 9, 11}, 5, 1, 0);  // the fold-each form
-        BitsliceStyle copy, crc, lane;
+        BitsliceStyle copy, crc, lane, nib;
         copy.copy_through = true;
         crc.copy_through = crc.crc = true;
         lane = crc;
         lane.crc_lane = true;
+        nib = lane;
+        nib.crc_nib = true;
         fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
-             kBsNetworkVersion;
+             bitslice_source(tiny5, 0, nib) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -277,7 +279,7 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
     BsEntry& e = *ep;
     const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
-                                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0);
+                                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
@@ -375,9 +377,9 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
                                 std::shared_ptr<void>& hold, bool copy, int crc)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
-    if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold
+    if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
         const int pos = crc & 7;
-        crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (crc & 8);
+        crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (crc & 24);
     }
     copy = copy || crc;
     depth = copy ? 0 : bitslice_depth(depth, K);

@@ -273,6 +273,11 @@ __device__ __forceinline__ u32 piece_r0(const u32* t, u32 a, u32 b, u32 c, u32 d
 {
     return x3(lmap8(t, a), lmap8(t + 1024, b), lmap8(t + 2048, c)) ^ lmap8(t + 3072, d);
 }
+// the same through nibble tables: dword w's 8 fields at tab + 128 w (conflict-free 16-entry tables)
+__device__ __forceinline__ u32 piece_r0n(const u32* t, u32 a, u32 b, u32 c, u32 d)
+{
+    return x3(lmap4(t, a), lmap4(t + 128, b), lmap4(t + 256, c)) ^ lmap4(t + 384, d);
+}
 )HIP";
 
 }  // namespace
@@ -380,7 +385,9 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         const bool lane_fold = fold_each || style.crc_lane;
         const int NS = net.K + net.R;
         const int NP = style.crc_pos >= 4 ? 4 : style.crc_pos >= 2 ? 2 : 1;
-        const int words = bs_crc_words(NP);
+        const int words = bs_crc_words(NP, style.crc_nib);
+        const int pw = style.crc_nib ? 512 : 4096;  // piece-table words per position set
+        const char* pfn = style.crc_nib ? "piece_r0n" : "piece_r0";
         // the CRC of 4 pieces x0..x3 (4096 bytes apart) of fragment f: NP pieces per gap step, piece c
         // through position set c % NP
         auto crc4 = [&](const std::string& f, const char* x) {
@@ -392,7 +399,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                 else
                     s << "            " << sv << " = lmap4(gap, " << sv << ")";
                 for (int c = c0; c < c0 + NP; c++)
-                    s << " ^ piece_r0(ctab + " << (c % NP) * 4096 << ", " << x << c << "[0], " << x << c << "[1], "
+                    s << " ^ " << pfn << "(ctab + " << (c % NP) * pw << ", " << x << c << "[0], " << x << c << "[1], "
                       << x << c << "[2], " << x << c << "[3])";
                 s << ";\n";
             }
@@ -408,7 +415,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
           << "    __shared__ u32 xch[4 * " << NS << "];\n"
           << "    for (int i = threadIdx.x; i < " << lds_words << "; i += 256) ctab[i] = a.crc_img[i];\n"
           << "    __syncthreads();\n"
-          << "    const u32* gap = ctab + " << NP * 4096 << ";\n"
+          << "    const u32* gap = ctab + " << NP * pw << ";\n"
              "    const u32* level = gap + 128;\n"
              "    const u32* a1024 = level + 6 * 128;\n"
              "    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;\n";
@@ -611,15 +618,17 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 }
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
-                             bool crc, int crc_pos, bool crc_lane)
+                             bool crc, int crc_pos, bool crc_lane, bool crc_nib)
 {
     std::ostringstream s;
     // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
-    // sets, bit 4 lane-shift fold
+    // sets, bit 4 lane-shift fold, bit 5 nibble piece tables
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     if (copy || crc)
         s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " "
-          << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0)) << "\n";
+          << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
+              (crc && crc_nib ? 32 : 0))
+          << "\n";
     else
         s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
     for (size_t i = 0; i < coeff.size(); i++) s << coeff[i] << ((i + 1) % static_cast<size_t>(K) ? " " : "\n");
@@ -627,7 +636,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 }
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane)
+                            int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib)
 {
     std::istringstream s(text);
     std::string magic;
@@ -635,7 +644,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || (version != 1 && version != 2)) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 27 || (cp & 12) == 12 || depth != 0))
+    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 59 || (cp & 12) == 12 || depth != 0))
         return false;  // copy: register loads
     if ((cp & 2) && !(cp & 1)) return false;  // crc implies copy
     if ((cp >> 2) && !(cp & 2)) return false;
@@ -643,6 +652,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (crc) *crc = (cp & 2) != 0;
     if (crc_pos) *crc_pos = 1 << ((cp >> 2) & 3);
     if (crc_lane) *crc_lane = (cp & 16) != 0;
+    if (crc_nib) *crc_nib = (cp & 32) != 0;
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)
         if (!(s >> c) || c < 0 || c > 0xffff) return false;

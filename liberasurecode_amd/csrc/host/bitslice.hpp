@@ -65,11 +65,15 @@ struct BitsliceStyle {
     // crc variant: fold each wave's lane states with lane-shift tables (one map per lane, 32 KiB
     // more LDS) and an XOR reduction instead of the 6-level butterfly; always on for 5-8 outputs
     bool crc_lane = false;
+    // crc variant: piece tables of 16-entry nibble fields (2 KiB per position set, conflict-free,
+    // 32 lookups per 16-byte piece) instead of 256-entry byte tables (16 KiB, 16 lookups that
+    // conflict ~3.5-way in the LDS banks)
+    bool crc_nib = false;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
 // levels + A^1024
-constexpr int bs_crc_words(int npos) { return npos * 4 * 1024 + 8 * 128; }
+constexpr int bs_crc_words(int npos, bool nib = false) { return npos * (nib ? 512 : 4 * 1024) + 8 * 128; }
 constexpr int kBsCrcStep = 4096;  // bytes between a lane's consecutive pieces of one fragment
 constexpr int kBsCrcLaneWords = 8 * 16 * 64;  // lane-shift tables after bs_crc_words (fold-each form)
 std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
@@ -81,10 +85,10 @@ int bitslice_waves_per_simd(int R, bool crc = false);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
-                             bool crc = false, int crc_pos = 1, bool crc_lane = false);
+                             bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
-                            bool* crc_lane = nullptr);
+                            bool* crc_lane = nullptr, bool* crc_nib = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

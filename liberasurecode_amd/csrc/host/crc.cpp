@@ -89,13 +89,13 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
     return img;
 }
 
-std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos)
+std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos, bool nib)
 {
-    // npos sets of all-byte piece tables, set u shifted to the group's last piece
+    // npos sets of all-byte (or all-nibble) piece tables, set u shifted to the group's last piece
     // (A^(step*(npos-1-u)) folded in), then the gap map A^(step*npos) and the 6 butterfly levels
     // and A^1024 of build_fused_crc_image, then the lane-shift tables
-    const CrcImage pieces = build_crc_image(m, 8, 4, 4, false);
-    const size_t pw = 4 * 4 * 256;
+    const CrcImage pieces = build_crc_image(m, nib ? 4 : 8, 4, 4, false);
+    const size_t pw = nib ? 4 * 8 * 16 : 4 * 4 * 256;
     std::vector<uint32_t> w(static_cast<size_t>(npos) * pw + 8 * 128, 0);
     for (int u = 0; u < npos; u++) {
         const Mat32 sh = zero_shift(m, step * static_cast<uint64_t>(npos - 1 - u));

@@ -82,7 +82,8 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos = fa
 // step between a lane's pieces), A^(16*2^t) for t < 6 (in-wave butterfly), A^1024 (across waves).
 std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb = 1);
 // The bitsliced crc variant's image: npos position sets of byte piece tables (pieces `step` bytes
-// apart, each set shifted to the group's last piece) + gap A^(step*npos) + butterfly levels + A^1024.
-std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos);
+// apart, each set shifted to the group's last piece) + gap A^(step*npos) + butterfly levels + A^1024,
+// then the lane-shift tables; nib: the piece tables as 16-entry nibble fields (512 words per set).
+std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos, bool nib = false);
 
 }  // namespace ecamd

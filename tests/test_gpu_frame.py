@@ -378,7 +378,7 @@ def test_percall_crc_handoff(F, bs, legacy):
                                       (8, 4, 64 * 8192, 2), (3, 2, 40 * 8192, 9), (12, 6, 16384, 4),
                                       (20, 8, 4 * 8192, 3)])
 @pytest.mark.parametrize("legacy", [False, True])
-@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4", "bsl"])
+@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4", "bsl", "bsn", "bsn4"])
 def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkeypatch):
     """CHKSUM_CRC32 framed encode of objects that fill the payloads: the fused launch (codec +
     copy-through + payload checksums folded per range) against the copy-through encode + separate
@@ -395,8 +395,11 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     # payload sizes fall back to the LDS-table fused kernel or the copy-through encode + CRC pass
     bs_fits = m <= 8 and bs % 16384 == 0
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, 4 if bsv else mb)), "tune")
-    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4, "bsl": 0}.get(mb, 1)), "tune")
-    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_lane", 1 if mb == "bsl" else 0), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4, "bsl": 0, "bsn": 0, "bsn4": 4}.get(mb, 1)),
+               "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_lane", 1 if mb in ("bsl", "bsn", "bsn4") else 0), "tune")
+    # bsn*: the crc variant's piece tables as nibble fields (knob frame_crc_bs_nib)
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_bs_nib", 1 if mb in ("bsn", "bsn4") else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_nib", 1 if mb in ("nib", "nib1") else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_bs", 1 if bsv else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2 if bsv else 1), "tune")
@@ -418,6 +421,7 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
         _lib.dev().ecamd_tune(b"frame_crc_bs", -1)
         _lib.dev().ecamd_tune(b"frame_crc_pos", -1)
         _lib.dev().ecamd_tune(b"frame_crc_lane", -1)
+        _lib.dev().ecamd_tune(b"frame_crc_bs_nib", -1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
     if bs <= (1 << 16):
