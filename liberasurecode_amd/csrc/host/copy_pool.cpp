@@ -34,8 +34,17 @@
 namespace {
 
 constexpr int64_t kPiece = 256 << 10;     // bytes per piece handed to one thread
-constexpr int64_t kParallelMin = 2 << 20;  // smaller batches are copied by the caller alone
-// (1 MiB objects: 10 x 100 KiB fragments measured slower with the helpers than without)
+// Smaller batches are copied by the caller alone (ECAMD_COPY_MIN_KIB, default 2 MiB: 1 MiB objects,
+// 10 x 100 KiB fragments, measured slower with the helpers than without before they polled)
+int64_t parallel_min()
+{
+    static const int64_t bytes = [] {
+        const char* s = std::getenv("ECAMD_COPY_MIN_KIB");
+        const long v = s && *s ? std::atol(s) : 0;
+        return v > 0 ? static_cast<int64_t>(v) << 10 : int64_t(2) << 20;
+    }();
+    return bytes;
+}
 constexpr auto kHelperPoll = std::chrono::microseconds(300);  // helper polling before it sleeps
 constexpr int64_t kSoloNs = 5000000;  // another caller thread within 5 ms: copy alone
 
@@ -156,7 +165,7 @@ extern "C" int ecamd_host_copy(int n, void* const* dst, const void* const* src, 
     for (int i = 0; i < n; i++) total += std::max<int64_t>(0, len[i]);
     Pool& p = pool();
     const bool solo = solo_caller(p);
-    if (total < kParallelMin || !solo || !ensure_started(p) || !p.busy.try_lock()) {
+    if (total < parallel_min() || !solo || !ensure_started(p) || !p.busy.try_lock()) {
         copy_serial(n, dst, src, len);
         return 0;
     }

@@ -1,11 +1,8 @@
 #!/usr/bin/env python3
 """A/B of per-call latency settings (round 3): tools/latency_bench.py --codec own in child processes,
-interleaved rounds --
-  round2        ECAMD_FRONTEND_ZERO_ALL=1 ECAMD_COPY_THREADS=0 ECAMD_FRONTEND_POOL_MIB=0 (round-2 host path)
-  no-pool       lean zeroing, 4 copy helpers, no recycled buffers
-  default       lean zeroing, 4 copy helpers, recycled fragment / object buffers
-(earlier forms of this tool compared polling the staging streams, ECAMD_PERCALL_SPIN_US:
-profiles/r03_latency_ab2.log, r03_latency_ab3.log)
+interleaved rounds -- the copy helpers' batch threshold (ECAMD_COPY_MIN_KIB, default 2048) at 256 KiB
+and 1 MiB, and the helpers off.  Earlier forms of this tool compared the round-2 host path, the
+recycled buffers and polling the staging streams (profiles/r03_latency_ab1..4.log).
 One JSON line per (setting, round, checksum, size) with the median encode / decode latency."""
 import json
 import os
@@ -13,9 +10,10 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SETTINGS = {"round2": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0", "ECAMD_FRONTEND_POOL_MIB": "0"},
-            "no-pool": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_FRONTEND_POOL_MIB": "0"},
-            "default": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4", "ECAMD_FRONTEND_POOL_MIB": "256"}}
+SETTINGS = {"default": {},
+            "copy_min_256k": {"ECAMD_COPY_MIN_KIB": "256"},
+            "copy_min_1m": {"ECAMD_COPY_MIN_KIB": "1024"},
+            "no-helpers": {"ECAMD_COPY_THREADS": "0"}}
 
 
 def main():
