@@ -80,6 +80,20 @@ def main():
         rc, idx = E.fragments_needed(desc, [dest], [], n)
         need.append([dest, rc, idx])
     out["fragments_needed"] = need
+    # recycled buffers (frontend.cpp BufferPool): objects of different sizes and contents in turn,
+    # each encoded twice with other calls between; digests must repeat and every decode round-trip
+    pool = []
+    sizes = [(1 << 20) + 13, (3 << 20) - 7, (256 << 10) + 1, 2 << 20]
+    for rep in range(2):
+        for i, sz in enumerate(sizes):
+            o2 = bytes((j * 29 + i * 7 + (j >> 9)) & 0xFF for j in range(sz))
+            rc, d, p, fl = E.encode(desc, o2)
+            fr = E.fragments(d, k, fl) + E.fragments(p, m, fl)
+            E.lib().liberasurecode_encode_cleanup(desc, d, p)
+            rc2, back = E.decode(desc, fr[1:], fl)  # fragment 0 lost
+            rc3, sysd = E.decode(desc, fr[:k], fl)
+            pool.append([rep, sz, rc, sha(b"".join(fr)), rc2 == 0 and back == o2, rc3 == 0 and sysd == o2])
+    out["pool"] = pool
     out["libs"] = mapped_codecs()  # before destroy: the backend library is dlclose()d there
     out["destroy"] = E.lib().liberasurecode_instance_destroy(desc)
     print(json.dumps(out))

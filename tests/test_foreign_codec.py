@@ -63,6 +63,10 @@ def test_frontend_over_reference_codec(name, ct):
     assert all(rc == 0 and idx and d not in idx and (name == "xor" or len(idx) == res["k"])
                for d, rc, idx in res["fragments_needed"]), res["fragments_needed"]
     assert res["destroy"] == 0
+    pool = res["pool"]  # recycled fragment / object buffers: same bytes every time, exact decodes
+    assert all(rc == 0 and dec and sysd for _, _, rc, _, dec, sysd in pool), pool
+    half = len(pool) // 2
+    assert [x[3] for x in pool[:half]] == [x[3] for x in pool[half:]], "encode digests changed on reuse"
     libs = res["libs"]
     assert "oracle/_ref/libXorcode.so.1" in libs, libs  # the frontend's DT_NEEDED, from the reference
     if name == "rs":
@@ -79,5 +83,5 @@ def test_own_codec_matches_reference_codec(name, ct):
     assert own["create"] > 0 and own["encode_rc"] == 0
     assert any("libecamd.so" in x for x in own["libs"]), own["libs"]
     assert own["fragments_sha256"] == ref["fragments_sha256"]
-    for key in ("decode", "reconstruct", "fragments_needed"):
+    for key in ("decode", "reconstruct", "fragments_needed", "pool"):
         assert own[key] == ref[key], key
