@@ -240,6 +240,14 @@ struct Tuning {
     Knob frame_copy_grid{1};      // framed split / join stream kernels: 1 = one workgroup per tile
                                   //   (systematic join, Swift 1 MiB segments 0.83 -> 0.91 of the copy
                                   //   probe, C3 0.97 -> 1.02; tools/frame_bench.py), 0 = 8 per CU
+    Knob xor_threads{0};          // xor_stream_kernel: threads per workgroup = the tile (16 B per lane per
+                                  //   fragment): 64 / 128 / 256 for 1 / 2 / 4 KiB tiles; 0 = by shape: 64
+                                  //   for passes of more than 4 inputs over fragments of kXorNarrowMin and
+                                  //   more, else 256.  One-wave 1 KiB tiles at 1 MiB: (10,5,3) encode
+                                  //   0.722-0.728 -> 0.790-0.792 of 8 TB/s, (10,6,4) 0.784-0.786 ->
+                                  //   0.797-0.800, decodes 5-7% faster; (3,3,3) at 1 MiB and (10,6,4) at
+                                  //   64 KiB 0.7-3.5% slower, 4 KiB fragments 2% slower (two runs,
+                                  //   tools/xor_threads_ab.py, profiles/r03_xor_threads_ab1.log, _ab2.log)
     Knob xor_grid{1};             // xor_stream_kernel: 1 = one workgroup per tile, 0 = resident slots
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
@@ -276,6 +284,7 @@ int dev_tune(const char* key)
     if (k == "frame_copy_grid") return g_tune.frame_copy_grid;
     if (k == "frame_crc_lane") return g_tune.frame_crc_lane;
     if (k == "frame_crc_bs_nib") return g_tune.frame_crc_bs_nib;
+    if (k == "xor_threads") return g_tune.xor_threads;
     if (k == "frame_unfused") return g_tune.frame_unfused;
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     if (k == "crc_pos") return g_tune.crc_pos;
@@ -773,6 +782,8 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
     return 0;
 }
 
+constexpr int64_t kXorNarrowMin = 256 << 10;  // fragment bytes from which flat XOR takes 1 KiB tiles
+
 template <bool PTRS>
 int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const int64_t* in_off,
                const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st)
@@ -792,11 +803,15 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                 a.masks[r] = col0 < 32 ? (masks[row0 + r] >> col0) : 0u;
             }
             Geometry g;
-            int rc = geometry(dev, 0, bs, nstripes, g);
+            const bool use_stream = !PTRS && g_tune.stream && stream_offsets(a, bs);
+            const int xt = g_tune.xor_threads ? g_tune.xor_threads
+                                               : (a.ncols > 4 && bs >= kXorNarrowMin ? 64 : 256);
+            const bool narrow = use_stream && (xt == 64 || xt == 128);  // only the stream kernel
+            int rc = geometry(dev, 0, bs, nstripes, g, 1, narrow ? xt : 1024);
             if (rc) return rc;
             a.ntiles = g.ntiles;
             a.tiles_per_stripe = g.tiles_per_stripe;
-            if (!PTRS && g_tune.stream && stream_offsets(a, bs)) {
+            if (use_stream) {
                 // geometry: 256 threads, one workgroup per 4 KiB tile (xor_grid; the dispatcher
                 // hands each freed slot the next tile: (10,6,4) encode 0.753 -> 0.790 of 8 TB/s,
                 // (3,3,3) 0.717 -> 0.743, profiles/r03_xor_grid.log); long passes as several
@@ -805,7 +820,8 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                 // else 2 (tools/xor_geom_sweep.py, profiles/r03_xor_geom.log)
                 const int wgs = g_tune.xor_wgs > 0 ? g_tune.xor_wgs : (a.ncols > 4 && a.nrows >= 3 ? 3 : 2);
                 const int64_t slots = static_cast<int64_t>(cu_count(dev)) * wgs;
-                const int knob = g_tune.xor_tiles_per_slot;
+                // narrower tiles: the same bytes per launch (tiles per slot scaled by 256 / threads)
+                const int knob = g_tune.xor_tiles_per_slot * (256 / g.threads);
                 rc = for_each_launch(a, nstripes, g.tiles_per_stripe, static_cast<uint64_t>(slots),
                                      static_cast<uint64_t>(std::max(knob, 0)), [&](ApplyArgs& c, int n) {
                     c.ntiles = g.tiles_per_stripe * static_cast<uint32_t>(n);
@@ -1507,6 +1523,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_bs_nib = value > 0;  // <= 0: the default (byte tables)
     } else if (k == "frame_copy_grid") {
         g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
+    } else if (k == "xor_threads") {
+        g_tune.xor_threads = value == 64 || value == 128 || value == 256 ? value : 0;  // else by shape
     } else if (k == "xor_grid") {
         g_tune.xor_grid = value != 0;  // < 0: the default (1)
     } else if (k == "bs_tiles_per_slot") {
