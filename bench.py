@@ -225,23 +225,31 @@ def cpu_baseline(k, m, F, missing, threads, target_s):
 # ------------------------------------------------------------------ GPU helpers ----
 
 def measured_copy_peak(D, stream, nbytes=1 << 30):
-    """Second roofline denominator: non-temporal 16 B/lane copy of 1 GiB on this GPU (GB/s), from
-    the measurement library (liberasurecode_amd/lib/libecamd_probe.so, not the product)."""
+    """Second roofline denominator: the fastest of two non-temporal 16 B/lane copies of 1 GiB on this
+    GPU (GB/s) from the measurement library (liberasurecode_amd/lib/libecamd_probe.so, not the
+    product) -- the round-1 probe (2 resident 256-lane workgroups per CU, 4 chunks per lane, grid-
+    stride) and one one-wave workgroup per 1 KiB tile in dispatcher order, which copies ~15% faster
+    (DESIGN.md §4).  Returns (GB/s, per-probe GB/s)."""
     from liberasurecode_amd import _lib
     p = _lib.probe()
     buf = D.DeviceBuffer(2 * nbytes)
     a, b = D.Event(), D.Event()
-    best = 0.0
+    probes = {"grid_stride_4x256": lambda: p.ecamd_probe_bw(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes,
+                                                            stream.handle),
+              "wave_per_1KiB_tile": lambda: p.ecamd_probe_copy_tiles(64, buf.ptr + nbytes, buf.ptr, nbytes,
+                                                                     stream.handle)}
+    rates = {}
     for _ in range(3):
-        _lib.check(p.ecamd_probe_bw(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes, stream.handle),
-                   "copy probe")
-        a.record(stream)
-        for _ in range(4):
-            p.ecamd_probe_bw(0, 4, 2, buf.ptr + nbytes, buf.ptr, nbytes, stream.handle)
-        b.record(stream)
-        best = max(best, 2 * nbytes * 4 / (a.elapsed_ms(b) * 1e-3) / 1e9)
+        for name, fn in probes.items():
+            _lib.check(fn(), "copy probe " + name)
+            a.record(stream)
+            for _ in range(4):
+                fn()
+            b.record(stream)
+            rate = 2 * nbytes * 4 / (a.elapsed_ms(b) * 1e-3) / 1e9
+            rates[name] = max(rates.get(name, 0.0), rate)
     buf.free()
-    return best
+    return max(rates.values()), {k: round(v, 1) for k, v in rates.items()}
 
 
 def dispatches_per_pass(k, width, F, S, cus):
@@ -564,7 +572,7 @@ def main():
 
     out = None
     if rank == 0:
-        copy_gbs = measured_copy_peak(D, stream)
+        copy_gbs, copy_probes = measured_copy_peak(D, stream)
         summ, summ_src = profile_summary(args.config)
         # the committed trace describes ONE command (bench.py --gpus 1, its config and stripes):
         # quote it only for a run of that shape
@@ -632,6 +640,7 @@ def main():
                          "encode_pass_ms": round(sum(enc_ms) / len(enc_ms), 4),
                          "decode_pass_ms": round(sum(dec_ms) / len(dec_ms), 4),
                          "copy_peak_measured": round(copy_gbs, 1),
+                         "copy_probes": copy_probes,
                          "frac_of_measured_copy": round(achieved / copy_gbs, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "trace": trace},

@@ -21,6 +21,10 @@ const char *ecamd_probe_last_error(void);
 int ecamd_probe_stream_copy(void *d_dst, const void *d_src, int64_t bytes, void *stream);
 /* kind 0 copy / 1 read-only / 2 write-only over `bytes`, unroll in {1,4,8} 16-B loads per lane in
  * flight, grid = CUs x wgs_per_cu workgroups of 256 lanes (bandwidth ceilings for DESIGN.md). */
+/* Copy of `bytes` (a multiple of threads*16) with one workgroup of `threads` (64 / 128 / 256) lanes per
+ * tile of threads*16 bytes, 16 B per lane, non-temporal, in dispatcher order: with one-wave 1 KiB
+ * tiles the fastest HBM copy measured here. */
+int ecamd_probe_copy_tiles(int threads, void *d_dst, const void *d_src, int64_t bytes, void *stream);
 int ecamd_probe_bw(int kind, int unroll, int wgs_per_cu, void *d_dst, const void *d_src,
                          int64_t bytes, void *stream);
 /* Codec-shaped streaming probe: K fragment reads and R fragment writes per tile over nstripes

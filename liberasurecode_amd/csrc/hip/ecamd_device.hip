@@ -237,6 +237,9 @@ struct Tuning {
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
+    Knob frame_copy_threads{0};   // framed split / join stream kernels: lanes per tile (64 / 128 / 256; 0 = by
+                                  //   shape: 64 for 16-byte-multiple payloads, else 256, ecamd_frame_api.hip)
+    Knob frame_copy_u{0};         //   and 16-byte chunks per lane (1 / 4; 0 = 1)
     Knob frame_copy_grid{1};      // framed split / join stream kernels: 1 = one workgroup per tile
                                   //   (systematic join, Swift 1 MiB segments 0.83 -> 0.91 of the copy
                                   //   probe, C3 0.97 -> 1.02; tools/frame_bench.py), 0 = 8 per CU
@@ -285,6 +288,8 @@ int dev_tune(const char* key)
     if (k == "frame_crc_lane") return g_tune.frame_crc_lane;
     if (k == "frame_crc_bs_nib") return g_tune.frame_crc_bs_nib;
     if (k == "xor_threads") return g_tune.xor_threads;
+    if (k == "frame_copy_threads") return g_tune.frame_copy_threads;
+    if (k == "frame_copy_u") return g_tune.frame_copy_u;
     if (k == "frame_unfused") return g_tune.frame_unfused;
     if (k == "crc_gap_bits") return g_tune.crc_gap_bits;
     if (k == "crc_pos") return g_tune.crc_pos;
@@ -1523,6 +1528,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_bs_nib = value > 0;  // <= 0: the default (byte tables)
     } else if (k == "frame_copy_grid") {
         g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
+    } else if (k == "frame_copy_threads") {
+        g_tune.frame_copy_threads = value == 64 || value == 128 || value == 256 ? value : 0;
+    } else if (k == "frame_copy_u") {
+        g_tune.frame_copy_u = value == 1 || value == 4 ? value : 0;
     } else if (k == "xor_threads") {
         g_tune.xor_threads = value == 64 || value == 128 || value == 256 ? value : 0;  // else by shape
     } else if (k == "xor_grid") {

@@ -242,12 +242,12 @@ __global__ void frame_split_kernel(const SplitArgs a)
 }
 
 // Streaming forms of the two copies for objects / stripes whose offsets fit 32 bits: a tile is
-// kCopyU x 256 lanes x 16 B of one data fragment of one stripe (t -> stripe, fragment, tile: 32-bit
+// kCopyU x blockDim lanes x 16 B of one data fragment of one stripe (t -> stripe, fragment, tile: 32-bit
 // index math once per tile), loads and stores are buffer ops on one resource per stripe with
 // 32-bit offsets, and the unaligned side of the copy (object offset j*bs when bs % 16 != 0) takes
 // unaligned 16-byte buffer accesses -- as the copy-through codec launch does -- instead of bytes.
 // Only the chunk that straddles two payloads or the object's end goes byte by byte.
-constexpr int kCopyU = 4;
+// kCopyU (template parameter of the two kernels below): chunks per lane and tile, 4 or 1.
 
 __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int dw, int by);
 
@@ -255,10 +255,12 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // realigned in registers from the two aligned object chunks under it when j*bs % 16 != 0 (aligned
 // loads and stores on both sides); the payload's last chunk, anything reaching past the object's
 // end (zero padded) and a window whose second chunk would reach past the object go byte by byte.
+template <int kCopyU>
 __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs a)
 {
+    const uint32_t T = blockDim.x;  // lanes per tile (64 / 128 / 256)
     const uint32_t per_frag = static_cast<uint32_t>((a.bs + 15) / 16);  // payload chunks
-    const uint32_t tpf = (per_frag + 256 * kCopyU - 1) / (256 * kCopyU);
+    const uint32_t tpf = (per_frag + T * kCopyU - 1) / (T * kCopyU);
     const uint32_t ntiles = tpf * static_cast<uint32_t>(a.k) * static_cast<uint32_t>(a.nstripes);
     const int bs = static_cast<int>(a.bs);
     const int size = static_cast<int>(a.size);
@@ -276,7 +278,7 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         u32x4 v0[kCopyU], v1[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int src = lo + c * 16;
             const int q = src >> 4;
             const bool fast = c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
@@ -286,7 +288,7 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int c = static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             if (c >= static_cast<int>(per_frag)) continue;
             const int src = lo + c * 16;
             const int q = src >> 4;
@@ -306,6 +308,8 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         }
     }
 }
+template __global__ void frame_split_stream_kernel<1>(const SplitArgs);
+template __global__ void frame_split_stream_kernel<4>(const SplitArgs);
 
 // Bytes [d, d + 16) of the 32-byte pair (lo, hi), d = 4 * dw + by wave-uniform: v_alignbyte on
 // the dword pairs (realigns an unaligned 16-byte window from two aligned loads).
@@ -337,13 +341,15 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // The straddling chunk is one lane's store too: the last 16 payload bytes of j-1, realigned, joined
 // with the first bytes of j.  Only the object's final partial chunk goes byte by byte, so nothing
 // is written outside [0, size).  Needs bs >= 32 (the host falls back to frame_join_kernel).
+template <int kCopyU>
 __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
 {
+    const uint32_t T = blockDim.x;  // lanes per tile (64 / 128 / 256)
     const int bs = static_cast<int>(a.bs);
     const int bs16 = (bs + 15) & ~15;
     const int size = static_cast<int>(a.size);
     const uint32_t per_frag = static_cast<uint32_t>(bs / 16 + 2);
-    const uint32_t tpf = (per_frag + 256 * kCopyU - 1) / (256 * kCopyU);
+    const uint32_t tpf = (per_frag + T * kCopyU - 1) / (T * kCopyU);
     const uint32_t ntiles = tpf * static_cast<uint32_t>(k) * static_cast<uint32_t>(a.nstripes);
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t sj = t / tpf;
@@ -363,7 +369,7 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         u32x4 v0[kCopyU], v1[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
             const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi;
             v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
@@ -372,7 +378,7 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * 256 + threadIdx.x);
+            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             if (ch >= c1) continue;
             const int A = ch << 4;
             if (A >= lo && A + 16 <= hi) {
@@ -400,6 +406,8 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         }
     }
 }
+template __global__ void frame_join_stream_kernel<1>(const JoinArgs, int);
+template __global__ void frame_join_stream_kernel<4>(const JoinArgs, int);
 
 // fragments_to_string: object bytes [0, size) = data payloads 0..k-1 concatenated.
 __global__ void frame_join_kernel(const JoinArgs a)

@@ -251,11 +251,31 @@ bool copy_fits32(int k, int64_t frag_stride, int64_t bs, int64_t obj_size)
            (k - 1) * frag_stride + kHeaderBytes + bs + 16 < lim && k * bs < lim;
 }
 
-// Tiles of kCopyU x 256 chunks per (stripe, data fragment); 8 resident 256-thread workgroups per CU
-// (grid-stride), or one workgroup per tile (knob frame_copy_grid).
-int copy_grid(int dev, int64_t chunks_per_frag, int k, int nstripes)
+// Lanes and chunks per lane of the split / join stream tiles (knobs frame_copy_threads 64 / 128 /
+// 256, frame_copy_u 1 / 4).  By default one chunk per lane: one-wave 1 KiB tiles when the payloads
+// are 16-byte multiples, 4-wave 4 KiB tiles when they are not (the realigning path).  Systematic
+// join, ~2.5 GiB of objects: 1 MiB payloads 0.757 -> 0.830 of 8 TB/s, 4 MiB 0.761 -> 0.825, 16 KiB
+// 0.62 -> 0.77 against the round's first 16 KiB tiles; Swift's 1 MiB segments (bs = 104858) 0.648
+// -> 0.705 (tools/copy_shape_ab.py, profiles/r03_copy_shape_ab1.log, _ab2.log).
+struct CopyShape {
+    int threads = 256, u = 1;
+};
+CopyShape copy_shape(int64_t bs)
 {
-    const int64_t tiles = (chunks_per_frag + 1023) / 1024 * k * static_cast<int64_t>(nstripes);
+    CopyShape c;
+    c.threads = bs % 16 == 0 ? 64 : 256;
+    const int t = dev_tune("frame_copy_threads"), u = dev_tune("frame_copy_u");
+    if (t == 64 || t == 128 || t == 256) c.threads = t;
+    if (u == 1 || u == 4) c.u = u;
+    return c;
+}
+
+// Tiles of u x threads chunks per (stripe, data fragment); 8 resident 256-thread workgroups per CU
+// (grid-stride), or one workgroup per tile (knob frame_copy_grid).
+int copy_grid(int dev, int64_t chunks_per_frag, int k, int nstripes, const CopyShape& cs)
+{
+    const int64_t per = static_cast<int64_t>(cs.threads) * cs.u;
+    const int64_t tiles = (chunks_per_frag + per - 1) / per * k * static_cast<int64_t>(nstripes);
     const int64_t cap = dev_tune("frame_copy_grid") ? (int64_t{1} << 30) : static_cast<int64_t>(dev_cu_count(dev)) * 8;
     return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(tiles, cap)));
 }
@@ -510,10 +530,14 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
     }
     SplitArgs sa{static_cast<const uint8_t*>(d_obj), obj_stride, static_cast<int64_t>(obj_size),
                  frags, stripe_stride, frag_stride, bs, k, nstripes, aligned ? 1 : 0};
-    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0)
-        hipLaunchKernelGGL(frame_split_stream_kernel,
-                           dim3(copy_grid(dev, (bs + 15) / 16, k, nstripes)), dim3(256), 0, st, sa);
-    else
+    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0) {
+        const CopyShape cs = copy_shape(bs);
+        const dim3 grid(copy_grid(dev, (bs + 15) / 16, k, nstripes, cs)), block(cs.threads);
+        if (cs.u == 1)
+            hipLaunchKernelGGL(frame_split_stream_kernel<1>, grid, block, 0, st, sa);
+        else
+            hipLaunchKernelGGL(frame_split_stream_kernel<4>, grid, block, 0, st, sa);
+    } else
         hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),
                            dim3(256), 0, st, sa);
     HIP_TRY(hipGetLastError());
@@ -580,10 +604,14 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
                 static_cast<int64_t>(obj_size), nstripes,
                 (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
     if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && bs >= 32 &&
-        dev_tune("frame_copy_stream") != 0)
-        hipLaunchKernelGGL(frame_join_stream_kernel, dim3(copy_grid(dev, bs / 16 + 2, k, nstripes)),
-                           dim3(256), 0, static_cast<hipStream_t>(stream), ja, k);
-    else
+        dev_tune("frame_copy_stream") != 0) {
+        const CopyShape cs = copy_shape(bs);
+        const dim3 grid(copy_grid(dev, bs / 16 + 2, k, nstripes, cs)), block(cs.threads);
+        if (cs.u == 1)
+            hipLaunchKernelGGL(frame_join_stream_kernel<1>, grid, block, 0, static_cast<hipStream_t>(stream), ja, k);
+        else
+            hipLaunchKernelGGL(frame_join_stream_kernel<4>, grid, block, 0, static_cast<hipStream_t>(stream), ja, k);
+    } else
         hipLaunchKernelGGL(frame_join_kernel,
                            dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),
                            dim3(256), 0, static_cast<hipStream_t>(stream), ja);

@@ -94,6 +94,23 @@ int ecamd_probe_bw(int kind, int unroll, int wgs_per_cu, void* dst, const void* 
     return 0;
 }
 
+int ecamd_probe_copy_tiles(int threads, void* dst, const void* src, int64_t bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (threads != 64 && threads != 128 && threads != 256) return fail(-22, "copy tiles: threads 64 / 128 / 256");
+    const int64_t tile = static_cast<int64_t>(threads) * 16;
+    if (bytes < tile || bytes % tile || bytes / tile >= (int64_t{1} << 31)) return fail(-22, "copy tiles: bytes");
+    static uint32_t* sink = nullptr;
+    if (!sink) HIP_TRY(hipMalloc(&sink, 1024 * sizeof(uint32_t)));
+    hipLaunchKernelGGL(bw_probe_kernel<1>, dim3(static_cast<unsigned>(bytes / tile)), dim3(threads), 0,
+                       static_cast<hipStream_t>(stream), static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src),
+                       bytes, 0, sink);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void* d_table, void* stream)
 {
     int dev = 0;

@@ -67,7 +67,7 @@ def main():
     d.ecamd_tune(b"bitslice", 2)  # run-time compiled kernels ready before any timing (steady state)
     st = D.Stream()
     import bench
-    copy_gbs = bench.measured_copy_peak(D, st)
+    copy_gbs = bench.measured_copy_peak(D, st)[0]
     print(json.dumps({"copy_probe_GBps": round(copy_gbs, 1)}), flush=True)
     fb = frame.FrameBatch(frame.RS_VAND, k, m, size, S, align=args.align)
     print(json.dumps({"align": args.align, "frag_stride": fb.frag_stride, "head": fb.head}), flush=True)
