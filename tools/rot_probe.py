@@ -33,6 +33,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "slots":  # which slots of a C3 stripe a
                         [1, 4, 7, 10], [0, 13, 6, 7])]
     GEOMS = [("stride_x8", 256, 8), ("tile", 256, 0)]
     ORDERS = (0,)
+if len(sys.argv) > 1 and sys.argv[1] == "geom5":  # tile widths, C5 (20 + 8, 4 MiB) data and mixed rebuilds
+    SHAPES = [("c5_rebuild_0_7", 20, 8, 4 << 20, 32, slots(list(range(8)), 28)),
+              ("c5_rebuild_mixed", 20, 8, 4 << 20, 32, slots([0, 2, 4, 6, 20, 22, 24, 26], 28))]
+    GEOMS = [("tile16k_4wave_ch4", 256, 0, 4), ("tile4k_1wave_ch4", 64, 0, 4), ("tile8k_2wave_ch4", 128, 0, 4),
+             ("tile1k_1wave", 64, 0, 1), ("tile4k", 256, 0, 1)]
+    ORDERS = (0,)
 if len(sys.argv) > 1 and sys.argv[1] == "geom":  # tile widths, C3 contiguous and mixed writes
     SHAPES = [("c3", 10, 4, 1 << 20, 256, None), ("c3_mixed", 10, 4, 1 << 20, 256, slots([0, 5, 10, 13]))]
     GEOMS = [("tile4k", 256, 0, 1), ("tile1k_1wave", 64, 0, 1), ("tile16k_4wave_ch4", 256, 0, 4),
