@@ -20,9 +20,17 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 K, M, F, S = 10, 4, 1 << 20, 256
 OPS = {"encode": None, "decode_0123": [0, 1, 2, 3], "decode_mixed": [0, 5, 10, 13]}
+if len(sys.argv) > 1 and sys.argv[1] == "c2":  # C2: k=4 m=2, 64 KiB x 4096 stripes (1 KiB nibble image)
+    K, M, F, S = 4, 2, 64 << 10, 4096
+    OPS = {"encode": None, "decode_01": [0, 1], "decode_mixed": [0, 4]}
 # label: (threads, stream_chunk, stream_nib, tiles_per_slot)
 VARIANTS = {"default": (0, -1, 0, 0), "wave1k_nib": (64, 1, 1, 128), "wave1k_bytes": (64, 1, 0, 128),
             "wg4k_nib": (256, 1, 1, 32), "default_nib": (0, -1, 1, 0), "wave1k_nib_tps512": (64, 1, 1, 512)}
+if len(sys.argv) > 2 and sys.argv[2] == "chunk":  # one workgroup per 1 / 2 / 4 tiles only, more rounds
+    VARIANTS = {"default": (0, -1, 0, 0), "chunk1": (0, 1, 0, 0), "chunk2": (0, 2, 0, 0), "chunk4": (0, 4, 0, 0)}
+elif len(sys.argv) > 1 and sys.argv[1] == "c2":
+    VARIANTS = {"default": (0, -1, 0, 0), "wave1k_nib": (64, 1, 1, 0), "wave1k_bytes": (64, 1, 0, 0),
+                "wave2k_bytes": (128, 1, 0, 0), "wg4k_bytes": (256, 1, 0, 0), "default_nib": (0, -1, 1, 0)}
 
 
 def set_variant(d, v):
@@ -41,7 +49,7 @@ def timed(fn, st, n=14, skip=4):
     return statistics.median(ev[i].elapsed_ms(ev[i + 1]) for i in range(skip, n))
 
 
-def main(rounds=3):
+def main(rounds=5 if len(sys.argv) > 2 else 3):
     d = _lib.dev()
     st = D.Stream()
     lay = D.Layout.alloc(K + M, F, S)
@@ -75,7 +83,7 @@ def main(rounds=3):
                 res.setdefault((name, op), []).append(timed(lambda: run(op), st))
     for (name, op), ts in res.items():
         ms = statistics.median(ts)
-        print(json.dumps({"variant": name, "op": op, "ms": round(ms, 4),
+        print(json.dumps({"shape": f"k{K}m{M}", "variant": name, "op": op, "ms": round(ms, 4),
                           "frac": round(algo / (ms * 1e-3) / 8e12, 4)}), flush=True)
     set_variant(d, (0, -1, 0, 0))
 
