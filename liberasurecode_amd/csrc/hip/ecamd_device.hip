@@ -223,7 +223,11 @@ struct Tuning {
                             //   dispatcher balancing them, as bs_grid), 0: grid-stride over the
                             //   slots; -1 (default): 2 when the tables are at most 8 KiB (C2 encode
                             //   0.783 -> 0.803 of 8 TB/s), else 0 -- a workgroup per range reloads
-                            //   the tables (C3's 40 KiB: 0.739 -> 0.64-0.69, tools/stream_chunk_ab.py)
+                            //   the tables (C3's 40 KiB: 0.739 -> 0.64-0.69, tools/stream_chunk_ab.py);
+                            //   1 instead of 2 when the outputs are not consecutive fragments (C2's
+                            //   mixed decode {0,4}: 0.721 -> 0.764, while encode / {0,1} lose 0.5-0.8%
+                            //   with 1, tools/c3_tile_ab.py c2 chunk, profiles/r03_c2_chunk_ab.log;
+                            //   the policy in place: mixed 0.718 -> 0.768, r03_c2_chunk_ab2.log)
     Knob stream_nib{0};     //   nibble tables: 0 never, 1 always, 2 for 8-output passes only
     Knob stream_pf{0};      //   next group's loads issued before the lookups (1) or after (0);
                             //   0 measured faster at C2 / C3 / C5 (tools/stream_sweep.py)
@@ -538,6 +542,28 @@ int for_each_launch(const ApplyArgs& a, int nstripes, uint64_t tiles_per_stripe,
     return 0;
 }
 
+// True when the output fragments of a pass are one run of consecutive slots (an encode's parity, a
+// decode of adjacent fragments) -- the write pattern the 2-tile ranges suit.  The slot spacing is the
+// smallest distance between any two fragments the pass touches (inputs and outputs).
+bool outputs_consecutive(const ApplyArgs& a, int64_t bs)
+{
+    if (a.nrows <= 1) return true;
+    std::vector<int64_t> offs;
+    for (int j = 0; j < a.ncols; j++) offs.push_back(a.in_off[j]);
+    for (int r = 0; r < a.nrows; r++) offs.push_back(a.out_off[r]);
+    std::sort(offs.begin(), offs.end());
+    int64_t slot = INT64_MAX;
+    for (size_t i = 1; i < offs.size(); i++)
+        if (offs[i] > offs[i - 1]) slot = std::min(slot, offs[i] - offs[i - 1]);
+    if (slot == INT64_MAX || slot < bs) return false;
+    int64_t lo = a.out_off[0], hi = a.out_off[0];
+    for (int r = 1; r < a.nrows; r++) {
+        lo = std::min(lo, a.out_off[r]);
+        hi = std::max(hi, a.out_off[r]);
+    }
+    return hi - lo == slot * (a.nrows - 1);
+}
+
 int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch, bool nib,
                        int64_t bs, int nstripes, hipStream_t st)
 {
@@ -557,7 +583,8 @@ int launch_stream_pass(ApplyArgs a, int dev, size_t lds_bytes, int width, int ch
         c.tiles_per_stripe = h.tiles_per_stripe;
         c.tile_order = g_tune.stream_order;
         int grid = h.grid;
-        const int chunk = g_tune.stream_chunk >= 0 ? g_tune.stream_chunk : (h.lds <= 8192 ? 2 : 0);
+        int chunk = g_tune.stream_chunk;
+        if (chunk < 0) chunk = h.lds <= 8192 ? (outputs_consecutive(c, bs) ? 2 : 1) : 0;
         if (chunk > 0) {  // contiguous ranges of `chunk` tiles, one per workgroup
             const uint64_t per = static_cast<uint64_t>(chunk);
             grid = static_cast<int>(std::min<uint64_t>((h.ntiles + per - 1) / per, 1u << 30));
