@@ -82,9 +82,9 @@ int ecamd_fragments_needed_batch(int backend, int k, int m, int hd, const int *r
  * every one of ndev visible devices, or the comma-separated subset named by spec (the
  * ECAMD_PERCALL_DEVICES environment variable; NULL or "" = all; out-of-range or repeated ids are
  * dropped, and a spec naming none of them means all).  Writes up to max ids to devs, returns the
- * count.  Call n of a process goes to devs[n % count] -- except with the spec "current", where
- * every call runs on the caller's current device (one process per GPU: liberasurecode_amd/shard.py
- * sets it for its ranks). */
+ * count.  Call n of a process goes to devs[n % count].  One process per GPU names its device
+ * ("3": liberasurecode_amd/shard.py does so for its ranks); the spec "current" (not parsed here)
+ * makes the per-call path use the device current on the thread of its first call, resolved once. */
 int ecamd_percall_device_plan(int ndev, const char *spec, int *devs, int max);
 
 /* Host copies of one per-call request (host/copy_pool.cpp): dst[i] <- src[i], len[i] bytes, i < n,

@@ -62,7 +62,8 @@ uint32_t zcrc(const void* p, size_t n)
 // handed out again to a request of between half its size and its size, so the next call writes
 // into pages that are already mapped instead of faulting fresh ones in (a copy into fresh pages
 // runs at ~40% of a copy into mapped ones).  Every buffer is an ordinary posix_memalign block: a
-// caller that free()s one directly just returns it to libc.
+// caller that free()s one directly just returns it to libc (the reference's own tests do,
+// test/liberasurecode_test.c:1110); the address's record is refreshed by every later allocation.
 class BufferPool {
 public:
     void* get(size_t n)
@@ -84,10 +85,17 @@ public:
         }
         void* p = nullptr;
         if (posix_memalign(&p, 16, n ? n : 1) != 0) return nullptr;
-        if (n >= kMin && limit() > 0) {
+        // Every fresh block refreshes its address's record: a pooled block the caller free()d
+        // directly may come back from libc at the same address for a smaller request, and must
+        // then never be recycled as the large block it once was.
+        if (limit() > 0) {
             std::lock_guard<std::mutex> lk(mu_);
-            if (caps_.size() > 65536) caps_.clear();  // callers free()d many directly: forget them
-            caps_[p] = n;
+            if (n >= kMin) {
+                if (caps_.size() > 65536) caps_.clear();  // callers free()d many directly: forget them
+                caps_[p] = n;
+            } else if (!caps_.empty()) {
+                caps_.erase(p);
+            }
         }
         return p;
     }

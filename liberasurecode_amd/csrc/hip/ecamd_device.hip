@@ -544,12 +544,18 @@ int for_each_launch(const ApplyArgs& a, int nstripes, uint64_t tiles_per_stripe,
 
 // True when the output fragments of a pass are one run of consecutive slots (an encode's parity, a
 // decode of adjacent fragments) -- the write pattern the 2-tile ranges suit.  The slot spacing is the
-// smallest distance between any two fragments the pass touches (inputs and outputs).
+// smallest distance between any two fragments the pass touches (inputs and outputs) when both live
+// in one layout; a copy-through pass reads objects (in_base != out_base), so its inputs count by the
+// payload slots they are copied to when those share the outputs' layout, else only its outputs.
 bool outputs_consecutive(const ApplyArgs& a, int64_t bs)
 {
     if (a.nrows <= 1) return true;
     std::vector<int64_t> offs;
-    for (int j = 0; j < a.ncols; j++) offs.push_back(a.in_off[j]);
+    if (a.in_base == a.out_base && a.in_stride == a.out_stride)
+        for (int j = 0; j < a.ncols; j++) offs.push_back(a.in_off[j]);
+    else if (a.copy_records && a.copy_base == a.out_base && a.copy_stride == a.out_stride)
+        for (int j = 0; j < a.ncols; j++)  // the inputs' payload slots, beside the outputs
+            if (a.copy_off[j] >= 0) offs.push_back(a.copy_off[j]);
     for (int r = 0; r < a.nrows; r++) offs.push_back(a.out_off[r]);
     std::sort(offs.begin(), offs.end());
     int64_t slot = INT64_MAX;
@@ -1039,7 +1045,29 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         }
         for (int r = 0; r < map->R; r++) b.min_len = std::min(b.min_len, len_of(out_len, r));
         b.limited = b.min_len < bs ? 1 : 0;
+        // The bitsliced kernel covers whole 16 KiB tiles only; the rest of each fragment must then
+        // run on the stream kernel (the pointer-free LDS-table kernels cannot start at an offset).
+        // A row group whose passes cannot all take it (more than 20 inputs per pass, offsets past
+        // 2 GiB) skips the bitsliced kernel instead of failing after writing part of the output.
+        const int64_t cover = (b.limited ? std::min<int64_t>(bs, b.min_len) : bs) / kBsTile * kBsTile;
+        auto tail_on_stream = [&](int g) {
+            for (const auto& p : map->passes) {
+                if (p.row0 / 8 != g) continue;
+                if (p.ncols > 4 * kStreamGroups) return false;
+                ApplyArgs t{};
+                t.ncols = p.ncols;
+                t.nrows = std::min(p.width, map->R - p.row0);
+                for (int j = 0; j < p.ncols; j++) {
+                    t.in_off[j] = in_off[p.col0 + j];
+                    t.copy_off[j] = copy_off[p.col0 + j];
+                }
+                for (int r = 0; r < t.nrows; r++) t.out_off[r] = out_off[p.row0 + r];
+                if (!stream_offsets(t, bs) || (p.row0 == 0 && !stream_copy_offsets(t, bs))) return false;
+            }
+            return true;
+        };
         for (int g = 0; g * 8 < map->R && g_tune.stream; g++) {
+            if (cover < bs && !tail_on_stream(g)) continue;
             int brc = 0;
             b.copy_records = g == 0 ? 1 : 0;  // (recomputed from copy_off inside)
             bs_done[static_cast<size_t>(g)] =

@@ -473,6 +473,20 @@ int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t 
         int dev = 0;
         (void)hipGetDevice(&dev);
         std::lock_guard<std::mutex> lk(entry->ev_mu);
+        // Callers that create and destroy streams (per-call slots, user streams) would grow the map
+        // for as long as the entry stays cached: drop the events of other streams that completed.
+        if (entry->last_launch.size() >= 8) {
+            for (auto it = entry->last_launch.begin(); it != entry->last_launch.end();) {
+                if (it->first != std::make_pair(dev, st) && it->second &&
+                    hipEventQuery(it->second) == hipSuccess) {
+                    (void)hipEventDestroy(it->second);
+                    it = entry->last_launch.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+            (void)hipGetLastError();
+        }
         hipEvent_t& ev = entry->last_launch[{dev, st}];
         if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
         if (ev) (void)hipEventRecord(ev, st);

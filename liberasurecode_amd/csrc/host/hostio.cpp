@@ -162,16 +162,23 @@ struct Staging {
 std::mutex g_pool_mu;
 std::vector<std::vector<Staging*>> g_pool;  // by device
 
+// ECAMD_PERCALL_DEVICES: device indices ("3", "0,2,4"), or "current" -- the device current on the
+// thread whose call builds the plan, resolved ONCE: a worker thread that never selected a device
+// would otherwise report device 0 and send a rank's calls to another rank's GPU (shard.py passes
+// the rank's index explicitly).
 struct DevicePlan {
     std::vector<int> devs;
-    bool current = false;  // ECAMD_PERCALL_DEVICES=current: the caller's current device
     std::atomic<unsigned> next{0};
     DevicePlan()
     {
         const int n = ecamd_device_count();
         if (n <= 0) return;
         const char* spec = std::getenv("ECAMD_PERCALL_DEVICES");
-        current = spec && std::strcmp(spec, "current") == 0;
+        int cur = -1;
+        if (spec && std::strcmp(spec, "current") == 0 && ecamd_get_device(&cur) == 0 && cur >= 0 && cur < n) {
+            devs.assign(1, cur);
+            return;
+        }
         devs.resize(static_cast<size_t>(n));
         devs.resize(static_cast<size_t>(ecamd_percall_device_plan(n, spec, devs.data(), n)));
     }
@@ -181,8 +188,6 @@ int pick_device()
 {
     static DevicePlan plan;  // thread-safe one-time initialisation
     if (plan.devs.empty()) return -1;
-    int cur = -1;
-    if (plan.current && ecamd_get_device(&cur) == 0 && cur >= 0) return cur;
     return plan.devs[plan.next.fetch_add(1, std::memory_order_relaxed) % plan.devs.size()];
 }
 

@@ -38,6 +38,14 @@ def split_range(rank: int, world: int, total: int):
     return first, base + (1 if rank < extra else 0)
 
 
+def percall_devices_spec(device):
+    """ECAMD_PERCALL_DEVICES value that pins a rank's per-call host-buffer path (hostio.cpp) to
+    its own GPU: the device index itself."""
+    if device is None or int(device) < 0:
+        raise ValueError("a rank without a GPU has no per-call device")
+    return str(int(device))
+
+
 class DeviceCollision(RuntimeError):
     """Two ranks of one host were placed on the same GPU."""
 
@@ -123,8 +131,10 @@ class Coordinator:
             ident = {"device": self.device, "pci_domain": int(p.pci_domain_id),
                      "pci_bus": int(p.pci_bus_id), "pci_device": int(p.pci_device_id),
                      "device_count": ndev, "name": p.name}
-            # the per-call host-buffer path (hostio.cpp) stays on this rank's GPU
-            os.environ.setdefault("ECAMD_PERCALL_DEVICES", "current")
+            # the per-call host-buffer path (hostio.cpp) stays on this rank's GPU, whichever
+            # thread of the rank calls it (an explicit index: a worker thread's current device
+            # would be device 0)
+            os.environ.setdefault("ECAMD_PERCALL_DEVICES", percall_devices_spec(self.device))
         fake = _fake_identity(self.local, self.world)
         if fake is not None:
             ident = fake

@@ -39,6 +39,36 @@ def mapped_codecs():
     return sorted(libs)
 
 
+def direct_free(desc, k, m):
+    """Fragments freed with libc free() instead of liberasurecode_encode_cleanup, as the reference's
+    own tests do (test/liberasurecode_test.c:1110, test/libec_slap.c:224,300).  glibc then hands
+    the same addresses to smaller requests; the frontend's recycled-buffer pool must not take such a
+    smaller block for the large one it once was (a later large encode would overflow it).
+    Returns one [round, encode rc, exact round trip] per large encode."""
+    import ctypes as C
+    libc = C.CDLL(None)
+    libc.free.argtypes = [C.c_void_p]
+    res = []
+    for rnd in range(3):
+        big = bytes((j * 7 + rnd * 11 + (j >> 10)) & 0xFF for j in range(k * (96 << 10) + 5))
+        rc, d, p, fl = E.encode(desc, big)
+        fr = E.fragments(d, k, fl) + E.fragments(p, m, fl)
+        ok = rc == 0 and E.decode(desc, fr[1:], fl) == (0, big)
+        res.append([rnd, rc, ok])
+        for i in range(k):
+            libc.free(d[i])
+        for i in range(m):
+            libc.free(p[i])
+        # smaller objects (fragments under the pool's 64 KiB floor) returned through the cleanup
+        for j in range(2 * (k + m)):
+            sm = bytes(((j + 1) * (i + 3)) & 0xFF for i in range(k * (8 << 10) + j))
+            rc2, d2, p2, fl2 = E.encode(desc, sm)
+            fr2 = E.fragments(d2, k, fl2) + E.fragments(p2, m, fl2)
+            E.lib().liberasurecode_encode_cleanup(desc, d2, p2)
+            res.append([rnd, rc2, rc2 == 0 and E.decode(desc, fr2[1:], fl2) == (0, sm)])
+    return res
+
+
 def main():
     name = sys.argv[1]
     ct = int(sys.argv[2]) if len(sys.argv) > 2 else E.CHKSUM_NONE
@@ -94,6 +124,7 @@ def main():
             rc3, sysd = E.decode(desc, fr[:k], fl)
             pool.append([rep, sz, rc, sha(b"".join(fr)), rc2 == 0 and back == o2, rc3 == 0 and sysd == o2])
     out["pool"] = pool
+    out["direct_free"] = direct_free(desc, k, m)
     out["libs"] = mapped_codecs()  # before destroy: the backend library is dlclose()d there
     out["destroy"] = E.lib().liberasurecode_instance_destroy(desc)
     print(json.dumps(out))

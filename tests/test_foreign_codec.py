@@ -67,6 +67,8 @@ def test_frontend_over_reference_codec(name, ct):
     assert all(rc == 0 and dec and sysd for _, _, rc, _, dec, sysd in pool), pool
     half = len(pool) // 2
     assert [x[3] for x in pool[:half]] == [x[3] for x in pool[half:]], "encode digests changed on reuse"
+    df = res["direct_free"]  # fragments free()d directly, then smaller ones recycled (BufferPool)
+    assert df and all(rc == 0 and ok for _, rc, ok in df), [x for x in df if not (x[1] == 0 and x[2])]
     libs = res["libs"]
     assert "oracle/_ref/libXorcode.so.1" in libs, libs  # the frontend's DT_NEEDED, from the reference
     if name == "rs":
@@ -83,5 +85,5 @@ def test_own_codec_matches_reference_codec(name, ct):
     assert own["create"] > 0 and own["encode_rc"] == 0
     assert any("libecamd.so" in x for x in own["libs"]), own["libs"]
     assert own["fragments_sha256"] == ref["fragments_sha256"]
-    for key in ("decode", "reconstruct", "fragments_needed", "pool"):
+    for key in ("decode", "reconstruct", "fragments_needed", "pool", "direct_free"):
         assert own[key] == ref[key], key

@@ -618,6 +618,46 @@ def test_frame_split_stream_matches_first_version(F, name, k, m, hd):
         assert all(out[0][2, i].tobytes() == want[i] for i in range(k + m)), size
 
 
+@pytest.mark.parametrize("k,m,tiles,extra", [(24, 6, 3, 48), (27, 5, 2, 4000), (21, 8, 1, 16), (24, 6, 3, 0)])
+def test_frame_bitsliced_wide_ragged(F, k, m, tiles, extra):
+    """More than 20 inputs (the stream kernel's limit per pass) with payloads that are not whole
+    16 KiB tiles: the bitsliced kernel could cover the whole tiles only, and the table passes of
+    such maps cannot run the remainder on the stream kernel, so the framed encode / decode-join
+    must take the LDS-table kernels for the whole fragment (no error after a partial write).
+    Whole tiles (extra 0) still take the bitsliced kernel (launch counter)."""
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    S = 2
+    bs = tiles * 16384 + extra
+    size = k * bs - 5 if extra else k * bs
+    objs = _objects(S, size, k + m + extra)
+    lost = list(range(0, 2 * m, 2))[:m]
+    try:
+        _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2), "tune")
+        n0 = _bs_launches()
+        fb = F.FrameBatch(be, k, m, size, S, checksum=ec_api.CHKSUM_NONE)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        got = fb.fragments()
+        bad = got.copy()
+        bad[:, lost] = 0x6B
+        fb.upload_fragments(bad)
+        stride = (size + 16 + 15) // 16 * 16
+        d = DeviceBuffer(S * stride)
+        d.upload(np.full(S * stride, 0xA5, dtype=np.uint8))
+        fb.decode(lost, d, obj_stride=stride)
+        joined = d.download().reshape(S, stride)
+        ran = _bs_launches() - n0
+    finally:
+        _lib.dev().ecamd_tune(b"bitslice", 1)
+    for s in range(S):
+        want = expected_stripe(be, k, m, 0, objs[s], ec_api.CHKSUM_NONE)
+        assert all(got[s, i].tobytes() == want[i] for i in range(k + m)), s
+        assert joined[s, :size].tobytes() == objs[s]
+        assert (joined[s, size:] == 0xA5).all()
+    assert (ran > 0) == (extra == 0), ran
+
+
 def _bs_launches():
     import ctypes as C
     from liberasurecode_amd import _lib

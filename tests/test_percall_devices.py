@@ -47,8 +47,21 @@ def test_round_robin_balance():
 
 
 def test_current_spec_plans_every_device():
-    """ECAMD_PERCALL_DEVICES=current: the plan keeps every device (the pool may serve any of
-    them) and each call runs on the caller's current device (hostio.cpp pick_device) -- what
-    liberasurecode_amd/shard.py sets for its one-process-per-GPU ranks."""
+    """ECAMD_PERCALL_DEVICES=current is not a list of ids: the id parser keeps every device;
+    hostio.cpp resolves "current" itself, once, to the device current when the plan is built."""
     assert plan(8, "current") == list(range(8))
+
+
+def test_rank_spec_pins_one_device():
+    """shard.py pins each rank's per-call path to its own GPU with an explicit index (a worker
+    thread of the rank that never selected a device must not fall back to device 0)."""
+    from liberasurecode_amd.shard import percall_devices_spec
+    for dev in range(8):
+        spec = percall_devices_spec(dev)
+        assert plan(8, spec) == [dev]
+        calls = [plan(8, spec)[n % 1] for n in range(16)]
+        assert set(calls) == {dev}
+    import pytest
+    with pytest.raises(ValueError):
+        percall_devices_spec(-1)
 
