@@ -18,8 +18,10 @@ touches the GPU (fresh child processes, no exec) and relays rank 0's line.
 Extra fields: "roofline" (the dominant kernel, HIP-event timed per launch on its launch stream; peak =
 8 TB/s spec, plus a live copy probe; "trace" = the same figure from the committed rocprofv3 kernel
 trace of this command), "cpu_baseline" (the reference codec compiled from its sources -- or the
-oracle restatement when that build is absent -- on the host's usable cores; rank 0 at N=1), and
-"c5" (BASELINE configs[4], k=20 m=8 4 MiB: rebuild of 8 lost fragments, outside the timed steps).
+oracle restatement when that build is absent -- on the host's usable cores; at every N, timed by
+rank 0 after all GPU work while the other ranks wait on a gloo barrier), and "c5" (BASELINE
+configs[4], k=20 m=8 4 MiB: rebuild of 8 lost fragments, outside the timed steps, on every rank at
+once with per-rank figures).
 """
 import argparse
 import json
@@ -37,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # second decode pattern per config, data and parity mixed
 MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}
 GIB = float(1 << 30)
-ROUND = "r03"  # profiles/<round>_* written by tools/gpu_prof.sh for this bench
+ROUND = "r04"  # profiles/<round>_* written by tools/gpu_prof.sh for this bench
 
 CONFIGS = {
     # name: (k, m, fragment bytes, stripes per GPU, decode erasures, description)
@@ -48,6 +50,8 @@ CONFIGS = {
     "c5": (20, 8, 4 << 20, 32, list(range(8)),
            "C5 liberasurecode_rs_vand k=20 m=8, 4 MiB fragments, encode + decode(8 data missing)"),
 }
+# c5 fields gathered from every rank (the rest of the c5 object is rank 0's)
+C5_PER_RANK = ("encode_frac", "rebuild8_data_frac", "rebuild8_mixed_frac", "reconstruct_x8_gibs")
 STRONG_TOTAL = 2048  # C4 strong scaling, 2048 C3 stripes over all GPUs
 
 
@@ -421,6 +425,22 @@ def peer_scatter(D, stream, home, ndev, S=8, reps=5):
         lay.buf.free()
 
 
+def rank0_cpu_baseline(co, args, k, m, F, missing):
+    """The host-CPU baseline at every N (north_star: "from the same run"): rank 0 times it after
+    every GPU measurement of the run, while the other ranks wait on a gloo barrier (blocked in a
+    socket read, not spinning on a core).  Returns rank 0's figure (None elsewhere / when off)."""
+    if args.no_cpu_baseline:
+        return None
+    co.cpu_barrier()  # every rank is done with the GPU
+    out = None
+    if co.rank == 0:
+        usable = usable_cores()[0]
+        out = cpu_baseline(k, m, F, missing, args.cpu_threads or usable, args.cpu_seconds)
+        out["ranks_idle"] = co.world - 1
+    co.cpu_barrier()
+    return out
+
+
 # ------------------------------------------------------------------ main ----
 
 def main():
@@ -461,16 +481,17 @@ def main():
 
     if args.dry_run:
         co.barrier()
+        per_rank_stripes = [int(x) for x in co.per_rank(S)]
+        cpu = rank0_cpu_baseline(co, args, k, m, F, missing)
         if rank == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": ranks_seen,
-                              "scaling": args.scaling, "total_stripes": total_stripes,
-                              "stripes_per_rank": [int(x) for x in co.reduce(
-                                  [float(S) if r == rank else 0.0 for r in range(world)], "sum")],
-                              "covered_once": True, "coord_backend": co.coord_backend,
-                              "devices": co.devices, "shared_devices": co.shared_devices}),
-                  flush=True)
-        else:
-            co.reduce([float(S) if r == rank else 0.0 for r in range(world)], "sum")
+            line = {"dry_run": True, "n_gpus": world, "ranks_seen": ranks_seen,
+                    "scaling": args.scaling, "total_stripes": total_stripes,
+                    "stripes_per_rank": per_rank_stripes,
+                    "covered_once": True, "coord_backend": co.coord_backend,
+                    "devices": co.devices, "shared_devices": co.shared_devices}
+            if cpu is not None:
+                line["cpu_baseline"] = cpu
+            print(json.dumps(line), flush=True)
         co.close()
         return
 
@@ -546,6 +567,7 @@ def main():
     # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2 // per_pass
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+    per_rank_launch_ms = co.per_rank(launch_ms)
     bitsliced = width == 8 and _lib.dev().ecamd_bitslice_available()
     kernel = ("ecamd_bs_kernel" if bitsliced else f"gf16_hybrid_kernel<{(k + 3) // 4}>" if width == 8 else
               f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>")
@@ -581,9 +603,8 @@ def main():
         trace_match = (summ is not None and summ.get("config") == args.config and
                        prof_world == world and prof_stripes == S and args.scaling == "weak")
         kd = kernel_entry(summ, kernel) or {}
-        traffic = kd.get("hbm_bytes_per_launch")
-        if traffic is not None and S != prof_stripes:
-            traffic = int(traffic * S / prof_stripes)  # profile ran at its own S
+        # PMC traffic is a measurement of the profiled command only: quoted for a run of that shape
+        traffic = kd.get("hbm_bytes_per_launch") if trace_match else None
         trace = None if trace_match else {
             "omitted": f"{summ_src} profiles config={(summ or {}).get('config')} "
                        f"gpus={prof_world} stripes={prof_stripes}, not this run"}
@@ -634,31 +655,47 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kernel,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": summ_src,
+                         "traffic_source": (summ_src if trace_match else
+                                            "none: the committed PMC profile is of another run shape "
+                                            "(see trace.omitted)"),
                          "launch_ms": round(launch_ms, 4),
+                         "per_rank_launch_ms": [round(x, 4) for x in per_rank_launch_ms],
+                         "per_rank_frac": [round(algo_bytes / (x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                           for x in per_rank_launch_ms],
                          "dispatches_per_pass": per_pass,
                          "encode_pass_ms": round(sum(enc_ms) / len(enc_ms), 4),
                          "decode_pass_ms": round(sum(dec_ms) / len(dec_ms), 4),
                          "copy_peak_measured": round(copy_gbs, 1),
+                         "copy_peak_rank": 0,
                          "copy_probes": copy_probes,
                          "frac_of_measured_copy": round(achieved / copy_gbs, 4),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "trace": trace},
         }
     lay.buf.free()
+    # C5 (BASELINE configs[4]) on every rank at once, after one barrier: each GPU rebuilds its own
+    # 32 stripes under the same concurrent load as the timed steps
+    if not args.no_c5 and args.config == "c3":
+        co.barrier()
+        c5 = c5_rebuild(D, stream)
+        per_rank_c5 = {key: co.per_rank(c5[key]) for key in C5_PER_RANK}
+        if rank == 0:
+            c5["ranks"] = f"all {world} ranks at once" if world > 1 else "one rank"
+            c5["per_rank"] = {key: [round(x, 4) for x in v] for key, v in per_rank_c5.items()}
+            out["c5"] = c5
+    co.barrier()
     if rank == 0:
-        if not args.no_c5 and args.config == "c3":
-            out["c5"] = c5_rebuild(D, stream)
         ndev = torch.cuda.device_count()
         if world > 1 and not args.no_scatter:  # (one visible GPU: the all-local rehearsal)
             try:
                 out["peer_scatter"] = peer_scatter(D, stream, co.device or 0, ndev)
             except Exception as e:  # evidence only: never costs the bench line
                 out["peer_scatter"] = {"error": str(e)[:300]}
-        if not args.no_cpu_baseline and world == 1:
-            usable = usable_cores()[0]
-            out["cpu_baseline"] = cpu_baseline(k, m, F, missing, args.cpu_threads or usable,
-                                               args.cpu_seconds)
+    torch.cuda.synchronize()
+    cpu = rank0_cpu_baseline(co, args, k, m, F, missing)
+    if rank == 0:
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     co.barrier()
     co.close()

@@ -844,7 +844,8 @@ ec_backend_t liberasurecode_backend_instance_get_by_desc(int desc) { return find
 
 int liberasurecode_backend_available(const ec_backend_id_t backend_id)
 {
-    if (backend_id >= EC_BACKENDS_MAX) return 0;
+    // the reference's C enum compares unsigned (gcc), so negative ids are out of range too
+    if (static_cast<unsigned>(backend_id) >= EC_BACKENDS_MAX) return 0;
     void* so = open_backend(kBackends[backend_id]);
     if (!so) return 0;
     dlclose(so);
@@ -854,7 +855,9 @@ int liberasurecode_backend_available(const ec_backend_id_t backend_id)
 int liberasurecode_instance_create(const ec_backend_id_t id, struct ec_args* args)
 {
     if (!args) return -EINVALIDPARAMS;
-    if (id >= EC_BACKENDS_MAX) return -EBACKENDNOTSUPP;
+    // unsigned as in the reference's C (gcc gives ec_backend_id_t an unsigned type): -1 is
+    // -EBACKENDNOTSUPP there (test/liberasurecode_test.c:630-631), not an index below the table
+    if (static_cast<unsigned>(id) >= EC_BACKENDS_MAX) return -EBACKENDNOTSUPP;
     if (args->k < 0 || args->m < 0) return -EINVALIDPARAMS;
     if (args->k + args->m > EC_MAX_FRAGMENTS) {
         LOGE("Total number of fragments (k + m) must be less than %d\n", EC_MAX_FRAGMENTS);

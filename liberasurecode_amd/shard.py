@@ -228,6 +228,20 @@ class Coordinator:
         else:
             self.dist.barrier()
 
+    def cpu_barrier(self):
+        """Barrier over gloo (a CPU tensor, also under "cpu:gloo,cuda:nccl"): ranks waiting here
+        block in a socket read rather than in a GPU synchronize, e.g. while rank 0 times the
+        host-CPU baseline on the cores they share."""
+        if self.world == 1:
+            return
+        t = self.torch.zeros(1, dtype=self.torch.float64)
+        self.dist.all_reduce(t)
+
+    def per_rank(self, value):
+        """Every rank's `value` (a float), in rank order, on every rank."""
+        v = [float(value) if r == self.rank else 0.0 for r in range(self.world)]
+        return self.reduce(v, op="sum")
+
     def reduce(self, values, op="max"):
         """All-reduce a list of floats (max or sum); identity when world == 1."""
         values = list(values)

@@ -62,6 +62,43 @@ def test_rs_vand_exports_exactly_reference_symbols():
     assert declared("liberasurecode_rs_vand.h") == REF_RS_VAND_SYMS
 
 
+# liberasurecode.sym:1-28 of the reference: the frontend's export contract
+REF_LIBERASURECODE_SYMS = sorted("""alloc_and_set_buffer get_backend_id get_backend_version
+get_data_ptr_from_fragment get_fragment_partition get_libec_version is_invalid_fragment
+is_invalid_fragment_header liberasurecode_backend_available liberasurecode_backend_instance_get_by_desc
+liberasurecode_crc32_alt liberasurecode_decode liberasurecode_decode_cleanup liberasurecode_encode
+liberasurecode_encode_cleanup liberasurecode_exit liberasurecode_fragments_needed
+liberasurecode_get_aligned_data_size liberasurecode_get_fragment_metadata liberasurecode_get_fragment_size
+liberasurecode_get_minimum_encode_size liberasurecode_get_version liberasurecode_init
+liberasurecode_instance_create liberasurecode_instance_destroy liberasurecode_reconstruct_fragment
+liberasurecode_verify_fragment_metadata liberasurecode_verify_stripe_metadata""".split())
+
+SYM_FILES = {"liberasurecode.so.1": ("liberasurecode.sym", REF_LIBERASURECODE_SYMS),
+             "liberasurecode_rs_vand.so.1": ("liberasurecode_rs_vand.sym", REF_RS_VAND_SYMS),
+             "libXorcode.so.1": ("libXorcode.sym", REF_XORCODE_SYMS)}
+
+
+def check_symbols_get(path):
+    """check-symbols.sh:15-21 get(): `nm --dynamic --defined-only | cut -c18- | LC_COLLATE=C sort`
+    -- every defined dynamic symbol with its type letter, so data symbols or linker extras would
+    show up too."""
+    out = subprocess.run(["nm", "--dynamic", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    return sorted((l[17:] for l in out.splitlines() if l.strip()), key=lambda x: x.encode())
+
+
+@pytest.mark.parametrize("lib", sorted(SYM_FILES))
+def test_check_symbols_contract(lib):
+    """The reference CI's symbol gate (check-symbols.sh check, :23-28) applied to the drop-ins:
+    the listing equals the reference's .sym file line for line ("T name" x 28 / 13 / 5)."""
+    sym, names = SYM_FILES[lib]
+    want = ["T " + n for n in sorted(names, key=lambda x: x.encode())]
+    assert check_symbols_get(os.path.join(LIB, lib)) == want
+    ref = os.path.join("/root/reference", sym)
+    if os.path.exists(ref):  # the build container: the embedded list is the reference's file
+        assert [l for l in open(ref).read().splitlines() if l.strip()] == want
+
+
 def test_soname():
     out = subprocess.run(["readelf", "-d", os.path.join(LIB, "liberasurecode_rs_vand.so.1")],
                          capture_output=True, text=True, check=True).stdout

@@ -27,13 +27,25 @@ def run_bench(*args, env=None):
                                                     (2, "strong", [1024, 1024]),
                                                     (3, "strong", [683, 683, 682])])
 def test_launcher_starts_ranks_and_covers_every_stripe(gpus, scaling, per_rank):
-    r = run_bench("--gpus", str(gpus), "--dry-run", "--scaling", scaling)
+    r = run_bench("--gpus", str(gpus), "--dry-run", "--scaling", scaling, "--cpu-seconds", "0.2")
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["dry_run"] and line["covered_once"]
     assert line["n_gpus"] == gpus and line["ranks_seen"] == gpus
     assert line["stripes_per_rank"] == per_rank
     assert line["total_stripes"] == sum(per_rank)
+    # north_star: the host-CPU baseline "from the same run" at every GPU count -- rank 0 times it
+    # while the other ranks wait on a gloo barrier
+    cpu = line["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] in ("reference", "port")
+    assert cpu["ranks_idle"] == gpus - 1
+    assert "k=10 m=4" in cpu["sample"]
+
+
+def test_dry_run_without_cpu_baseline():
+    r = run_bench("--gpus", "2", "--dry-run", "--no-cpu-baseline")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "cpu_baseline" not in json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def test_mismatched_world_fails_loudly():
@@ -43,10 +55,11 @@ def test_mismatched_world_fails_loudly():
 
 
 def test_single_rank_dry_run():
-    r = run_bench("--dry-run")
+    r = run_bench("--dry-run", "--cpu-seconds", "0.2")
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1 and line["stripes_per_rank"] == [256]
+    assert line["cpu_baseline"]["ranks_idle"] == 0
 
 
 @pytest.mark.parametrize("k,width,F,S,cus,want", [
@@ -77,7 +90,7 @@ def test_ranks_sharing_a_gpu_fail_loudly():
 
 
 def test_distinct_devices_reported():
-    r = run_bench("--gpus", "2", "--dry-run",
+    r = run_bench("--gpus", "2", "--dry-run", "--no-cpu-baseline",
                   env={"ECAMD_FAKE_DEVICES": "0,1", "ECAMD_FAKE_DEVICE_COUNT": "8"})
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
