@@ -510,6 +510,15 @@ def main():
     D.rs_encode(k, m, lay, stream=stream)
     D.rs_decode(k, m, missing, lay, stream=stream)
     stream.synchronize()
+    # which kernel a pass runs, and in how many launches: the run-time compiled bitsliced kernel
+    # (3-4 outputs in one-wave 4 KiB tiles, 5-8 in 16 KiB tiles) counts its launches
+    import ctypes
+    bs_count = _lib.dev().ecamd_bitslice_launches
+    bs_count.restype = ctypes.c_longlong
+    n0 = bs_count()
+    D.rs_encode(k, m, lay, stream=stream)
+    stream.synchronize()
+    bs_per_pass = bs_count() - n0
 
     ev = [(D.Event(), D.Event(), D.Event()) for _ in range(args.steps)]
 
@@ -560,7 +569,8 @@ def main():
     # dominant kernel: the stream kernel (C3 encode and decode: 10 in, 4 out per launch); a pass
     # (one rs_encode / rs_decode call) may run as several launches of it, see dispatches_per_pass
     width = 2 if max(m, len(missing)) <= 2 else (4 if max(m, len(missing)) <= 4 else 8)
-    per_pass = dispatches_per_pass(k, width, F, S, torch.cuda.get_device_properties(
+    bitsliced = bs_per_pass > 0
+    per_pass = bs_per_pass if bitsliced else dispatches_per_pass(k, width, F, S, torch.cuda.get_device_properties(
         torch.cuda.current_device()).multi_processor_count)
     pass_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
     launch_ms = pass_ms / per_pass  # HIP events bracket whole passes: gaps between launches count
@@ -568,9 +578,10 @@ def main():
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2 // per_pass
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     per_rank_launch_ms = co.per_rank(launch_ms)
-    bitsliced = width == 8 and _lib.dev().ecamd_bitslice_available()
     kernel = ("ecamd_bs_kernel" if bitsliced else f"gf16_hybrid_kernel<{(k + 3) // 4}>" if width == 8 else
               f"gf16_stream_kernel<{width}, {(k + 3) // 4}, 1, false, false>")
+    kernel_form = (("bitsliced, one-wave 4 KiB tiles" if width <= 4 else "bitsliced, 16 KiB tiles")
+                   if bitsliced else "LDS split tables")
 
     # The survey's second decode pattern per config, outside the timed steps:
     # erasures mixing data and parity.  Every rank decodes its own shard at once (as in the timed
@@ -652,7 +663,7 @@ def main():
             "coord_backend": co.coord_backend,
             "devices": co.devices,
             "shared_devices": co.shared_devices,
-            "roofline": {"bound": "hbm", "kernel": kernel,
+            "roofline": {"bound": "hbm", "kernel": kernel, "kernel_form": kernel_form,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": (summ_src if trace_match else

@@ -14,6 +14,7 @@
 #include <syslog.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -721,6 +722,79 @@ int prepare_decode(int k, int m, char** data, char** parity, const int* missing,
     return 0;
 }
 
+// ECAMD_FRONTEND_DECODE_DIRECT=0 turns decode_direct off (A/B runs, tools/percall_ab.py).
+bool decode_direct_on()
+{
+    static const bool on = [] {
+        const char* f = getenv("ECAMD_FRONTEND_DECODE_DIRECT");
+        return !(f && f[0] == '0');
+    }();
+    return on;
+}
+
+// liberasurecode_decode straight into the object, in front of this repo's rs_vand codec only: the
+// rebuilt data payloads are written by the codec (its staging unpack) at their places in the
+// decoded object, and only the surviving data payloads are copied there.  The reference allocates a
+// fragment per missing index, rebuilds the missing parity too (the shim's rebuild_parity = 1,
+// src/backends/rs_vand/liberasurecode_rs_vand.c:100-101, discarded by a decode) and concatenates
+// every data payload afterwards (fragments_to_string, erasurecode_preprocessing.c:269-370): two
+// host passes over the rebuilt bytes and a device pass over unneeded parity.  Same bytes out, same
+// error codes.  Returns 1 (nothing done) when the surviving data fragments disagree on size or
+// orig_data_size -- the general path then handles them exactly as the reference does.
+int decode_direct(ec_backend* be, char** data, char** parity, int* missing, char** out,
+                  uint64_t* out_len)
+{
+    auto* r = static_cast<RsDesc*>(be->desc.backend_desc);
+    const int k = r->k, m = r->m;
+    bool gone[EC_MAX_FRAGMENTS] = {};
+    for (int i = 0; missing[i] >= 0; i++) gone[missing[i]] = true;
+    int orig = -1, bs = -1;
+    for (int i = 0; i < k + m && orig < 0; i++) {  // prepare_decode's first surviving fragment
+        char* f = i < k ? data[i] : parity[i - k];
+        if (gone[i] || !f) continue;
+        orig = frag_orig_size(f);
+        if (orig < 0) return -EBADHEADER;
+        bs = frag_size(f);
+        if (bs < 0) return -EBADHEADER;
+    }
+    if (orig < 0) return 1;
+    for (int i = 0; i < k; i++)
+        if (!gone[i] && data[i] && (frag_size(data[i]) != bs || frag_orig_size(data[i]) != orig)) return 1;
+    const int64_t span = static_cast<int64_t>(k) * bs;
+    const size_t cap = static_cast<size_t>(std::max<int64_t>(orig, span));
+    char* obj = static_cast<char*>(buf_alloc(cap ? cap : 1));
+    if (!obj) return -ENOMEM;
+    std::vector<char*> dp(k), pp(m, nullptr);  // missing parity: not rebuilt, never touched
+    for (int i = 0; i < k; i++) dp[i] = gone[i] ? obj + static_cast<int64_t>(i) * bs : payload(data[i]);
+    for (int i = 0; i < m; i++)
+        if (!gone[k + i]) pp[i] = payload(parity[i]);
+    int rc = 0;
+    {
+        ExecCheck ex(r->hooks);
+        rc = r->decode(r->matrix, dp.data(), pp.data(), k, m, missing, bs, 0);
+        if (ex.failed()) {
+            buf_free(obj);
+            LOGE("Encountered error in backend decode function!");
+            return -EIO;
+        }
+    }
+    CopyBatch cb;
+    for (int i = 0; i < k; i++) {
+        const int64_t off = static_cast<int64_t>(i) * bs;
+        const int64_t take = std::min<int64_t>(bs, orig - off);
+        if (take <= 0) break;
+        if (!gone[i])
+            cb.add(obj + off, payload(data[i]), take);
+        else if (rc != 0)  // the codec refused (more than m missing): the zeroed slots of the reference
+            std::memset(obj + off, 0, static_cast<size_t>(take));
+    }
+    cb.run(&r->hooks);
+    if (orig > span) std::memset(obj + span, 0, static_cast<size_t>(orig - span));
+    *out = obj;
+    *out_len = static_cast<uint64_t>(orig);
+    return 0;
+}
+
 // is_invalid_fragment_metadata (erasurecode.c:1156-1187), caller holds the read lock
 int check_metadata(int desc, fragment_metadata_t* md)
 {
@@ -1081,6 +1155,10 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
                                      parity.data(), missing.data());
     int orig = 0, bs = 0;
     const bool realign = !(be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND && hooks_of(be).ours());
+    if (ret == 0 && !realign && !zero_all() && decode_direct_on()) {
+        const int d = decode_direct(be, data.data(), parity.data(), missing.data(), out_data, out_data_len);
+        if (d <= 0) return d;  // else irregular fragments: the general path below
+    }
     if (ret == 0)
         ret = prepare_decode(k, m, data.data(), parity.data(), missing.data(), &orig, &bs,
                              fragment_len, owned, realign);

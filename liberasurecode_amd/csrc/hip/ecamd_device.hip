@@ -241,6 +241,9 @@ struct Tuning {
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
+    Knob frame_copy_dpp{0};       // framed split / join stream kernels, realigning path (bs % 16 != 0): 1 =
+                                  //   each lane's second aligned chunk from its neighbour lane (DPP
+                                  //   wave_shl:1), one load per lane; 0 = two loads per lane
     Knob frame_copy_threads{0};   // framed split / join stream kernels: lanes per tile (64 / 128 / 256; 0 = by
                                   //   shape: 64 for 16-byte-multiple payloads, else 256, ecamd_frame_api.hip)
     Knob frame_copy_u{0};         //   and 16-byte chunks per lane (1 / 4; 0 = 1)
@@ -256,6 +259,16 @@ struct Tuning {
                                   //   64 KiB 0.7-3.5% slower, 4 KiB fragments 2% slower (two runs,
                                   //   tools/xor_threads_ab.py, profiles/r03_xor_threads_ab1.log, _ab2.log)
     Knob xor_grid{1};             // xor_stream_kernel: 1 = one workgroup per tile, 0 = resident slots
+    Knob bs_wave{1};              // ecamd_bs_kernel in one-wave workgroups of 4 KiB tiles (64 lanes x 4
+                                  //   chunks 1 KiB apart, built with a 2-wave register budget) instead of
+                                  //   4-wave 16 KiB tiles: 1 (default) row groups of bs_wave_min_rows..4
+                                  //   outputs take it (below bitslice_min_rows); 2 every bitsliced launch
+                                  //   too (5..8 outputs: slower, C5 rebuild 0.738 -> 0.690); 0 never.
+                                  //   Plain maps only (not copy-through / crc).  C3, three interleaved
+                                  //   rounds (tools/bs_wave_ab.py, profiles/r04_bs_wave_ab1.log): encode
+                                  //   0.733 -> 0.746, decode {0,1,2,3} 0.734 -> 0.742, mixed {0,5,10,13}
+                                  //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
+    Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (2..4)
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
@@ -289,6 +302,7 @@ int dev_tune(const char* key)
     if (k == "crc_bits") return g_tune.crc_bits;
     if (k == "crc_wgs") return g_tune.crc_wgs;
     if (k == "frame_copy_grid") return g_tune.frame_copy_grid;
+    if (k == "frame_copy_dpp") return g_tune.frame_copy_dpp;
     if (k == "frame_crc_lane") return g_tune.frame_crc_lane;
     if (k == "frame_crc_bs_nib") return g_tune.frame_crc_bs_nib;
     if (k == "xor_threads") return g_tune.xor_threads;
@@ -330,9 +344,9 @@ struct ecamd_map {
 
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy = false, int crc = 0);
+                                std::shared_ptr<void>& hold, bool copy = false, int crc = 0, bool wave = false);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
-                    const std::shared_ptr<void>& hold);
+                    const std::shared_ptr<void>& hold, int threads = 256);
 }  // namespace ecamd
 
 namespace {
@@ -637,17 +651,24 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     *rc = 0;
     const int mode = g_tune.bitslice;
     const int K = map->K;
-    if (!mode || nrows < g_tune.bitslice_min_rows || nrows > kBsMaxR || K > kBsMaxK || bs < kBsTile)
-        return 0;
+    if (!mode || nrows > kBsMaxR || K > kBsMaxK) return 0;
     if (!copy_off && (base.copy_records || base.limited)) return 0;
     if (copy_off && bitslice_depth(g_tune.bitslice_depth, K) != 0) return 0;  // ring form: no copy-through
-    const int64_t cover = (base.limited ? std::min<int64_t>(bs, base.min_len) : bs) / kBsTile * kBsTile;
-    if (cover < kBsTile) return 0;
     ApplyArgs a = base;
     a.ncols = K;
     a.nrows = nrows;
     for (int j = 0; j < K; j++) a.in_off[j] = in_off[j];
     for (int r = 0; r < nrows; r++) a.out_off[r] = out_off[row0 + r];
+    // one-wave 4 KiB tiles (knob bs_wave): 3-4-output maps (C3 encode and decodes) run best in the
+    // finest dispatcher-balanced units the 4-chunk transpose allows -- interleaved output slots
+    // ({0,5,10,13}) above all; 5-8-output maps keep the 4-wave 16 KiB tiles
+    const bool narrow = !copy_off && g_tune.bs_wave >= 1 && nrows >= g_tune.bs_wave_min_rows && nrows <= 4;
+    const bool wave = !copy_off && (narrow || g_tune.bs_wave == 2);
+    if (nrows < g_tune.bitslice_min_rows && !narrow) return 0;
+    const int64_t tile = wave ? kBsTileWave : kBsTile;
+    if (bs < tile) return 0;
+    const int64_t cover = (base.limited ? std::min<int64_t>(bs, base.min_len) : bs) / tile * tile;
+    if (cover < tile) return 0;
     if (!stream_offsets(a, bs)) return 0;
     if (copy_off) {
         for (int j = 0; j < K; j++) a.copy_off[j] = copy_off[j];
@@ -658,8 +679,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         for (int j = 0; j < K; j++)
             sub[static_cast<size_t>(r) * K + j] = map->coeff[static_cast<size_t>(row0 + r) * K + j];
     std::shared_ptr<void> hold;  // the kernel's module stays loaded until the launch is enqueued
-    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, g_tune.bitslice_depth, mode == 2, hold,
-                                         copy_off != nullptr);
+    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, wave ? 0 : static_cast<int>(g_tune.bitslice_depth),
+                                         mode == 2, hold, copy_off != nullptr, 0, wave);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -669,7 +690,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     b.stripe_list = a.stripe_list;
     b.in_records = a.in_records;
     b.out_records = a.out_records;
-    b.tiles_per_stripe = static_cast<uint32_t>(cover / kBsTile);
+    b.tiles_per_stripe = static_cast<uint32_t>(cover / tile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     for (int j = 0; j < K; j++) b.in_off[j] = a.in_off32[j];
     for (int r = 0; r < nrows; r++) b.out_off[r] = a.out_off32[r];
@@ -694,7 +715,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     }
     // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
     // one 4-wave workgroup per wave per SIMD the kernel is built for (2 for 5..8 outputs)
-    const int64_t slots = static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows);
+    // (one-wave workgroups: 4 per such slot, so a launch keeps its bytes)
+    const int64_t slots = static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows) * (wave ? 4 : 1);
     // long passes as several launches (bs_tiles_per_slot; as launch_stream_pass)
     const uint64_t limit = static_cast<uint64_t>(std::max(0, static_cast<int>(g_tune.bs_tiles_per_slot)));
     int per = nstripes;
@@ -715,7 +737,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
         // bs_grid 1: one workgroup per tile (the dispatcher balances the tiles); 0: the resident slots
         const int64_t grid = g_tune.bs_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots);
-        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold);
+        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256);
     }
     return *rc ? 0 : cover;
 }
@@ -1581,6 +1603,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_lane = value != 0;  // < 0: the default (1)
     } else if (k == "frame_crc_bs_nib") {
         g_tune.frame_crc_bs_nib = value > 0;  // <= 0: the default (byte tables)
+    } else if (k == "frame_copy_dpp") {
+        g_tune.frame_copy_dpp = value > 0;  // <= 0: the default (0)
     } else if (k == "frame_copy_grid") {
         g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
     } else if (k == "frame_copy_threads") {
@@ -1591,6 +1615,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.xor_threads = value == 64 || value == 128 || value == 256 ? value : 0;  // else by shape
     } else if (k == "xor_grid") {
         g_tune.xor_grid = value != 0;  // < 0: the default (1)
+    } else if (k == "bs_wave") {
+        g_tune.bs_wave = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
+    } else if (k == "bs_wave_min_rows") {
+        g_tune.bs_wave_min_rows = value >= 2 && value <= 4 ? value : 3;  // else the default
     } else if (k == "bs_tiles_per_slot") {
         g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {

@@ -255,7 +255,20 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // realigned in registers from the two aligned object chunks under it when j*bs % 16 != 0 (aligned
 // loads and stores on both sides); the payload's last chunk, anything reaching past the object's
 // end (zero padded) and a window whose second chunk would reach past the object go byte by byte.
-template <int kCopyU>
+// The next lane's 16 bytes (lane 63: whatever `own` is; the caller loads that lane's itself): a
+// wave's consecutive lanes hold consecutive aligned chunks, so the second chunk under a realigned
+// window is the neighbour's first -- one load per lane instead of two (DPP wave_shl:1, VALU only).
+__device__ __forceinline__ u32x4 next_lane16(const u32x4& v)
+{
+    auto shl1 = [](uint32_t x) {
+        return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x130, 0xf, 0xf, false));
+    };
+    return u32x4{shl1(v.x), shl1(v.y), shl1(v.z), shl1(v.w)};
+}
+
+// kDpp (knob frame_copy_dpp): the realigning path takes each lane's second aligned chunk from its
+// neighbour lane (next_lane16) and only the last lane of a wave loads its own.
+template <int kCopyU, bool kDpp>
 __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs a)
 {
     const uint32_t T = blockDim.x;  // lanes per tile (64 / 128 / 256)
@@ -282,9 +295,25 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
             const int src = lo + c * 16;
             const int q = src >> 4;
             const bool fast = c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
-            v0[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
-            v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
-                robj, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
+            if (kDpp && delta) {  // every lane's aligned chunk (past the object: zeros), the neighbour's next
+                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, q << 4, 0, 2);
+                v1[u] = u32x4{0u, 0u, 0u, 0u};
+            } else {
+                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
+                v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                    robj, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
+            }
+        }
+        if (kDpp && delta) {
+#pragma unroll
+            for (int u = 0; u < kCopyU; ++u) v1[u] = next_lane16(v0[u]);
+            if ((threadIdx.x & 63u) == 63u) {
+#pragma unroll
+                for (int u = 0; u < kCopyU; ++u) {
+                    const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
+                    v1[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, (((lo + c * 16) >> 4) << 4) + 16, 0, 2);
+                }
+            }
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
@@ -308,8 +337,10 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         }
     }
 }
-template __global__ void frame_split_stream_kernel<1>(const SplitArgs);
-template __global__ void frame_split_stream_kernel<4>(const SplitArgs);
+template __global__ void frame_split_stream_kernel<1, false>(const SplitArgs);
+template __global__ void frame_split_stream_kernel<4, false>(const SplitArgs);
+template __global__ void frame_split_stream_kernel<1, true>(const SplitArgs);
+template __global__ void frame_split_stream_kernel<4, true>(const SplitArgs);
 
 // Bytes [d, d + 16) of the 32-byte pair (lo, hi), d = 4 * dw + by wave-uniform: v_alignbyte on
 // the dword pairs (realigns an unaligned 16-byte window from two aligned loads).
@@ -341,7 +372,7 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // The straddling chunk is one lane's store too: the last 16 payload bytes of j-1, realigned, joined
 // with the first bytes of j.  Only the object's final partial chunk goes byte by byte, so nothing
 // is written outside [0, size).  Needs bs >= 32 (the host falls back to frame_join_kernel).
-template <int kCopyU>
+template <int kCopyU, bool kDpp>
 __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
 {
     const uint32_t T = blockDim.x;  // lanes per tile (64 / 128 / 256)
@@ -372,9 +403,28 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
             const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
             const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi;
-            v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
-            v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
-                rpay, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
+            if (kDpp && delta) {  // every lane's aligned chunk (outside the payload row: zeros)
+                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, q >= 0 ? q << 4 : static_cast<int>(0x80000000u),
+                                                              0, 2);
+                v1[u] = u32x4{0u, 0u, 0u, 0u};
+            } else {
+                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
+                v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rpay, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
+            }
+        }
+        if (kDpp && delta) {
+#pragma unroll
+            for (int u = 0; u < kCopyU; ++u) v1[u] = next_lane16(v0[u]);
+            if ((threadIdx.x & 63u) == 63u) {
+#pragma unroll
+                for (int u = 0; u < kCopyU; ++u) {
+                    const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
+                    const int q = ((ch << 4) - lo) >> 4;
+                    v1[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, q >= -1 ? (q << 4) + 16 : static_cast<int>(0x80000000u),
+                                                                  0, 2);
+                }
+            }
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
@@ -406,8 +456,10 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         }
     }
 }
-template __global__ void frame_join_stream_kernel<1>(const JoinArgs, int);
-template __global__ void frame_join_stream_kernel<4>(const JoinArgs, int);
+template __global__ void frame_join_stream_kernel<1, false>(const JoinArgs, int);
+template __global__ void frame_join_stream_kernel<4, false>(const JoinArgs, int);
+template __global__ void frame_join_stream_kernel<1, true>(const JoinArgs, int);
+template __global__ void frame_join_stream_kernel<4, true>(const JoinArgs, int);
 
 // fragments_to_string: object bytes [0, size) = data payloads 0..k-1 concatenated.
 __global__ void frame_join_kernel(const JoinArgs a)

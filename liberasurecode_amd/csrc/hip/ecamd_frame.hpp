@@ -85,9 +85,9 @@ __global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict_
 __global__ void frame_split_kernel(const SplitArgs a);
 __global__ void frame_join_kernel(const JoinArgs a);
 // 32-bit-offset streaming forms (objects < 2 GiB, stripes < 2 GiB): tiles of 4 x 256 x 16 B
-template <int kCopyU>
+template <int kCopyU, bool kDpp>
 __global__ void frame_split_stream_kernel(const SplitArgs a);
-template <int kCopyU>
+template <int kCopyU, bool kDpp>
 __global__ void frame_join_stream_kernel(const JoinArgs a, int k);
 __global__ void frame_verify_kernel(const CrcArgs a, const uint32_t* __restrict__ img_zlib,
                                     const uint32_t* __restrict__ img_legacy,

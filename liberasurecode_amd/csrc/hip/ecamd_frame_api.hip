@@ -533,10 +533,13 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
     if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && dev_tune("frame_copy_stream") != 0) {
         const CopyShape cs = copy_shape(bs);
         const dim3 grid(copy_grid(dev, (bs + 15) / 16, k, nstripes, cs)), block(cs.threads);
+        const bool dpp = dev_tune("frame_copy_dpp") != 0;
         if (cs.u == 1)
-            hipLaunchKernelGGL(frame_split_stream_kernel<1>, grid, block, 0, st, sa);
+            hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<1, true> : frame_split_stream_kernel<1, false>), grid,
+                               block, 0, st, sa);
         else
-            hipLaunchKernelGGL(frame_split_stream_kernel<4>, grid, block, 0, st, sa);
+            hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<4, true> : frame_split_stream_kernel<4, false>), grid,
+                               block, 0, st, sa);
     } else
         hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),
                            dim3(256), 0, st, sa);
@@ -607,10 +610,13 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
         dev_tune("frame_copy_stream") != 0) {
         const CopyShape cs = copy_shape(bs);
         const dim3 grid(copy_grid(dev, bs / 16 + 2, k, nstripes, cs)), block(cs.threads);
+        const bool dpp = dev_tune("frame_copy_dpp") != 0;
         if (cs.u == 1)
-            hipLaunchKernelGGL(frame_join_stream_kernel<1>, grid, block, 0, static_cast<hipStream_t>(stream), ja, k);
+            hipLaunchKernelGGL((dpp ? frame_join_stream_kernel<1, true> : frame_join_stream_kernel<1, false>), grid,
+                               block, 0, static_cast<hipStream_t>(stream), ja, k);
         else
-            hipLaunchKernelGGL(frame_join_stream_kernel<4>, grid, block, 0, static_cast<hipStream_t>(stream), ja, k);
+            hipLaunchKernelGGL((dpp ? frame_join_stream_kernel<4, true> : frame_join_stream_kernel<4, false>), grid,
+                               block, 0, static_cast<hipStream_t>(stream), ja, k);
     } else
         hipLaunchKernelGGL(frame_join_kernel,
                            dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),

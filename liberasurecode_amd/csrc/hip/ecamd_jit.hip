@@ -178,6 +178,7 @@ struct BsEntry {
     bool copy = false;    // copy-through variant (framed paths)
     int crc = 0;          // copy-through + payload CRC32 variant: position table sets (1, 2, 4), 0 = none;
                           //   + 8: lane-shift fold, + 16: nibble piece tables
+    bool wave = false;    // one-wave workgroups, 4 KiB tiles (BitsliceStyle::threads 64)
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -246,7 +247,9 @@ const std::string& generator_fingerprint()
     std::call_once(once, [] {
         const BitsliceNet tiny = bitslice_network({3}, 1, 1, 0);
         const BitsliceNet tiny5 = bitslice_network({3, 5, 7, 9, 11}, 5, 1, 0);  // the fold-each form
-        BitsliceStyle copy, crc, lane, nib;
+        BitsliceStyle copy, crc, lane, nib, wave;
+        wave.threads = 64;
+        wave.waves = 2;
         copy.copy_through = true;
         crc.copy_through = crc.crc = true;
         lane = crc;
@@ -255,7 +258,7 @@ const std::string& generator_fingerprint()
         nib.crc_nib = true;
         fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
-             bitslice_source(tiny5, 0, nib) + kBsNetworkVersion;
+             bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -279,7 +282,8 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
     BsEntry& e = *ep;
     const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
-                                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0);
+                                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0,
+                                             e.wave);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
@@ -374,7 +378,7 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
 // bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
 // keeps the kernel's module loaded until the caller has enqueued its launch.
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy, int crc)
+                                std::shared_ptr<void>& hold, bool copy, int crc, bool wave)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
     if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
@@ -382,8 +386,9 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (crc & 24);
     }
     copy = copy || crc;
-    depth = copy ? 0 : bitslice_depth(depth, K);
-    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1)};
+    wave = wave && !crc;
+    depth = (copy || wave) ? 0 : bitslice_depth(depth, K);
+    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0)};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
     std::unique_lock<std::mutex> lk(g_jit_mu);
@@ -411,9 +416,10 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->depth = depth;
         slot->copy = copy;
         slot->crc = crc;
+        slot->wave = wave;
         slot->arch = device_arch(dev);
         // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
-        slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 ? 2 : 0);
+        slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 && !wave ? 2 : 0);
         start_compile(slot, wait);
     }
     const std::shared_ptr<BsEntry> ep = slot;
@@ -459,11 +465,12 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
 }
 
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
-                    const std::shared_ptr<void>& hold)
+                    const std::shared_ptr<void>& hold, int threads)
 {
     BsArgs a = args;
     void* params[] = {&a};
-    const hipError_t e = hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1, 256, 1, 1, 0, st,
+    const hipError_t e = hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1,
+                                               static_cast<unsigned>(threads == 64 ? 64 : 256), 1, 1, 0, st,
                                                params, nullptr);
     if (e != hipSuccess)
         return dev_fail(ECAMD_EHIP, "hipModuleLaunchKernel(bitslice): %s", hipGetErrorString(e));

@@ -301,8 +301,13 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
       << (D ? "LDS ring of " + std::to_string(D) + " inputs per wave" : std::string("register loads")) << "\n";
     s << kPrelude;
     if (style.crc) s << kPreludeCrc;
-    const int wpe = bitslice_waves_per_simd(net.R, style.crc);
-    s << "extern \"C\" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
+    const int wpe = (!style.crc && style.waves >= 1 && style.waves <= 8) ? style.waves
+                                                                        : bitslice_waves_per_simd(net.R, style.crc);
+    // one-wave tiles only in the plain / copy-through register form
+    const int T = (!style.crc && !D && style.threads == 64) ? 64 : 256;
+    const int CS = T * 16;  // bytes between a lane's 4 chunks of one fragment
+    const int TILE = T * 64;
+    s << "extern \"C\" __global__ void __launch_bounds__(" << T << ") __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
       << wpe << ")))\n"
          "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
     auto ref = [](int v) {
@@ -368,7 +373,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "                const v4u v = {acc[r][4 * c], acc[r][4 * c + 1], acc[r][4 * c + 2], acc[r][4 * c + 3]};\n"
              "                __builtin_amdgcn_raw_buffer_store_b128(v, "
           << rout << ", a.out_off[r] + " << off
-          << " + c * 4096, 0, 2);\n"
+          << " + c * " << CS << ", 0, 2);\n"
              "            }\n"
              "        }\n";
     };
@@ -503,7 +508,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "        const u32 sl = t / a.tiles_per_stripe;\n"
              "        const u32 s = a.stripe_list ? (u32)a.stripe_list[sl] : sl;\n"
              "        const i32 off = (i32)(t - sl * a.tiles_per_stripe) * "
-          << kBsTile
+          << TILE
           << " + (i32)threadIdx.x * 16;\n"
              "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
              "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
@@ -524,10 +529,10 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             s << "        {  // input " << j << "\n            u32 P[16];\n"
               << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
               << "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
-              << "] + off + c * 4096, 0, 2);\n"
+              << "] + off + c * " << CS << ", 0, 2);\n"
               << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
               << (style.copy_through ? "                __builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" + std::to_string(j) +
-                                                 " + off + c * 4096, 0, 2);  // copy-through\n"
+                                                 " + off + c * " + std::to_string(CS) + ", 0, 2);  // copy-through\n"
                                            : std::string())
               << "            }\n"
               << (style.copy_through ? "            __builtin_amdgcn_sched_barrier(0);  // stores leave before the network\n"
@@ -618,16 +623,20 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 }
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
-                             bool crc, int crc_pos, bool crc_lane, bool crc_nib)
+                             bool crc, int crc_pos, bool crc_lane, bool crc_nib, bool wave)
 {
     std::ostringstream s;
     // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
-    // sets, bit 4 lane-shift fold, bit 5 nibble piece tables
+    // sets, bit 4 lane-shift fold, bit 5 nibble piece tables, bit 6 one-wave tiles (not with crc),
+    // bit 7 the register budget of 2 waves per SIMD (set with bit 6: the compiler then keeps the
+    // dense decode networks of <= 4 outputs in ~128 VGPRs without spilling, which a 4-wave budget
+    // of exactly 128 does not -- the occupancy follows the registers actually used)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
-    if (copy || crc)
+    wave = wave && !crc;
+    if (copy || crc || wave)
         s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
-              (crc && crc_nib ? 32 : 0))
+              (crc && crc_nib ? 32 : 0) | (wave ? 64 | 128 : 0))
           << "\n";
     else
         s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
@@ -636,7 +645,8 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 }
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
-                            int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib)
+                            int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib,
+                            bool* wave, bool* budget2)
 {
     std::istringstream s(text);
     std::string magic;
@@ -644,15 +654,18 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || (version != 1 && version != 2)) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 59 || (cp & 12) == 12 || depth != 0))
-        return false;  // copy: register loads
+    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 255 || (cp & 12) == 12 || depth != 0))
+        return false;  // copy / one-wave tiles: register loads
     if ((cp & 2) && !(cp & 1)) return false;  // crc implies copy
-    if ((cp >> 2) && !(cp & 2)) return false;
+    if ((cp & 192) && (cp & 2)) return false;  // the crc variant keeps 16 KiB tiles and its budget
+    if (((cp >> 2) & 15) && !(cp & 2)) return false;  // bits 2-5 describe the crc variant
     if (copy) *copy = (cp & 1) != 0;
     if (crc) *crc = (cp & 2) != 0;
     if (crc_pos) *crc_pos = 1 << ((cp >> 2) & 3);
     if (crc_lane) *crc_lane = (cp & 16) != 0;
     if (crc_nib) *crc_nib = (cp & 32) != 0;
+    if (wave) *wave = (cp & 64) != 0;
+    if (budget2) *budget2 = (cp & 128) != 0;
     coeff.assign(static_cast<size_t>(R) * K, 0);
     for (int& c : coeff)
         if (!(s >> c) || c < 0 || c > 0xffff) return false;

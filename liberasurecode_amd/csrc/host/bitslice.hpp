@@ -69,6 +69,13 @@ struct BitsliceStyle {
     // 32 lookups per 16-byte piece) instead of 256-entry byte tables (16 KiB, 16 lookups that
     // conflict ~3.5-way in the LDS banks)
     bool crc_nib = false;
+    // lanes per workgroup of the plain / copy-through register form: 256 (a tile is 16 KiB of every
+    // fragment, a lane's 4 chunks 4 KiB apart) or 64 (one-wave tiles of 4 KiB, chunks 1 KiB apart:
+    // the dispatcher then balances 4x finer work units, which interleaved output slots favour)
+    int threads = 256;
+    // waves per SIMD the plain / copy-through form is built for (its register budget); 0: by R
+    // (bitslice_waves_per_simd)
+    int waves = 0;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
@@ -85,13 +92,16 @@ int bitslice_waves_per_simd(int R, bool crc = false);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
-                             bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false);
+                             bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false,
+                             bool wave = false);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
-                            bool* crc_lane = nullptr, bool* crc_nib = nullptr);
+                            bool* crc_lane = nullptr, bool* crc_nib = nullptr, bool* wave = nullptr,
+                            bool* budget2 = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)
+constexpr int kBsTileWave = 4096;  // the same for one-wave workgroups (BitsliceStyle::threads 64)
 constexpr int kBsMaxK = 32;
 constexpr int kBsMaxR = 8;
 struct BsArgs {

@@ -55,10 +55,10 @@ int main(int argc, char** argv)
     ss << in.rdbuf();
     std::vector<int> coeff;
     int R = 0, K = 0, cap = 0, depth = 0;
-    bool copy = false, crc = false, crc_lane = false, crc_nib = false;
+    bool copy = false, crc = false, crc_lane = false, crc_nib = false, wave = false, budget2 = false;
     int crc_pos = 1;
     if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy, &crc, &crc_pos, &crc_lane,
-                                       &crc_nib)) {
+                                       &crc_nib, &wave, &budget2)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
@@ -68,6 +68,9 @@ int main(int argc, char** argv)
     style.crc_pos = crc_pos;
     style.crc_lane = crc_lane;
     style.crc_nib = crc_nib;
+    style.threads = wave ? 64 : 256;
+    style.waves = budget2 ? 2 : 0;
+    if (const char* v = std::getenv("ECAMD_BS_WPE")) style.waves = std::atoi(v);  // experiment only
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
     std::remove(argv[1]);

@@ -5,7 +5,9 @@ whatever earlier tests left in the kernel cache.  A per-process counter of bitsl
 (ecamd_bitslice_launches) proves which one ran.  Covers every golden case with 5..8 outputs per
 row group over whole 16 KiB tiles (the bitsliced kernel's domain): C5 encode, the C5 rebuild-8
 patterns the bench times ({0..7} and the mixed {0,2,4,6,20,22,24,26}) at 4 MiB, inconsistent
-("garbage") inputs, ragged tails, k = 24 / 32.
+("garbage") inputs, ragged tails, k = 24 / 32 -- and, since round 4, every case with 3..4 outputs
+over at least one 4 KiB tile, which the one-wave form of the kernel takes (C3 encode and the
+decodes {0,1,2,3} / {0,5,10,13} the bench times, at 1 MiB).
 Reference: src/builtin/rs_vand/liberasurecode_rs_vand.c:399-410 (encode), :426-481 (decode)."""
 import ctypes as C
 import hashlib
@@ -38,8 +40,11 @@ def launches():
     return f()
 
 
+BS_TILE_WAVE = 4096  # one-wave tiles of 3..4-output maps (knob bs_wave, default 1; round 4)
+
+
 def _bitsliced_shape(k, outputs, bs):
-    return 5 <= outputs <= 8 and k <= 32 and bs >= BS_TILE
+    return k <= 32 and ((5 <= outputs <= 8 and bs >= BS_TILE) or (3 <= outputs <= 4 and bs >= BS_TILE_WAVE))
 
 
 ENC = [c for c in GOLD["encode"] if c["pattern"] is None and _bitsliced_shape(c["k"], c["m"], c["bs"])]
@@ -68,8 +73,9 @@ def test_cases_cover_the_bench_patterns():
     assert (20, 1 << 22, (0, 2, 4, 6, 20, 22, 24, 26), False) in pats
     assert (20, 1 << 22, tuple(range(8)), True) in pats
     assert any(c["k"] == 20 and c["m"] == 8 and c["bs"] == 1 << 22 for c in ENC)
-    c3 = {(c["k"], c["bs"], tuple(c["missing"])) for c in GOLD["decode"]}
+    c3 = {(c["k"], c["bs"], tuple(c["missing"])) for c in DEC}  # on the one-wave bitsliced kernel
     assert (10, 1 << 20, (0, 5, 10, 13)) in c3 and (10, 1 << 20, (0, 1, 2, 3)) in c3
+    assert any(c["k"] == 10 and c["m"] == 4 and c["bs"] == 1 << 20 for c in ENC)
 
 
 @pytest.mark.parametrize("case", ENC, ids=lambda c: f"{c['k']}-{c['m']}-{c['bs']}")

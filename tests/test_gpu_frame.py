@@ -563,13 +563,17 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
         stride = (size + 16 + 15) // 16 * 16 + 32
         got = []
         try:
-            # (stream kernel, one workgroup per tile, lanes per tile, chunks per lane)
-            for knob, grid, lanes, u in ((1, 0, 256, 4), (1, 1, 256, 4), (0, 0, 256, 4), (1, 1, 64, 1),
-                                         (1, 1, 64, 4), (1, 1, 128, 1), (1, 0, 64, 1)):
+            # (stream kernel, one workgroup per tile, lanes per tile, chunks per lane, DPP neighbour
+            # chunks on the realigning path)
+            for knob, grid, lanes, u, dpp in ((1, 0, 256, 4, 0), (1, 1, 256, 4, 0), (0, 0, 256, 4, 0),
+                                              (1, 1, 64, 1, 0), (1, 1, 64, 4, 0), (1, 1, 128, 1, 0),
+                                              (1, 0, 64, 1, 0), (1, 1, 256, 1, 1), (1, 1, 64, 1, 1),
+                                              (1, 1, 256, 4, 1), (1, 0, 128, 1, 1)):
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_stream", knob), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_grid", grid), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_threads", lanes), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_u", u), "tune")
+                _lib.check(_lib.dev().ecamd_tune(b"frame_copy_dpp", dpp), "tune")
                 d = DeviceBuffer(S * stride)
                 d.upload(np.full(S * stride, 0xA5, dtype=np.uint8))
                 fb.decode(lost, d, obj_stride=stride)
@@ -579,6 +583,7 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
             _lib.dev().ecamd_tune(b"frame_copy_grid", 1)
             _lib.dev().ecamd_tune(b"frame_copy_threads", 0)
             _lib.dev().ecamd_tune(b"frame_copy_u", 0)
+            _lib.dev().ecamd_tune(b"frame_copy_dpp", -1)
         for i in range(1, len(got)):
             assert np.array_equal(got[0], got[i]), (size, i)
         for s in range(S):
@@ -599,11 +604,13 @@ def test_frame_split_stream_matches_first_version(F, name, k, m, hd):
         out = []
         try:
             _lib.check(_lib.dev().ecamd_tune(b"frame_unfused", 1), "tune")
-            # (stream kernel, lanes per tile, chunks per lane)
-            for knob, lanes, u in ((1, 256, 4), (0, 256, 4), (1, 64, 1), (1, 128, 1), (1, 64, 4)):
+            # (stream kernel, lanes per tile, chunks per lane, DPP neighbour chunks)
+            for knob, lanes, u, dpp in ((1, 256, 4, 0), (0, 256, 4, 0), (1, 64, 1, 0), (1, 128, 1, 0),
+                                        (1, 64, 4, 0), (1, 256, 1, 1), (1, 64, 1, 1), (1, 256, 4, 1)):
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_stream", knob), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_threads", lanes), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_u", u), "tune")
+                _lib.check(_lib.dev().ecamd_tune(b"frame_copy_dpp", dpp), "tune")
                 fb = F.FrameBatch(be, k, m, size, S, hd=hd or 3, checksum=ec_api.CHKSUM_CRC32)
                 fb.encode(_upload_objects(objs, fb.obj_stride))
                 out.append(fb.fragments())
@@ -612,6 +619,7 @@ def test_frame_split_stream_matches_first_version(F, name, k, m, hd):
             _lib.dev().ecamd_tune(b"frame_unfused", 0)
             _lib.dev().ecamd_tune(b"frame_copy_threads", 0)
             _lib.dev().ecamd_tune(b"frame_copy_u", 0)
+            _lib.dev().ecamd_tune(b"frame_copy_dpp", -1)
         for i in range(1, len(out)):
             assert np.array_equal(out[0], out[i]), (size, i)
         want = expected_stripe(be, k, m, hd, objs[2], ec_api.CHKSUM_CRC32)

@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""A/B of the bitsliced kernel in one-wave 4 KiB tiles (knob bs_wave, round 4) against the default
+kernels (development tool).
+
+C3 (k=10 m=4, 1 MiB, 256 stripes): encode, decode of data {0,1,2,3} and of the mixed {0,5,10,13}
+under
+  tables      the defaults of round 3 (LDS-table stream kernel for <= 4 outputs)
+  wave1       bs_wave 1: outputs that are not consecutive slots (the mixed decode) on the bitsliced
+              kernel in one-wave 4 KiB tiles, built with a 2-wave register budget
+  wave2_all   bs_wave 2 + bitslice_min_rows 4: every pass on the one-wave bitsliced kernel
+  bs4_16k     bitslice_min_rows 4, bs_wave 0: 4-wave 16 KiB tiles (round 3's C3 trial)
+C5 (k=20 m=8, 4 MiB, 32 stripes): rebuild of {0..7} and the mixed {0,2,4,6,20,22,24,26} with
+bs_wave 0 / 1 / 2.
+Every variant's bytes are checked equal to the tables' output first, and the launch counter says
+whether the bitsliced kernel ran.  Interleaved rounds after a settle, HIP events per launch, median
+fraction of 8 TB/s of the algorithmic bytes ((k + outputs) x F per stripe)."""
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+
+from liberasurecode_amd import _lib  # noqa: E402
+from liberasurecode_amd import device as D  # noqa: E402
+
+C3 = (10, 4, 1 << 20, 256, {"encode": None, "decode": [0, 1, 2, 3], "decode_mixed": [0, 5, 10, 13]})
+C5 = (20, 8, 4 << 20, 32, {"rebuild_data": list(range(8)), "rebuild_mixed": [0, 2, 4, 6, 20, 22, 24, 26]})
+C2 = (4, 2, 64 << 10, 4096, {"encode": None, "decode": [0, 1], "decode_mixed": [0, 4]})
+# round 4, first run (profiles/r04_bs_wave_ab1.log): bs_wave 0 (tables), 1 = then only outputs that are
+# not consecutive slots, 2 + bitslice_min_rows 4 = every C3 pass, bitslice_min_rows 4 alone = 4-wave
+# 16 KiB tiles (decodes spilled there and fell back to the tables).  Now bs_wave 1 is the default
+# for 3-4-output maps.
+VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave": 0, "bitslice_min_rows": 4}},
+            "c2": {"tables": {}, "wave_2rows": {"bs_wave_min_rows": 2}},
+            "c5": {"wave0": {}, "wave2": {"bs_wave": 2}}}
+DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0}
+
+
+def launches():
+    f = _lib.dev().ecamd_bitslice_launches
+    f.restype = C.c_longlong
+    return f()
+
+
+def apply(d, knobs):
+    for k, v in DEFAULTS.items():
+        d.ecamd_tune(k.encode(), v)
+    for k, v in knobs.items():
+        d.ecamd_tune(k.encode(), v)
+
+
+def run(cfg, rounds=3, n=30, skip=10):
+    K, M, F, S, ops = {"c3": C3, "c2": C2, "c5": C5}[cfg]
+    d = _lib.dev()
+    d.ecamd_tune(b"bitslice", 2)
+    lay = D.Layout.alloc(K + M, F, S)
+    st = D.Stream()
+    lay.fill_splitmix(nfrags=K, stream=st)
+    D.rs_encode(K, M, lay, stream=st)
+    src = lay.download_stripes()
+
+    def op_fn(pat):
+        if pat is None:
+            return lambda: D.rs_encode(K, M, lay, stream=st)
+        return lambda: D.rs_decode(K, M, pat, lay, stream=st)
+
+    # exactness and which kernel runs: every variant rebuilds every op from the same fragments
+    ran = {}
+    for vname, knobs in VARIANTS[cfg].items():
+        apply(d, knobs)
+        for op, pat in ops.items():
+            lay.upload_stripes(src)
+            n0 = launches()
+            op_fn(pat)()
+            st.synchronize()
+            assert (lay.download_stripes() == src).all(), (vname, op)
+            ran[(vname, op)] = launches() - n0
+    for _ in range(60):
+        op_fn(list(ops.values())[0])()
+    st.synchronize()
+    res = {}
+    for rnd in range(rounds):
+        for vname, knobs in VARIANTS[cfg].items():
+            apply(d, knobs)
+            for op, pat in ops.items():
+                fn = op_fn(pat)
+                outs = M if pat is None else len(pat)
+                algo = S * (K + outs) * F
+                ev = [D.Event() for _ in range(n + 1)]
+                ev[0].record(st)
+                for i in range(n):
+                    fn()
+                    ev[i + 1].record(st)
+                st.synchronize()
+                ms = statistics.median(ev[i].elapsed_ms(ev[i + 1]) for i in range(skip, n))
+                res.setdefault((vname, op), []).append(algo / (ms * 1e-3) / 8e12)
+                print(json.dumps({"cfg": cfg, "round": rnd, "variant": vname, "op": op, "ms": round(ms, 4),
+                                  "frac": round(algo / (ms * 1e-3) / 8e12, 4),
+                                  "bitsliced_launches": ran[(vname, op)]}), flush=True)
+    for (vname, op), v in res.items():
+        print(json.dumps({"cfg": cfg, "summary": vname, "op": op, "median_frac": round(statistics.median(v), 4),
+                          "bitsliced_launches": ran[(vname, op)]}), flush=True)
+    apply(d, {})
+    d.ecamd_tune(b"bitslice", 1)
+    lay.buf.free()
+
+
+if __name__ == "__main__":
+    for cfg in (sys.argv[1:] or ["c3", "c2", "c5"]):
+        run(cfg)

@@ -17,7 +17,9 @@ import torch  # noqa: E402,F401
 from liberasurecode_amd import _lib, frame  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
-SHAPES = [(256, 4), (64, 4), (64, 1), (128, 1), (256, 1)]
+SHAPES = [(256, 4, 0), (64, 4, 0), (64, 1, 0), (128, 1, 0), (256, 1, 0)]
+if len(sys.argv) > 1 and sys.argv[1] == "dpp":  # round 4: knob frame_copy_dpp on the realigning path
+    SHAPES = [(256, 1, 0), (256, 1, 1), (64, 1, 0), (64, 1, 1), (128, 1, 1), (256, 4, 1)]
 
 
 def main(rounds=5, reps=10):
@@ -26,6 +28,10 @@ def main(rounds=5, reps=10):
     cases = [("c3", frame.RS_VAND, 10, 4, 10 << 20, 256),
              ("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
              ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
+    if len(sys.argv) > 1 and sys.argv[1] == "dpp":
+        cases = [("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
+                 ("c3_plus_6", frame.RS_VAND, 10, 4, (10 << 20) + 6 * 10, 256),
+                 ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
     if len(sys.argv) > 1 and sys.argv[1] == "sizes":  # the join over payload sizes, ~2.5 GiB of objects each
         cases = [(f"join_bs_{bs}", frame.RS_VAND, 10, 4, 10 * bs, (2560 << 20) // (10 * bs))
                  for bs in (4 << 20, 1 << 20, 512 << 10, 256 << 10, 131072, 104858, 65536, 16384)]
@@ -38,15 +44,16 @@ def main(rounds=5, reps=10):
         enc = tag.endswith("encode")
         fn = (lambda: fb.encode(obj, stream=st)) if enc else (lambda: fb.decode([], out, stream=st))
         ref = None
-        for t, u in SHAPES:
+        for t, u, dp in SHAPES:
             d.ecamd_tune(b"frame_copy_threads", t)
             d.ecamd_tune(b"frame_copy_u", u)
+            d.ecamd_tune(b"frame_copy_dpp", dp)
             fn()
             st.synchronize()
             got = fb.fragments() if enc else out.download()
             if ref is None:
                 ref = got
-            assert (got == ref).all(), (tag, t, u)
+            assert (got == ref).all(), (tag, t, u, dp)
             del got
         del ref
         times = {sh: [] for sh in SHAPES}
@@ -54,19 +61,21 @@ def main(rounds=5, reps=10):
         for _ in range(20):
             fn()
         for _ in range(rounds):
-            for t, u in SHAPES:
+            for t, u, dp in SHAPES:
                 d.ecamd_tune(b"frame_copy_threads", t)
                 d.ecamd_tune(b"frame_copy_u", u)
+                d.ecamd_tune(b"frame_copy_dpp", dp)
                 fn()
                 a.record(st)
                 for _ in range(reps):
                     fn()
                 b.record(st)
                 st.synchronize()
-                times[(t, u)].append(a.elapsed_ms(b) / reps)
-        for (t, u), ts in times.items():
+                times[(t, u, dp)].append(a.elapsed_ms(b) / reps)
+        for (t, u, dp), ts in times.items():
             ms = statistics.median(ts)
-            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "tile_bytes": t * u * 16, "ms": round(ms, 4)}
+            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": dp, "tile_bytes": t * u * 16,
+                   "ms": round(ms, 4)}
             if not enc:
                 rec["frac"] = round(2 * S * size / (ms * 1e-3) / 8e12, 4)
             print(json.dumps(rec), flush=True)
@@ -75,6 +84,7 @@ def main(rounds=5, reps=10):
         del fb
     d.ecamd_tune(b"frame_copy_threads", 0)
     d.ecamd_tune(b"frame_copy_u", 0)
+    d.ecamd_tune(b"frame_copy_dpp", 0)
 
 
 if __name__ == "__main__":

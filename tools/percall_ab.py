@@ -8,6 +8,8 @@ interleaved rounds, 1 and 8 caller threads, three settings --
                 with the helper threads of host/copy_pool.cpp)
   lean+helpers+pool  ... and the frontend's recycled fragment / object buffers (ECAMD_FRONTEND_POOL_MIB,
                 default 256; the others run with 0)
+  lean+helpers+pool+direct  ... and decode straight into the object (round 4, frontend.cpp
+                decode_direct, ECAMD_FRONTEND_DECODE_DIRECT; the default -- the others run without)
 (the staging chunk, ECAMD_PERCALL_CHUNK_KIB, measured at 2 and 4 MiB against the default 8 MiB in round 3:
 no gain, profiles/r03_percall_ab1.log).  The order of the settings rotates every round.
 One JSON line per run."""
@@ -23,11 +25,14 @@ SETTINGS = {"ref-zeroing": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS"
             "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
                              "ECAMD_FRONTEND_POOL_MIB": "0"},
             "lean+helpers+pool": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                                  "ECAMD_FRONTEND_POOL_MIB": "256"}}
+                                  "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "0"},
+            "lean+helpers+pool+direct": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                                         "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "1"}}
 
 
 def run(setting, threads, objects):
     env = dict(os.environ, **SETTINGS[setting])
+    env.setdefault("ECAMD_FRONTEND_DECODE_DIRECT", "0")
     r = subprocess.run([sys.executable, os.path.join(HERE, "e2e_bench.py"), "--per-call-only",
                         "--threads", str(threads), "--objects", str(objects)],
                        capture_output=True, text=True, timeout=300, env=env)
