@@ -269,6 +269,7 @@ struct Tuning {
                                   //   0.733 -> 0.746, decode {0,1,2,3} 0.734 -> 0.742, mixed {0,5,10,13}
                                   //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
     Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (2..4)
+    Knob bs_wave_copy{0};         //   1: copy-through maps (framed encode / decode-join) too
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
@@ -644,6 +645,16 @@ int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, siz
 // also stored at copy_base + s*copy_stride + copy_off[j] (< 0: not copied) as it is loaded, and
 // when base.limited (objects shorter than the k payloads) only the whole tiles below base.min_len
 // are taken -- the LDS-table passes run the rest byte-exactly.
+// One-wave 4 KiB tiles for a bitsliced row group of `nrows` outputs (knobs bs_wave, bs_wave_min_rows,
+// bs_wave_copy); `narrow`: the group takes the bitsliced kernel below bitslice_min_rows for it.
+bool bs_wave_tiles(int nrows, bool copy, bool* narrow)
+{
+    const bool ok = !copy || g_tune.bs_wave_copy;
+    const bool n = ok && g_tune.bs_wave >= 1 && nrows >= g_tune.bs_wave_min_rows && nrows <= 4;
+    if (narrow) *narrow = n;
+    return ok && (n || g_tune.bs_wave == 2);
+}
+
 int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyArgs& base,
                         const int64_t* in_off, const int64_t* out_off, int64_t bs, int nstripes,
                         hipStream_t st, int* rc, const int64_t* copy_off = nullptr)
@@ -662,8 +673,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     // one-wave 4 KiB tiles (knob bs_wave): 3-4-output maps (C3 encode and decodes) run best in the
     // finest dispatcher-balanced units the 4-chunk transpose allows -- interleaved output slots
     // ({0,5,10,13}) above all; 5-8-output maps keep the 4-wave 16 KiB tiles
-    const bool narrow = !copy_off && g_tune.bs_wave >= 1 && nrows >= g_tune.bs_wave_min_rows && nrows <= 4;
-    const bool wave = !copy_off && (narrow || g_tune.bs_wave == 2);
+    bool narrow = false;
+    const bool wave = bs_wave_tiles(nrows, copy_off != nullptr, &narrow);
     if (nrows < g_tune.bitslice_min_rows && !narrow) return 0;
     const int64_t tile = wave ? kBsTileWave : kBsTile;
     if (bs < tile) return 0;
@@ -1071,7 +1082,10 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         // run on the stream kernel (the pointer-free LDS-table kernels cannot start at an offset).
         // A row group whose passes cannot all take it (more than 20 inputs per pass, offsets past
         // 2 GiB) skips the bitsliced kernel instead of failing after writing part of the output.
-        const int64_t cover = (b.limited ? std::min<int64_t>(bs, b.min_len) : bs) / kBsTile * kBsTile;
+        auto cover_of = [&](int g) {  // bytes the group's bitsliced launch would cover
+            const int64_t tile = bs_wave_tiles(std::min(8, map->R - g * 8), true, nullptr) ? kBsTileWave : kBsTile;
+            return (b.limited ? std::min<int64_t>(bs, b.min_len) : bs) / tile * tile;
+        };
         auto tail_on_stream = [&](int g) {
             for (const auto& p : map->passes) {
                 if (p.row0 / 8 != g) continue;
@@ -1089,7 +1103,7 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
             return true;
         };
         for (int g = 0; g * 8 < map->R && g_tune.stream; g++) {
-            if (cover < bs && !tail_on_stream(g)) continue;
+            if (cover_of(g) < bs && !tail_on_stream(g)) continue;
             int brc = 0;
             b.copy_records = g == 0 ? 1 : 0;  // (recomputed from copy_off inside)
             bs_done[static_cast<size_t>(g)] =
@@ -1617,6 +1631,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.xor_grid = value != 0;  // < 0: the default (1)
     } else if (k == "bs_wave") {
         g_tune.bs_wave = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
+    } else if (k == "bs_wave_copy") {
+        g_tune.bs_wave_copy = value > 0;  // <= 0: the default (0)
     } else if (k == "bs_wave_min_rows") {
         g_tune.bs_wave_min_rows = value >= 2 && value <= 4 ? value : 3;  // else the default
     } else if (k == "bs_tiles_per_slot") {
