@@ -166,6 +166,17 @@ void ecamd_percall_crc_disarm(void);
  * each codec call and fails the call (-EIO) instead of stamping unwritten fragments. */
 void ecamd_percall_reset(void);
 int ecamd_percall_status(void);
+/* Per-call input tees (used by liberasurecode.so.1 around encode and decode): while armed on the
+ * calling thread, the synchronous calls above pack input `key[i]` -- when it is one of their input
+ * pointers -- by reading bytes [0, len[i]) from src[i] (the rest from key[i]) and writing them to
+ * dst2[i] as well, so a host copy the frontend would make anyway (object -> data payloads on
+ * encode, surviving data payloads -> decoded object on decode) rides on the staging pack instead of
+ * reading its source a second time.  disarm writes into done[i] (may be NULL) how many of the
+ * len[i] bytes were delivered to dst2[i] -- all of them or none -- and forgets the tees; the
+ * caller copies whatever was not delivered.  n <= 64.  0, or ECAMD_EINVAL. */
+int ecamd_percall_tee_arm(int n, const void *const *key, const void *const *src, void *const *dst2,
+                          const int64_t *len);
+void ecamd_percall_tee_disarm(int64_t *done);
 /* Fault injection for tests: site "staging" makes the next `count` staging acquisitions of the
  * synchronous host-buffer calls fail with ECAMD_ENOMEM (0 disarms). */
 int ecamd_fault_inject(const char *site, int count);

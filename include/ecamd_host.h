@@ -94,6 +94,12 @@ int ecamd_percall_device_plan(int ndev, const char *spec, int *devs, int max);
  * (-22) for null arrays.  Used by the per-call staging (pack / unpack) and by liberasurecode.so.1
  * for its object <-> fragment copies. */
 int ecamd_host_copy(int n, void *const *dst, const void *const *src, const int64_t *len);
+/* The same with a second destination per copy: dst[i] <- src[i] and, when dst2 and dst2[i] are
+ * not null, dst2[i] <- src[i], reading the source from DRAM once (each 256 KiB piece is copied to
+ * dst2 and then from there, cache-resident, to dst).  Used by the per-call staging pack when the
+ * frontend hands it an input tee (ecamd_percall_tee_arm, ecamd.h). */
+int ecamd_host_copy2(int n, void *const *dst, void *const *dst2, const void *const *src,
+                     const int64_t *len);
 
 /* Bitsliced GF(2^16) maps (host/bitslice.hpp): the XOR network built for an R x K matrix
  * (R <= 8, K <= 32, at most `cap` shared temporaries per input) evaluated on 32 words per input

@@ -241,7 +241,10 @@ struct CodecHooks {
     void (*exec_reset)(void) = nullptr;                          // ecamd_percall_reset / _status
     int (*exec_status)(void) = nullptr;
     int (*copy)(int, void* const*, const void* const*, const int64_t*) = nullptr;  // ecamd_host_copy
+    int (*tee_arm)(int, const void* const*, const void* const*, void* const*, const int64_t*) = nullptr;
+    void (*tee_disarm)(int64_t*) = nullptr;  // ecamd_percall_tee_*
     bool crc() const { return crc_arm && crc_lookup && crc_disarm; }
+    bool tee() const { return tee_arm && tee_disarm; }
     bool ours() const { return exec_reset && exec_status; }
 };
 
@@ -257,6 +260,9 @@ CodecHooks resolve_hooks(void* so)
     h.exec_status = reinterpret_cast<int (*)(void)>(dlsym(so, "ecamd_percall_status"));
     h.copy = reinterpret_cast<int (*)(int, void* const*, const void* const*, const int64_t*)>(
         dlsym(so, "ecamd_host_copy"));
+    h.tee_arm = reinterpret_cast<int (*)(int, const void* const*, const void* const*, void* const*,
+                                         const int64_t*)>(dlsym(so, "ecamd_percall_tee_arm"));
+    h.tee_disarm = reinterpret_cast<void (*)(int64_t*)>(dlsym(so, "ecamd_percall_tee_disarm"));
     dlerror();
     return h;
 }
@@ -630,6 +636,45 @@ struct CopyBatch {
     }
 };
 
+// These copies ride on this repo's codec's staging pack (ecamd_percall_tee_arm, include/ecamd.h):
+// the codec, packing input key[i], reads it from the copy's source and writes the copy's
+// destination too, so the source leaves DRAM once.  Armed only when every key is a codec input of
+// the coming call; whatever the codec did not deliver (it refused, or failed) is copied here after.
+struct TeeCopies {
+    const CodecHooks& h;
+    CopyBatch cb;
+    std::vector<const void*> key;
+    bool armed = false;
+    explicit TeeCopies(const CodecHooks& hooks) : h(hooks) {}
+    void add(const void* k, void* d, const void* sr, int64_t n)
+    {
+        if (n <= 0) return;
+        key.push_back(k);
+        cb.add(d, sr, n);
+    }
+    void start(bool use_tee)  // before the codec call
+    {
+        armed = use_tee && h.tee() && !key.empty() && key.size() <= 64 &&
+                h.tee_arm(static_cast<int>(key.size()), key.data(), cb.src.data(), cb.dst.data(), cb.len.data()) == 0;
+        if (!armed) cb.run(&h);  // no tees: the copies now, as without them
+    }
+    void finish()  // after the codec call
+    {
+        if (!armed) return;
+        std::vector<int64_t> done(key.size(), 0);
+        h.tee_disarm(done.data());
+        armed = false;
+        CopyBatch rest;
+        for (size_t i = 0; i < key.size(); i++)
+            if (done[i] < cb.len[i]) rest.add(cb.dst[i], cb.src[i], cb.len[i]);
+        rest.run(&h);
+    }
+    ~TeeCopies()
+    {
+        if (armed) h.tee_disarm(nullptr);
+    }
+};
+
 // fragments_to_string (erasurecode_preprocessing.c:269-370): concatenate data payloads.
 int assemble(int k, char** frags, int n, char** out, uint64_t* out_len, const CodecHooks* h)
 {
@@ -722,6 +767,16 @@ int prepare_decode(int k, int m, char** data, char** parity, const int* missing,
     return 0;
 }
 
+// ECAMD_FRONTEND_TEE=0 turns the staging-pack tees off (TeeCopies; A/B runs, tools/percall_ab.py).
+bool tee_on()
+{
+    static const bool on = [] {
+        const char* f = getenv("ECAMD_FRONTEND_TEE");
+        return !(f && f[0] == '0');
+    }();
+    return on;
+}
+
 // ECAMD_FRONTEND_DECODE_DIRECT=0 turns decode_direct off (A/B runs, tools/percall_ab.py).
 bool decode_direct_on()
 {
@@ -768,6 +823,15 @@ int decode_direct(ec_backend* be, char** data, char** parity, int* missing, char
     for (int i = 0; i < k; i++) dp[i] = gone[i] ? obj + static_cast<int64_t>(i) * bs : payload(data[i]);
     for (int i = 0; i < m; i++)
         if (!gone[k + i]) pp[i] = payload(parity[i]);
+    // surviving data payloads -> object: on the codec's staging pack (they are all among its first
+    // k inputs), else after the call
+    TeeCopies cb(r->hooks);
+    for (int i = 0; i < k; i++) {
+        const int64_t off = static_cast<int64_t>(i) * bs;
+        const int64_t take = std::min<int64_t>(bs, orig - off);
+        if (take > 0 && !gone[i]) cb.add(payload(data[i]), obj + off, payload(data[i]), take);
+    }
+    cb.start(tee_on());
     int rc = 0;
     {
         ExecCheck ex(r->hooks);
@@ -778,17 +842,13 @@ int decode_direct(ec_backend* be, char** data, char** parity, int* missing, char
             return -EIO;
         }
     }
-    CopyBatch cb;
-    for (int i = 0; i < k; i++) {
-        const int64_t off = static_cast<int64_t>(i) * bs;
+    cb.finish();
+    for (int i = 0; i < k && rc != 0; i++) {  // the codec refused (more than m missing): the zeroed
+        const int64_t off = static_cast<int64_t>(i) * bs;  // slots of the reference
         const int64_t take = std::min<int64_t>(bs, orig - off);
         if (take <= 0) break;
-        if (!gone[i])
-            cb.add(obj + off, payload(data[i]), take);
-        else if (rc != 0)  // the codec refused (more than m missing): the zeroed slots of the reference
-            std::memset(obj + off, 0, static_cast<size_t>(take));
+        if (gone[i]) std::memset(obj + off, 0, static_cast<size_t>(take));
     }
-    cb.run(&r->hooks);
     if (orig > span) std::memset(obj + span, 0, static_cast<size_t>(orig - span));
     *out = obj;
     *out_len = static_cast<uint64_t>(orig);
@@ -1049,7 +1109,9 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
             // parity byte.  A foreign codec gets zeroed buffers throughout.
             const bool lean = hooks_of(be).ours() && !zero_all();
             const bool lean_parity = lean && be->common.id == EC_BACKEND_LIBERASURECODE_RS_VAND;
-            CopyBatch cb;
+            // object -> data payloads: on the codec's staging pack when it offers tees
+            TeeCopies cb(hooks_of(be));
+            const bool tee = lean && tee_on();
             for (int i = 0; i < k + m && ret == 0; i++) {
                 char* f = new_fragment(bs + meta, !(i < k ? lean : lean_parity));
                 if (!f) {
@@ -1064,14 +1126,16 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
                         zero_outside(payload(f), static_cast<size_t>(bs + meta), lo,
                                      lo + static_cast<size_t>(take > 0 ? take : 0));
                     }
-                    if (left > 0) cb.add(payload(f) + off, src, take);
+                    if (left > 0) cb.add(payload(f) + off, payload(f) + off, src, take);
                     src += take;
                     left -= take;
                 } else {
                     parity[i - k] = f;
                 }
             }
-            if (ret == 0) cb.run(&hooks_of(be));  // object -> data payloads
+            // with tees the copies happen inside the codec call (every data payload is its input;
+            // the payloads start at offset 0 for both backends), else right here
+            if (ret == 0) cb.start(tee && off == 0);
             CrcArm arm(be, be->args.uargs.ct == CHKSUM_CRC32);  // through the stamping below
             if (ret == 0) {
                 std::vector<char*> dp(k), pp(m);
@@ -1079,6 +1143,7 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
                 for (int i = 0; i < m; i++) pp[i] = payload(parity[i]);
                 ret = be->common.ops->encode(be->desc.backend_desc, dp.data(), pp.data(), bs);
                 if (ret > 0) ret = 0;  // only negative returns are failures (erasurecode.c:454-461)
+                cb.finish();
             }
             if (ret == 0) {
                 // finalize_fragments_after_encode (erasurecode_postprocessing.c:71-93)

@@ -44,6 +44,24 @@ thread_local CrcRecord t_crc;
 // and the frontend reads this to fail the call instead of stamping stale parity.
 thread_local int t_exec_rc = 0;
 
+// Input tees of the calling thread (ecamd_percall_tee_arm): packing input `key` reads bytes
+// [0, len) from `src` and also writes them to `dst2`.
+struct Tee {
+    const void* key;
+    const char* src;
+    char* dst2;
+    int64_t len;
+    int64_t done = 0;
+};
+thread_local std::vector<Tee> t_tee;
+
+Tee* find_tee(const void* key)
+{
+    for (auto& t : t_tee)
+        if (t.key == key) return &t;
+    return nullptr;
+}
+
 int note_exec(int rc)
 {
     if (rc != 0 && t_exec_rc == 0) t_exec_rc = rc;
@@ -289,6 +307,9 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     std::vector<void*> cdst(static_cast<size_t>(nfr));
     std::vector<const void*> csrc(static_cast<size_t>(nfr));
     std::vector<int64_t> clen(static_cast<size_t>(nfr));
+    std::vector<void*> pdst, pdst2;  // the pack with tees
+    std::vector<const void*> psrc;
+    std::vector<int64_t> plen;
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
         int r = wait_stream(st->slot[s].stream, chunk * nfr >= kSpinMinBytes);
@@ -314,12 +335,36 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         if ((rc = drain(s))) break;
         const int64_t off = c * chunk;
         const int64_t n = std::min(chunk, bs - off);
-        for (int j = 0; j < K; j++) {
-            cdst[j] = sl.h_pin + j * chunk;
-            csrc[j] = in[j] + off;
-            clen[j] = n;
+        if (t_tee.empty()) {
+            for (int j = 0; j < K; j++) {
+                cdst[j] = sl.h_pin + j * chunk;
+                csrc[j] = in[j] + off;
+                clen[j] = n;
+            }
+            ecamd_host_copy(K, cdst.data(), csrc.data(), clen.data());  // pack
+        } else {  // pack, the tees' bytes also to their second destination
+            pdst.clear();
+            pdst2.clear();
+            psrc.clear();
+            plen.clear();
+            auto add = [&](void* d, void* d2, const void* sr, int64_t len) {
+                pdst.push_back(d);
+                pdst2.push_back(d2);
+                psrc.push_back(sr);
+                plen.push_back(len);
+            };
+            for (int j = 0; j < K; j++) {
+                char* d = sl.h_pin + j * chunk;
+                Tee* te = find_tee(in[j]);
+                const int64_t a = te && off < te->len ? std::min(n, te->len - off) : 0;
+                if (a > 0) {
+                    add(d, te->dst2 + off, te->src + off, a);
+                    te->done += a;
+                }
+                if (a < n) add(d + a, nullptr, in[j] + off + a, n - a);
+            }
+            ecamd_host_copy2(static_cast<int>(pdst.size()), pdst.data(), pdst2.data(), psrc.data(), plen.data());
         }
-        ecamd_host_copy(K, cdst.data(), csrc.data(), clen.data());  // pack
         // One DMA each way per chunk (the slabs are [K inputs | R outputs] x chunk, contiguous):
         // for small fragments the per-call cost is API latency, not bytes.  A short last chunk
         // also moves the stale tail of each slot, which the kernel and the unpack never read.
@@ -465,6 +510,26 @@ void ecamd_percall_crc_disarm(void)
 }
 
 void ecamd_percall_reset(void) { t_exec_rc = 0; }
+
+int ecamd_percall_tee_arm(int n, const void* const* key, const void* const* src, void* const* dst2,
+                          const int64_t* len)
+{
+    t_tee.clear();
+    if (n < 0 || n > 64 || (n > 0 && (!key || !src || !dst2 || !len))) return ECAMD_EINVAL;
+    for (int i = 0; i < n; i++) {  // one entry per argument (done[i] of disarm); null ones never match
+        const bool ok = key[i] && src[i] && dst2[i] && len[i] > 0;
+        t_tee.push_back({ok ? key[i] : nullptr, static_cast<const char*>(src[i]), static_cast<char*>(dst2[i]),
+                         ok ? len[i] : 0});
+    }
+    return 0;
+}
+
+void ecamd_percall_tee_disarm(int64_t* done)
+{
+    if (done)
+        for (size_t i = 0; i < t_tee.size(); i++) done[i] = t_tee[i].done;
+    t_tee.clear();
+}
 
 int ecamd_percall_status(void) { return t_exec_rc; }
 

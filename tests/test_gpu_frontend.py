@@ -336,3 +336,29 @@ def test_frontend_on_dirty_heap(zero_all):
     assert res["perturbed"], "glibc did not perturb the heap: the test proves nothing"
     assert res["cases"] >= 150
     assert res["failures"] == []
+
+
+def test_decode_direct_matches_general_path():
+    """Encode with the object -> payload copies on the codec's staging pack (tees) and
+    liberasurecode_decode straight into the object (frontend.cpp decode_direct: rebuilt data
+    unpacked in place, missing parity not rebuilt, surviving payloads copied once) against the
+    general path in the reference's order (fresh fragments for every missing index, parity rebuilt,
+    fragments_to_string afterwards; ECAMD_FRONTEND_DECODE_DIRECT=0): identical return codes and
+    objects for every erasure pattern sampled, and for irregular survivors (another payload size or
+    orig_data_size in a data fragment's header, a duplicate fragment), which the direct path hands
+    back to the general one."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    res = {}
+    # (decode straight into the object, staging-pack tees for the object <-> payload copies)
+    for direct, tee in (("1", "1"), ("1", "0"), ("0", "0")):
+        env = dict(os.environ, ECAMD_FRONTEND_DECODE_DIRECT=direct, ECAMD_FRONTEND_TEE=tee)
+        r = subprocess.run([sys.executable, os.path.join(here, "percall_decode_run.py")], capture_output=True,
+                           text=True, timeout=240, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[direct + tee] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["11"] == res["10"] == res["00"]
+    assert all(ok for _, _, _, ok in res["11"] if ok is not None), [x for x in res["11"] if x[3] is False][:5]
+    assert sum(1 for _, rc, _, ok in res["11"] if ok) > 100

@@ -101,3 +101,32 @@ def test_copy_helpers_off_and_fork(env):
                        capture_output=True, text=True, timeout=120, env=e)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith("OK")
+
+
+@pytest.mark.parametrize("sizes", [[0], [1], [17, 0, 5], [(256 << 10) + 3] * 7, [3 << 20, 5, (1 << 20) + 17],
+                                   [10 << 20]])
+@pytest.mark.parametrize("second", ["all", "some"])
+def test_copy2_exact(sizes, second):
+    """ecamd_host_copy2: every copy lands in dst and -- where a second destination is given -- in
+    dst2 too, byte-exact, guard bytes intact (the per-call staging pack with frontend tees)."""
+    h = lib()
+    h.ecamd_host_copy2.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(len(sizes) * 7 + sum(sizes) % 997)
+    srcs = [rng.integers(0, 256, n, dtype=np.uint8) for n in sizes]
+    d1 = [np.full(n + 64, 0xEE, np.uint8) for n in sizes]
+    d2 = [np.full(n + 64, 0xDD, np.uint8) for n in sizes]
+    use2 = [second == "all" or i % 2 == 0 for i in range(len(sizes))]
+    n = len(sizes)
+    dst = (C.c_void_p * n)(*[x.ctypes.data for x in d1])
+    dst2 = (C.c_void_p * n)(*[x.ctypes.data if u else None for x, u in zip(d2, use2)])
+    src = (C.c_void_p * n)(*[x.ctypes.data for x in srcs])
+    ln = (C.c_int64 * n)(*[x.nbytes for x in srcs])
+    assert h.ecamd_host_copy2(n, dst, dst2, src, ln) == 0
+    for s, a, b, u in zip(srcs, d1, d2, use2):
+        assert np.array_equal(a[:len(s)], s) and (a[len(s):] == 0xEE).all()
+        if u:
+            assert np.array_equal(b[:len(s)], s)
+            assert (b[len(s):] == 0xDD).all()
+        else:
+            assert (b == 0xDD).all()
+    assert h.ecamd_host_copy2(1, None, None, None, None) == -22

@@ -1,17 +1,16 @@
 #!/usr/bin/env python3
-"""A/B of the per-call host path (round 3): tools/e2e_bench.py --per-call-only in child processes,
-interleaved rounds, 1 and 8 caller threads, three settings --
-  ref-zeroing   ECAMD_FRONTEND_ZERO_ALL=1 ECAMD_COPY_THREADS=0  (the frontend zeroes every buffer in
-                full as the reference does; every copy on the caller's thread)
-  lean          ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=0  (only uncovered bytes zeroed)
-  lean+helpers  ECAMD_FRONTEND_ZERO_ALL=0 ECAMD_COPY_THREADS=4  (default: copies of a call shared
-                with the helper threads of host/copy_pool.cpp)
-  lean+helpers+pool  ... and the frontend's recycled fragment / object buffers (ECAMD_FRONTEND_POOL_MIB,
-                default 256; the others run with 0)
-  lean+helpers+pool+direct  ... and decode straight into the object (round 4, frontend.cpp
-                decode_direct, ECAMD_FRONTEND_DECODE_DIRECT; the default -- the others run without)
-(the staging chunk, ECAMD_PERCALL_CHUNK_KIB, measured at 2 and 4 MiB against the default 8 MiB in round 3:
-no gain, profiles/r03_percall_ab1.log).  The order of the settings rotates every round.
+"""A/B of the per-call host path: tools/e2e_bench.py --per-call-only in child processes,
+interleaved rounds, 1 and 8 caller threads, settings --
+  ref-zeroing  the frontend zeroes every buffer in full as the reference does, every copy on the
+               caller's thread, no recycled buffers, the reference's decode order
+  r03-default  round 3's defaults: lean zeroing, 4 copy helpers (host/copy_pool.cpp), recycled
+               fragment / object buffers (ECAMD_FRONTEND_POOL_MIB 256)
+  direct       + decode straight into the object (round 4, frontend.cpp decode_direct,
+               ECAMD_FRONTEND_DECODE_DIRECT)
+  direct+tee   + the object <-> data payload copies riding on the codec's staging pack (round 4,
+               TeeCopies / ecamd_percall_tee_arm, ECAMD_FRONTEND_TEE) -- the default
+Each run reports encode / decode GiB/s without and with the caller's own read of the outputs
+(GIL-free memmove, e2e_bench.py per_call).  The order of the settings rotates every round.
 One JSON line per run."""
 import json
 import os
@@ -20,19 +19,21 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SETTINGS = {"ref-zeroing": {"ECAMD_FRONTEND_ZERO_ALL": "1", "ECAMD_COPY_THREADS": "0",
-                            "ECAMD_FRONTEND_POOL_MIB": "0"},
-            "lean": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "0", "ECAMD_FRONTEND_POOL_MIB": "0"},
-            "lean+helpers": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                             "ECAMD_FRONTEND_POOL_MIB": "0"},
-            "lean+helpers+pool": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                                  "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "0"},
-            "lean+helpers+pool+direct": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
-                                         "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "1"}}
+                            "ECAMD_FRONTEND_POOL_MIB": "0", "ECAMD_FRONTEND_DECODE_DIRECT": "0",
+                            "ECAMD_FRONTEND_TEE": "0"},
+            "r03-default": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                            "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "0",
+                            "ECAMD_FRONTEND_TEE": "0"},
+            "direct": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                       "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "1",
+                       "ECAMD_FRONTEND_TEE": "0"},
+            "direct+tee": {"ECAMD_FRONTEND_ZERO_ALL": "0", "ECAMD_COPY_THREADS": "4",
+                           "ECAMD_FRONTEND_POOL_MIB": "256", "ECAMD_FRONTEND_DECODE_DIRECT": "1",
+                           "ECAMD_FRONTEND_TEE": "1"}}
 
 
 def run(setting, threads, objects):
     env = dict(os.environ, **SETTINGS[setting])
-    env.setdefault("ECAMD_FRONTEND_DECODE_DIRECT", "0")
     r = subprocess.run([sys.executable, os.path.join(HERE, "e2e_bench.py"), "--per-call-only",
                         "--threads", str(threads), "--objects", str(objects)],
                        capture_output=True, text=True, timeout=300, env=env)
