@@ -215,7 +215,8 @@ struct Tuning {
                             //   LDS ring 2 / 4 deep; tools/c5_prof.py C5_MODES A/B
     Knob stream_hybrid{1};  //   8-output passes: one input in 4 looks its hi table up via L1
     Knob stream_order{0};   //   tile order: bit 0 contiguous range per workgroup, bit 1 XCD-grouped
-    Knob stream_realign{0}; //   copy-through inputs at offsets that are not multiples of 16: 1 = aligned
+    Knob stream_realign{0}; //   copy-through inputs at offsets that are not multiples of 16: 2 = one aligned
+                            //   load per lane, the window's second chunk from the next lane (DPP); 1 = aligned
                             //   loads realigned in registers (gf16_realign_kernel), 0 = unaligned 16-byte
                             //   loads -- measured faster (Swift segments 1.366 vs 1.444 ms, C3 + 10 B
                             //   1.226 vs 1.281 ms, tools/realign_ab.py, profiles/r03_realign_ab.log)
@@ -469,14 +470,16 @@ int launch_stream(const ApplyArgs& a, int width, int ch, bool pf, bool nib, dim3
     bool unaligned = false;  // inputs at offsets that are not multiples of 16 (objects, j*bs)
     for (int j = 0; j < a.ncols; j++) unaligned = unaligned || (a.in_off32[j] & 15) != 0;
     if (unaligned && width <= 4 && ch == 1 && !nib && g_tune.stream_realign) {
+        ApplyArgs ra = a;
+        ra.realign_dpp = g_tune.stream_realign == 2 ? 1 : 0;
         // aligned loads realigned in registers (ecamd_stream.hpp, RA)
 #define RA_(W)                                                                                    \
     switch ((a.ncols + 3) / 4) {                                                                  \
-    case 1: hipLaunchKernelGGL((gf16_realign_kernel<W, 1>), grid, block, lds, st, a); break;      \
-    case 2: hipLaunchKernelGGL((gf16_realign_kernel<W, 2>), grid, block, lds, st, a); break;      \
-    case 3: hipLaunchKernelGGL((gf16_realign_kernel<W, 3>), grid, block, lds, st, a); break;      \
-    case 4: hipLaunchKernelGGL((gf16_realign_kernel<W, 4>), grid, block, lds, st, a); break;      \
-    default: hipLaunchKernelGGL((gf16_realign_kernel<W, 5>), grid, block, lds, st, a); break;     \
+    case 1: hipLaunchKernelGGL((gf16_realign_kernel<W, 1>), grid, block, lds, st, ra); break;      \
+    case 2: hipLaunchKernelGGL((gf16_realign_kernel<W, 2>), grid, block, lds, st, ra); break;      \
+    case 3: hipLaunchKernelGGL((gf16_realign_kernel<W, 3>), grid, block, lds, st, ra); break;      \
+    case 4: hipLaunchKernelGGL((gf16_realign_kernel<W, 4>), grid, block, lds, st, ra); break;      \
+    default: hipLaunchKernelGGL((gf16_realign_kernel<W, 5>), grid, block, lds, st, ra); break;     \
     }
         if (width == 2) {
             RA_(2)
@@ -1600,7 +1603,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "stream_hybrid") {
         g_tune.stream_hybrid = value;
     } else if (k == "stream_realign") {
-        g_tune.stream_realign = value > 0;  // < 0: the default (0)
+        g_tune.stream_realign = value >= 2 ? 2 : value > 0 ? 1 : 0;  // < 0: the default (0)
     } else if (k == "stream_chunk") {
         g_tune.stream_chunk = std::max(-1, std::min(value, 1 << 16));  // -1: by table size
     } else if (k == "stream_order") {

@@ -258,7 +258,7 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // The next lane's 16 bytes (lane 63: whatever `own` is; the caller loads that lane's itself): a
 // wave's consecutive lanes hold consecutive aligned chunks, so the second chunk under a realigned
 // window is the neighbour's first -- one load per lane instead of two (DPP wave_shl:1, VALU only).
-__device__ __forceinline__ u32x4 next_lane16(const u32x4& v)
+static __device__ __forceinline__ u32x4 next_lane16(const u32x4& v)
 {
     auto shl1 = [](uint32_t x) {
         return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x130, 0xf, 0xf, false));

@@ -41,6 +41,8 @@ struct ApplyArgs {
     uint32_t copy_records;            // gf16_stream_kernel copy-through: 0 = off; else range of
     int32_t copy_off32[kMaxCols];     //   copy_base per stripe and 32-bit copy_off (< 0: skip)
     int tile_order;                   // gf16_stream_kernel: 1 = contiguous tile range per workgroup
+    int realign_dpp;                  // gf16_realign_kernel: the second aligned chunk of each lane's
+                                      //   window from the next lane (DPP), the last lane loads its own
     const int32_t* stripe_list;       // gf16_stream_kernel: logical stripe s is stripe_list[s] of the
                                       //   strided layout (heterogeneous decode groups); null = s
 };

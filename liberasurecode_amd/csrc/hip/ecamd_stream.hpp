@@ -167,6 +167,15 @@ __device__ __forceinline__ void input_mac(const ApplyArgs& a, const uint8_t* lds
     }
 }
 
+// The next lane's 16 bytes (DPP wave_shl:1; lane 63 gets zeros -- its caller loads its own).
+__device__ __forceinline__ v4u next_lane16(const v4u& v)
+{
+    auto shl1 = [](uint32_t x) {
+        return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x130, 0xf, 0xf, false));
+    };
+    return v4u{shl1(v[0]), shl1(v[1]), shl1(v[2]), shl1(v[3])};
+}
+
 // Bytes [d, d + 16) of the 32-byte pair (lo, hi), d wave-uniform (a scalar branch picks the
 // dword shift, v_alignbyte the byte shift).
 __device__ __forceinline__ v4u realign16(const v4u& lo, const v4u& hi, int d)
@@ -197,6 +206,30 @@ __device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile&
 {
     if constexpr (RA) {
         v4u y[4][CH];
+        if (a.realign_dpp) {  // one aligned load per lane; the neighbour lane holds the next chunk
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int j = 4 * G + i;
+                const int base = (j < a.ncols) ? (a.in_off32[j] & ~15) + t.off : static_cast<int>(0x80000000u);
+#pragma unroll
+                for (int c = 0; c < CH; c++) x[i][c] = __builtin_amdgcn_raw_buffer_load_b128(t.rin, base + c * t.cstride, 0, 2);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < CH; c++) y[i][c] = next_lane16(x[i][c]);
+            if ((threadIdx.x & 63u) == 63u) {  // the wave's last lane: its next chunk is the next wave's
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int j = 4 * G + i;
+#pragma unroll
+                    for (int c = 0; c < CH; c++)
+                        y[i][c] = __builtin_amdgcn_raw_buffer_load_b128(
+                            t.rin, (j < a.ncols && (a.in_off32[j] & 15)) ? (a.in_off32[j] & ~15) + t.off + c * t.cstride + 16
+                                                                         : static_cast<int>(0x80000000u), 0, 2);
+                }
+            }
+        } else {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const int j = 4 * G + i;
@@ -208,6 +241,7 @@ __device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile&
                     t.rin, (j < a.ncols && (a.in_off32[j] & 15)) ? base + c * t.cstride + 16
                                                                  : static_cast<int>(0x80000000u), 0, 2);
             }
+        }
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
