@@ -432,24 +432,26 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
 @pytest.mark.parametrize("k,m,size", [(10, 4, 10 * 104858 - 4), (4, 2, 4 * 65536 + 6), (10, 4, (10 << 20) + 10)])
 def test_frame_encode_realigned_loads_match(F, k, m, size):
     """Copy-through encode of objects whose chunks start at offsets that are not multiples of 16:
-    the aligned-loads-realigned-in-registers kernel (knob stream_realign 1, gf16_realign_kernel)
-    writes the same fragments as the unaligned-load kernel, CRC32 included."""
+    the aligned-loads-realigned-in-registers kernel (knob stream_realign 1, gf16_realign_kernel; 2:
+    the window's second chunk from the next lane) writes the same fragments as the unaligned-load
+    kernel, with and without CRC32."""
     from liberasurecode_amd import _lib
     be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
     S = 3
     objs = _objects(S, size, k * 17 + size)
-    out = []
-    try:
-        for ra in (1, 0):
-            _lib.check(_lib.dev().ecamd_tune(b"stream_realign", ra), "tune")
-            fb = F.FrameBatch(be, k, m, size, S, checksum=ec_api.CHKSUM_CRC32)
-            fb.encode(_upload_objects(objs, fb.obj_stride))
-            out.append(fb.fragments())
-    finally:
-        _lib.dev().ecamd_tune(b"stream_realign", 0)
-    assert np.array_equal(out[0], out[1])
-    want = expected_stripe(be, k, m, 0, objs[1], ec_api.CHKSUM_CRC32)
-    assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
+    for ct in (ec_api.CHKSUM_CRC32, ec_api.CHKSUM_NONE):
+        out = []
+        try:
+            for ra in (2, 1, 0):  # 2: one aligned load per lane, the next chunk from the next lane (DPP)
+                _lib.check(_lib.dev().ecamd_tune(b"stream_realign", ra), "tune")
+                fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
+                fb.encode(_upload_objects(objs, fb.obj_stride))
+                out.append(fb.fragments())
+        finally:
+            _lib.dev().ecamd_tune(b"stream_realign", 0)
+        assert np.array_equal(out[0], out[2]) and np.array_equal(out[1], out[2])
+        want = expected_stripe(be, k, m, 0, objs[1], ct)
+        assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
 
 
 @pytest.mark.parametrize("k,m,size", [(10, 4, 1 << 20), (10, 4, (1 << 20) + 7), (10, 4, 3 * 104858 + 5),
