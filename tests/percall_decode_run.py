@@ -41,7 +41,11 @@ def main():
                 out.append([f"{k},{m},{size},{list(lost)}", rc, sha(data), rc == 0 and data == obj])
             # irregular survivors: the direct path must hand them to the general one
             lost = [0, k]  # a data and a parity fragment gone: the codec runs
-            for field, val in (("size", 4096), ("orig", size + 5), ("orig", max(0, size - 9))):
+            bs = flen - 80
+            # a claimed payload size beyond the real one would make the reference read past the
+            # fragments (prepare_fragments_for_decode takes it for the blocksize): only smaller ones
+            cases = ([("size", bs - 2)] if bs > 2 else []) + [("orig", size + 5), ("orig", max(0, size - 9))]
+            for field, val in cases:
                 bad = bytearray(frags[1])
                 if field == "size":
                     bad[4:8] = val.to_bytes(4, "little")
