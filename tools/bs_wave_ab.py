@@ -61,6 +61,7 @@ def run(cfg, rounds=3, n=30, skip=10):
     st = D.Stream()
     lay.fill_splitmix(nfrags=K, stream=st)
     D.rs_encode(K, M, lay, stream=st)
+    st.synchronize()  # the download does not wait for `st`
     src = lay.download_stripes()
 
     def op_fn(pat):

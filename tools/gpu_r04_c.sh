@@ -4,6 +4,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
+timeout -k 10 300 python tools/bs_wave_ab.py c2 c5 > gpurun_out/r04_bs_wave_ab3.log 2>&1 || { echo "AB3 rc=$?"; tail -20 gpurun_out/r04_bs_wave_ab3.log; exit 1; }
 timeout -k 10 300 python tools/copy_shape_ab.py dpp > gpurun_out/r04_copy_dpp_ab.log 2>&1 || { echo "DPP rc=$?"; tail -20 gpurun_out/r04_copy_dpp_ab.log; exit 1; }
 timeout -k 10 300 python tools/frame_wave_ab.py > gpurun_out/r04_frame_wave_ab.log 2>&1 || { echo "FRAMEWAVE rc=$?"; tail -20 gpurun_out/r04_frame_wave_ab.log; exit 1; }
 timeout -k 10 300 python tools/realign_ab.py > gpurun_out/r04_realign_ab.log 2>&1 || { echo "REALIGN rc=$?"; tail -20 gpurun_out/r04_realign_ab.log; exit 1; }
