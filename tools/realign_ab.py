@@ -35,11 +35,11 @@ def main(rounds=5, reps=5):
                 fb.encode(obj, stream=st)
                 st.synchronize()
                 got.append(fb.fragments())
-            assert (got[0] == got[1]).all(), (tag, ct)
+            assert (got[0] == got[2]).all() and (got[1] == got[2]).all(), (tag, ct)
             del got
             for _ in range(20):
                 fb.encode(obj, stream=st)
-            times = {1: [], 0: []}
+            times = {2: [], 1: [], 0: []}
             a, b = D.Event(), D.Event()
             for _ in range(rounds):
                 for ra in (2, 1, 0):
