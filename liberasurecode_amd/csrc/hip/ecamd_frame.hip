@@ -295,9 +295,12 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
             const int src = lo + c * 16;
             const int q = src >> 4;
             const bool fast = c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
-            if (kDpp && delta) {  // every lane's aligned chunk (past the object: zeros), the neighbour's next
+            if (kDpp && delta) {  // every lane's aligned chunk (past the object: zeros), the neighbour's next;
+                // the wave's last lane loads its own second chunk in the same burst (the other lanes'
+                // offsets are out of range: no memory access)
                 v0[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, q << 4, 0, 2);
-                v1[u] = u32x4{0u, 0u, 0u, 0u};
+                v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                    robj, (threadIdx.x & 63u) == 63u ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
             } else {
                 v0[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
                 v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
@@ -305,14 +308,11 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
             }
         }
         if (kDpp && delta) {
+            const bool last = (threadIdx.x & 63u) == 63u;
 #pragma unroll
-            for (int u = 0; u < kCopyU; ++u) v1[u] = next_lane16(v0[u]);
-            if ((threadIdx.x & 63u) == 63u) {
-#pragma unroll
-                for (int u = 0; u < kCopyU; ++u) {
-                    const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
-                    v1[u] = __builtin_amdgcn_raw_buffer_load_b128(robj, (((lo + c * 16) >> 4) << 4) + 16, 0, 2);
-                }
+            for (int u = 0; u < kCopyU; ++u) {
+                const u32x4 n = next_lane16(v0[u]);
+                v1[u] = last ? v1[u] : n;
             }
         }
 #pragma unroll
@@ -403,10 +403,12 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
             const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
             const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi;
-            if (kDpp && delta) {  // every lane's aligned chunk (outside the payload row: zeros)
+            if (kDpp && delta) {  // every lane's aligned chunk (outside the payload row: zeros); the
+                // wave's last lane loads its own second chunk in the same burst
                 v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, q >= 0 ? q << 4 : static_cast<int>(0x80000000u),
                                                               0, 2);
-                v1[u] = u32x4{0u, 0u, 0u, 0u};
+                v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rpay, (threadIdx.x & 63u) == 63u && q >= -1 ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
             } else {
                 v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
                 v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
@@ -414,16 +416,11 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
             }
         }
         if (kDpp && delta) {
+            const bool last = (threadIdx.x & 63u) == 63u;
 #pragma unroll
-            for (int u = 0; u < kCopyU; ++u) v1[u] = next_lane16(v0[u]);
-            if ((threadIdx.x & 63u) == 63u) {
-#pragma unroll
-                for (int u = 0; u < kCopyU; ++u) {
-                    const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
-                    const int q = ((ch << 4) - lo) >> 4;
-                    v1[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, q >= -1 ? (q << 4) + 16 : static_cast<int>(0x80000000u),
-                                                                  0, 2);
-                }
+            for (int u = 0; u < kCopyU; ++u) {
+                const u32x4 n = next_lane16(v0[u]);
+                v1[u] = last ? v1[u] : n;
             }
         }
 #pragma unroll

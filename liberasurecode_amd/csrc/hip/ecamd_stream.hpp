@@ -207,28 +207,26 @@ __device__ __forceinline__ void load_group(const ApplyArgs& a, const StreamTile&
     if constexpr (RA) {
         v4u y[4][CH];
         if (a.realign_dpp) {  // one aligned load per lane; the neighbour lane holds the next chunk
-#pragma unroll
+            const bool last = (threadIdx.x & 63u) == 63u;  // its next chunk is the next wave's: loaded in
+#pragma unroll                                              // the same burst (other lanes: out of range)
             for (int i = 0; i < 4; i++) {
                 const int j = 4 * G + i;
                 const int base = (j < a.ncols) ? (a.in_off32[j] & ~15) + t.off : static_cast<int>(0x80000000u);
+                const bool need = last && j < a.ncols && (a.in_off32[j] & 15);
 #pragma unroll
-                for (int c = 0; c < CH; c++) x[i][c] = __builtin_amdgcn_raw_buffer_load_b128(t.rin, base + c * t.cstride, 0, 2);
+                for (int c = 0; c < CH; c++) {
+                    x[i][c] = __builtin_amdgcn_raw_buffer_load_b128(t.rin, base + c * t.cstride, 0, 2);
+                    y[i][c] = __builtin_amdgcn_raw_buffer_load_b128(
+                        t.rin, need ? base + c * t.cstride + 16 : static_cast<int>(0x80000000u), 0, 2);
+                }
             }
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
-                for (int c = 0; c < CH; c++) y[i][c] = next_lane16(x[i][c]);
-            if ((threadIdx.x & 63u) == 63u) {  // the wave's last lane: its next chunk is the next wave's
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int j = 4 * G + i;
-#pragma unroll
-                    for (int c = 0; c < CH; c++)
-                        y[i][c] = __builtin_amdgcn_raw_buffer_load_b128(
-                            t.rin, (j < a.ncols && (a.in_off32[j] & 15)) ? (a.in_off32[j] & ~15) + t.off + c * t.cstride + 16
-                                                                         : static_cast<int>(0x80000000u), 0, 2);
+                for (int c = 0; c < CH; c++) {
+                    const v4u n = next_lane16(x[i][c]);
+                    y[i][c] = last ? y[i][c] : n;
                 }
-            }
         } else {
 #pragma unroll
         for (int i = 0; i < 4; i++) {

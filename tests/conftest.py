@@ -22,9 +22,14 @@ def _built():
     if not os.path.isdir("/root/reference"):
         yield
         return
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "oracle"], check=True)
-    if os.path.isdir("/root/reference"):
+    import fcntl
+    # one build at a time: pytest-xdist workers each run this fixture, and two makes writing the
+    # same .so at once hand a half-written library to a test that loads it
+    with open(os.path.join(ROOT, ".pytest_build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "oracle"], check=True)
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
-    subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "liberasurecode_amd", "csrc")],
-                   check=True)
+        subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "liberasurecode_amd", "csrc")],
+                       check=True)
+        fcntl.flock(lock, fcntl.LOCK_UN)
     yield

@@ -117,7 +117,7 @@ def main():
         # bitsliced 0 = the LDS-table fused kernel (byte tables, 2 workgroups per CU)
         # (..., lane-shift fold)
         variants = [(0, 1, 2, 4, 0), (1, 2, 0, 64, 0), (1, 2, 0, 64, 1), (1, 1, 0, 64, 0), (1, 1, 0, 64, 1),
-                    (1, 2, 0, 32, 1)]
+                    (1, 2, 0, 32, 1), (1, 1, 0, 32, 1), (1, 1, 0, 16, 1)]
         d.ecamd_tune(b"bitslice", 2)
         for bsv, pos, wgs, units, lane in variants:  # compile the crc variants outside the timing
             d.ecamd_tune(b"frame_crc_bs", bsv)
