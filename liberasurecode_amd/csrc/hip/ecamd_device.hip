@@ -242,9 +242,14 @@ struct Tuning {
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
-    Knob frame_copy_dpp{0};       // framed split / join stream kernels, realigning path (bs % 16 != 0): 1 =
+    Knob frame_crc_cover{1};      // framed CRC32 encode of payloads that are not whole 16 KiB tiles (Swift's
+                                  //   1 MiB segments): the crc variant over the whole tiles + tail codec +
+                                  //   tail CRC (ecamd_frame_api.hip encode_crc_cover); 0 = codec + CRC pass
+    Knob frame_copy_dpp{1};       // framed split / join stream kernels, realigning path (bs % 16 != 0): 1 =
                                   //   each lane's second aligned chunk from its neighbour lane (DPP
-                                  //   wave_shl:1), one load per lane; 0 = two loads per lane
+                                  //   wave_shl:1, the last lane's own load issued in the same burst);
+                                  //   0 = two loads per lane.  Swift segment join 0.704 -> 0.726 of 8 TB/s,
+                                  //   C3 + 6 B 0.724 -> 0.715 (noise level; profiles/r04_copy_dpp_ab2.log)
     Knob frame_copy_threads{0};   // framed split / join stream kernels: lanes per tile (64 / 128 / 256; 0 = by
                                   //   shape: 64 for 16-byte-multiple payloads, else 256, ecamd_frame_api.hip)
     Knob frame_copy_u{0};         //   and 16-byte chunks per lane (1 / 4; 0 = 1)
@@ -322,6 +327,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_mb") return g_tune.frame_crc_mb;
     if (k == "frame_crc_nib") return g_tune.frame_crc_nib;
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
+    if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
@@ -1201,7 +1207,7 @@ bool copy_aligned_payloads(const void* obj, const void* payload0, int64_t obj_st
 
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                   void* stream, int64_t obj_size)
+                   void* stream, int64_t obj_size, int64_t from)
 {
     std::shared_ptr<RsEntry> e;
     int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
@@ -1210,16 +1216,19 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
     if (obj_size < 0) obj_size = k * bs;
     if (obj_size > k * bs || !copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
         return fail(ECAMD_EINVAL, "copy-through encode needs 16-byte aligned objects and payloads");
+    if (from < 0 || from % 16 || from >= bs) return fail(ECAMD_EINVAL, "copy-through encode: bad range start");
+    // bytes [from, bs) of every payload: object chunk j from j*bs + from, payloads from + from
     std::vector<int64_t> in_off, out_off, copy_off, in_len;
     for (int i : e->inputs) {
-        in_off.push_back(static_cast<int64_t>(i) * bs);
-        copy_off.push_back(static_cast<int64_t>(i) * frag_stride);
-        in_len.push_back(std::max<int64_t>(0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(i) * bs)));
+        in_off.push_back(static_cast<int64_t>(i) * bs + from);
+        copy_off.push_back(static_cast<int64_t>(i) * frag_stride + from);
+        in_len.push_back(
+            std::max<int64_t>(0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(i) * bs) - from));
     }
-    for (int o : e->outputs) out_off.push_back(static_cast<int64_t>(o) * frag_stride);
+    for (int o : e->outputs) out_off.push_back(static_cast<int64_t>(o) * frag_stride + from);
     auto* p0 = static_cast<uint8_t*>(payload0);
     return map_apply_copy(*e, static_cast<const uint8_t*>(obj), obj_stride, in_off, p0,
-                          stripe_stride, out_off, p0, stripe_stride, copy_off, bs, nstripes, stream,
+                          stripe_stride, out_off, p0, stripe_stride, copy_off, bs - from, nstripes, stream,
                           &in_len);
 }
 
@@ -1317,17 +1326,23 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
 
 int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                           int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos)
+                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos,
+                          int64_t cover)
 {
     const int mode = g_tune.bitslice;
+    if (cover < 0) cover = bs;
     // more than 4 outputs: the kernel folds every tile on its own (bitslice.cpp fold_each), q = tiles
-    if (!mode || m > kBsMaxR || k > kBsMaxK || bs % kBsTile || nstripes <= 0 || q <= 0 || (bs / kBsTile) % q ||
-        (m > 4 && q != bs / kBsTile))
+    if (!mode || m > kBsMaxR || k > kBsMaxK || cover % kBsTile || cover <= 0 || cover > bs || nstripes <= 0 ||
+        q <= 0 || (cover / kBsTile) % q || (m > 4 && q != cover / kBsTile))
         return ECAMD_EINVAL;
     std::shared_ptr<RsEntry> e;
     int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
     if (rc) return rc;
-    if (!e->map || !copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)) return ECAMD_EINVAL;
+    // whole payloads: the object chunks j*bs are 16-byte aligned; partial cover (objects that do not
+    // fill k 16 KiB-multiple payloads): the object side is read with unaligned loads
+    if (!e->map || !(cover == bs ? copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)
+                                 : copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)))
+        return ECAMD_EINVAL;
     for (int j = 0; j < k; j++)
         if (e->inputs[j] != j) return ECAMD_EINVAL;
     for (int r = 0; r < m; r++)
@@ -1360,7 +1375,7 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     b.out_stride = a.out_stride;
     b.in_records = a.in_records;
     b.out_records = a.out_records;
-    b.tiles_per_stripe = static_cast<uint32_t>(bs / kBsTile);
+    b.tiles_per_stripe = static_cast<uint32_t>(cover / kBsTile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     for (int j = 0; j < k; j++) {
         b.in_off[j] = a.in_off32[j];
@@ -1374,7 +1389,7 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     b.crc_img = d_img;
     b.crc_partial = d_partial;
     b.crc_q = q;
-    b.crc_per = static_cast<int32_t>(bs / kBsTile / q);
+    b.crc_per = static_cast<int32_t>(cover / kBsTile / q);
     b.crc_nfrag = k + m;
     const int64_t units = static_cast<int64_t>(nstripes) * q;
     // one work unit per workgroup by default: the dispatcher hands the next unit to whichever CU
@@ -1580,6 +1595,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_copy_stream = value;
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
+    } else if (k == "frame_crc_cover") {
+        g_tune.frame_crc_cover = value;  // 0 off, anything else on
     } else if (k == "frame_unfused") {
         g_tune.frame_unfused = value != 0;
     } else if (k == "stream") {
@@ -1621,7 +1638,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "frame_crc_bs_nib") {
         g_tune.frame_crc_bs_nib = value > 0;  // <= 0: the default (byte tables)
     } else if (k == "frame_copy_dpp") {
-        g_tune.frame_copy_dpp = value > 0;  // <= 0: the default (0)
+        g_tune.frame_copy_dpp = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_copy_grid") {
         g_tune.frame_copy_grid = value != 0;  // < 0: the default (1)
     } else if (k == "frame_copy_threads") {

@@ -49,7 +49,8 @@ struct DevImage {
 
 std::mutex g_mu;
 std::map<std::tuple<int, int, int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J, G, pos
-std::map<std::pair<int, void*>, std::pair<uint32_t*, size_t>> g_scratch;     // dev, stream
+std::map<std::tuple<int, void*, int>, std::pair<uint32_t*, size_t>> g_scratch;  // dev, stream, slot
+std::map<std::tuple<int, int, int64_t>, uint32_t*> g_shift_maps;                 // dev, legacy, bytes
 
 int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** out)
 {
@@ -68,11 +69,30 @@ int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** 
     return 0;
 }
 
-// Per-(device, stream) scratch for span partials; calls on one stream are ordered, so reuse is safe.
-int scratch(int dev, void* stream, size_t words, uint32_t** out)
+// Field tables (8-bit fields, 4 x 256 words) of A^nbytes in device memory, cached.
+int shift_map(int dev, bool legacy, int64_t nbytes, const uint32_t** out)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    auto& e = g_scratch[{dev, stream}];
+    auto key = std::make_tuple(dev, legacy ? 1 : 0, nbytes);
+    auto it = g_shift_maps.find(key);
+    if (it == g_shift_maps.end()) {
+        std::vector<uint32_t> w(1024);
+        field_tables(zero_shift(CrcMachine(legacy), static_cast<uint64_t>(nbytes)), 8, w.data());
+        uint32_t* d = nullptr;
+        HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(d, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        it = g_shift_maps.emplace(key, d).first;
+    }
+    *out = it->second;
+    return 0;
+}
+
+// Per-(device, stream) scratch for span partials; calls on one stream are ordered, so reuse is safe.
+// Slot 1 holds values that must outlive a run_crc on the same stream (its partials use slot 0).
+int scratch(int dev, void* stream, size_t words, uint32_t** out, int slot = 0)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& e = g_scratch[std::make_tuple(dev, stream, slot)];
     if (e.second < words) {
         if (e.first) {
             HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
@@ -378,21 +398,31 @@ int fused_ranges(int dev, int64_t tiles, int nstripes, int default_per_cu)
 }
 
 // crc_finalize_kernel over the q ranges of every payload of the batch and the 80-byte headers.
+// cover < bs: the ranges span the payloads' first `cover` bytes and tail_crc[item] holds the CRC32
+// of the rest (bs - cover bytes), folded in after them.
 int finalize_ranges(int dev, const Code& c, bool legacy, uint64_t obj_size, uint8_t* frags, int64_t ss,
-                    int64_t fs, int64_t bs, int nstripes, const uint32_t* partial, int q, void* stream)
+                    int64_t fs, int64_t bs, int nstripes, const uint32_t* partial, int q, void* stream,
+                    int64_t cover = -1, const uint32_t* tail_crc = nullptr)
 {
     const int nf = c.k + c.m;
-    const int J = static_cast<int>(bs / q / 1024);  // KiB per range
+    if (cover < 0) cover = bs;
+    const int J = static_cast<int>(cover / q / 1024);  // KiB per range
     const DevImage* di = nullptr;
     int rc = image(dev, legacy, 5, J, 8, false, &di);
     if (rc) return rc;
     CrcArgs a{};
+    if (cover < bs) {
+        if (!tail_crc) return dev_fail(ECAMD_EINVAL, "finalize: ranges end before the payload, no tail CRC");
+        if ((rc = shift_map(dev, legacy, bs - cover, &a.tail_map))) return rc;
+        a.tail_crc = tail_crc;
+        a.tail_c0 = zero_shift(CrcMachine(legacy), static_cast<uint64_t>(bs - cover)).apply(~0u);
+    }
     a.base = frags;
     a.stripe_stride = ss;
     a.frag_stride = fs;
     a.payload_off = kHeaderBytes;
-    a.len = bs;
-    a.body = bs;
+    a.len = cover;  // (no byte steps: the ranges end exactly at `cover`)
+    a.body = cover;
     a.items = static_cast<int64_t>(nstripes) * nf;
     a.nfrag = nf;
     a.nspans = q;
@@ -435,6 +465,54 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
                                partial, q, stream, npos | (lane ? 8 : 0) | (nib ? 16 : 0));
     if (rc) return rc;
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
+}
+
+// Objects that do not fill k payloads of whole 16 KiB tiles (Swift's 1 MiB segments: bs = 104858,
+// object chunks at unaligned offsets j*bs, the last one 4 bytes short): the bitsliced crc variant
+// over the tiles every payload holds in full ([0, cover), cover = the last chunk's whole tiles),
+// then the copy-through codec over [cover, bs) of every payload, the CRC32 of those tails on their
+// own (run_crc), and the finalize folding each tail into its payload's ranges:
+// r0(X || Y) = A^|Y| r0(X) ^ r0(Y).  ECAMD_EINVAL, nothing launched, when it does not apply or the
+// bitsliced kernel is still compiling: the caller runs the copy-through encode + CRC pass.
+int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64_t obj_stride,
+                     uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs, int nstripes,
+                     void* stream)
+{
+    constexpr int64_t kTile = 16384;
+    if (dev_tune("frame_crc_cover") == 0 || dev_tune("frame_crc_bs") == 0 || dev_tune("frame_crc_fused") == 0 ||
+        c.m > 8 || bs % 2 || nstripes <= 0)
+        return ECAMD_EINVAL;
+    const int64_t last = static_cast<int64_t>(obj_size) - (c.k - 1) * bs;  // bytes of the last data chunk
+    const int64_t cover = std::min(bs, last) / kTile * kTile;
+    if (last <= 0 || cover < kTile) return ECAMD_EINVAL;
+    const int64_t tail = bs - cover;
+    const int nf = c.k + c.m;
+    const int q = c.m > 4 ? static_cast<int>(cover / kTile) : fused_ranges(dev, cover / kTile, nstripes, 64);
+    uint32_t *partial = nullptr, *tail_crc = nullptr;
+    int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * q, &partial, 1);
+    if (rc) return rc;
+    if (tail && (rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf, &tail_crc, 2))) return rc;
+    const uint32_t* img = nullptr;
+    const bool lane = c.m > 4 || dev_tune("frame_crc_lane") != 0;
+    int npos = dev_tune("frame_crc_pos");
+    if (npos <= 0) npos = lane && c.m <= 4 ? 1 : 2;
+    const bool nib = dev_tune("frame_crc_bs_nib") > 0;
+    if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos, nib))) return rc;
+    rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                               partial, q, stream, npos | (lane ? 8 : 0) | (nib ? 16 : 0), cover);
+    if (rc) return rc;
+    if (tail) {
+        // from here on a failure is an error, not a fallback: part of the payloads is written
+        if ((rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, stream,
+                                 static_cast<int64_t>(obj_size), cover)))
+            return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail codec failed") : rc;
+        HeaderArgs none{};
+        if ((rc = run_crc(dev, legacy, true, frags, ss, fs, kHeaderBytes + cover, nf, tail, nstripes, tail_crc,
+                          none, stream)))
+            return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail CRC failed") : rc;
+    }
+    return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream, cover,
+                           tail_crc);
 }
 
 int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64_t obj_stride,
@@ -508,6 +586,9 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
             rc = encode_crc_fused(dev, c, legacy_crc(), d_obj, obj_stride, obj_size, frags, stripe_stride,
                                   frag_stride, bs, nstripes, stream);
             if (rc != ECAMD_EINVAL) return rc;
+            rc = encode_crc_cover(dev, c, legacy_crc(), d_obj, obj_stride, obj_size, frags, stripe_stride,
+                                  frag_stride, bs, nstripes, stream);
+            if (rc != ECAMD_EINVAL) return rc;
         }
         rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes,
                             stream);
@@ -520,7 +601,13 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
         dev_tune("frame_copy_padded") != 0) {
         // Objects that do not fill the payloads exactly (any size: Swift's 1 MiB segments give
         // bs = 104858): the same copy-through launch reads each chunk j*bs of the object with
-        // unaligned loads and reads zeros past the object's end, so no split pass either.
+        // unaligned loads and reads zeros past the object's end, so no split pass either; with
+        // CRC32 checksums the whole tiles also fold them in the same launch (encode_crc_cover).
+        if (checksum == kChksumCrc32) {
+            rc = encode_crc_cover(dev, c, legacy_crc(), d_obj, obj_stride, obj_size, frags, stripe_stride,
+                                  frag_stride, bs, nstripes, stream);
+            if (rc != ECAMD_EINVAL) return rc;
+        }
         rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes,
                             stream, static_cast<int64_t>(obj_size));
         if (rc) return rc;

@@ -40,10 +40,11 @@ int dev_tune(const char* key);                      // current value of an ecamd
 // obj + s*obj_stride + j*bs) and copied into payload j while the parity is computed
 // (payload f of stripe s at payload0 + s*stripe_stride + f*frag_stride).  Objects of obj_size
 // bytes (< 0: k*bs) are zero-padded past their end (prepare_fragments_for_encode).  16-byte aligned
-// object base / stride and payloads; bs even (the object side may be read unaligned).
+// object base / stride and payloads; bs even (the object side may be read unaligned).  from > 0 (a
+// multiple of 16): only bytes [from, bs) of every payload (the rest of a partly fused encode).
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                   void* stream, int64_t obj_size = -1);
+                   void* stream, int64_t obj_size = -1, int64_t from = 0);
 
 // rs_vand decode straight into objects: the missing data fragments (at least one, -1 terminated
 // `missing`) are computed into their object positions (j*bs) and the available data inputs are
@@ -67,7 +68,8 @@ size_t fused_crc_lds(int k, int m, int mb, bool nib = false);  // LDS bytes of t
 // nothing launched, when it does not apply or the kernel is not compiled yet.
 int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                           int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos = 1);
+                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos = 1,
+                          int64_t cover = -1);  // cover: the first `cover` bytes of each payload only
 // fused image words with byte tables for the first mb dwords of a piece, nibble tables after
 constexpr int crc_fused_words(int mb = 1) { return mb * 1024 + (4 - mb) * 128 + 8 * 128; }
 

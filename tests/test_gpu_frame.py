@@ -429,6 +429,44 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
         assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
 
 
+@pytest.mark.parametrize("k,m,size", [(10, 4, 1 << 20), (10, 4, 3 * (1 << 20) + 7), (4, 2, 3 * 4 * 16384 - 6),
+                                      (6, 3, 6 * 16384 + 6 * 100), (12, 6, 65536 * 12 - 24), (20, 8, 20 * 40000),
+                                      (10, 4, 10 * (5 * 16384 + 16)), (3, 2, 3 * 16384 - 2)])
+@pytest.mark.parametrize("legacy", [False, True])
+def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
+    """CHKSUM_CRC32 framed encode of payloads that are not whole 16 KiB tiles (Swift's 1 MiB segments,
+    bs = 104858): the bitsliced crc variant over each payload's whole tiles, the codec and CRC32 of
+    the rest on their own, the finalize folding them together (knob frame_crc_cover) -- against the
+    copy-through encode + separate CRC pass, and the restated reference framing for one stripe."""
+    from liberasurecode_amd import _lib
+    if legacy:
+        monkeypatch.setenv("LIBERASURECODE_WRITE_LEGACY_CRC", "1")
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    S = 3
+    objs = _objects(S, size, k * 11 + m + size)
+    out = []
+    _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2), "tune")
+    try:
+        for cover in (1, 0):
+            _lib.check(_lib.dev().ecamd_tune(b"frame_crc_cover", cover), "tune")
+            n0 = _bs_launches()
+            fb = F.FrameBatch(be, k, m, size, S)
+            fb.encode(_upload_objects(objs, fb.obj_stride))
+            out.append(fb.fragments())
+            bs = fb.blocksize
+            last = size - (k - 1) * bs
+            if cover and last >= 16384:
+                assert _bs_launches() > n0, "the bitsliced crc variant did not run"
+            elif cover:
+                assert _bs_launches() == n0, "a bitsliced kernel ran on a shape it does not take"
+    finally:
+        _lib.dev().ecamd_tune(b"frame_crc_cover", 1)
+        _lib.dev().ecamd_tune(b"bitslice", 1)
+    assert np.array_equal(out[0], out[1])
+    want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
+    assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
+
+
 @pytest.mark.parametrize("k,m,size", [(10, 4, 10 * 104858 - 4), (4, 2, 4 * 65536 + 6), (10, 4, (10 << 20) + 10)])
 def test_frame_encode_realigned_loads_match(F, k, m, size):
     """Copy-through encode of objects whose chunks start at offsets that are not multiples of 16:

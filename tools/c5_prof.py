@@ -8,7 +8,10 @@ dispatch order, so the summary takes launches 10..29 of each run as the steady s
 settles over the first ~20 launches of a VALU-dense kernel): ecamd_bs_kernel dispatches 38, 68, 98
 (after 3 compile-time launches), gf16_hybrid_kernel 36, 66, 96 (after 1).  Prints the HIP-event rate of each steady window too.
 C5_MODES="2:0,2:4,0:0" picks other (bitslice, bitslice_depth) sequences, e.g. for A/B runs;
-C5_K / C5_M / C5_S other shapes (m = 8)."""
+C5_K / C5_M / C5_S other shapes (m = 8).
+PROF_CFG=c3: the same sequence at C3 (k=10 m=4, 1 MiB, 256 stripes) with the decodes of data
+{0,1,2,3} and of the mixed {0,5,10,13} -- every pass on the one-wave bitsliced kernel, then on the
+LDS-table stream kernel (gf16_stream_kernel): the same dispatch indices (tools/gpu_prof_c3ops.sh)."""
 import json
 import os
 import sys
@@ -24,6 +27,9 @@ K, M = int(os.environ.get("C5_K", 20)), int(os.environ.get("C5_M", 8))  # other 
 F, S = 4 << 20, int(os.environ.get("C5_S", 32))
 WARM = 25
 PATTERNS = {"rebuild8_data": list(range(8)), "rebuild8_mixed": [0, 2, 4, 6, K, K + 2, K + 4, K + 6]}
+if os.environ.get("PROF_CFG") == "c3":
+    K, M, F, S = 10, 4, 1 << 20, 256
+    PATTERNS = {"decode_0123": [0, 1, 2, 3], "decode_mixed": [0, 5, 10, 13]}
 
 
 def main(n=30, skip=10):

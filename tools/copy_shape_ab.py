@@ -84,7 +84,7 @@ def main(rounds=5, reps=10):
         del fb
     d.ecamd_tune(b"frame_copy_threads", 0)
     d.ecamd_tune(b"frame_copy_u", 0)
-    d.ecamd_tune(b"frame_copy_dpp", 0)
+    d.ecamd_tune(b"frame_copy_dpp", -1)
 
 
 if __name__ == "__main__":
