@@ -54,6 +54,11 @@ int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
  * shift, 3 v_bfe_u32, 4 v_and_b32, 5 v_perm_b32, 6 v_lshl_or_b32, 7 conflict-free ds_read_b128 +
  * wait). */
 int ecamd_probe_valu(int op, int wgs_per_cu, int iters, void *stream);
+/* Unaligned-copy probe: `bytes` (a multiple of 4096) copied in one-workgroup 4 KiB tiles with one side
+ * displaced by `shift` (0..15) bytes; mode 0 aligned, 1 unaligned 16-byte loads, 2 two aligned loads
+ * realigned, 3 one aligned load + the next lane's (DPP), 4 dword-aligned 16-byte load + one dword,
+ * 5 unaligned 16-byte stores.  Buffers need bytes + 32 of room. */
+int ecamd_probe_unaligned(int mode, int shift, void *d_dst, const void *d_src, int64_t bytes, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -39,4 +39,7 @@ __global__ void stream_copy_kernel(uint4* __restrict__ dst, const uint4* __restr
 template <int OP>
 __global__ void valu_probe_kernel(int iters, uint32_t seed, uint32_t* sink);
 
+template <int MODE>
+__global__ void unaligned_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int shift);
+
 }  // namespace ecamd

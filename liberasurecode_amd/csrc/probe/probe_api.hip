@@ -216,4 +216,28 @@ int ecamd_probe_valu(int op, int wgs_per_cu, int iters, void* stream)
     return 0;
 }
 
+int ecamd_probe_unaligned(int mode, int shift, void* dst, const void* src, int64_t bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (mode < 0 || mode > 5 || shift < 0 || shift > 15 || bytes < 4096 || bytes % 4096 ||
+        bytes / 4096 >= (int64_t{1} << 31) || !aligned16(dst) || !aligned16(src))
+        return fail(-22, "unaligned probe: mode 0..5, shift 0..15, bytes a multiple of 4096, aligned buffers");
+    const dim3 grid(static_cast<unsigned>(bytes / 4096)), block(256);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    auto* d = static_cast<uint8_t*>(dst);
+    auto* s = static_cast<const uint8_t*>(src);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(unaligned_probe_kernel<0>, grid, block, 0, st, d, s, bytes, shift); break;
+    case 1: hipLaunchKernelGGL(unaligned_probe_kernel<1>, grid, block, 0, st, d, s, bytes, shift); break;
+    case 2: hipLaunchKernelGGL(unaligned_probe_kernel<2>, grid, block, 0, st, d, s, bytes, shift); break;
+    case 3: hipLaunchKernelGGL(unaligned_probe_kernel<3>, grid, block, 0, st, d, s, bytes, shift); break;
+    case 4: hipLaunchKernelGGL(unaligned_probe_kernel<4>, grid, block, 0, st, d, s, bytes, shift); break;
+    default: hipLaunchKernelGGL(unaligned_probe_kernel<5>, grid, block, 0, st, d, s, bytes, shift); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 }  // extern "C"

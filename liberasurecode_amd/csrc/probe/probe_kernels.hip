@@ -297,3 +297,75 @@ template __global__ void valu_probe_kernel<10>(int, uint32_t, uint32_t*);
 template __global__ void valu_probe_kernel<11>(int, uint32_t, uint32_t*);
 
 }  // namespace ecamd
+
+namespace ecamd {
+
+// Unaligned-copy probe (sweeps only): `bytes` copied in one-workgroup 4 KiB tiles (256 lanes x 16 B)
+// between an aligned side and a side displaced by `shift` bytes -- what the framed copies and the
+// copy-through codec see at object offsets j*bs when bs % 16 != 0.  MODE 0: both sides aligned
+// (shift ignored); 1: 16-byte buffer loads at src + shift; 2: two aligned loads + v_alignbyte
+// window; 3: one aligned load, the second chunk from the next lane (DPP wave_shl:1, lane 63 loads
+// its own); 4: dword-aligned 16-byte load at floor4(src + shift) + one dword load, v_alignbyte;
+// 5: aligned loads, 16-byte buffer stores at dst + shift (the join's side).
+template <int MODE>
+__global__ void __launch_bounds__(256) unaligned_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes,
+                                                              int shift)
+{
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const int64_t tile = 4096;
+    const int64_t t = blockIdx.x;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src) + t * tile, 0, 4096 + 32, 0x00020000);
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + t * tile, 0, 4096 + 32, 0x00020000);
+    const int off = static_cast<int>(threadIdx.x) * 16;
+    v4 v;
+    if (MODE == 0 || MODE == 5) {
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 2);
+    } else if (MODE == 1) {
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + shift, 0, 2);
+    } else if (MODE == 2 || MODE == 3) {
+        const int q = (off + shift) & ~15, d = shift & 15;
+        const v4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs, q, 0, 2);
+        const bool last = (threadIdx.x & 63u) == 63u;
+        v4 hi = __builtin_amdgcn_raw_buffer_load_b128(rs, MODE == 2 || last ? q + 16 : static_cast<int>(0x80000000u), 0, 2);
+        if (MODE == 3) {
+            auto shl1 = [](uint32_t x) {
+                return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x130, 0xf, 0xf, false));
+            };
+            const v4 n = v4{shl1(lo.x), shl1(lo.y), shl1(lo.z), shl1(lo.w)};
+            hi = last ? hi : n;
+        }
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int dw = d >> 2, by = d & 3;
+        v4 o;
+        switch (dw) {
+        case 0: o = v4{w[0], w[1], w[2], w[3]}; break;
+        case 1: o = v4{w[1], w[2], w[3], w[4]}; break;
+        case 2: o = v4{w[2], w[3], w[4], w[5]}; break;
+        default: o = v4{w[3], w[4], w[5], w[6]}; break;
+        }
+        if (by) {
+            const uint32_t nx = dw == 0 ? w[4] : dw == 1 ? w[5] : dw == 2 ? w[6] : w[7];
+            o = v4{__builtin_amdgcn_alignbyte(o.y, o.x, by), __builtin_amdgcn_alignbyte(o.z, o.y, by),
+                   __builtin_amdgcn_alignbyte(o.w, o.z, by), __builtin_amdgcn_alignbyte(nx, o.w, by)};
+        }
+        v = o;
+    } else {  // MODE 4
+        const int a4 = (off + shift) & ~3, by = (off + shift) & 3;
+        const v4 lo = __builtin_amdgcn_raw_buffer_load_b128(rs, a4, 0, 2);
+        const uint32_t nx = __builtin_amdgcn_raw_buffer_load_b32(rs, by ? a4 + 16 : static_cast<int>(0x80000000u), 0, 2);
+        v = by ? v4{__builtin_amdgcn_alignbyte(lo.y, lo.x, by), __builtin_amdgcn_alignbyte(lo.z, lo.y, by),
+                    __builtin_amdgcn_alignbyte(lo.w, lo.z, by), __builtin_amdgcn_alignbyte(nx, lo.w, by)}
+               : lo;
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(v, rd, MODE == 5 ? off + shift : off, 0, 2);
+    (void)bytes;
+}
+
+template __global__ void unaligned_probe_kernel<0>(uint8_t*, const uint8_t*, int64_t, int);
+template __global__ void unaligned_probe_kernel<1>(uint8_t*, const uint8_t*, int64_t, int);
+template __global__ void unaligned_probe_kernel<2>(uint8_t*, const uint8_t*, int64_t, int);
+template __global__ void unaligned_probe_kernel<3>(uint8_t*, const uint8_t*, int64_t, int);
+template __global__ void unaligned_probe_kernel<4>(uint8_t*, const uint8_t*, int64_t, int);
+template __global__ void unaligned_probe_kernel<5>(uint8_t*, const uint8_t*, int64_t, int);
+
+}  // namespace ecamd

@@ -5,8 +5,7 @@
 #   PROF_CFG=c3 tools/summarize_prof.py c3ops r04 --command "PROF_CFG=c3 python3 tools/c5_prof.py" \
 #     --algo-bytes 3758096384 --window bs_encode:ecamd_bs_kernel:38:20 \
 #     --window bs_decode_0123:ecamd_bs_kernel:68:20 --window bs_decode_mixed:ecamd_bs_kernel:98:20 \
-#     --window lds_encode:gf16_stream_kernel:36:20 --window lds_decode_0123:gf16_stream_kernel:66:20 \
-#     --window lds_decode_mixed:gf16_stream_kernel:96:20
+#     (the LDS-table passes run as 2 launches each: their HIP-event rates are in the log)
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
