@@ -242,6 +242,9 @@ struct Tuning {
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
+    Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
+                                  //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
+                                  //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
     Knob frame_crc_cover{1};      // framed CRC32 encode of payloads that are not whole 16 KiB tiles (Swift's
                                   //   1 MiB segments): the crc variant over the whole tiles + tail codec +
                                   //   tail CRC (ecamd_frame_api.hip encode_crc_cover); 0 = codec + CRC pass
@@ -275,7 +278,12 @@ struct Tuning {
                                   //   0.733 -> 0.746, decode {0,1,2,3} 0.734 -> 0.742, mixed {0,5,10,13}
                                   //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
     Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (2..4)
-    Knob bs_wave_copy{0};         //   1: copy-through maps (framed encode / decode-join) too
+    Knob bs_wave_copy{2};         //   copy-through maps (framed encode / decode-join): 1 too, 2 (default) when
+                                  //   their inputs start at offsets that are not multiples of 16 (object
+                                  //   chunks j*bs, realigned loads -- knob bs_realign): Swift segments'
+                                  //   encode 0.590 -> 0.626 of 8 TB/s against the LDS-table stream kernel,
+                                  //   while aligned C3 keeps the tables (0.692 vs 0.656) and so does the
+                                  //   decode-join (aligned inputs; profiles/r04_frame_wave_ab2.log); 0 never
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
@@ -328,6 +336,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_nib") return g_tune.frame_crc_nib;
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
+    if (k == "bs_realign") return g_tune.bs_realign;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
@@ -352,7 +361,8 @@ struct ecamd_map {
 
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy = false, int crc = 0, bool wave = false);
+                                std::shared_ptr<void>& hold, bool copy = false, int crc = 0, bool wave = false,
+                                const std::vector<int>* in_shift = nullptr);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
                     const std::shared_ptr<void>& hold, int threads = 256);
 }  // namespace ecamd
@@ -656,9 +666,32 @@ int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, siz
 // are taken -- the LDS-table passes run the rest byte-exactly.
 // One-wave 4 KiB tiles for a bitsliced row group of `nrows` outputs (knobs bs_wave, bs_wave_min_rows,
 // bs_wave_copy); `narrow`: the group takes the bitsliced kernel below bitslice_min_rows for it.
-bool bs_wave_tiles(int nrows, bool copy, bool* narrow)
+// Realigned copy-through inputs (knob bs_realign): the byte shift of each input's offset, and the
+// buffer size that keeps the realigned kernel inside the bytes it covers -- each input's last window
+// ends at in_off + cover and the aligned chunk under it at the next 16-byte boundary, which stays in
+// the object's last 16-byte granule (objects are 16-byte aligned).  No shift: `shifts` empty and
+// the records unchanged.
+uint32_t realign_records(const ApplyArgs& a, int K, int64_t cover, bool copy, std::vector<int>& shifts)
 {
-    const bool ok = !copy || g_tune.bs_wave_copy;
+    shifts.clear();
+    if (!copy || !g_tune.bs_realign) return a.in_records;
+    bool any = false;
+    int64_t end = 0;
+    for (int j = 0; j < K; j++) {
+        shifts.push_back(a.in_off32[j] & 15);
+        any = any || (a.in_off32[j] & 15);
+        end = std::max<int64_t>(end, (static_cast<int64_t>(a.in_off32[j]) + cover + 15) & ~int64_t(15));
+    }
+    if (!any) {
+        shifts.clear();
+        return a.in_records;
+    }
+    return static_cast<uint32_t>(std::min<int64_t>(a.in_records, end));
+}
+
+bool bs_wave_tiles(int nrows, bool copy, bool* narrow, bool unaligned = false)
+{
+    const bool ok = !copy || g_tune.bs_wave_copy == 1 || (g_tune.bs_wave_copy == 2 && unaligned && g_tune.bs_realign);
     const bool n = ok && g_tune.bs_wave >= 1 && nrows >= g_tune.bs_wave_min_rows && nrows <= 4;
     if (narrow) *narrow = n;
     return ok && (n || g_tune.bs_wave == 2);
@@ -683,7 +716,9 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     // finest dispatcher-balanced units the 4-chunk transpose allows -- interleaved output slots
     // ({0,5,10,13}) above all; 5-8-output maps keep the 4-wave 16 KiB tiles
     bool narrow = false;
-    const bool wave = bs_wave_tiles(nrows, copy_off != nullptr, &narrow);
+    bool unaligned = false;
+    for (int j = 0; j < K; j++) unaligned = unaligned || (in_off[j] & 15);
+    const bool wave = bs_wave_tiles(nrows, copy_off != nullptr, &narrow, unaligned);
     if (nrows < g_tune.bitslice_min_rows && !narrow) return 0;
     const int64_t tile = wave ? kBsTileWave : kBsTile;
     if (bs < tile) return 0;
@@ -699,8 +734,10 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         for (int j = 0; j < K; j++)
             sub[static_cast<size_t>(r) * K + j] = map->coeff[static_cast<size_t>(row0 + r) * K + j];
     std::shared_ptr<void> hold;  // the kernel's module stays loaded until the launch is enqueued
+    std::vector<int> shifts;
+    const uint32_t in_records = realign_records(a, K, cover, copy_off != nullptr, shifts);
     hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, wave ? 0 : static_cast<int>(g_tune.bitslice_depth),
-                                         mode == 2, hold, copy_off != nullptr, 0, wave);
+                                         mode == 2, hold, copy_off != nullptr, 0, wave, &shifts);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -708,7 +745,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     b.in_stride = a.in_stride;
     b.out_stride = a.out_stride;
     b.stripe_list = a.stripe_list;
-    b.in_records = a.in_records;
+    b.in_records = in_records;
     b.out_records = a.out_records;
     b.tiles_per_stripe = static_cast<uint32_t>(cover / tile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
@@ -1091,8 +1128,11 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         // run on the stream kernel (the pointer-free LDS-table kernels cannot start at an offset).
         // A row group whose passes cannot all take it (more than 20 inputs per pass, offsets past
         // 2 GiB) skips the bitsliced kernel instead of failing after writing part of the output.
+        bool unaligned = false;
+        for (int64_t o : in_off) unaligned = unaligned || (o & 15);
         auto cover_of = [&](int g) {  // bytes the group's bitsliced launch would cover
-            const int64_t tile = bs_wave_tiles(std::min(8, map->R - g * 8), true, nullptr) ? kBsTileWave : kBsTile;
+            const int64_t tile =
+                bs_wave_tiles(std::min(8, map->R - g * 8), true, nullptr, unaligned) ? kBsTileWave : kBsTile;
             return (b.limited ? std::min<int64_t>(bs, b.min_len) : bs) / tile * tile;
         };
         auto tail_on_stream = [&](int g) {
@@ -1366,14 +1406,16 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     std::shared_ptr<void> hold;
     // crc_pos: position sets (1, 2, 4) + 8 for the lane-shift fold (which 5-8 outputs always take)
     // + 16 for nibble piece tables
-    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
+    std::vector<int> shifts;
+    const uint32_t in_records = realign_records(a, k, cover, true, shifts);
+    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos, false, &shifts);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
     b.out_base = a.out_base;
     b.in_stride = a.in_stride;
     b.out_stride = a.out_stride;
-    b.in_records = a.in_records;
+    b.in_records = in_records;
     b.out_records = a.out_records;
     b.tiles_per_stripe = static_cast<uint32_t>(cover / kBsTile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
@@ -1597,6 +1639,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_crc_cover") {
         g_tune.frame_crc_cover = value;  // 0 off, anything else on
+    } else if (k == "bs_realign") {
+        g_tune.bs_realign = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_unfused") {
         g_tune.frame_unfused = value != 0;
     } else if (k == "stream") {
@@ -1652,7 +1696,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_wave") {
         g_tune.bs_wave = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
     } else if (k == "bs_wave_copy") {
-        g_tune.bs_wave_copy = value > 0;  // <= 0: the default (0)
+        g_tune.bs_wave_copy = value < 0 ? 2 : std::min(value, 2);  // < 0: the default (2)
     } else if (k == "bs_wave_min_rows") {
         g_tune.bs_wave_min_rows = value >= 2 && value <= 4 ? value : 3;  // else the default
     } else if (k == "bs_tiles_per_slot") {

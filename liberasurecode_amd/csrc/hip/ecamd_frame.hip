@@ -271,6 +271,12 @@ static __device__ __forceinline__ u32x4 next_lane16(const u32x4& v)
     return u32x4{shl1(v.x), shl1(v.y), shl1(v.z), shl1(v.w)};
 }
 
+// the low n bytes of x (n <= 0: none, n >= 4: all)
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t x, int n)
+{
+    return n >= 4 ? x : n <= 0 ? 0u : x & ((1u << (8 * n)) - 1u);
+}
+
 // kDpp (knob frame_copy_dpp): the realigning path takes each lane's second aligned chunk from its
 // neighbour lane (next_lane16) and only the last lane of a wave loads its own.
 template <int kCopyU, bool kDpp>
@@ -299,7 +305,8 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
             const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int src = lo + c * 16;
             const int q = src >> 4;
-            const bool fast = c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
+            // the window lies inside the object (the payload's last, partial chunk included)
+            const bool fast = src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
             if (kDpp && delta) {  // every lane's aligned chunk (past the object: zeros), the neighbour's next;
                 // the wave's last lane loads its own second chunk in the same burst (the other lanes'
                 // offsets are out of range: no memory access)
@@ -327,8 +334,14 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
             const int src = lo + c * 16;
             const int q = src >> 4;
             u32x4 v;
-            if (c * 16 + 16 <= bs && src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size)) {
+            const bool in_obj = src + 16 <= size && (delta == 0 || (q << 4) + 32 <= size);
+            if (c * 16 + 16 <= bs && in_obj) {
                 v = delta ? window16(v0[u], v1[u], dw, by) : v0[u];
+            } else if (in_obj) {  // the payload's last, partial chunk inside the object:
+                // its window masked to the payload's bs - 16c bytes (the rest is zero padding)
+                v = delta ? window16(v0[u], v1[u], dw, by) : v0[u];
+                const int n = bs - c * 16;
+                v = u32x4{keep_bytes(v.x, n), keep_bytes(v.y, n - 4), keep_bytes(v.z, n - 8), keep_bytes(v.w, n - 12)};
             } else {  // ragged end: bytes, zero padded
                 int n = size - src;
                 n = n < 0 ? 0 : n;
@@ -374,9 +387,11 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // aligned store of payload bytes [p, p + 16) (p = 16ch - lo), realigned in registers from the two
 // aligned payload chunks under it when bs % 16 != 0 (Swift's 1 MiB segments at k = 10: bs = 104858);
 // the payload rows are read up to their 16-byte-rounded length, which the fragment layout reserves.
-// The straddling chunk is one lane's store too: the last 16 payload bytes of j-1, realigned, joined
-// with the first bytes of j.  Only the object's final partial chunk goes byte by byte, so nothing
-// is written outside [0, size).  Needs bs >= 32 (the host falls back to frame_join_kernel).
+// The straddling chunk is an ordinary lane too (round 4): its first load fetches the last 16 bytes
+// of payload j-1 (one unaligned load, same instruction as every lane's -- the loads address the
+// whole stripe) and its second the first chunk of payload j, so the same realignment merges them,
+// with no dependent loads after the burst.  Only the object's final partial chunk goes byte by byte,
+// so nothing is written outside [0, size).  Needs bs >= 32 (the host falls back to frame_join_kernel).
 template <int kCopyU, bool kDpp>
 __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
 {
@@ -384,9 +399,11 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
     const int bs = static_cast<int>(a.bs);
     const int bs16 = (bs + 15) & ~15;
     const int size = static_cast<int>(a.size);
+    const int fs = static_cast<int>(a.frag_stride);
     const uint32_t per_frag = static_cast<uint32_t>(bs / 16 + 2);
     const uint32_t tpf = (per_frag + T * kCopyU - 1) / (T * kCopyU);
     const uint32_t ntiles = tpf * static_cast<uint32_t>(k) * static_cast<uint32_t>(a.nstripes);
+    constexpr int kOut = static_cast<int>(0x80000000u);  // out of range: no memory access, zeros
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const uint32_t sj = t / tpf;
         const uint32_t tc = t - sj * tpf;
@@ -398,26 +415,32 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         const int c0 = lo >> 4, c1 = hi < size ? hi >> 4 : (size + 15) >> 4;
         const int delta = (16 - (lo & 15)) & 15;  // p mod 16 for every chunk of this payload
         const int dw = delta >> 2, by = delta & 3;
-        const uint8_t* pay = a.frags + static_cast<int64_t>(s) * a.stripe_stride + j * a.frag_stride + kHeaderBytes;
-        const auto rpay = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay), 0, bs16, 0x00020000);
+        const uint8_t* stripe = a.frags + static_cast<int64_t>(s) * a.stripe_stride;
+        const uint8_t* pay = stripe + j * fs + kHeaderBytes;
+        const int pay_off = j * fs + kHeaderBytes;  // payload j in the stripe (32-bit: copy_fits32)
+        const auto rstr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(stripe), 0,
+                                                            (k - 1) * fs + kHeaderBytes + bs16, 0x00020000);
         uint8_t* ob = a.obj + static_cast<int64_t>(s) * a.obj_stride;
         const auto robj = __builtin_amdgcn_make_buffer_rsrc(ob, 0, size, 0x00020000);
         u32x4 v0[kCopyU], v1[kCopyU];
+        bool strad[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
             const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
-            const bool fast = (ch << 4) >= lo && (ch << 4) + 16 <= hi;
-            if (kDpp && delta) {  // every lane's aligned chunk (outside the payload row: zeros); the
+            // the chunk payloads j-1 and j share: its window is (last 16 bytes of j-1 || chunk 0 of j)
+            strad[u] = delta && j > 0 && ch == c0 && (c0 << 4) + 16 <= hi;
+            const bool fast = ((ch << 4) >= lo || strad[u]) && (ch << 4) + 16 <= hi;
+            const int first = strad[u] ? pay_off - fs + bs - 16 : pay_off + (q << 4);
+            if (kDpp && delta) {  // every lane's aligned chunk (before the payload row: zeros); the
                 // wave's last lane loads its own second chunk in the same burst
-                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, q >= 0 ? q << 4 : static_cast<int>(0x80000000u),
-                                                              0, 2);
+                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rstr, q >= 0 || strad[u] ? first : kOut, 0, 2);
                 v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
-                    rpay, (threadIdx.x & 63u) == 63u && q >= -1 ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
+                    rstr, (threadIdx.x & 63u) == 63u && q >= -1 ? pay_off + (q << 4) + 16 : kOut, 0, 2);
             } else {
-                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rpay, fast ? q << 4 : static_cast<int>(0x80000000u), 0, 2);
-                v1[u] = __builtin_amdgcn_raw_buffer_load_b128(
-                    rpay, fast && delta ? (q << 4) + 16 : static_cast<int>(0x80000000u), 0, 2);
+                v0[u] = __builtin_amdgcn_raw_buffer_load_b128(rstr, fast ? first : kOut, 0, 2);
+                v1[u] = __builtin_amdgcn_raw_buffer_load_b128(rstr, fast && delta ? pay_off + (q << 4) + 16 : kOut, 0,
+                                                              2);
             }
         }
         if (kDpp && delta) {
@@ -433,28 +456,14 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
             const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             if (ch >= c1) continue;
             const int A = ch << 4;
-            if (A >= lo && A + 16 <= hi) {
+            if ((A >= lo || strad[u]) && A + 16 <= hi) {
                 __builtin_amdgcn_raw_buffer_store_b128(delta ? window16(v0[u], v1[u], dw, by) : v0[u], robj, A, 0, 2);
                 continue;
             }
-            if (A < lo && A + 16 <= hi) continue;  // the straddling chunk: below
+            if (A < lo && A + 16 <= hi) continue;  // (not reached: the straddling chunk is stored above)
             // the object's final partial chunk (bytes before lo, if any, from payload j-1)
             const int b1 = A + 16 < hi ? A + 16 : hi;
             for (int b = A; b < b1; ++b) ob[b] = b < lo ? pay[b - lo - a.frag_stride + bs] : pay[b - lo];
-        }
-        // chunk c0 straddles payloads j-1 and j: lane 0 of the payload's first tile
-        if (tc == 0 && (lo & 15) && (c0 << 4) + 16 <= hi && threadIdx.x == 0) {
-            const int d = lo - (c0 << 4);  // bytes from payload j-1
-            const auto rprev = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay - a.frag_stride), 0,
-                                                                 bs16, 0x00020000);
-            const int a0 = (bs - 16) & ~15, e = bs & 15;
-            const u32x4 l0 = __builtin_amdgcn_raw_buffer_load_b128(rprev, a0, 0, 2);
-            const u32x4 l1 = __builtin_amdgcn_raw_buffer_load_b128(rprev, e ? a0 + 16 : static_cast<int>(0x80000000u),
-                                                                   0, 2);
-            const u32x4 tail = e ? window16(l0, l1, e >> 2, e & 3) : l0;  // payload j-1 bytes [bs-16, bs)
-            const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(rpay, 0, 0, 2);
-            __builtin_amdgcn_raw_buffer_store_b128(window16(tail, head, (16 - d) >> 2, (16 - d) & 3), robj, c0 << 4,
-                                                   0, 2);
         }
     }
 }

@@ -179,6 +179,7 @@ struct BsEntry {
     int crc = 0;          // copy-through + payload CRC32 variant: position table sets (1, 2, 4), 0 = none;
                           //   + 8: lane-shift fold, + 16: nibble piece tables
     bool wave = false;    // one-wave workgroups, 4 KiB tiles (BitsliceStyle::threads 64)
+    std::vector<int> shifts;  // copy-through inputs' byte shifts (BitsliceStyle::in_shift), empty: none
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -256,9 +257,13 @@ const std::string& generator_fingerprint()
         lane.crc_lane = true;
         nib = lane;
         nib.crc_nib = true;
+        BitsliceStyle shifted = copy, crc_shifted = lane;
+        shifted.in_shift = {6};
+        crc_shifted.in_shift = {10};
         fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
-             bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + kBsNetworkVersion;
+             bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + bitslice_source(tiny, 0, shifted) +
+             bitslice_source(tiny, 0, crc_shifted) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -283,7 +288,7 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     BsEntry& e = *ep;
     const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                                              e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0,
-                                             e.wave);
+                                             e.wave, &e.shifts);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
@@ -378,7 +383,8 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
 // bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
 // keeps the kernel's module loaded until the caller has enqueued its launch.
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy, int crc, bool wave)
+                                std::shared_ptr<void>& hold, bool copy, int crc, bool wave,
+                                const std::vector<int>* in_shift)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
     if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
@@ -390,6 +396,17 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     depth = (copy || wave) ? 0 : bitslice_depth(depth, K);
     std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0)};
     key.insert(key.end(), coeff.begin(), coeff.end());
+    std::vector<int> shifts;  // realigned copy-through inputs: their own kernel (and cache entry)
+    if (copy && in_shift)
+        for (int j = 0; j < K; j++) {
+            const int v = j < static_cast<int>(in_shift->size()) ? ((*in_shift)[static_cast<size_t>(j)] & 15) : 0;
+            shifts.push_back(v);
+        }
+    if (std::find_if(shifts.begin(), shifts.end(), [](int v) { return v != 0; }) == shifts.end()) shifts.clear();
+    if (!shifts.empty()) {
+        key.push_back(-1);
+        key.insert(key.end(), shifts.begin(), shifts.end());
+    }
     std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
     std::unique_lock<std::mutex> lk(g_jit_mu);
     for (size_t i = 0; i < g_running.size();) {  // reap finished compilers, freeing their slots
@@ -417,6 +434,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->copy = copy;
         slot->crc = crc;
         slot->wave = wave;
+        slot->shifts = shifts;
         slot->arch = device_arch(dev);
         // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
         slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 && !wave ? 2 : 0);

@@ -197,6 +197,22 @@ __device__ __forceinline__ u32 bfi(u32 m, u32 x, u32 y)
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(x), "v"(y));
     return r;
 }
+// realigned 16-byte window D bytes into the 32-byte pair (lo, the next aligned chunk): the next
+// chunk is the neighbour lane's lo (DPP wave_shl:1); lane 63 has no neighbour and keeps `own`, the
+// chunk it loaded itself (bound_ctrl off: an out-of-range source leaves the old value)
+template <int D>
+__device__ __forceinline__ v4u rlg(v4u lo, v4u own)
+{
+    u32 w[8] = {lo[0], lo[1], lo[2], lo[3], 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[4 + i] = (u32)__builtin_amdgcn_update_dpp((int)own[i], (int)lo[i], 0x130, 0xf, 0xf, false);
+    constexpr int dw = D >> 2, by = D & 3;
+    if constexpr (by == 0)
+        return v4u{w[dw], w[dw + 1], w[dw + 2], w[dw + 3]};
+    else
+        return v4u{__builtin_amdgcn_alignbyte(w[dw + 1], w[dw], by), __builtin_amdgcn_alignbyte(w[dw + 2], w[dw + 1], by),
+                   __builtin_amdgcn_alignbyte(w[dw + 3], w[dw + 2], by), __builtin_amdgcn_alignbyte(w[dw + 4], w[dw + 3], by)};
+}
 // 16x16 bit transpose inside each 16-bit half of 16 dwords (an involution): bytes by v_perm,
 // then 4-, 2- and 1-bit blocks by shift + bit select.
 __device__ __forceinline__ void tr16(u32 (&A)[16])
@@ -310,6 +326,12 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     s << "extern \"C\" __global__ void __launch_bounds__(" << T << ") __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
       << wpe << ")))\n"
          "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
+    auto shift_of = [&](int j) {
+        return j < static_cast<int>(style.in_shift.size()) ? (style.in_shift[static_cast<size_t>(j)] & 15) : 0;
+    };
+    bool any_shift = false;
+    for (int j = 0; j < net.K; j++) any_shift = any_shift || shift_of(j) != 0;
+    if (any_shift && !D) s << "    const bool l63 = (threadIdx.x & 63u) == 63u;\n";
     auto ref = [](int v) {
         char b[24];
         if (v < 16)
@@ -449,9 +471,20 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         acc_init();
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
-            for (int c = 0; c < 4; c++)
-                s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
-                  << "] + off + " << c * 4096 << ", 0, 2);\n";
+            if (const int d = shift_of(j)) {  // aligned chunk + the neighbour's, realigned
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xa" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                      << "] - " << d << " + off + " << c * 4096 << ", 0, 2);\n";
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xh" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off[" << j
+                      << "] - " << d << " + off + " << c * 4096 + 16 << " : (i32)0x80000000u, 0, 2);\n";
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xq" << c << " = rlg<" << d << ">(xa" << c << ", xh" << c << ");\n";
+            } else {
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                      << "] + off + " << c * 4096 << ", 0, 2);\n";
+            }
             for (int c = 0; c < 4; c++)
                 s << "            __builtin_amdgcn_raw_buffer_store_b128(xq" << c << ", rcopy, cofs" << j << " + off + "
                   << c * 4096 << ", 0, 2);  // copy-through\n";
@@ -526,10 +559,19 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         }
         acc_init();
         for (int j = 0; j < net.K; j++) {
-            s << "        {  // input " << j << "\n            u32 P[16];\n"
-              << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
-              << "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
-              << "] + off + c * " << CS << ", 0, 2);\n"
+            s << "        {  // input " << j << "\n            u32 P[16];\n";
+            const int d = shift_of(j);
+            if (d) {  // aligned chunks + the neighbours', realigned (BitsliceStyle::in_shift)
+                s << "            v4u xa[4], xh[4];\n"
+                  << "#pragma unroll\n            for (int c = 0; c < 4; c++) xa[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off["
+                  << j << "] - " << d << " + off + c * " << CS << ", 0, 2);\n"
+                  << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off["
+                  << j << "] - " << d << " + off + c * " << CS << " + 16 : (i32)0x80000000u, 0, 2);\n";
+            }
+            s << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
+              << (d ? "                const v4u x = rlg<" + std::to_string(d) + ">(xa[c], xh[c]);\n"
+                    : "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" + std::to_string(j) +
+                          "] + off + c * " + std::to_string(CS) + ", 0, 2);\n")
               << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
               << (style.copy_through ? "                __builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" + std::to_string(j) +
                                                  " + off + c * " + std::to_string(CS) + ", 0, 2);  // copy-through\n"
@@ -623,7 +665,8 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 }
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
-                             bool crc, int crc_pos, bool crc_lane, bool crc_nib, bool wave)
+                             bool crc, int crc_pos, bool crc_lane, bool crc_nib, bool wave,
+                             const std::vector<int>* in_shift)
 {
     std::ostringstream s;
     // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
@@ -633,12 +676,18 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // of exactly 128 does not -- the occupancy follows the registers actually used)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     wave = wave && !crc;
-    if (copy || crc || wave)
-        s << "ecamd-bitslice-request 2\n" << R << " " << K << " " << cap << " " << depth << " "
+    bool shifted = false;
+    if (in_shift && (copy || crc))
+        for (int j = 0; j < K && j < static_cast<int>(in_shift->size()); j++) shifted = shifted || ((*in_shift)[j] & 15);
+    if (copy || crc || wave) {
+        s << "ecamd-bitslice-request " << (shifted ? 3 : 2) << "\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
               (crc && crc_nib ? 32 : 0) | (wave ? 64 | 128 : 0))
           << "\n";
-    else
+        if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
+            for (int j = 0; j < K; j++)
+                s << (j < static_cast<int>(in_shift->size()) ? ((*in_shift)[j] & 15) : 0) << (j + 1 < K ? " " : "\n");
+    } else
         s << "ecamd-bitslice-request 1\n" << R << " " << K << " " << cap << " " << depth << "\n";
     for (size_t i = 0; i < coeff.size(); i++) s << coeff[i] << ((i + 1) % static_cast<size_t>(K) ? " " : "\n");
     return s.str();
@@ -646,16 +695,28 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib,
-                            bool* wave, bool* budget2)
+                            bool* wave, bool* budget2, std::vector<int>* in_shift)
 {
     std::istringstream s(text);
     std::string magic;
     int version = 0, cp = 0;
-    if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || (version != 1 && version != 2)) return false;
+    if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version == 2 && (!(s >> cp) || cp < 0 || cp > 255 || (cp & 12) == 12 || depth != 0))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 255 || (cp & 12) == 12 || depth != 0))
         return false;  // copy / one-wave tiles: register loads
+    if (in_shift) in_shift->clear();
+    if (version == 3) {  // shifts: copy-through inputs only, at least one non-zero
+        if (!(cp & 1)) return false;
+        bool any = false;
+        for (int j = 0; j < K; j++) {
+            int v = 0;
+            if (!(s >> v) || v < 0 || v > 15) return false;
+            any = any || v;
+            if (in_shift) in_shift->push_back(v);
+        }
+        if (!any) return false;
+    }
     if ((cp & 2) && !(cp & 1)) return false;  // crc implies copy
     if ((cp & 192) && (cp & 2)) return false;  // the crc variant keeps 16 KiB tiles and its budget
     if (((cp >> 2) & 15) && !(cp & 2)) return false;  // bits 2-5 describe the crc variant

@@ -76,6 +76,12 @@ struct BitsliceStyle {
     // waves per SIMD the plain / copy-through form is built for (its register budget); 0: by R
     // (bitslice_waves_per_simd)
     int waves = 0;
+    // copy-through forms: input j's bytes start in_shift[j] (0..15) past a 16-byte boundary (object
+    // chunks at j*bs when bs % 16 != 0).  Non-zero: each lane loads the ALIGNED chunk under its
+    // window, takes the next one from its neighbour lane (DPP wave_shl:1; the wave's last lane loads
+    // its own) and realigns in registers (v_alignbyte, compile-time shift), instead of an unaligned
+    // 16-byte load.  Empty: every input aligned, or unaligned loads.
+    std::vector<int> in_shift;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
@@ -91,13 +97,15 @@ int bitslice_depth(int depth, int K);
 int bitslice_waves_per_simd(int R, bool crc = false);
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
+// in_shift (copy-through only): per-input byte shifts of BitsliceStyle::in_shift; any non-zero makes
+// a version-3 request (a line of K shifts after the flags).
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
                              bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false,
-                             bool wave = false);
+                             bool wave = false, const std::vector<int>* in_shift = nullptr);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
                             bool* crc_lane = nullptr, bool* crc_nib = nullptr, bool* wave = nullptr,
-                            bool* budget2 = nullptr);
+                            bool* budget2 = nullptr, std::vector<int>* in_shift = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

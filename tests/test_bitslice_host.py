@@ -103,3 +103,41 @@ def test_jitc_builds_a_request(tmp_path):
         bad.write_text(text)
         assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2
     assert not (tmp_path / "bad.co").exists()
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so") or not shutil.which("/opt/rocm/bin/hipcc"),
+                    reason="needs hiprtc and hipcc")
+@pytest.mark.parametrize("flags,tag", [(19, "crc"), (193, "wave_copy")])
+def test_jitc_builds_realigned_inputs(tmp_path, flags, tag):
+    """Version-3 requests (round 4): copy-through inputs at offsets that are not multiples of 16 --
+    Swift's object chunks j*104858 -- get aligned loads + the neighbour lane's chunk, realigned with
+    a compile-time shift (BitsliceStyle::in_shift); the crc variant and the one-wave copy form both
+    build, the crc one without scratch.  Malformed shift lines are refused."""
+    G = orc.generator(10, 4)
+    shifts = [(j * 104858) % 16 for j in range(10)]
+    rows = [" ".join(str(c) for c in G[100 + 10 * r:100 + 10 * (r + 1)]) for r in range(4)]
+    head = f"ecamd-bitslice-request 3\n4 10 16 0 {flags}\n"  # cap 16: the step the JIT reaches (40 spills)
+    req = tmp_path / "bs.req"
+    req.write_text(head + " ".join(map(str, shifts)) + "\n" + "\n".join(rows) + "\n")
+    out = tmp_path / "bs.co"
+    env = dict(os.environ, ECAMD_JIT_KEEP_SOURCE="1")
+    r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert out.read_bytes()[:4] == b"\x7fELF"
+    src = (tmp_path / "bs.hip").read_text()
+    assert "rlg<10>(" in src and "rlg<4>(" in src and "l63 ?" in src
+    assert "a.in_off[0] + off" in src  # input 0 (shift 0) keeps its plain loads
+    if tag == "crc":
+        hip = tmp_path / "k.hip"
+        hip.write_text("#include <hip/hip_runtime.h>\n" + src)
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S",
+                            "-o", str(tmp_path / "k.s"), str(hip)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "ScratchSize: 0" in (tmp_path / "k.s").read_text()
+    bad = tmp_path / "bad.req"
+    body = "\n".join(rows) + "\n"
+    for text in (head + "16 " + " ".join(map(str, shifts[1:])) + "\n" + body,  # shift out of range
+                 head + " ".join("0" for _ in shifts) + "\n" + body,          # no shift: version 2's job
+                 "ecamd-bitslice-request 3\n4 10 40 0 64\n" + " ".join(map(str, shifts)) + "\n" + body):  # no copy
+        bad.write_text(text)
+        assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2

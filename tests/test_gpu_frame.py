@@ -447,8 +447,11 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
     out = []
     _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2), "tune")
     try:
-        for cover in (1, 0):
+        # (frame_crc_cover, bs_realign): the crc variant reads the object chunks realigned from
+        # aligned loads + the neighbour lane's (default) or with unaligned loads
+        for cover, realign in ((1, 1), (0, 1), (1, 0)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_cover", cover), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
             n0 = _bs_launches()
             fb = F.FrameBatch(be, k, m, size, S)
             fb.encode(_upload_objects(objs, fb.obj_stride))
@@ -462,7 +465,8 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
     finally:
         _lib.dev().ecamd_tune(b"frame_crc_cover", 1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
-    assert np.array_equal(out[0], out[1])
+        _lib.dev().ecamd_tune(b"bs_realign", -1)
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[2], out[1])
     want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
     assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
 
@@ -505,13 +509,20 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
     S = 3
     objs = _objects(S, size, k * 13 + m + size)
     out = []
-    for padded in (1, 0):
-        _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
-        fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
-        fb.encode(_upload_objects(objs, fb.obj_stride))
-        out.append(fb.fragments())
-    _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
-    assert np.array_equal(out[0], out[1])
+    try:
+        # (frame_copy_padded, bitslice): the copy-through launch on the bitsliced kernel (one-wave
+        # tiles with realigned loads when the object chunks are unaligned, knob bs_wave_copy 2), on
+        # the LDS tables, and the split-then-encode path
+        for padded, mode in ((1, 2), (1, 0), (0, 1)):
+            _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+            fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
+            fb.encode(_upload_objects(objs, fb.obj_stride))
+            out.append(fb.fragments())
+    finally:
+        _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
+        _lib.dev().ecamd_tune(b"bitslice", 1)
+    assert np.array_equal(out[0], out[2]) and np.array_equal(out[1], out[2])
     want = expected_stripe(be, k, m, 0, objs[1], ct)
     assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
 
@@ -732,8 +743,11 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
             else [0, 2, 4, 6, k, k + 2, k + 4, k + 6][:m])
     frags, joined = [], []
     try:
-        for mode in (2, 0):
+        # (bitslice, bs_realign): unaligned object chunks (bs % 16 != 0) read as aligned chunks + the
+        # neighbour lane's, realigned (default), or with unaligned loads
+        for mode, realign in ((2, 1), (0, 1), (2, 0)):
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
             n0 = _bs_launches()
             # no checksum: with CRC32 a one-pass map that fits takes the fused CRC kernel instead
             fb = F.FrameBatch(be, k, m, size, S, checksum=ec_api.CHKSUM_NONE)
@@ -753,11 +767,12 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
             assert (ran > 0) == (mode == 2), (mode, ran)
     finally:
         _lib.dev().ecamd_tune(b"bitslice", 1)
-    assert np.array_equal(frags[0], frags[1])
+        _lib.dev().ecamd_tune(b"bs_realign", -1)
+    assert np.array_equal(frags[0], frags[1]) and np.array_equal(frags[2], frags[1])
     want = expected_stripe(be, k, m, 0, objs[1], ec_api.CHKSUM_NONE)
     assert all(frags[0][1, i].tobytes() == want[i] for i in range(k + m))
     if lost is not None:
-        assert np.array_equal(joined[0], joined[1])
+        assert np.array_equal(joined[0], joined[1]) and np.array_equal(joined[2], joined[1])
         for s in range(S):
             assert joined[0][s, :size].tobytes() == objs[s]
             assert (joined[0][s, size:] == 0xA5).all()

@@ -2,7 +2,8 @@
 """A/B of the framed CHKSUM_CRC32 encode of payloads that are not whole 16 KiB tiles (knob
 frame_crc_cover, round 4; development tool): 1 = the bitsliced crc variant over each payload's whole
 tiles + the codec and CRC32 of the rest + a finalize folding them (ecamd_frame_api.hip
-encode_crc_cover), 0 = the copy-through encode + a separate CRC pass over the payloads.  Shapes:
+encode_crc_cover; bs_realign 1 reads the unaligned object chunks as aligned chunks + the neighbour
+lane's, realigned, 0 with unaligned loads), 0 = the copy-through encode + a separate CRC pass.  Shapes:
 Swift's 1 MiB segments (2560 x 1 MiB, bs = 104858: 6 whole tiles + 6554 bytes), C3 objects 10 bytes
 longer (bs = 1048578), and 4 MiB objects at k = 10 (bs = 419432).  Fragments checked equal across
 the variants first; interleaved rounds, median; fraction of 8 TB/s of the algorithmic bytes (objects
@@ -19,7 +20,7 @@ import torch  # noqa: E402,F401
 from liberasurecode_amd import _lib, frame  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
-VARIANTS = {"cover_fused": 1, "codec_then_crc": 0}
+VARIANTS = {"cover_fused": (1, 1), "cover_fused_unaligned_loads": (1, 0), "codec_then_crc": (0, 1)}
 
 
 def main(rounds=5, reps=10):
@@ -34,7 +35,8 @@ def main(rounds=5, reps=10):
         _lib.check(d.ecamd_fill_splitmix(obj.ptr, fb.obj_stride, 0, 1, size, S, 0, 0x3C, st.handle), "fill")
         ref = None
         for v in VARIANTS.values():
-            d.ecamd_tune(b"frame_crc_cover", v)
+            d.ecamd_tune(b"frame_crc_cover", v[0])
+            d.ecamd_tune(b"bs_realign", v[1])
             fb.encode(obj, stream=st)
             st.synchronize()
             got = fb.fragments()
@@ -50,7 +52,8 @@ def main(rounds=5, reps=10):
         a, b = D.Event(), D.Event()
         for _ in range(rounds):
             for vname, v in VARIANTS.items():
-                d.ecamd_tune(b"frame_crc_cover", v)
+                d.ecamd_tune(b"frame_crc_cover", v[0])
+                d.ecamd_tune(b"bs_realign", v[1])
                 fb.encode(obj, stream=st)
                 a.record(st)
                 for _ in range(reps):
@@ -65,6 +68,7 @@ def main(rounds=5, reps=10):
         obj.free()
         del fb
     d.ecamd_tune(b"frame_crc_cover", 1)
+    d.ecamd_tune(b"bs_realign", -1)
     d.ecamd_tune(b"bitslice", 1)
 
 

@@ -69,7 +69,7 @@ def main(rounds=3, reps=10):
         obj.free()
         out.free()
         del fb
-    d.ecamd_tune(b"bs_wave_copy", 0)
+    d.ecamd_tune(b"bs_wave_copy", -1)
     d.ecamd_tune(b"bitslice", 1)
 
 
