@@ -245,6 +245,10 @@ struct Tuning {
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
+    Knob frame_tail_bs{1};        // framed RS encode of objects that do not fill the payloads: the payloads'
+                                  //   rest past the whole tiles by a streaming split + the plain bitsliced
+                                  //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
+                                  //   0 = the LDS-table copy-through launch
     Knob frame_crc_cover{1};      // framed CRC32 encode of payloads that are not whole 16 KiB tiles (Swift's
                                   //   1 MiB segments): the crc variant over the whole tiles + tail codec +
                                   //   tail CRC (ecamd_frame_api.hip encode_crc_cover); 0 = codec + CRC pass
@@ -336,6 +340,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_nib") return g_tune.frame_crc_nib;
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
+    if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "bs_realign") return g_tune.bs_realign;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
@@ -1247,7 +1252,7 @@ bool copy_aligned_payloads(const void* obj, const void* payload0, int64_t obj_st
 
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                   void* stream, int64_t obj_size, int64_t from)
+                   void* stream, int64_t obj_size, int64_t from, int64_t to)
 {
     std::shared_ptr<RsEntry> e;
     int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
@@ -1256,19 +1261,22 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
     if (obj_size < 0) obj_size = k * bs;
     if (obj_size > k * bs || !copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
         return fail(ECAMD_EINVAL, "copy-through encode needs 16-byte aligned objects and payloads");
-    if (from < 0 || from % 16 || from >= bs) return fail(ECAMD_EINVAL, "copy-through encode: bad range start");
-    // bytes [from, bs) of every payload: object chunk j from j*bs + from, payloads from + from
+    if (to < 0) to = bs;
+    if (from < 0 || from % 16 || to > bs || from >= to || (to < bs && to % 16))
+        return fail(ECAMD_EINVAL, "copy-through encode: bad range [%lld, %lld)", (long long)from, (long long)to);
+    // bytes [from, to) of every payload: object chunk j from j*bs + from, payloads from + from
+    const int64_t len = to - from;
     std::vector<int64_t> in_off, out_off, copy_off, in_len;
     for (int i : e->inputs) {
         in_off.push_back(static_cast<int64_t>(i) * bs + from);
         copy_off.push_back(static_cast<int64_t>(i) * frag_stride + from);
-        in_len.push_back(
-            std::max<int64_t>(0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(i) * bs) - from));
+        in_len.push_back(std::min(len, std::max<int64_t>(
+                                           0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(i) * bs) - from)));
     }
     for (int o : e->outputs) out_off.push_back(static_cast<int64_t>(o) * frag_stride + from);
     auto* p0 = static_cast<uint8_t*>(payload0);
     return map_apply_copy(*e, static_cast<const uint8_t*>(obj), obj_stride, in_off, p0,
-                          stripe_stride, out_off, p0, stripe_stride, copy_off, bs - from, nstripes, stream,
+                          stripe_stride, out_off, p0, stripe_stride, copy_off, len, nstripes, stream,
                           &in_len);
 }
 
@@ -1637,6 +1645,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_copy_stream = value;
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
+    } else if (k == "frame_tail_bs") {
+        g_tune.frame_tail_bs = value;  // 0 off, anything else on
     } else if (k == "frame_crc_cover") {
         g_tune.frame_crc_cover = value;  // 0 off, anything else on
     } else if (k == "bs_realign") {

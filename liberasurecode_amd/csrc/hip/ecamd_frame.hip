@@ -284,7 +284,8 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
 {
     const uint32_t T = blockDim.x;  // lanes per tile (64 / 128 / 256)
     const uint32_t per_frag = static_cast<uint32_t>((a.bs + 15) / 16);  // payload chunks
-    const uint32_t tpf = (per_frag + T * kCopyU - 1) / (T * kCopyU);
+    const uint32_t cfrom = static_cast<uint32_t>(a.from >> 4);           // first chunk copied
+    const uint32_t tpf = (per_frag - cfrom + T * kCopyU - 1) / (T * kCopyU);
     const uint32_t ntiles = tpf * static_cast<uint32_t>(a.k) * static_cast<uint32_t>(a.nstripes);
     const int bs = static_cast<int>(a.bs);
     const int size = static_cast<int>(a.size);
@@ -302,7 +303,7 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         u32x4 v0[kCopyU], v1[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
+            const int c = static_cast<int>(cfrom + (tc * kCopyU + u) * T + threadIdx.x);
             const int src = lo + c * 16;
             const int q = src >> 4;
             // the window lies inside the object (the payload's last, partial chunk included)
@@ -329,7 +330,7 @@ __global__ void __launch_bounds__(256) frame_split_stream_kernel(const SplitArgs
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int c = static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
+            const int c = static_cast<int>(cfrom + (tc * kCopyU + u) * T + threadIdx.x);
             if (c >= static_cast<int>(per_frag)) continue;
             const int src = lo + c * 16;
             const int q = src >> 4;

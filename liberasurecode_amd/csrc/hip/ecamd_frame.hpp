@@ -59,6 +59,7 @@ struct SplitArgs {
     int k;
     int nstripes;
     int aligned;     // object base / stride / bs all 16-byte multiples
+    int64_t from;    // streaming split only: payload bytes [from, bs) (a multiple of 16), 0 = all
 };
 
 struct JoinArgs {

@@ -389,12 +389,16 @@ int fused_image(int dev, bool legacy, int mb, const uint32_t** out, int tile = 8
 // copy-through encode + separate CRC pass instead.
 // Ranges per payload for the fused CRC kernels: enough work units (stripes x ranges) to fill the
 // chip, each a long sequential run of whole tiles.
+// q divides `tiles`: the smallest divisor that gives per_cu units per CU, else one tile per unit (odd
+// tile counts -- C3 objects 10 bytes long have 63 whole tiles per payload -- once took q = 1, one
+// unit per stripe: 0.51 of 8 TB/s instead of 0.6x).
 int fused_ranges(int dev, int64_t tiles, int nstripes, int default_per_cu)
 {
-    int q = 1;
     const int64_t per_cu = dev_tune("frame_crc_units") > 0 ? dev_tune("frame_crc_units") : default_per_cu;
-    while (tiles % (2 * q) == 0 && static_cast<int64_t>(nstripes) * q < per_cu * dev_cu_count(dev)) q *= 2;
-    return q;
+    const int64_t want = per_cu * dev_cu_count(dev);
+    for (int64_t q = 1; q < tiles; q++)
+        if (tiles % q == 0 && static_cast<int64_t>(nstripes) * q >= want) return static_cast<int>(q);
+    return static_cast<int>(std::max<int64_t>(1, tiles));
 }
 
 // crc_finalize_kernel over the q ranges of every payload of the batch and the 80-byte headers.
@@ -467,6 +471,43 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
 }
 
+// The rest [from, bs) of every payload of an RS copy-through encode whose first `from` bytes are
+// done (bytes [0, from) of the data payloads written): a streaming split copies the object chunks'
+// rest into the data payloads (zero padded past the object's end and through the 16-byte slack),
+// then the plain encode runs over the payloads' last n whole 4 KiB tiles [r16 - 4096 n, r16), r16 =
+// bs rounded up to 16 -- overlapping [0, from) where it recomputes the same parity bytes -- on the
+// bitsliced one-wave kernel the C3 encode uses.  The LDS-table copy-through launch it replaces spent
+// most of its time staging 40 KiB of tables per workgroup for ~2.5-6.5 KiB of work per stripe
+// (profiles/r04_swift_prof_*: 0.10-0.17 ms of a 1.3-1.5 ms encode).  ECAMD_EINVAL, nothing
+// launched, when it does not apply (payloads shorter than the tiles, 32-bit offsets, knob
+// frame_tail_bs 0).
+int encode_tail(int dev, const Code& c, const void* obj, int64_t obj_stride, uint64_t obj_size, uint8_t* frags,
+                int64_t ss, int64_t fs, int64_t bs, int nstripes, int64_t from, void* stream)
+{
+    constexpr int64_t kTile = 4096;
+    const int64_t r16 = (bs + 15) & ~int64_t(15);
+    const int64_t n = (r16 - from + kTile - 1) / kTile;
+    const int64_t t0 = r16 - n * kTile;
+    if (dev_tune("frame_tail_bs") == 0 || from <= 0 || from % 16 || from >= bs || t0 < 0 ||
+        !copy_fits32(c.k, fs, bs, static_cast<int64_t>(obj_size)) || dev_tune("frame_copy_stream") == 0)
+        return ECAMD_EINVAL;
+    SplitArgs sa{static_cast<const uint8_t*>(obj), obj_stride, static_cast<int64_t>(obj_size), frags, ss, fs, bs,
+                 c.k, nstripes, 0, from};
+    const CopyShape cs = copy_shape(bs);
+    const dim3 grid(copy_grid(dev, (r16 - from) / 16, c.k, nstripes, cs)), block(cs.threads);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool dpp = dev_tune("frame_copy_dpp") != 0;
+    if (cs.u == 1)
+        hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<1, true> : frame_split_stream_kernel<1, false>), grid, block,
+                           0, st, sa);
+    else
+        hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<4, true> : frame_split_stream_kernel<4, false>), grid, block,
+                           0, st, sa);
+    HIP_TRY(hipGetLastError());
+    const int rc = ecamd_rs_encode(c.k, c.m, frags + kHeaderBytes + t0, ss, fs, n * kTile, nstripes, stream);
+    return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail encode failed") : rc;
+}
+
 // Objects that do not fill k payloads of whole 16 KiB tiles (Swift's 1 MiB segments: bs = 104858,
 // object chunks at unaligned offsets j*bs, the last one 4 bytes short): the bitsliced crc variant
 // over the tiles every payload holds in full ([0, cover), cover = the last chunk's whole tiles),
@@ -503,9 +544,11 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
     if (rc) return rc;
     if (tail) {
         // from here on a failure is an error, not a fallback: part of the payloads is written
-        if ((rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, stream,
-                                 static_cast<int64_t>(obj_size), cover)))
-            return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail codec failed") : rc;
+        rc = encode_tail(dev, c, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, stream);
+        if (rc == ECAMD_EINVAL)
+            rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, stream,
+                                static_cast<int64_t>(obj_size), cover);
+        if (rc) return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail codec failed") : rc;
         HeaderArgs none{};
         if ((rc = run_crc(dev, legacy, true, frags, ss, fs, kHeaderBytes + cover, nf, tail, nstripes, tail_crc,
                           none, stream)))
@@ -608,8 +651,24 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
                                   frag_stride, bs, nstripes, stream);
             if (rc != ECAMD_EINVAL) return rc;
         }
-        rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes,
-                            stream, static_cast<int64_t>(obj_size));
+        // the whole 4 KiB tiles every payload holds on the copy-through launch, the rest by
+        // encode_tail (split + plain encode of the payloads' last tiles)
+        const int64_t last = static_cast<int64_t>(obj_size) - (k - 1) * bs;
+        const int64_t cover = last > 0 ? std::min(bs, last) / 4096 * 4096 : 0;
+        rc = ECAMD_EINVAL;
+        if (cover > 0 && cover < bs && dev_tune("frame_tail_bs") != 0) {
+            if ((rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, stream,
+                                     static_cast<int64_t>(obj_size), 0, cover)))
+                return rc;
+            rc = encode_tail(dev, c, d_obj, obj_stride, obj_size, frags, stripe_stride, frag_stride, bs, nstripes,
+                             cover, stream);
+            if (rc == ECAMD_EINVAL)
+                rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, stream,
+                                    static_cast<int64_t>(obj_size), cover);
+        } else {
+            rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes,
+                                stream, static_cast<int64_t>(obj_size));
+        }
         if (rc) return rc;
         return run_crc(dev, legacy_crc(), checksum == kChksumCrc32, frags, stripe_stride,
                        frag_stride, kHeaderBytes, k + m, bs, nstripes, nullptr,

@@ -41,10 +41,11 @@ int dev_tune(const char* key);                      // current value of an ecamd
 // (payload f of stripe s at payload0 + s*stripe_stride + f*frag_stride).  Objects of obj_size
 // bytes (< 0: k*bs) are zero-padded past their end (prepare_fragments_for_encode).  16-byte aligned
 // object base / stride and payloads; bs even (the object side may be read unaligned).  from > 0 (a
-// multiple of 16): only bytes [from, bs) of every payload (the rest of a partly fused encode).
+// multiple of 16): only bytes [from, bs) of every payload (the rest of a partly fused encode); to > 0:
+// only bytes [from, to).
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                   void* stream, int64_t obj_size = -1, int64_t from = 0);
+                   void* stream, int64_t obj_size = -1, int64_t from = 0, int64_t to = -1);
 
 // rs_vand decode straight into objects: the missing data fragments (at least one, -1 terminated
 // `missing`) are computed into their object positions (j*bs) and the available data inputs are

@@ -447,11 +447,13 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
     out = []
     _lib.check(_lib.dev().ecamd_tune(b"bitslice", 2), "tune")
     try:
-        # (frame_crc_cover, bs_realign): the crc variant reads the object chunks realigned from
-        # aligned loads + the neighbour lane's (default) or with unaligned loads
-        for cover, realign in ((1, 1), (0, 1), (1, 0)):
+        # (frame_crc_cover, bs_realign, frame_tail_bs): the crc variant reads the object chunks
+        # realigned from aligned loads + the neighbour lane's (default) or with unaligned loads; the
+        # payloads' rest by split + plain encode of their last tiles (default) or the LDS-table launch
+        for cover, realign, tail in ((1, 1, 1), (0, 1, 1), (1, 0, 1), (1, 1, 0)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_cover", cover), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
             n0 = _bs_launches()
             fb = F.FrameBatch(be, k, m, size, S)
             fb.encode(_upload_objects(objs, fb.obj_stride))
@@ -466,7 +468,8 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         _lib.dev().ecamd_tune(b"frame_crc_cover", 1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"bs_realign", -1)
-    assert np.array_equal(out[0], out[1]) and np.array_equal(out[2], out[1])
+        _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
+    assert all(np.array_equal(o, out[1]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
     assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
 
@@ -513,16 +516,19 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         # (frame_copy_padded, bitslice): the copy-through launch on the bitsliced kernel (one-wave
         # tiles with realigned loads when the object chunks are unaligned, knob bs_wave_copy 2), on
         # the LDS tables, and the split-then-encode path
-        for padded, mode in ((1, 2), (1, 0), (0, 1)):
+        # (+ frame_tail_bs: the payloads' rest past the whole tiles by split + plain encode, or not)
+        for padded, mode, tail in ((1, 2, 1), (1, 0, 1), (0, 1, 1), (1, 2, 0)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
             fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
     finally:
         _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
-    assert np.array_equal(out[0], out[2]) and np.array_equal(out[1], out[2])
+        _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
+    assert all(np.array_equal(o, out[2]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[1], ct)
     assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
 
