@@ -245,6 +245,8 @@ struct Tuning {
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
+    Knob frame_join_obj{1};       // systematic framed decode of payloads that are not 16-byte multiples: the
+                                  //   object-tiled join (frame_join_obj_kernel); 0 = payload-tiled stream join
     Knob frame_tail_bs{1};        // framed RS encode of objects that do not fill the payloads: the payloads'
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
@@ -341,6 +343,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
+    if (k == "frame_join_obj") return g_tune.frame_join_obj;
     if (k == "bs_realign") return g_tune.bs_realign;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
@@ -672,10 +675,9 @@ int launch_ptrs_stream(const ApplyArgs& a, int width, dim3 grid, dim3 block, siz
 // One-wave 4 KiB tiles for a bitsliced row group of `nrows` outputs (knobs bs_wave, bs_wave_min_rows,
 // bs_wave_copy); `narrow`: the group takes the bitsliced kernel below bitslice_min_rows for it.
 // Realigned copy-through inputs (knob bs_realign): the byte shift of each input's offset, and the
-// buffer size that keeps the realigned kernel inside the bytes it covers -- each input's last window
-// ends at in_off + cover and the aligned chunk under it at the next 16-byte boundary, which stays in
-// the object's last 16-byte granule (objects are 16-byte aligned).  No shift: `shifts` empty and
-// the records unchanged.
+// buffer size the realigned kernel needs -- each input's last window ends at in_off + cover and the
+// aligned chunk under it at the next 16-byte boundary, which stays in the object's last 16-byte
+// granule (objects are 16-byte aligned).  No shift: `shifts` empty and the records unchanged.
 uint32_t realign_records(const ApplyArgs& a, int K, int64_t cover, bool copy, std::vector<int>& shifts)
 {
     shifts.clear();
@@ -691,7 +693,9 @@ uint32_t realign_records(const ApplyArgs& a, int K, int64_t cover, bool copy, st
         shifts.clear();
         return a.in_records;
     }
-    return static_cast<uint32_t>(std::min<int64_t>(a.in_records, end));
+    // exactly `end`: the caller's records (max in_off + bs) may stop inside the last aligned chunk
+    // when bs is the covered range itself, and the buffer unit zeroes every dword past the records
+    return static_cast<uint32_t>(end);
 }
 
 bool bs_wave_tiles(int nrows, bool copy, bool* narrow, bool unaligned = false)
@@ -1645,6 +1649,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_copy_stream = value;
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
+    } else if (k == "frame_join_obj") {
+        g_tune.frame_join_obj = value;  // 0 off, anything else on
     } else if (k == "frame_tail_bs") {
         g_tune.frame_tail_bs = value;  // 0 off, anything else on
     } else if (k == "frame_crc_cover") {

@@ -473,6 +473,75 @@ template __global__ void frame_join_stream_kernel<4, false>(const JoinArgs, int)
 template __global__ void frame_join_stream_kernel<1, true>(const JoinArgs, int);
 template __global__ void frame_join_stream_kernel<4, true>(const JoinArgs, int);
 
+// fragments_to_string over OBJECT tiles (round 4, payloads that are not 16-byte multiples, bs >=
+// 4096 + 32): workgroup t writes object bytes [4096 tt, 4096 tt + 4096) of stripe s -- aligned
+// 4 KiB of the object, so no workgroup shares a cache line with another and no tile is partial
+// (the payload-tiled kernel above has a ragged last tile per payload and stores 1 KiB runs that
+// start mid-line).  A tile spans at most two payloads j0 = o0 / bs and j0 + 1.  Lane L stores
+// object chunk o = o0 + 16 L: the window [p, p + 16) of its payload, p = o - j*bs, realigned from
+// the aligned chunk under p and the next one, which is the neighbour lane's (DPP wave_shl:1; the
+// wave's last lane loads its own).  The chunk that straddles the boundary b1 = (j0 + 1) bs takes
+// payload j0's bytes [p, bs) -- its aligned chunk, and the next one it loads itself -- and payload
+// j0 + 1's first bytes, the neighbour lane's chunk; a lane whose window ends exactly at b1 loads its
+// next chunk itself too.  The object's final partial chunk goes byte by byte; nothing is written
+// past `size`.
+__global__ void __launch_bounds__(256) frame_join_obj_kernel(const JoinArgs a, int k)
+{
+    const int bs = static_cast<int>(a.bs);
+    const int bs16 = (bs + 15) & ~15;
+    const int size = static_cast<int>(a.size);
+    const int fs = static_cast<int>(a.frag_stride);
+    const uint32_t tpo = static_cast<uint32_t>((size + 4095) / 4096);
+    const uint32_t ntiles = tpo * static_cast<uint32_t>(a.nstripes);
+    constexpr int kOut = static_cast<int>(0x80000000u);
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t s = t / tpo;
+        const int o0 = static_cast<int>(t - s * tpo) * 4096;
+        const int j0 = o0 / bs;  // wave-uniform
+        const int b1 = (j0 + 1) * bs;
+        const int o = o0 + static_cast<int>(threadIdx.x) * 16;
+        const bool strad = o < b1 && o + 16 > b1 && b1 < size;
+        // the last lane of payload j0 (its window ends at or past b1): its next aligned chunk is not a
+        // neighbour's, which holds payload j0 + 1
+        const bool edge = o < b1 && o + 16 >= b1 && b1 < size;
+        const int j = o >= b1 ? j0 + 1 : j0;
+        const int p = o - j * bs;
+        const int q = p >> 4, d = p & 15;
+        const int pay = j * fs + kHeaderBytes;
+        const uint8_t* stripe = a.frags + static_cast<int64_t>(s) * a.stripe_stride;
+        const auto rstr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(stripe), 0,
+                                                            (k - 1) * fs + kHeaderBytes + bs16, 0x00020000);
+        uint8_t* ob = a.obj + static_cast<int64_t>(s) * a.obj_stride;
+        const auto robj = __builtin_amdgcn_make_buffer_rsrc(ob, 0, size, 0x00020000);
+        const bool last = (threadIdx.x & 63u) == 63u;
+        // one burst: every lane's aligned chunk; the wave's last lane its next one (the straddling
+        // lane's next is payload j0 + 1's first chunk); the straddling lane payload j0's next chunk
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rstr, o < size ? pay + (q << 4) : kOut, 0, 2);
+        const u32x4 own = __builtin_amdgcn_raw_buffer_load_b128(
+            rstr, last && o < size ? (strad ? pay + fs : pay + (q << 4) + 16) : kOut, 0, 2);
+        const u32x4 nx = __builtin_amdgcn_raw_buffer_load_b128(rstr, edge ? pay + (q << 4) + 16 : kOut, 0, 2);
+        const u32x4 n = next_lane16(v0);
+        const u32x4 v1 = last ? own : n;
+        if (o >= size) continue;
+        if (o + 16 <= size) {
+            u32x4 v = d ? window16(v0, edge ? nx : v1, d >> 2, d & 3) : v0;
+            if (strad) {  // bytes [0, c) from payload j0, the rest from payload j0 + 1's first chunk (v1)
+                const int c = b1 - o;
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                const u32x4 h = window16(z, v1, (16 - c) >> 2, (16 - c) & 3);  // c zero bytes, then v1
+                v = u32x4{keep_bytes(v.x, c) | h.x, keep_bytes(v.y, c - 4) | h.y, keep_bytes(v.z, c - 8) | h.z,
+                          keep_bytes(v.w, c - 12) | h.w};
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, robj, o, 0, 2);
+        } else {  // the object's final partial chunk
+            for (int b = o; b < size; ++b) {
+                const int jj = b / bs;
+                ob[b] = stripe[jj * fs + kHeaderBytes + (b - jj * bs)];
+            }
+        }
+    }
+}
+
 // fragments_to_string: object bytes [0, size) = data payloads 0..k-1 concatenated.
 __global__ void frame_join_kernel(const JoinArgs a)
 {

@@ -622,10 +622,13 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
         try:
             # (stream kernel, one workgroup per tile, lanes per tile, chunks per lane, DPP neighbour
             # chunks on the realigning path)
-            for knob, grid, lanes, u, dpp in ((1, 0, 256, 4, 0), (1, 1, 256, 4, 0), (0, 0, 256, 4, 0),
-                                              (1, 1, 64, 1, 0), (1, 1, 64, 4, 0), (1, 1, 128, 1, 0),
-                                              (1, 0, 64, 1, 0), (1, 1, 256, 1, 1), (1, 1, 64, 1, 1),
-                                              (1, 1, 256, 4, 1), (1, 0, 128, 1, 1)):
+            # the payload-tiled join (frame_join_obj 0) in every shape, then the object-tiled join
+            # (default for bs % 16 != 0, bs >= 4128)
+            for knob, grid, lanes, u, dpp, obj in ((1, 0, 256, 4, 0, 0), (1, 1, 256, 4, 0, 0), (0, 0, 256, 4, 0, 0),
+                                                   (1, 1, 64, 1, 0, 0), (1, 1, 64, 4, 0, 0), (1, 1, 128, 1, 0, 0),
+                                                   (1, 0, 64, 1, 0, 0), (1, 1, 256, 1, 1, 0), (1, 1, 64, 1, 1, 0),
+                                                   (1, 1, 256, 4, 1, 0), (1, 0, 128, 1, 1, 0), (1, 1, 256, 1, 1, 1)):
+                _lib.check(_lib.dev().ecamd_tune(b"frame_join_obj", obj), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_stream", knob), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_grid", grid), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"frame_copy_threads", lanes), "tune")
@@ -641,6 +644,7 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
             _lib.dev().ecamd_tune(b"frame_copy_threads", 0)
             _lib.dev().ecamd_tune(b"frame_copy_u", 0)
             _lib.dev().ecamd_tune(b"frame_copy_dpp", -1)
+            _lib.dev().ecamd_tune(b"frame_join_obj", 1)
         for i in range(1, len(got)):
             assert np.array_equal(got[0], got[i]), (size, i)
         for s in range(S):

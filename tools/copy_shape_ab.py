@@ -20,6 +20,10 @@ from liberasurecode_amd import device as D  # noqa: E402
 SHAPES = [(256, 4, 0), (64, 4, 0), (64, 1, 0), (128, 1, 0), (256, 1, 0)]
 if len(sys.argv) > 1 and sys.argv[1] == "dpp":  # round 4: knob frame_copy_dpp on the realigning path
     SHAPES = [(256, 1, 0), (256, 1, 1), (64, 1, 0), (64, 1, 1), (128, 1, 1), (256, 4, 1)]
+# round 4: the object-tiled join (knob frame_join_obj) beside the payload-tiled shapes; lanes 0 marks it
+OBJ = len(sys.argv) > 1 and sys.argv[1] == "obj"
+if OBJ:
+    SHAPES = [(256, 1, 1), (128, 1, 1), (0, 1, 1)]
 
 
 def main(rounds=5, reps=10):
@@ -28,7 +32,7 @@ def main(rounds=5, reps=10):
     cases = [("c3", frame.RS_VAND, 10, 4, 10 << 20, 256),
              ("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
              ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
-    if len(sys.argv) > 1 and sys.argv[1] == "dpp":
+    if len(sys.argv) > 1 and sys.argv[1] in ("dpp", "obj"):
         cases = [("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
                  ("c3_plus_6", frame.RS_VAND, 10, 4, (10 << 20) + 6 * 10, 256),
                  ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
@@ -48,6 +52,7 @@ def main(rounds=5, reps=10):
             d.ecamd_tune(b"frame_copy_threads", t)
             d.ecamd_tune(b"frame_copy_u", u)
             d.ecamd_tune(b"frame_copy_dpp", dp)
+            d.ecamd_tune(b"frame_join_obj", 1 if t == 0 else 0)
             fn()
             st.synchronize()
             got = fb.fragments() if enc else out.download()
@@ -65,6 +70,7 @@ def main(rounds=5, reps=10):
                 d.ecamd_tune(b"frame_copy_threads", t)
                 d.ecamd_tune(b"frame_copy_u", u)
                 d.ecamd_tune(b"frame_copy_dpp", dp)
+                d.ecamd_tune(b"frame_join_obj", 1 if t == 0 else 0)
                 fn()
                 a.record(st)
                 for _ in range(reps):
@@ -74,7 +80,8 @@ def main(rounds=5, reps=10):
                 times[(t, u, dp)].append(a.elapsed_ms(b) / reps)
         for (t, u, dp), ts in times.items():
             ms = statistics.median(ts)
-            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": dp, "tile_bytes": t * u * 16,
+            rec = {"op": tag, "lanes": t if t else "object_tiles_256", "chunks_per_lane": u, "dpp": dp,
+                   "tile_bytes": t * u * 16 if t else 4096,
                    "ms": round(ms, 4)}
             if not enc:
                 rec["frac"] = round(2 * S * size / (ms * 1e-3) / 8e12, 4)
@@ -85,6 +92,7 @@ def main(rounds=5, reps=10):
     d.ecamd_tune(b"frame_copy_threads", 0)
     d.ecamd_tune(b"frame_copy_u", 0)
     d.ecamd_tune(b"frame_copy_dpp", -1)
+    d.ecamd_tune(b"frame_join_obj", 1)
 
 
 if __name__ == "__main__":

@@ -10,4 +10,6 @@ tail -2 gpurun_out/r04_frame_tests_i.log
 timeout -k 10 300 python tools/cover_ab.py > gpurun_out/r04_cover_ab3.log 2>&1 || { echo "COVER rc=$?"; tail -20 gpurun_out/r04_cover_ab3.log; exit 1; }
 cat gpurun_out/r04_cover_ab3.log
 bash tools/gpu_prof_swift.sh || exit 1
+timeout -k 10 300 python tools/copy_shape_ab.py obj > gpurun_out/r04_join_obj_ab.log 2>&1 || { echo "OBJ rc=$?"; tail -20 gpurun_out/r04_join_obj_ab.log; exit 1; }
+cat gpurun_out/r04_join_obj_ab.log
 echo R04_I_OK
