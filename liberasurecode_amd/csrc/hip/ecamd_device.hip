@@ -245,8 +245,8 @@ struct Tuning {
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
-    Knob frame_join_obj{1};       // systematic framed decode of payloads that are not 16-byte multiples: the
-                                  //   object-tiled join (frame_join_obj_kernel); 0 = payload-tiled stream join
+    Knob frame_join_align{0};     // systematic framed decode: 1 = a payload's join tiles start on object chunks
+                                  //   that are multiples of the tile (whole aligned lines per workgroup)
     Knob frame_tail_bs{1};        // framed RS encode of objects that do not fill the payloads: the payloads'
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
@@ -343,7 +343,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
-    if (k == "frame_join_obj") return g_tune.frame_join_obj;
+    if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
@@ -1418,9 +1418,12 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     std::shared_ptr<void> hold;
     // crc_pos: position sets (1, 2, 4) + 8 for the lane-shift fold (which 5-8 outputs always take)
     // + 16 for nibble piece tables
-    std::vector<int> shifts;
-    const uint32_t in_records = realign_records(a, k, cover, true, shifts);
-    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos, false, &shifts);
+    // the crc variant keeps unaligned loads for object chunks at offsets that are not multiples of
+    // 16: the realigned form measured no faster there (Swift segments 1.496 vs 1.486 ms, 4 MiB
+    // objects 1.544 vs 1.542, profiles/r04_cover_ab2.log) and its larger register need spills at
+    // some shift patterns (C3 objects 10 bytes long), which then fall back to the codec + CRC pass
+    const uint32_t in_records = a.in_records;
+    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1649,8 +1652,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_copy_stream = value;
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
-    } else if (k == "frame_join_obj") {
-        g_tune.frame_join_obj = value;  // 0 off, anything else on
+    } else if (k == "frame_join_align") {
+        g_tune.frame_join_align = value > 0 ? 1 : 0;  // <= 0: off (the default)
     } else if (k == "frame_tail_bs") {
         g_tune.frame_tail_bs = value;  // 0 off, anything else on
     } else if (k == "frame_crc_cover") {

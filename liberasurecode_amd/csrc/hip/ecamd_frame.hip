@@ -393,15 +393,18 @@ __device__ __forceinline__ u32x4 window16(const u32x4& lo, const u32x4& hi, int 
 // whole stripe) and its second the first chunk of payload j, so the same realignment merges them,
 // with no dependent loads after the burst.  Only the object's final partial chunk goes byte by byte,
 // so nothing is written outside [0, size).  Needs bs >= 32 (the host falls back to frame_join_kernel).
+// tile_align (knob frame_join_align): a payload's tiles start at object chunks that are multiples of
+// the tile (T x kCopyU chunks), so every workgroup's stores cover whole aligned object lines; the
+// lanes before the payload's first chunk idle.
 template <int kCopyU, bool kDpp>
-__global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k)
+__global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a, int k, int tile_align)
 {
     const uint32_t T = blockDim.x;  // lanes per tile (64 / 128 / 256)
     const int bs = static_cast<int>(a.bs);
     const int bs16 = (bs + 15) & ~15;
     const int size = static_cast<int>(a.size);
     const int fs = static_cast<int>(a.frag_stride);
-    const uint32_t per_frag = static_cast<uint32_t>(bs / 16 + 2);
+    const uint32_t per_frag = static_cast<uint32_t>(bs / 16 + 2 + (tile_align ? T * kCopyU - 1 : 0));
     const uint32_t tpf = (per_frag + T * kCopyU - 1) / (T * kCopyU);
     const uint32_t ntiles = tpf * static_cast<uint32_t>(k) * static_cast<uint32_t>(a.nstripes);
     constexpr int kOut = static_cast<int>(0x80000000u);  // out of range: no memory access, zeros
@@ -414,6 +417,8 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         const int hi = lo + bs < size ? lo + bs : size;
         if (hi <= lo) continue;  // payload past the object's end (wave-uniform)
         const int c0 = lo >> 4, c1 = hi < size ? hi >> 4 : (size + 15) >> 4;
+        const int cb = tile_align ? c0 & ~static_cast<int>(T * kCopyU - 1) : c0;  // the tiles' first chunk
+        if (cb + static_cast<int>(tc * kCopyU * T) >= c1) continue;  // an aligned payload's spare last tile
         const int delta = (16 - (lo & 15)) & 15;  // p mod 16 for every chunk of this payload
         const int dw = delta >> 2, by = delta & 3;
         const uint8_t* stripe = a.frags + static_cast<int64_t>(s) * a.stripe_stride;
@@ -427,7 +432,7 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         bool strad[kCopyU];
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
+            const int ch = cb + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
             const int q = ((ch << 4) - lo) >> 4;  // aligned payload chunk under the window's start
             // the chunk payloads j-1 and j share: its window is (last 16 bytes of j-1 || chunk 0 of j)
             strad[u] = delta && j > 0 && ch == c0 && (c0 << 4) + 16 <= hi;
@@ -454,8 +459,8 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         }
 #pragma unroll
         for (int u = 0; u < kCopyU; ++u) {
-            const int ch = c0 + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
-            if (ch >= c1) continue;
+            const int ch = cb + static_cast<int>((tc * kCopyU + u) * T + threadIdx.x);
+            if (ch >= c1 || ch < c0) continue;  // (before c0: the idle lanes of an aligned first tile)
             const int A = ch << 4;
             if ((A >= lo || strad[u]) && A + 16 <= hi) {
                 __builtin_amdgcn_raw_buffer_store_b128(delta ? window16(v0[u], v1[u], dw, by) : v0[u], robj, A, 0, 2);
@@ -468,79 +473,10 @@ __global__ void __launch_bounds__(256) frame_join_stream_kernel(const JoinArgs a
         }
     }
 }
-template __global__ void frame_join_stream_kernel<1, false>(const JoinArgs, int);
-template __global__ void frame_join_stream_kernel<4, false>(const JoinArgs, int);
-template __global__ void frame_join_stream_kernel<1, true>(const JoinArgs, int);
-template __global__ void frame_join_stream_kernel<4, true>(const JoinArgs, int);
-
-// fragments_to_string over OBJECT tiles (round 4, payloads that are not 16-byte multiples, bs >=
-// 4096 + 32): workgroup t writes object bytes [4096 tt, 4096 tt + 4096) of stripe s -- aligned
-// 4 KiB of the object, so no workgroup shares a cache line with another and no tile is partial
-// (the payload-tiled kernel above has a ragged last tile per payload and stores 1 KiB runs that
-// start mid-line).  A tile spans at most two payloads j0 = o0 / bs and j0 + 1.  Lane L stores
-// object chunk o = o0 + 16 L: the window [p, p + 16) of its payload, p = o - j*bs, realigned from
-// the aligned chunk under p and the next one, which is the neighbour lane's (DPP wave_shl:1; the
-// wave's last lane loads its own).  The chunk that straddles the boundary b1 = (j0 + 1) bs takes
-// payload j0's bytes [p, bs) -- its aligned chunk, and the next one it loads itself -- and payload
-// j0 + 1's first bytes, the neighbour lane's chunk; a lane whose window ends exactly at b1 loads its
-// next chunk itself too.  The object's final partial chunk goes byte by byte; nothing is written
-// past `size`.
-__global__ void __launch_bounds__(256) frame_join_obj_kernel(const JoinArgs a, int k)
-{
-    const int bs = static_cast<int>(a.bs);
-    const int bs16 = (bs + 15) & ~15;
-    const int size = static_cast<int>(a.size);
-    const int fs = static_cast<int>(a.frag_stride);
-    const uint32_t tpo = static_cast<uint32_t>((size + 4095) / 4096);
-    const uint32_t ntiles = tpo * static_cast<uint32_t>(a.nstripes);
-    constexpr int kOut = static_cast<int>(0x80000000u);
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const uint32_t s = t / tpo;
-        const int o0 = static_cast<int>(t - s * tpo) * 4096;
-        const int j0 = o0 / bs;  // wave-uniform
-        const int b1 = (j0 + 1) * bs;
-        const int o = o0 + static_cast<int>(threadIdx.x) * 16;
-        const bool strad = o < b1 && o + 16 > b1 && b1 < size;
-        // the last lane of payload j0 (its window ends at or past b1): its next aligned chunk is not a
-        // neighbour's, which holds payload j0 + 1
-        const bool edge = o < b1 && o + 16 >= b1 && b1 < size;
-        const int j = o >= b1 ? j0 + 1 : j0;
-        const int p = o - j * bs;
-        const int q = p >> 4, d = p & 15;
-        const int pay = j * fs + kHeaderBytes;
-        const uint8_t* stripe = a.frags + static_cast<int64_t>(s) * a.stripe_stride;
-        const auto rstr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(stripe), 0,
-                                                            (k - 1) * fs + kHeaderBytes + bs16, 0x00020000);
-        uint8_t* ob = a.obj + static_cast<int64_t>(s) * a.obj_stride;
-        const auto robj = __builtin_amdgcn_make_buffer_rsrc(ob, 0, size, 0x00020000);
-        const bool last = (threadIdx.x & 63u) == 63u;
-        // one burst: every lane's aligned chunk; the wave's last lane its next one (the straddling
-        // lane's next is payload j0 + 1's first chunk); the straddling lane payload j0's next chunk
-        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rstr, o < size ? pay + (q << 4) : kOut, 0, 2);
-        const u32x4 own = __builtin_amdgcn_raw_buffer_load_b128(
-            rstr, last && o < size ? (strad ? pay + fs : pay + (q << 4) + 16) : kOut, 0, 2);
-        const u32x4 nx = __builtin_amdgcn_raw_buffer_load_b128(rstr, edge ? pay + (q << 4) + 16 : kOut, 0, 2);
-        const u32x4 n = next_lane16(v0);
-        const u32x4 v1 = last ? own : n;
-        if (o >= size) continue;
-        if (o + 16 <= size) {
-            u32x4 v = d ? window16(v0, edge ? nx : v1, d >> 2, d & 3) : v0;
-            if (strad) {  // bytes [0, c) from payload j0, the rest from payload j0 + 1's first chunk (v1)
-                const int c = b1 - o;
-                const u32x4 z = {0u, 0u, 0u, 0u};
-                const u32x4 h = window16(z, v1, (16 - c) >> 2, (16 - c) & 3);  // c zero bytes, then v1
-                v = u32x4{keep_bytes(v.x, c) | h.x, keep_bytes(v.y, c - 4) | h.y, keep_bytes(v.z, c - 8) | h.z,
-                          keep_bytes(v.w, c - 12) | h.w};
-            }
-            __builtin_amdgcn_raw_buffer_store_b128(v, robj, o, 0, 2);
-        } else {  // the object's final partial chunk
-            for (int b = o; b < size; ++b) {
-                const int jj = b / bs;
-                ob[b] = stripe[jj * fs + kHeaderBytes + (b - jj * bs)];
-            }
-        }
-    }
-}
+template __global__ void frame_join_stream_kernel<1, false>(const JoinArgs, int, int);
+template __global__ void frame_join_stream_kernel<4, false>(const JoinArgs, int, int);
+template __global__ void frame_join_stream_kernel<1, true>(const JoinArgs, int, int);
+template __global__ void frame_join_stream_kernel<4, true>(const JoinArgs, int, int);
 
 // fragments_to_string: object bytes [0, size) = data payloads 0..k-1 concatenated.
 __global__ void frame_join_kernel(const JoinArgs a)

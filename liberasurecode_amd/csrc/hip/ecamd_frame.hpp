@@ -96,9 +96,7 @@ __global__ void frame_join_kernel(const JoinArgs a);
 template <int kCopyU, bool kDpp>
 __global__ void frame_split_stream_kernel(const SplitArgs a);
 template <int kCopyU, bool kDpp>
-__global__ void frame_join_stream_kernel(const JoinArgs a, int k);
-// object-tiled form for payloads that are not 16-byte multiples (bs >= 4128, 16-byte aligned objects)
-__global__ void frame_join_obj_kernel(const JoinArgs a, int k);
+__global__ void frame_join_stream_kernel(const JoinArgs a, int k, int tile_align);
 __global__ void frame_verify_kernel(const CrcArgs a, const uint32_t* __restrict__ img_zlib,
                                     const uint32_t* __restrict__ img_legacy,
                                     const uint32_t* __restrict__ crc, int64_t bs,

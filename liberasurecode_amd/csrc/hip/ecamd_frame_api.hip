@@ -752,23 +752,19 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     JoinArgs ja{frags, stripe_stride, frag_stride, bs, static_cast<uint8_t*>(d_obj), obj_stride,
                 static_cast<int64_t>(obj_size), nstripes,
                 (a16(d_obj) && obj_stride % 16 == 0 && bs % 16 == 0) ? 1 : 0};
-    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && bs % 16 && bs >= 4096 + 32 &&
-        a16(d_obj) && obj_stride % 16 == 0 && dev_tune("frame_copy_stream") != 0 && dev_tune("frame_join_obj") != 0) {
-        // payloads that are not 16-byte multiples (Swift's segments): object-aligned 4 KiB tiles
-        const int64_t tiles = (static_cast<int64_t>(obj_size) + 4095) / 4096 * nstripes;
-        hipLaunchKernelGGL(frame_join_obj_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(tiles, int64_t{1} << 30))),
-                           dim3(256), 0, static_cast<hipStream_t>(stream), ja, k);
-    } else if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && bs >= 32 &&
+    if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && bs >= 32 &&
         dev_tune("frame_copy_stream") != 0) {
         const CopyShape cs = copy_shape(bs);
-        const dim3 grid(copy_grid(dev, bs / 16 + 2, k, nstripes, cs)), block(cs.threads);
+        const int align = dev_tune("frame_join_align") != 0 && a16(d_obj) && obj_stride % 16 == 0 ? 1 : 0;
+        const int64_t span = static_cast<int64_t>(cs.threads) * cs.u;
+        const dim3 grid(copy_grid(dev, bs / 16 + 2 + (align ? span - 1 : 0), k, nstripes, cs)), block(cs.threads);
         const bool dpp = dev_tune("frame_copy_dpp") != 0;
         if (cs.u == 1)
             hipLaunchKernelGGL((dpp ? frame_join_stream_kernel<1, true> : frame_join_stream_kernel<1, false>), grid,
-                               block, 0, static_cast<hipStream_t>(stream), ja, k);
+                               block, 0, static_cast<hipStream_t>(stream), ja, k, align);
         else
             hipLaunchKernelGGL((dpp ? frame_join_stream_kernel<4, true> : frame_join_stream_kernel<4, false>), grid,
-                               block, 0, static_cast<hipStream_t>(stream), ja, k);
+                               block, 0, static_cast<hipStream_t>(stream), ja, k, align);
     } else
         hipLaunchKernelGGL(frame_join_kernel,
                            dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),

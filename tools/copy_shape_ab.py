@@ -20,10 +20,9 @@ from liberasurecode_amd import device as D  # noqa: E402
 SHAPES = [(256, 4, 0), (64, 4, 0), (64, 1, 0), (128, 1, 0), (256, 1, 0)]
 if len(sys.argv) > 1 and sys.argv[1] == "dpp":  # round 4: knob frame_copy_dpp on the realigning path
     SHAPES = [(256, 1, 0), (256, 1, 1), (64, 1, 0), (64, 1, 1), (128, 1, 1), (256, 4, 1)]
-# round 4: the object-tiled join (knob frame_join_obj) beside the payload-tiled shapes; lanes 0 marks it
-OBJ = len(sys.argv) > 1 and sys.argv[1] == "obj"
-if OBJ:
-    SHAPES = [(256, 1, 1), (128, 1, 1), (0, 1, 1)]
+# round 4: join tiles starting on aligned object chunks (knob frame_join_align); dpp 2 marks them
+if len(sys.argv) > 1 and sys.argv[1] == "align":
+    SHAPES = [(256, 1, 1), (256, 1, 2), (128, 1, 1), (128, 1, 2)]
 
 
 def main(rounds=5, reps=10):
@@ -32,7 +31,7 @@ def main(rounds=5, reps=10):
     cases = [("c3", frame.RS_VAND, 10, 4, 10 << 20, 256),
              ("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
              ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
-    if len(sys.argv) > 1 and sys.argv[1] in ("dpp", "obj"):
+    if len(sys.argv) > 1 and sys.argv[1] in ("dpp", "align"):
         cases = [("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
                  ("c3_plus_6", frame.RS_VAND, 10, 4, (10 << 20) + 6 * 10, 256),
                  ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
@@ -51,8 +50,8 @@ def main(rounds=5, reps=10):
         for t, u, dp in SHAPES:
             d.ecamd_tune(b"frame_copy_threads", t)
             d.ecamd_tune(b"frame_copy_u", u)
-            d.ecamd_tune(b"frame_copy_dpp", dp)
-            d.ecamd_tune(b"frame_join_obj", 1 if t == 0 else 0)
+            d.ecamd_tune(b"frame_copy_dpp", 1 if dp else 0)
+            d.ecamd_tune(b"frame_join_align", 1 if dp == 2 else 0)
             fn()
             st.synchronize()
             got = fb.fragments() if enc else out.download()
@@ -69,8 +68,8 @@ def main(rounds=5, reps=10):
             for t, u, dp in SHAPES:
                 d.ecamd_tune(b"frame_copy_threads", t)
                 d.ecamd_tune(b"frame_copy_u", u)
-                d.ecamd_tune(b"frame_copy_dpp", dp)
-                d.ecamd_tune(b"frame_join_obj", 1 if t == 0 else 0)
+                d.ecamd_tune(b"frame_copy_dpp", 1 if dp else 0)
+                d.ecamd_tune(b"frame_join_align", 1 if dp == 2 else 0)
                 fn()
                 a.record(st)
                 for _ in range(reps):
@@ -80,8 +79,8 @@ def main(rounds=5, reps=10):
                 times[(t, u, dp)].append(a.elapsed_ms(b) / reps)
         for (t, u, dp), ts in times.items():
             ms = statistics.median(ts)
-            rec = {"op": tag, "lanes": t if t else "object_tiles_256", "chunks_per_lane": u, "dpp": dp,
-                   "tile_bytes": t * u * 16 if t else 4096,
+            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": 1 if dp else 0, "aligned_tiles": dp == 2,
+                   "tile_bytes": t * u * 16,
                    "ms": round(ms, 4)}
             if not enc:
                 rec["frac"] = round(2 * S * size / (ms * 1e-3) / 8e12, 4)
@@ -92,7 +91,7 @@ def main(rounds=5, reps=10):
     d.ecamd_tune(b"frame_copy_threads", 0)
     d.ecamd_tune(b"frame_copy_u", 0)
     d.ecamd_tune(b"frame_copy_dpp", -1)
-    d.ecamd_tune(b"frame_join_obj", 1)
+    d.ecamd_tune(b"frame_join_align", -1)
 
 
 if __name__ == "__main__":
