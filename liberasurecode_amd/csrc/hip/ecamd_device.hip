@@ -245,8 +245,11 @@ struct Tuning {
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
-    Knob frame_join_align{0};     // systematic framed decode: 1 = a payload's join tiles start on object chunks
-                                  //   that are multiples of the tile (whole aligned lines per workgroup)
+    Knob frame_join_align{2};     // systematic framed decode: a payload's join tiles start on object chunks that
+                                  //   are multiples of the tile (whole aligned lines per workgroup): 1 always,
+                                  //   2 (default) on the realigning path (bs % 16 != 0): Swift segments
+                                  //   0.754 -> 0.766, C3 + 6 B 0.689 -> 0.792 of 8 TB/s with 4 KiB tiles
+                                  //   (profiles/r04_join_align_ab.log); 0 never
     Knob frame_tail_bs{1};        // framed RS encode of objects that do not fill the payloads: the payloads'
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
@@ -1653,7 +1656,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "frame_crc_fused") {
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_join_align") {
-        g_tune.frame_join_align = value > 0 ? 1 : 0;  // <= 0: off (the default)
+        g_tune.frame_join_align = value < 0 ? 2 : std::min(value, 2);  // < 0: the default (2)
     } else if (k == "frame_tail_bs") {
         g_tune.frame_tail_bs = value;  // 0 off, anything else on
     } else if (k == "frame_crc_cover") {

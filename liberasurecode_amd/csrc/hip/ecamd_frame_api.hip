@@ -755,7 +755,8 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     if (copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size)) && bs >= 32 &&
         dev_tune("frame_copy_stream") != 0) {
         const CopyShape cs = copy_shape(bs);
-        const int align = dev_tune("frame_join_align") != 0 && a16(d_obj) && obj_stride % 16 == 0 ? 1 : 0;
+        const int ja_knob = dev_tune("frame_join_align");
+        const int align = (ja_knob == 1 || (ja_knob == 2 && bs % 16)) && a16(d_obj) && obj_stride % 16 == 0 ? 1 : 0;
         const int64_t span = static_cast<int64_t>(cs.threads) * cs.u;
         const dim3 grid(copy_grid(dev, bs / 16 + 2 + (align ? span - 1 : 0), k, nstripes, cs)), block(cs.threads);
         const bool dpp = dev_tune("frame_copy_dpp") != 0;

@@ -644,7 +644,7 @@ def test_frame_systematic_decode_stream_join(F, name, k, m, hd, missing):
             _lib.dev().ecamd_tune(b"frame_copy_threads", 0)
             _lib.dev().ecamd_tune(b"frame_copy_u", 0)
             _lib.dev().ecamd_tune(b"frame_copy_dpp", -1)
-            _lib.dev().ecamd_tune(b"frame_join_align", 0)
+            _lib.dev().ecamd_tune(b"frame_join_align", -1)
         for i in range(1, len(got)):
             assert np.array_equal(got[0], got[i]), (size, i)
         for s in range(S):
