@@ -242,6 +242,8 @@ struct Tuning {
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
+    Knob bs_prefetch{0};          // one-wave bitsliced kernel: chunks (0, 2, 4) of the next input loaded before the
+                                  //   current input's network (BitsliceStyle::prefetch)
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
@@ -348,6 +350,7 @@ int dev_tune(const char* key)
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
+    if (k == "bs_prefetch") return g_tune.bs_prefetch;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
     return 0;
@@ -373,7 +376,7 @@ struct ecamd_map {
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
                                 std::shared_ptr<void>& hold, bool copy = false, int crc = 0, bool wave = false,
-                                const std::vector<int>* in_shift = nullptr);
+                                const std::vector<int>* in_shift = nullptr, int prefetch = 0);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
                     const std::shared_ptr<void>& hold, int threads = 256);
 }  // namespace ecamd
@@ -749,7 +752,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     std::vector<int> shifts;
     const uint32_t in_records = realign_records(a, K, cover, copy_off != nullptr, shifts);
     hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, wave ? 0 : static_cast<int>(g_tune.bitslice_depth),
-                                         mode == 2, hold, copy_off != nullptr, 0, wave, &shifts);
+                                         mode == 2, hold, copy_off != nullptr, 0, wave, &shifts,
+                                         wave ? static_cast<int>(g_tune.bs_prefetch) : 0);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1661,6 +1665,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_tail_bs = value;  // 0 off, anything else on
     } else if (k == "frame_crc_cover") {
         g_tune.frame_crc_cover = value;  // 0 off, anything else on
+    } else if (k == "bs_prefetch") {
+        g_tune.bs_prefetch = value == 2 || value == 4 ? value : 0;  // else 0 (the default)
     } else if (k == "bs_realign") {
         g_tune.bs_realign = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_unfused") {

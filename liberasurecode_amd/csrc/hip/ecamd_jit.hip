@@ -180,6 +180,7 @@ struct BsEntry {
                           //   + 8: lane-shift fold, + 16: nibble piece tables
     bool wave = false;    // one-wave workgroups, 4 KiB tiles (BitsliceStyle::threads 64)
     std::vector<int> shifts;  // copy-through inputs' byte shifts (BitsliceStyle::in_shift), empty: none
+    int prefetch = 0;         // one-wave form: chunks of the next input loaded ahead (BitsliceStyle::prefetch)
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -257,13 +258,14 @@ const std::string& generator_fingerprint()
         lane.crc_lane = true;
         nib = lane;
         nib.crc_nib = true;
-        BitsliceStyle shifted = copy, crc_shifted = lane;
+        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave;
+        wave_pf.prefetch = 4;
         shifted.in_shift = {6};
         crc_shifted.in_shift = {10};
         fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
              bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + bitslice_source(tiny, 0, shifted) +
-             bitslice_source(tiny, 0, crc_shifted) + kBsNetworkVersion;
+             bitslice_source(tiny, 0, crc_shifted) + bitslice_source(tiny5, 0, wave_pf) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -288,7 +290,7 @@ void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
     BsEntry& e = *ep;
     const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                                              e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0,
-                                             e.wave, &e.shifts);
+                                             e.wave, &e.shifts, e.prefetch);
     char name[32];
     std::snprintf(name, sizeof(name), "%016llx",
                   static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
@@ -384,7 +386,7 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
 // keeps the kernel's module loaded until the caller has enqueued its launch.
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
                                 std::shared_ptr<void>& hold, bool copy, int crc, bool wave,
-                                const std::vector<int>* in_shift)
+                                const std::vector<int>* in_shift, int prefetch)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
     if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
@@ -394,7 +396,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     copy = copy || crc;
     wave = wave && !crc;
     depth = (copy || wave) ? 0 : bitslice_depth(depth, K);
-    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0)};
+    prefetch = wave && (prefetch == 2 || prefetch == 4) ? prefetch : 0;
+    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0) | (prefetch << 9)};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::vector<int> shifts;  // realigned copy-through inputs: their own kernel (and cache entry)
     if (copy && in_shift)
@@ -435,6 +438,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->crc = crc;
         slot->wave = wave;
         slot->shifts = shifts;
+        slot->prefetch = prefetch;
         slot->arch = device_arch(dev);
         // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
         slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 && !wave ? 2 : 0);

@@ -558,6 +558,18 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                   << j << "] * a.copy_step);\n";
         }
         acc_init();
+        // prefetch (one-wave form): the first PF chunks of input j + 1 are loaded into xn[] before
+        // input j's network (not for realigned inputs, which take their loads at their turn)
+        const int PF = (T == 64 && (style.prefetch == 2 || style.prefetch == 4)) ? style.prefetch : 0;
+        auto pre = [&](int j) { return PF > 0 && j < net.K && shift_of(j) == 0; };
+        auto load_next = [&](int j) {
+            s << "#pragma unroll\n            for (int c = 0; c < " << PF << "; c++) xn[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off["
+              << j << "] + off + c * " << CS << ", 0, 2);\n";
+        };
+        if (PF) {
+            s << "        v4u xn[" << PF << "];\n";
+            if (pre(0)) load_next(0);
+        }
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
             const int d = shift_of(j);
@@ -568,17 +580,22 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                   << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off["
                   << j << "] - " << d << " + off + c * " << CS << " + 16 : (i32)0x80000000u, 0, 2);\n";
             }
+            const std::string ld = "__builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" + std::to_string(j) +
+                                   "] + off + c * " + std::to_string(CS) + ", 0, 2)";
             s << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
               << (d ? "                const v4u x = rlg<" + std::to_string(d) + ">(xa[c], xh[c]);\n"
-                    : "                const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" + std::to_string(j) +
-                          "] + off + c * " + std::to_string(CS) + ", 0, 2);\n")
+                    : pre(j) ? "                const v4u x = c < " + std::to_string(PF) + " ? xn[c < " + std::to_string(PF) +
+                                   " ? c : 0] : " + ld + ";\n"
+                             : "                const v4u x = " + ld + ";\n")
               << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
               << (style.copy_through ? "                __builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" + std::to_string(j) +
                                                  " + off + c * " + std::to_string(CS) + ", 0, 2);  // copy-through\n"
                                            : std::string())
               << "            }\n"
-              << (style.copy_through ? "            __builtin_amdgcn_sched_barrier(0);  // stores leave before the network\n"
-                                     : "");
+              ;
+            if (pre(j + 1)) load_next(j + 1);  // the next input's loads go out before this network
+            if (style.copy_through || pre(j + 1))
+                s << "            __builtin_amdgcn_sched_barrier(0);  // loads / stores leave before the network\n";
             network(j);
             s << "        }\n";
         }
@@ -666,23 +683,25 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
                              bool crc, int crc_pos, bool crc_lane, bool crc_nib, bool wave,
-                             const std::vector<int>* in_shift)
+                             const std::vector<int>* in_shift, int prefetch)
 {
     std::ostringstream s;
     // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
     // sets, bit 4 lane-shift fold, bit 5 nibble piece tables, bit 6 one-wave tiles (not with crc),
     // bit 7 the register budget of 2 waves per SIMD (set with bit 6: the compiler then keeps the
     // dense decode networks of <= 4 outputs in ~128 VGPRs without spilling, which a 4-wave budget
-    // of exactly 128 does not -- the occupancy follows the registers actually used)
+    // of exactly 128 does not -- the occupancy follows the registers actually used), bits 8-10 the
+    // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     wave = wave && !crc;
+    const int pf = wave && (prefetch == 2 || prefetch == 4) ? prefetch : 0;
     bool shifted = false;
     if (in_shift && (copy || crc))
         for (int j = 0; j < K && j < static_cast<int>(in_shift->size()); j++) shifted = shifted || ((*in_shift)[j] & 15);
     if (copy || crc || wave) {
         s << "ecamd-bitslice-request " << (shifted ? 3 : 2) << "\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
-              (crc && crc_nib ? 32 : 0) | (wave ? 64 | 128 : 0))
+              (crc && crc_nib ? 32 : 0) | (wave ? 64 | 128 : 0) | (pf << 8))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -695,7 +714,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib,
-                            bool* wave, bool* budget2, std::vector<int>* in_shift)
+                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch)
 {
     std::istringstream s(text);
     std::string magic;
@@ -703,8 +722,11 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 255 || (cp & 12) == 12 || depth != 0))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 2047 || (cp & 12) == 12 || depth != 0))
         return false;  // copy / one-wave tiles: register loads
+    const int pf = (cp >> 8) & 7;
+    if ((pf != 0 && pf != 2 && pf != 4) || (pf && !(cp & 64))) return false;  // prefetch: one-wave form only
+    if (prefetch) *prefetch = pf;
     if (in_shift) in_shift->clear();
     if (version == 3) {  // shifts: copy-through inputs only, at least one non-zero
         if (!(cp & 1)) return false;

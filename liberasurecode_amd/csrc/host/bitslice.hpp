@@ -82,6 +82,10 @@ struct BitsliceStyle {
     // its own) and realigns in registers (v_alignbyte, compile-time shift), instead of an unaligned
     // 16-byte load.  Empty: every input aligned, or unaligned loads.
     std::vector<int> in_shift;
+    // one-wave register form: chunks (0, 2 or 4) of input j + 1 loaded before input j's network, so a
+    // wave has the next input's loads in flight while it computes (the compiler otherwise issues each
+    // input's loads right before its use and waits for them at once)
+    int prefetch = 0;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
@@ -101,11 +105,12 @@ int bitslice_waves_per_simd(int R, bool crc = false);
 // a version-3 request (a line of K shifts after the flags).
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
                              bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false,
-                             bool wave = false, const std::vector<int>* in_shift = nullptr);
+                             bool wave = false, const std::vector<int>* in_shift = nullptr, int prefetch = 0);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
                             bool* crc_lane = nullptr, bool* crc_nib = nullptr, bool* wave = nullptr,
-                            bool* budget2 = nullptr, std::vector<int>* in_shift = nullptr);
+                            bool* budget2 = nullptr, std::vector<int>* in_shift = nullptr,
+                            int* prefetch = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

@@ -58,8 +58,9 @@ int main(int argc, char** argv)
     bool copy = false, crc = false, crc_lane = false, crc_nib = false, wave = false, budget2 = false;
     int crc_pos = 1;
     std::vector<int> shifts;
+    int prefetch = 0;
     if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy, &crc, &crc_pos, &crc_lane,
-                                       &crc_nib, &wave, &budget2, &shifts)) {
+                                       &crc_nib, &wave, &budget2, &shifts, &prefetch)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
@@ -72,6 +73,7 @@ int main(int argc, char** argv)
     style.threads = wave ? 64 : 256;
     style.waves = budget2 ? 2 : 0;
     style.in_shift = shifts;
+    style.prefetch = prefetch;
     if (const char* v = std::getenv("ECAMD_BS_WPE")) style.waves = std::atoi(v);  // experiment only
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;

@@ -141,3 +141,25 @@ def test_jitc_builds_realigned_inputs(tmp_path, flags, tag):
                  "ecamd-bitslice-request 3\n4 10 40 0 64\n" + " ".join(map(str, shifts)) + "\n" + body):  # no copy
         bad.write_text(text)
         assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs hiprtc")
+def test_jitc_prefetch_flag(tmp_path):
+    """Flag bits 8-10 (round 4): the one-wave form loads the first 2 / 4 chunks of the next input before
+    the current input's network (BitsliceStyle::prefetch); other values, or the flag without one-wave
+    tiles, are refused."""
+    G = orc.generator(10, 4)
+    rows = "\n".join(" ".join(str(c) for c in G[100 + 10 * r:100 + 10 * (r + 1)]) for r in range(4)) + "\n"
+    env = dict(os.environ, ECAMD_JIT_KEEP_SOURCE="1")
+    for pf in (2, 4):
+        req = tmp_path / f"pf{pf}.req"
+        req.write_text(f"ecamd-bitslice-request 2\n4 10 96 0 {192 | (pf << 8)}\n" + rows)
+        out = tmp_path / f"pf{pf}.co"
+        r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        src = (tmp_path / f"pf{pf}.hip").read_text()
+        assert f"v4u xn[{pf}];" in src and "xn[c] = __builtin_amdgcn_raw_buffer_load_b128" in src
+    bad = tmp_path / "bad.req"
+    for flags in (192 | (3 << 8), 1 | (4 << 8), 192 | (6 << 8)):
+        bad.write_text(f"ecamd-bitslice-request 2\n4 10 96 0 {flags}\n" + rows)
+        assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2

@@ -35,9 +35,11 @@ C2 = (4, 2, 64 << 10, 4096, {"encode": None, "decode": [0, 1], "decode_mixed": [
 # 16 KiB tiles (decodes spilled there and fell back to the tables).  Now bs_wave 1 is the default
 # for 3-4-output maps.
 VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave": 0, "bitslice_min_rows": 4}},
+            # round 4, later: the next input's chunks loaded before each network (knob bs_prefetch)
+            "c3pf": {"wave1": {}, "pf2": {"bs_prefetch": 2}, "pf4": {"bs_prefetch": 4}},
             "c2": {"tables": {}, "wave_2rows": {"bs_wave_min_rows": 2}},
             "c5": {"wave0": {}, "wave2": {"bs_wave": 2}}}
-DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0}
+DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": 0}
 
 
 def launches():
@@ -54,7 +56,7 @@ def apply(d, knobs):
 
 
 def run(cfg, rounds=3, n=30, skip=10):
-    K, M, F, S, ops = {"c3": C3, "c2": C2, "c5": C5}[cfg]
+    K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)
