@@ -242,8 +242,13 @@ struct Tuning {
                                   //   position set (C3 0.659 -> 0.686 of 8 TB/s against the butterfly
                                   //   with 2 sets, profiles/r03_fused_sweep_lane.log)
     Knob frame_crc_bs_nib{0};     // bitsliced crc variant: nibble piece tables (bitslice.hpp crc_nib)
-    Knob bs_prefetch{0};          // one-wave bitsliced kernel: chunks (0, 2, 4) of the next input loaded before the
-                                  //   current input's network (BitsliceStyle::prefetch)
+    Knob bs_prefetch{2};          // one-wave bitsliced copy-through kernel: chunks (0, 2, 4) of the next input
+                                  //   loaded before the current input's copy stores and network
+                                  //   (BitsliceStyle::prefetch). On GFX9 vmcnt retires loads and stores in
+                                  //   issue order, so without it every input's loads also wait for the
+                                  //   previous input's copy stores: C3 framed encode 0.657 -> 0.721, decode-join
+                                  //   0.637 -> 0.747 (profiles/r04_frame_wave_pf_ab2.log). Plain maps: neutral
+                                  //   (profiles/r04_bs_prefetch_ab.log), so they keep none
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
@@ -289,12 +294,12 @@ struct Tuning {
                                   //   0.733 -> 0.746, decode {0,1,2,3} 0.734 -> 0.742, mixed {0,5,10,13}
                                   //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
     Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (2..4)
-    Knob bs_wave_copy{2};         //   copy-through maps (framed encode / decode-join): 1 too, 2 (default) when
-                                  //   their inputs start at offsets that are not multiples of 16 (object
-                                  //   chunks j*bs, realigned loads -- knob bs_realign): Swift segments'
-                                  //   encode 0.590 -> 0.626 of 8 TB/s against the LDS-table stream kernel,
-                                  //   while aligned C3 keeps the tables (0.692 vs 0.656) and so does the
-                                  //   decode-join (aligned inputs; profiles/r04_frame_wave_ab2.log); 0 never
+    Knob bs_wave_copy{1};         //   copy-through maps (framed encode / decode-join): 1 (default) too, 2 only
+                                  //   when their inputs start at offsets that are not multiples of 16, 0 never.
+                                  //   With the prefetch (bs_prefetch) the one-wave form beats the LDS-table
+                                  //   stream kernel: C3 framed encode 0.694 -> 0.721, decode-join 0.739 ->
+                                  //   0.747, Swift decode-join 0.571 -> 0.603; Swift encode ties (0.64;
+                                  //   profiles/r04_frame_wave_pf_ab2.log)
     Knob bs_tiles_per_slot{16};   // ecamd_bs_kernel: the same for bitsliced passes (0: one launch;
                                   //   16: C5 x 128 stripes +3%, tools/bs_slot_sweep.py)
     Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
@@ -753,7 +758,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     const uint32_t in_records = realign_records(a, K, cover, copy_off != nullptr, shifts);
     hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, wave ? 0 : static_cast<int>(g_tune.bitslice_depth),
                                          mode == 2, hold, copy_off != nullptr, 0, wave, &shifts,
-                                         wave ? static_cast<int>(g_tune.bs_prefetch) : 0);
+                                         wave && copy_off ? static_cast<int>(g_tune.bs_prefetch) : 0);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1666,7 +1671,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "frame_crc_cover") {
         g_tune.frame_crc_cover = value;  // 0 off, anything else on
     } else if (k == "bs_prefetch") {
-        g_tune.bs_prefetch = value == 2 || value == 4 ? value : 0;  // else 0 (the default)
+        g_tune.bs_prefetch = value < 0 ? 2 : value == 2 || value == 4 ? value : 0;  // < 0: the default (2)
     } else if (k == "bs_realign") {
         g_tune.bs_realign = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_unfused") {
@@ -1724,7 +1729,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_wave") {
         g_tune.bs_wave = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
     } else if (k == "bs_wave_copy") {
-        g_tune.bs_wave_copy = value < 0 ? 2 : std::min(value, 2);  // < 0: the default (2)
+        g_tune.bs_wave_copy = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
     } else if (k == "bs_wave_min_rows") {
         g_tune.bs_wave_min_rows = value >= 2 && value <= 4 ? value : 3;  // else the default
     } else if (k == "bs_tiles_per_slot") {

@@ -561,39 +561,69 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         // prefetch (one-wave form): the first PF chunks of input j + 1 are loaded into xn[] before
         // input j's network (not for realigned inputs, which take their loads at their turn)
         const int PF = (T == 64 && (style.prefetch == 2 || style.prefetch == 4)) ? style.prefetch : 0;
-        auto pre = [&](int j) { return PF > 0 && j < net.K && shift_of(j) == 0; };
+        // (realigned inputs: their aligned chunks into xn[], the last lane's next ones into xnh[])
+        auto pre = [&](int j) { return PF > 0 && j < net.K; };
         auto load_next = [&](int j) {
+            const int d = shift_of(j);
             s << "#pragma unroll\n            for (int c = 0; c < " << PF << "; c++) xn[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off["
-              << j << "] + off + c * " << CS << ", 0, 2);\n";
+              << j << "]" << (d ? " - " + std::to_string(d) : std::string()) << " + off + c * " << CS << ", 0, 2);\n";
+            if (d)
+                s << "#pragma unroll\n            for (int c = 0; c < " << PF << "; c++) xnh[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off["
+                  << j << "] - " << d << " + off + c * " << CS << " + 16 : (i32)0x80000000u, 0, 2);\n";
         };
         if (PF) {
             s << "        v4u xn[" << PF << "];\n";
+            if (any_shift) s << "        v4u xnh[" << PF << "];\n";
             if (pre(0)) load_next(0);
         }
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
             const int d = shift_of(j);
             if (d) {  // aligned chunks + the neighbours', realigned (BitsliceStyle::in_shift)
-                s << "            v4u xa[4], xh[4];\n"
-                  << "#pragma unroll\n            for (int c = 0; c < 4; c++) xa[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off["
-                  << j << "] - " << d << " + off + c * " << CS << ", 0, 2);\n"
-                  << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off["
-                  << j << "] - " << d << " + off + c * " << CS << " + 16 : (i32)0x80000000u, 0, 2);\n";
+                const std::string la = "__builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" + std::to_string(j) + "] - " +
+                                       std::to_string(d) + " + off + c * " + std::to_string(CS) + ", 0, 2)";
+                const std::string lh = "__builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off[" + std::to_string(j) +
+                                       "] - " + std::to_string(d) + " + off + c * " + std::to_string(CS) +
+                                       " + 16 : (i32)0x80000000u, 0, 2)";
+                const std::string pfs = std::to_string(PF);
+                s << "            v4u xa[4], xh[4];\n";
+                if (pre(j))
+                    s << "#pragma unroll\n            for (int c = 0; c < 4; c++) xa[c] = c < " << pfs << " ? xn[c < " << pfs
+                      << " ? c : 0] : " << la << ";\n"
+                      << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = c < " << pfs << " ? xnh[c < " << pfs
+                      << " ? c : 0] : " << lh << ";\n";
+                else
+                    s << "#pragma unroll\n            for (int c = 0; c < 4; c++) xa[c] = " << la << ";\n"
+                      << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = " << lh << ";\n";
             }
             const std::string ld = "__builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" + std::to_string(j) +
                                    "] + off + c * " + std::to_string(CS) + ", 0, 2)";
-            s << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
-              << (d ? "                const v4u x = rlg<" + std::to_string(d) + ">(xa[c], xh[c]);\n"
-                    : pre(j) ? "                const v4u x = c < " + std::to_string(PF) + " ? xn[c < " + std::to_string(PF) +
-                                   " ? c : 0] : " + ld + ";\n"
-                             : "                const v4u x = " + ld + ";\n")
-              << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
-              << (style.copy_through ? "                __builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" + std::to_string(j) +
-                                                 " + off + c * " + std::to_string(CS) + ", 0, 2);  // copy-through\n"
-                                           : std::string())
-              << "            }\n"
-              ;
-            if (pre(j + 1)) load_next(j + 1);  // the next input's loads go out before this network
+            const std::string cst = "__builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" + std::to_string(j) +
+                                    " + off + c * " + std::to_string(CS) + ", 0, 2);  // copy-through\n";
+            if (PF && pre(j + 1) && style.copy_through) {
+                // the next input's loads go out BEFORE this input's copy stores: vmcnt retires memory
+                // operations in issue order, so waiting for those loads then does not wait for the stores
+                s << "            v4u xc[4];\n#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
+                  << (d ? "                xc[c] = rlg<" + std::to_string(d) + ">(xa[c], xh[c]);\n"
+                        : pre(j) ? "                xc[c] = c < " + std::to_string(PF) + " ? xn[c < " + std::to_string(PF) +
+                                       " ? c : 0] : " + ld + ";\n"
+                                 : "                xc[c] = " + ld + ";\n")
+                  << "                P[4 * c] = xc[c][0]; P[4 * c + 1] = xc[c][1]; P[4 * c + 2] = xc[c][2]; P[4 * c + 3] = xc[c][3];\n"
+                  << "            }\n";
+                load_next(j + 1);
+                s << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n                const v4u x = xc[c];\n"
+                  << "                " << cst << "            }\n";
+            } else {
+                s << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
+                  << (d ? "                const v4u x = rlg<" + std::to_string(d) + ">(xa[c], xh[c]);\n"
+                        : pre(j) ? "                const v4u x = c < " + std::to_string(PF) + " ? xn[c < " + std::to_string(PF) +
+                                       " ? c : 0] : " + ld + ";\n"
+                                 : "                const v4u x = " + ld + ";\n")
+                  << "                P[4 * c] = x[0]; P[4 * c + 1] = x[1]; P[4 * c + 2] = x[2]; P[4 * c + 3] = x[3];\n"
+                  << (style.copy_through ? "                " + cst : std::string())
+                  << "            }\n";
+                if (pre(j + 1)) load_next(j + 1);  // the next input's loads go out before this network
+            }
             if (style.copy_through || pre(j + 1))
                 s << "            __builtin_amdgcn_sched_barrier(0);  // loads / stores leave before the network\n";
             network(j);

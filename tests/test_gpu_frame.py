@@ -516,11 +516,14 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         # (frame_copy_padded, bitslice): the copy-through launch on the bitsliced kernel (one-wave
         # tiles with realigned loads when the object chunks are unaligned, knob bs_wave_copy 2), on
         # the LDS tables, and the split-then-encode path
-        # (+ frame_tail_bs: the payloads' rest past the whole tiles by split + plain encode, or not)
-        for padded, mode, tail in ((1, 2, 1), (1, 0, 1), (0, 1, 1), (1, 2, 0)):
+        # (+ frame_tail_bs: the payloads' rest past the whole tiles by split + plain encode, or not;
+        # + bs_prefetch: the copy-through kernel's next-input loads ahead of its copy stores, 0 / 2 / 4)
+        for padded, mode, tail, pf in ((1, 2, 1, 2), (1, 0, 1, 2), (0, 1, 1, 2), (1, 2, 0, 2), (1, 2, 1, 0),
+                                       (1, 2, 1, 4)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bs_prefetch", pf), "tune")
             fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
@@ -528,6 +531,7 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
+        _lib.dev().ecamd_tune(b"bs_prefetch", -1)
     assert all(np.array_equal(o, out[2]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[1], ct)
     assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
@@ -548,15 +552,23 @@ def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
     fb.encode(_upload_objects(objs, fb.obj_stride))
     stride = (size + 16 + 15) // 16 * 16  # 16+ guard bytes after every object
     got = []
-    for padded in (1, 0):
-        _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
-        host = np.full(S * stride, 0xA5, dtype=np.uint8)
-        d = DeviceBuffer(host.size)
-        d.upload(host)
-        fb.decode(missing, d, obj_stride=stride)
-        got.append(d.download().reshape(S, stride))
-    _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
-    assert np.array_equal(got[0], got[1])
+    try:
+        # (frame_copy_padded, bitslice, bs_prefetch): the one-wave bitsliced decode-join (copy-through,
+        # next input's loads ahead of the copy stores: 2 default, 0, 4), the LDS tables, decode + join
+        for padded, mode, pf in ((1, 2, 2), (1, 2, 0), (1, 2, 4), (1, 0, 2), (0, 1, 2)):
+            _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bs_prefetch", pf), "tune")
+            host = np.full(S * stride, 0xA5, dtype=np.uint8)
+            d = DeviceBuffer(host.size)
+            d.upload(host)
+            fb.decode(missing, d, obj_stride=stride)
+            got.append(d.download().reshape(S, stride))
+    finally:
+        _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
+        _lib.dev().ecamd_tune(b"bitslice", 1)
+        _lib.dev().ecamd_tune(b"bs_prefetch", -1)
+    assert all(np.array_equal(g, got[-1]) for g in got)
     for s in range(S):
         assert got[0][s, :size].tobytes() == objs[s]
         assert (got[0][s, size:] == 0xA5).all()

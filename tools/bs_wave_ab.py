@@ -35,11 +35,12 @@ C2 = (4, 2, 64 << 10, 4096, {"encode": None, "decode": [0, 1], "decode_mixed": [
 # 16 KiB tiles (decodes spilled there and fell back to the tables).  Now bs_wave 1 is the default
 # for 3-4-output maps.
 VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave": 0, "bitslice_min_rows": 4}},
-            # round 4, later: the next input's chunks loaded before each network (knob bs_prefetch)
+            # round 4, later: the next input's chunks loaded before each network (knob bs_prefetch; measured
+            # neutral here, profiles/r04_bs_prefetch_ab.log, so the library now applies it to copy-through maps only)
             "c3pf": {"wave1": {}, "pf2": {"bs_prefetch": 2}, "pf4": {"bs_prefetch": 4}},
             "c2": {"tables": {}, "wave_2rows": {"bs_wave_min_rows": 2}},
             "c5": {"wave0": {}, "wave2": {"bs_wave": 2}}}
-DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": 0}
+DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1}
 
 
 def launches():

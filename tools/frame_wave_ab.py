@@ -18,7 +18,10 @@ import torch  # noqa: E402,F401
 from liberasurecode_amd import _lib, frame  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
-VARIANTS = {"lds_tables_stream": 0, "bitsliced_wave": 1}
+# (bs_wave_copy, bs_prefetch): round 4, later: the next input's chunks loaded before each network and
+# before the current input's copy stores
+VARIANTS = {"lds_tables_stream": (0, 0), "bitsliced_wave": (1, 0), "bitsliced_wave_pf2": (1, 2),
+            "bitsliced_wave_pf4": (1, 4)}
 
 
 def main(rounds=3, reps=10):
@@ -36,7 +39,8 @@ def main(rounds=3, reps=10):
                "join_0123": (lambda: fb.decode([0, 1, 2, 3], out, stream=st), S * ((k + 4) * bs - 4 * bs + size))}
         ref = {}
         for vname, v in VARIANTS.items():
-            d.ecamd_tune(b"bs_wave_copy", v)
+            d.ecamd_tune(b"bs_wave_copy", v[0])
+            d.ecamd_tune(b"bs_prefetch", v[1])
             fb.encode(obj, stream=st)
             st.synchronize()
             frags = fb.fragments()
@@ -53,7 +57,8 @@ def main(rounds=3, reps=10):
         a, b = D.Event(), D.Event()
         for _ in range(rounds):
             for vname, v in VARIANTS.items():
-                d.ecamd_tune(b"bs_wave_copy", v)
+                d.ecamd_tune(b"bs_wave_copy", v[0])
+                d.ecamd_tune(b"bs_prefetch", v[1])
                 for op, (fn, _) in ops.items():
                     fn()
                     a.record(st)
@@ -70,6 +75,7 @@ def main(rounds=3, reps=10):
         out.free()
         del fb
     d.ecamd_tune(b"bs_wave_copy", -1)
+    d.ecamd_tune(b"bs_prefetch", -1)
     d.ecamd_tune(b"bitslice", 1)
 
 
