@@ -261,6 +261,9 @@ struct Tuning {
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
                                   //   0 = the LDS-table copy-through launch
+    Knob frame_crc_prefetch{0};   // bitsliced crc variant (<= 4 outputs; the 8-output form has no registers left):
+                                  //   chunks (0, 2, 4) of the next input loaded before the current input's
+                                  //   copy stores (BitsliceStyle::prefetch)
     Knob frame_crc_cover{1};      // framed CRC32 encode of payloads that are not whole 16 KiB tiles (Swift's
                                   //   1 MiB segments): the crc variant over the whole tiles + tail codec +
                                   //   tail CRC (ecamd_frame_api.hip encode_crc_cover); 0 = codec + CRC pass
@@ -352,6 +355,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_nib") return g_tune.frame_crc_nib;
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
+    if (k == "frame_crc_prefetch") return g_tune.frame_crc_prefetch;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
@@ -1435,7 +1439,8 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     // objects 1.544 vs 1.542, profiles/r04_cover_ab2.log) and its larger register need spills at
     // some shift patterns (C3 objects 10 bytes long), which then fall back to the codec + CRC pass
     const uint32_t in_records = a.in_records;
-    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos);
+    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
+                                         nullptr, m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1668,6 +1673,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_join_align = value < 0 ? 2 : std::min(value, 2);  // < 0: the default (2)
     } else if (k == "frame_tail_bs") {
         g_tune.frame_tail_bs = value;  // 0 off, anything else on
+    } else if (k == "frame_crc_prefetch") {
+        g_tune.frame_crc_prefetch = value == 2 || value == 4 ? value : 0;
     } else if (k == "frame_crc_cover") {
         g_tune.frame_crc_cover = value;  // 0 off, anything else on
     } else if (k == "bs_prefetch") {

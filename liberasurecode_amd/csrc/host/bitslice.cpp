@@ -469,6 +469,19 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         s << "        for (i32 t = (i32)rg * a.crc_per; t < (i32)(rg + 1) * a.crc_per; t++) {\n"
           << "        const i32 off = t * " << kBsTile << " + (i32)threadIdx.x * 16;\n";
         acc_init();
+        // prefetch (style.prefetch): the next unrealigned input's first PFc chunks go out before this
+        // input's copy stores (vmcnt retires in issue order: its loads then do not wait for the stores)
+        const int PFc = (style.prefetch == 2 || style.prefetch == 4) ? style.prefetch : 0;
+        auto cpre = [&](int j) { return PFc > 0 && j < net.K && shift_of(j) == 0; };
+        auto cload_next = [&](int j) {
+            for (int c = 0; c < PFc; c++)
+                s << "            xn[" << c << "] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j << "] + off + "
+                  << c * 4096 << ", 0, 2);\n";
+        };
+        if (PFc) {
+            s << "        v4u xn[" << PFc << "];\n";
+            if (cpre(0)) cload_next(0);
+        }
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
             if (const int d = shift_of(j)) {  // aligned chunk + the neighbour's, realigned
@@ -481,10 +494,15 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                 for (int c = 0; c < 4; c++)
                     s << "            const v4u xq" << c << " = rlg<" << d << ">(xa" << c << ", xh" << c << ");\n";
             } else {
-                for (int c = 0; c < 4; c++)
-                    s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
-                      << "] + off + " << c * 4096 << ", 0, 2);\n";
+                for (int c = 0; c < 4; c++) {
+                    if (cpre(j) && c < PFc)
+                        s << "            const v4u xq" << c << " = xn[" << c << "];\n";
+                    else
+                        s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                          << "] + off + " << c * 4096 << ", 0, 2);\n";
+                }
             }
+            if (cpre(j + 1)) cload_next(j + 1);
             for (int c = 0; c < 4; c++)
                 s << "            __builtin_amdgcn_raw_buffer_store_b128(xq" << c << ", rcopy, cofs" << j << " + off + "
                   << c * 4096 << ", 0, 2);  // copy-through\n";
@@ -724,7 +742,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     wave = wave && !crc;
-    const int pf = wave && (prefetch == 2 || prefetch == 4) ? prefetch : 0;
+    const int pf = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch : 0;
     bool shifted = false;
     if (in_shift && (copy || crc))
         for (int j = 0; j < K && j < static_cast<int>(in_shift->size()); j++) shifted = shifted || ((*in_shift)[j] & 15);
@@ -755,7 +773,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 2047 || (cp & 12) == 12 || depth != 0))
         return false;  // copy / one-wave tiles: register loads
     const int pf = (cp >> 8) & 7;
-    if ((pf != 0 && pf != 2 && pf != 4) || (pf && !(cp & 64))) return false;  // prefetch: one-wave form only
+    if ((pf != 0 && pf != 2 && pf != 4) || (pf && !(cp & 64) && !(cp & 2))) return false;  // one-wave / crc forms
     if (prefetch) *prefetch = pf;
     if (in_shift) in_shift->clear();
     if (version == 3) {  // shifts: copy-through inputs only, at least one non-zero
