@@ -257,6 +257,8 @@ struct Tuning {
                                   //   2 (default) on the realigning path (bs % 16 != 0): Swift segments
                                   //   0.754 -> 0.766, C3 + 6 B 0.689 -> 0.792 of 8 TB/s with 4 KiB tiles
                                   //   (profiles/r04_join_align_ab.log); 0 never
+    Knob frame_xor_copy{1};       // framed flat-XOR encode: copy-through XOR launch over the whole tiles (object
+                                  //   chunks -> data payloads + parity in one pass); 0 = split + XOR
     Knob frame_tail_bs{1};        // framed RS encode of objects that do not fill the payloads: the payloads'
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
@@ -357,6 +359,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
     if (k == "frame_crc_prefetch") return g_tune.frame_crc_prefetch;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
+    if (k == "frame_xor_copy") return g_tune.frame_xor_copy;
     if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
     if (k == "bs_prefetch") return g_tune.bs_prefetch;
@@ -926,12 +929,34 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
 
 constexpr int64_t kXorNarrowMin = 256 << 10;  // fragment bytes from which flat XOR takes 1 KiB tiles
 
+// copy_off (framed flat-XOR encode): input j is also stored at base_args.copy_base + s*copy_stride +
+// copy_off[j] by the first row group's launches -- whole stream-kernel tiles only: ECAMD_EINVAL, with
+// nothing launched, unless bs is a multiple of the tile and every offset fits the stream kernel.
 template <bool PTRS>
 int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const int64_t* in_off,
-               const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st)
+               const int64_t* out_off, int64_t bs, int nstripes, hipStream_t st,
+               const int64_t* copy_off = nullptr)
 {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
+    if (copy_off) {  // check the whole plan before the first launch
+        if (PTRS || K > 32 || !g_tune.stream || bs % 4096) return ECAMD_EINVAL;
+        ApplyArgs t = base_args;
+        t.ncols = K;
+        t.nrows = std::min(kMaxRows, R);
+        for (int j = 0; j < K; j++) {
+            t.in_off[j] = in_off[j];
+            t.copy_off[j] = copy_off[j];
+        }
+        for (int r = 0; r < t.nrows; r++) t.out_off[r] = out_off[r];
+        if (!stream_offsets(t, bs) || !stream_copy_offsets(t, bs)) return ECAMD_EINVAL;
+        for (int row0 = kMaxRows; row0 < R; row0 += kMaxRows) {
+            ApplyArgs u = t;
+            u.nrows = std::min(kMaxRows, R - row0);
+            for (int r = 0; r < u.nrows; r++) u.out_off[r] = out_off[row0 + r];
+            if (!stream_offsets(u, bs)) return ECAMD_EINVAL;
+        }
+    }
     for (int row0 = 0; row0 < R; row0 += kMaxRows) {
         for (int col0 = 0; col0 < K; col0 += 32) {
             ApplyArgs a = base_args;
@@ -946,6 +971,13 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             }
             Geometry g;
             const bool use_stream = !PTRS && g_tune.stream && stream_offsets(a, bs);
+            const bool copy = copy_off && row0 == 0;  // the first row group copies the inputs through
+            if (copy) {
+                for (int j = 0; j < a.ncols; j++) a.copy_off[j] = copy_off[col0 + j];
+                if (!stream_copy_offsets(a, bs)) return fail(ECAMD_EINVAL, "xor copy-through offsets");
+            } else {
+                a.copy_records = 0;
+            }
             const int xt = g_tune.xor_threads ? g_tune.xor_threads
                                                : (a.ncols > 4 && bs >= kXorNarrowMin ? 64 : 256);
             const bool narrow = use_stream && (xt == 64 || xt == 128);  // only the stream kernel
@@ -970,12 +1002,22 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                     const dim3 grid(static_cast<int>(std::max<int64_t>(
                         1, g_tune.xor_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots)))),
                         block(g.threads);
-                    switch ((c.ncols + 3) / 4) {
-                    case 1: hipLaunchKernelGGL((xor_stream_kernel<1>), grid, block, 0, st, c); break;
-                    case 2: hipLaunchKernelGGL((xor_stream_kernel<2>), grid, block, 0, st, c); break;
-                    case 3: hipLaunchKernelGGL((xor_stream_kernel<3>), grid, block, 0, st, c); break;
-                    case 4: hipLaunchKernelGGL((xor_stream_kernel<4>), grid, block, 0, st, c); break;
-                    default: hipLaunchKernelGGL((xor_stream_kernel<8>), grid, block, 0, st, c); break;
+                    if (copy) {  // (for_each_launch advanced copy_base with the stripes)
+                        switch ((c.ncols + 3) / 4) {
+                        case 1: hipLaunchKernelGGL((xor_stream_kernel<1, true>), grid, block, 0, st, c); break;
+                        case 2: hipLaunchKernelGGL((xor_stream_kernel<2, true>), grid, block, 0, st, c); break;
+                        case 3: hipLaunchKernelGGL((xor_stream_kernel<3, true>), grid, block, 0, st, c); break;
+                        case 4: hipLaunchKernelGGL((xor_stream_kernel<4, true>), grid, block, 0, st, c); break;
+                        default: hipLaunchKernelGGL((xor_stream_kernel<8, true>), grid, block, 0, st, c); break;
+                        }
+                    } else {
+                        switch ((c.ncols + 3) / 4) {
+                        case 1: hipLaunchKernelGGL((xor_stream_kernel<1, false>), grid, block, 0, st, c); break;
+                        case 2: hipLaunchKernelGGL((xor_stream_kernel<2, false>), grid, block, 0, st, c); break;
+                        case 3: hipLaunchKernelGGL((xor_stream_kernel<3, false>), grid, block, 0, st, c); break;
+                        case 4: hipLaunchKernelGGL((xor_stream_kernel<4, false>), grid, block, 0, st, c); break;
+                        default: hipLaunchKernelGGL((xor_stream_kernel<8, false>), grid, block, 0, st, c); break;
+                        }
                     }
                     HIP_TRY(hipGetLastError());
                     return 0;
@@ -1474,6 +1516,32 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     return bitslice_launch(fn, b, grid, static_cast<hipStream_t>(stream), hold);
 }
 
+int xor_encode_copy(const uint32_t* masks, int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int64_t cover, int nstripes, void* stream)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    if (nstripes <= 0 || cover <= 0) return 0;
+    if (!masks || k <= 0 || k > 32 || m <= 0 || cover > bs || cover % 4096 || !aligned16(obj) || obj_stride % 16 ||
+        !aligned16(payload0) || stripe_stride % 16 || frag_stride % 16)
+        return ECAMD_EINVAL;
+    std::vector<int64_t> in_off(static_cast<size_t>(k)), copy_off(static_cast<size_t>(k)), out_off(static_cast<size_t>(m));
+    for (int j = 0; j < k; j++) {
+        in_off[static_cast<size_t>(j)] = static_cast<int64_t>(j) * bs;
+        copy_off[static_cast<size_t>(j)] = static_cast<int64_t>(j) * frag_stride;
+    }
+    for (int r = 0; r < m; r++) out_off[static_cast<size_t>(r)] = static_cast<int64_t>(k + r) * frag_stride;
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(obj);
+    a.in_stride = obj_stride;
+    a.out_base = static_cast<uint8_t*>(payload0);
+    a.out_stride = stripe_stride;
+    a.copy_base = static_cast<uint8_t*>(payload0);
+    a.copy_stride = stripe_stride;
+    return launch_xor<false>(masks, m, k, a, in_off.data(), out_off.data(), cover, nstripes,
+                             static_cast<hipStream_t>(stream), copy_off.data());
+}
+
 int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
                    int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
                    void* stream, int64_t obj_size)
@@ -1671,6 +1739,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_fused = value;  // 0 off, anything else on
     } else if (k == "frame_join_align") {
         g_tune.frame_join_align = value < 0 ? 2 : std::min(value, 2);  // < 0: the default (2)
+    } else if (k == "frame_xor_copy") {
+        g_tune.frame_xor_copy = value;  // 0 off, anything else on
     } else if (k == "frame_tail_bs") {
         g_tune.frame_tail_bs = value;  // 0 off, anything else on
     } else if (k == "frame_crc_prefetch") {

@@ -471,6 +471,28 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream);
 }
 
+// prepare_fragments_for_encode for payload bytes [from, bs) only (from a multiple of 16; 0 = all):
+// the streaming split kernel (callers check copy_fits32).
+int split_range(int dev, int k, const void* obj, int64_t obj_stride, uint64_t obj_size, uint8_t* frags, int64_t ss,
+                int64_t fs, int64_t bs, int nstripes, int64_t from, void* stream)
+{
+    const int64_t r16 = (bs + 15) & ~int64_t(15);
+    SplitArgs sa{static_cast<const uint8_t*>(obj), obj_stride, static_cast<int64_t>(obj_size), frags, ss, fs, bs,
+                 k, nstripes, 0, from};
+    const CopyShape cs = copy_shape(bs);
+    const dim3 grid(copy_grid(dev, (r16 - from) / 16, k, nstripes, cs)), block(cs.threads);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool dpp = dev_tune("frame_copy_dpp") != 0;
+    if (cs.u == 1)
+        hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<1, true> : frame_split_stream_kernel<1, false>), grid, block,
+                           0, st, sa);
+    else
+        hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<4, true> : frame_split_stream_kernel<4, false>), grid, block,
+                           0, st, sa);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 // The rest [from, bs) of every payload of an RS copy-through encode whose first `from` bytes are
 // done (bytes [0, from) of the data payloads written): a streaming split copies the object chunks'
 // rest into the data payloads (zero padded past the object's end and through the 16-byte slack),
@@ -491,20 +513,9 @@ int encode_tail(int dev, const Code& c, const void* obj, int64_t obj_stride, uin
     if (dev_tune("frame_tail_bs") == 0 || from <= 0 || from % 16 || from >= bs || t0 < 0 ||
         !copy_fits32(c.k, fs, bs, static_cast<int64_t>(obj_size)) || dev_tune("frame_copy_stream") == 0)
         return ECAMD_EINVAL;
-    SplitArgs sa{static_cast<const uint8_t*>(obj), obj_stride, static_cast<int64_t>(obj_size), frags, ss, fs, bs,
-                 c.k, nstripes, 0, from};
-    const CopyShape cs = copy_shape(bs);
-    const dim3 grid(copy_grid(dev, (r16 - from) / 16, c.k, nstripes, cs)), block(cs.threads);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    const bool dpp = dev_tune("frame_copy_dpp") != 0;
-    if (cs.u == 1)
-        hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<1, true> : frame_split_stream_kernel<1, false>), grid, block,
-                           0, st, sa);
-    else
-        hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<4, true> : frame_split_stream_kernel<4, false>), grid, block,
-                           0, st, sa);
-    HIP_TRY(hipGetLastError());
-    const int rc = ecamd_rs_encode(c.k, c.m, frags + kHeaderBytes + t0, ss, fs, n * kTile, nstripes, stream);
+    int rc = split_range(dev, c.k, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, from, stream);
+    if (rc) return rc;
+    rc = ecamd_rs_encode(c.k, c.m, frags + kHeaderBytes + t0, ss, fs, n * kTile, nstripes, stream);
     return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail encode failed") : rc;
 }
 
@@ -673,6 +684,38 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
         return run_crc(dev, legacy_crc(), checksum == kChksumCrc32, frags, stripe_stride,
                        frag_stride, kHeaderBytes, k + m, bs, nstripes, nullptr,
                        header_args(c, checksum, bs, obj_size, 0), stream);
+    }
+    if (backend == kBackendXor && a16(d_obj) && obj_stride % 16 == 0 && dev_tune("frame_unfused") == 0 &&
+        dev_tune("frame_xor_copy") != 0 && dev_tune("frame_copy_stream") != 0 &&
+        copy_fits32(k, frag_stride, bs, static_cast<int64_t>(obj_size))) {
+        // flat XOR, copy-through (round 4): the whole 4 KiB tiles every object chunk holds in one
+        // launch that reads the chunks, writes the data payloads and the parity; the payloads' rest by
+        // the streaming split + the XOR of that range; then the CRC pass and headers.  Against split +
+        // XOR it moves 26 instead of 36 payload-sized units of HBM traffic per stripe at (10,6).
+        const int64_t last = static_cast<int64_t>(obj_size) - (k - 1) * bs;
+        const int64_t cover = last > 0 ? std::min(bs, last) / 4096 * 4096 : 0;
+        unsigned pb[32], db[32];
+        ecamd_xor_code_tables(k, m, hd, pb, db);
+        rc = cover > 0 ? xor_encode_copy(pb, k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, cover,
+                                         nstripes, stream)
+                       : ECAMD_EINVAL;
+        if (rc == 0 && cover < bs) {  // from here on a failure is an error: part of the payloads is written
+            rc = split_range(dev, k, d_obj, obj_stride, obj_size, frags, stripe_stride, frag_stride, bs, nstripes,
+                             cover, stream);
+            if (rc == 0) {
+                std::vector<int64_t> in_off(k), out_off(m);
+                for (int j = 0; j < k; j++) in_off[j] = j * frag_stride;
+                for (int r = 0; r < m; r++) out_off[r] = (k + r) * frag_stride;
+                rc = ecamd_xor_apply_strided(pb, m, k, p0 + cover, stripe_stride, in_off.data(), p0 + cover,
+                                             stripe_stride, out_off.data(), bs - cover, nstripes, stream);
+            }
+            if (rc) return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed xor encode: tail failed") : rc;
+        }
+        if (rc == 0)
+            return run_crc(dev, legacy_crc(), checksum == kChksumCrc32, frags, stripe_stride, frag_stride,
+                           kHeaderBytes, k + m, bs, nstripes, nullptr, header_args(c, checksum, bs, obj_size, 0),
+                           stream);
+        if (rc != ECAMD_EINVAL) return rc;
     }
     SplitArgs sa{static_cast<const uint8_t*>(d_obj), obj_stride, static_cast<int64_t>(obj_size),
                  frags, stripe_stride, frag_stride, bs, k, nstripes, aligned ? 1 : 0};

@@ -47,6 +47,14 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
                    void* stream, int64_t obj_size = -1, int64_t from = 0, int64_t to = -1);
 
+// Framed flat-XOR encode, copy-through: bytes [0, cover) of every payload (cover a multiple of 4096,
+// every object chunk at least that long) from objects of obj_stride bytes whose chunk j starts at j*bs
+// (unaligned loads when bs % 16 != 0): the data payloads are written as the chunks stream through the
+// XOR kernel, parity r = XOR of the chunks in masks[r].  ECAMD_EINVAL, nothing launched, when it
+// does not apply.
+int xor_encode_copy(const uint32_t* masks, int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int64_t cover, int nstripes, void* stream);
+
 // rs_vand decode straight into objects: the missing data fragments (at least one, -1 terminated
 // `missing`) are computed into their object positions (j*bs) and the available data inputs are
 // copied there by the same launch (fragments_to_string without a separate join pass).

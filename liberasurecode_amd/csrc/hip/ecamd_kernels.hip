@@ -151,8 +151,10 @@ template __global__ void xor_apply_kernel<8, true>(const ApplyArgs);
 // gf16_stream_kernel (ecamd_stream.hpp): buffer loads on one resource per stripe, the loads of a
 // group of 4 inputs unconditional (out-of-range offsets read zeros, no traffic), inputs unrolled.
 // Output r accumulates input j under the wave-uniform mask bit j of masks[r]: one v_bitop3 per
-// dword (acc ^ (x & m)), no branches.
-template <int KG>
+// dword (acc ^ (x & m)), no branches.  COPY (framed flat-XOR encode, round 4): every input is also
+// stored at copy_base + s*copy_stride + copy_off32[j] as it is loaded (object chunk -> data payload;
+// the caller runs whole tiles only).
+template <int KG, bool COPY>
 __global__ void __launch_bounds__(256) xor_stream_kernel(const ApplyArgs a)
 {
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
@@ -189,6 +191,17 @@ __global__ void __launch_bounds__(256) xor_stream_kernel(const ApplyArgs a)
                 const int o = (j < a.ncols) ? a.in_off32[j] + off : static_cast<int>(0x80000000u);
                 x[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, o, 0, 2);
             }
+            if constexpr (COPY) {
+                const auto rcopy = __builtin_amdgcn_make_buffer_rsrc(
+                    a.copy_base + static_cast<int64_t>(s) * a.copy_stride, 0, static_cast<int>(a.copy_records), 0x00020000);
+#pragma unroll
+                for (int i = 0; i < 4; i++) {  // skipped inputs: an out-of-range offset, dropped
+                    const int j = 4 * g + i;
+                    const int o = (j < a.ncols && a.copy_off32[j] >= 0) ? a.copy_off32[j] + off
+                                                                         : static_cast<int>(0x80000000u);
+                    __builtin_amdgcn_raw_buffer_store_b128(x[i], rcopy, o, 0, 2);
+                }
+            }
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int j = 4 * g + i;
@@ -212,11 +225,16 @@ __global__ void __launch_bounds__(256) xor_stream_kernel(const ApplyArgs a)
     }
 }
 
-template __global__ void xor_stream_kernel<1>(const ApplyArgs);
-template __global__ void xor_stream_kernel<2>(const ApplyArgs);
-template __global__ void xor_stream_kernel<3>(const ApplyArgs);
-template __global__ void xor_stream_kernel<4>(const ApplyArgs);
-template __global__ void xor_stream_kernel<8>(const ApplyArgs);
+template __global__ void xor_stream_kernel<1, false>(const ApplyArgs);
+template __global__ void xor_stream_kernel<2, false>(const ApplyArgs);
+template __global__ void xor_stream_kernel<3, false>(const ApplyArgs);
+template __global__ void xor_stream_kernel<4, false>(const ApplyArgs);
+template __global__ void xor_stream_kernel<8, false>(const ApplyArgs);
+template __global__ void xor_stream_kernel<1, true>(const ApplyArgs);
+template __global__ void xor_stream_kernel<2, true>(const ApplyArgs);
+template __global__ void xor_stream_kernel<3, true>(const ApplyArgs);
+template __global__ void xor_stream_kernel<4, true>(const ApplyArgs);
+template __global__ void xor_stream_kernel<8, true>(const ApplyArgs);
 
 // ---------------------------------------------------------------- synthetic data ----
 

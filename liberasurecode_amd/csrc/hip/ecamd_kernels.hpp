@@ -78,7 +78,7 @@ template <int W, int KG, int MB, bool NIB = false>
 __global__ void gf16_frame_crc_kernel(const ApplyArgs a, const FusedCrcArgs c);
 template <int W, bool PTRS>
 __global__ void xor_apply_kernel(const ApplyArgs a);
-template <int KG>
+template <int KG, bool COPY>
 __global__ void xor_stream_kernel(const ApplyArgs a);
 __global__ void splitmix_fill_kernel(FillArgs f);
 }  // namespace ecamd

@@ -801,3 +801,30 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
         for s in range(S):
             assert joined[0][s, :size].tobytes() == objs[s]
             assert (joined[0][s, size:] == 0xA5).all()
+
+
+@pytest.mark.parametrize("k,m,hd", [(10, 6, 4), (3, 3, 3), (12, 6, 4), (10, 5, 3), (20, 6, 4)])
+@pytest.mark.parametrize("ct", [ec_api.CHKSUM_CRC32, ec_api.CHKSUM_NONE])
+def test_frame_xor_copy_through_matches_split(F, k, m, hd, ct):
+    """Framed flat-XOR encode on the copy-through XOR launch (round 4, knob frame_xor_copy): the whole
+    4 KiB tiles every object chunk holds in one pass (object chunks -> data payloads + parity), the
+    rest by the streaming split + the XOR of that range -- fragments equal the split-then-XOR path's and
+    the restated framing, over sizes with bs % 16 != 0 (Swift's segments), chunks shorter than a tile
+    and tiny objects."""
+    from liberasurecode_amd import _lib
+    be = ec_api.EC_BACKEND_FLAT_XOR_HD
+    S = 3
+    for size in (1 << 20, 10 * 104858 - 3, 777777, k * 4096, k * 4096 + 2, 4096 * 3 + 5, 100, 1):
+        objs = _objects(S, size, k * 31 + m + size)
+        out = []
+        try:
+            for on in (1, 0):
+                _lib.check(_lib.dev().ecamd_tune(b"frame_xor_copy", on), "tune")
+                fb = F.FrameBatch(be, k, m, size, S, hd=hd, checksum=ct)
+                fb.encode(_upload_objects(objs, fb.obj_stride))
+                out.append(fb.fragments())
+        finally:
+            _lib.dev().ecamd_tune(b"frame_xor_copy", 1)
+        assert np.array_equal(out[0], out[1]), size
+        want = expected_stripe(be, k, m, hd, objs[S - 1], ct)
+        assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m)), size

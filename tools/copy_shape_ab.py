@@ -20,6 +20,10 @@ from liberasurecode_amd import device as D  # noqa: E402
 SHAPES = [(256, 4, 0), (64, 4, 0), (64, 1, 0), (128, 1, 0), (256, 1, 0)]
 if len(sys.argv) > 1 and sys.argv[1] == "dpp":  # round 4: knob frame_copy_dpp on the realigning path
     SHAPES = [(256, 1, 0), (256, 1, 1), (64, 1, 0), (64, 1, 1), (128, 1, 1), (256, 4, 1)]
+# round 4: the copy-through flat-XOR framed encode (knob frame_xor_copy) -- mode "xorcopy": the XOR
+# encode shapes only, dpp 3 marks frame_xor_copy 0 (split + XOR)
+if len(sys.argv) > 1 and sys.argv[1] == "xorcopy":
+    SHAPES = [(256, 1, 1), (256, 1, 3)]
 # round 4: join tiles starting on aligned object chunks (knob frame_join_align); dpp 2 marks them
 if len(sys.argv) > 1 and sys.argv[1] == "align":
     SHAPES = [(256, 1, 1), (256, 1, 2), (128, 1, 1), (128, 1, 2)]
@@ -31,7 +35,10 @@ def main(rounds=5, reps=10):
     cases = [("c3", frame.RS_VAND, 10, 4, 10 << 20, 256),
              ("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
              ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
-    if len(sys.argv) > 1 and sys.argv[1] in ("dpp", "align"):
+    if len(sys.argv) > 1 and sys.argv[1] == "xorcopy":
+        cases = [("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560),
+                 ("xor_c3_encode", frame.FLAT_XOR_HD, 10, 6, 10 << 20, 256)]
+    elif len(sys.argv) > 1 and sys.argv[1] in ("dpp", "align"):
         cases = [("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
                  ("c3_plus_6", frame.RS_VAND, 10, 4, (10 << 20) + 6 * 10, 256),
                  ("xor_swift_encode", frame.FLAT_XOR_HD, 10, 6, 1 << 20, 2560)]
@@ -52,6 +59,7 @@ def main(rounds=5, reps=10):
             d.ecamd_tune(b"frame_copy_u", u)
             d.ecamd_tune(b"frame_copy_dpp", 1 if dp else 0)
             d.ecamd_tune(b"frame_join_align", 1 if dp == 2 else 0)
+            d.ecamd_tune(b"frame_xor_copy", 0 if dp == 3 else 1)
             fn()
             st.synchronize()
             got = fb.fragments() if enc else out.download()
@@ -70,6 +78,7 @@ def main(rounds=5, reps=10):
                 d.ecamd_tune(b"frame_copy_u", u)
                 d.ecamd_tune(b"frame_copy_dpp", 1 if dp else 0)
                 d.ecamd_tune(b"frame_join_align", 1 if dp == 2 else 0)
+                d.ecamd_tune(b"frame_xor_copy", 0 if dp == 3 else 1)
                 fn()
                 a.record(st)
                 for _ in range(reps):
@@ -79,7 +88,7 @@ def main(rounds=5, reps=10):
                 times[(t, u, dp)].append(a.elapsed_ms(b) / reps)
         for (t, u, dp), ts in times.items():
             ms = statistics.median(ts)
-            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": 1 if dp else 0, "aligned_tiles": dp == 2,
+            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": 1 if dp else 0, "aligned_tiles": dp == 2, "xor_copy": dp != 3,
                    "tile_bytes": t * u * 16,
                    "ms": round(ms, 4)}
             if not enc:
@@ -92,6 +101,7 @@ def main(rounds=5, reps=10):
     d.ecamd_tune(b"frame_copy_u", 0)
     d.ecamd_tune(b"frame_copy_dpp", -1)
     d.ecamd_tune(b"frame_join_align", -1)
+    d.ecamd_tune(b"frame_xor_copy", 1)
 
 
 if __name__ == "__main__":
