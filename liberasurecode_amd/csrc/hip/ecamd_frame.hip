@@ -179,10 +179,11 @@ __global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict_
         }
         const uint8_t* p = frag + a.payload_off;
         for (int64_t i = a.body; i < a.len; ++i) acc = byte_step(T, acc, p[i], a.legacy);
-        if (a.tail_map) {
-            const uint32_t* tm = a.tail_map;
-            acc = tm[acc & 0xff] ^ tm[256 + ((acc >> 8) & 0xff)] ^ tm[512 + ((acc >> 16) & 0xff)] ^
-                  tm[768 + (acc >> 24)] ^ ~a.tail_crc[item] ^ a.tail_c0;
+        if (a.tail_crc) {
+            uint32_t sh = 0;
+#pragma unroll
+            for (int b = 0; b < 32; ++b) sh ^= (acc >> b & 1u) ? a.tail_cols[b] : 0u;
+            acc = sh ^ ~a.tail_crc[item] ^ a.tail_c0;
         }
         crc = ~(a.c0 ^ acc);
         if (crc_out) crc_out[item] = crc;

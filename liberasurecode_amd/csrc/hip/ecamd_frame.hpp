@@ -28,12 +28,12 @@ struct CrcArgs {
     uint32_t span_off;
     uint32_t t_off;
     // crc_finalize_kernel over ranges that end before the payload does: the CRC32 of the rest
-    // (tail_crc[item], a payload-tail checksum of tail bytes) is folded in as
-    // acc = A^tail(acc) ^ r0(tail), r0(tail) = ~tail_crc ^ tail_c0 (tail_c0 = A^tail(~0), tail_map =
-    // field tables of A^tail); null: the ranges end at `body`
-    const uint32_t* tail_map;
+    // (tail_crc[item], the checksum of the payload's last tail bytes) is folded in as
+    // acc = A^tail(acc) ^ r0(tail), r0(tail) = ~tail_crc ^ tail_c0 (tail_c0 = A^tail(~0), tail_cols =
+    // the 32 columns of A^tail); tail_crc null: the ranges end at `body`
     const uint32_t* tail_crc;
     uint32_t tail_c0;
+    uint32_t tail_cols[32];
 };
 
 struct HeaderArgs {

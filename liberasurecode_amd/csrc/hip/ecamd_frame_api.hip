@@ -50,7 +50,6 @@ struct DevImage {
 std::mutex g_mu;
 std::map<std::tuple<int, int, int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J, G, pos
 std::map<std::tuple<int, void*, int>, std::pair<uint32_t*, size_t>> g_scratch;  // dev, stream, slot
-std::map<std::tuple<int, int, int64_t>, uint32_t*> g_shift_maps;                 // dev, legacy, bytes
 
 int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** out)
 {
@@ -66,24 +65,6 @@ int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** 
         it = g_images.emplace(key, std::move(di)).first;
     }
     *out = it->second.get();
-    return 0;
-}
-
-// Field tables (8-bit fields, 4 x 256 words) of A^nbytes in device memory, cached.
-int shift_map(int dev, bool legacy, int64_t nbytes, const uint32_t** out)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_tuple(dev, legacy ? 1 : 0, nbytes);
-    auto it = g_shift_maps.find(key);
-    if (it == g_shift_maps.end()) {
-        std::vector<uint32_t> w(1024);
-        field_tables(zero_shift(CrcMachine(legacy), static_cast<uint64_t>(nbytes)), 8, w.data());
-        uint32_t* d = nullptr;
-        HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
-        HIP_TRY(hipMemcpy(d, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        it = g_shift_maps.emplace(key, d).first;
-    }
-    *out = it->second;
     return 0;
 }
 
@@ -417,9 +398,11 @@ int finalize_ranges(int dev, const Code& c, bool legacy, uint64_t obj_size, uint
     CrcArgs a{};
     if (cover < bs) {
         if (!tail_crc) return dev_fail(ECAMD_EINVAL, "finalize: ranges end before the payload, no tail CRC");
-        if ((rc = shift_map(dev, legacy, bs - cover, &a.tail_map))) return rc;
+        // A^tail as its 32 columns in the kernel arguments (no per-length device table to cache)
+        const Mat32 sh = zero_shift(CrcMachine(legacy), static_cast<uint64_t>(bs - cover));
+        for (int b = 0; b < 32; b++) a.tail_cols[b] = sh.col[b];
         a.tail_crc = tail_crc;
-        a.tail_c0 = zero_shift(CrcMachine(legacy), static_cast<uint64_t>(bs - cover)).apply(~0u);
+        a.tail_c0 = sh.apply(~0u);
     }
     a.base = frags;
     a.stripe_stride = ss;
