@@ -1434,10 +1434,13 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
     return 0;
 }
 
-int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
-                          int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
-                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos,
-                          int64_t cover)
+namespace {
+
+// The crc variant of the bitsliced kernel for the encode map `coeff` (m x k, row-major; RS
+// generator rows or a flat-XOR code's 0/1 parity masks) on `device`: see rs_encode_copy_crc_bs.
+int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, const void* obj, int64_t obj_stride,
+                       void* payload0, int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                       const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos, int64_t cover)
 {
     const int mode = g_tune.bitslice;
     if (cover < 0) cover = bs;
@@ -1445,19 +1448,11 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     if (!mode || m > kBsMaxR || k > kBsMaxK || cover % kBsTile || cover <= 0 || cover > bs || nstripes <= 0 ||
         q <= 0 || (cover / kBsTile) % q || (m > 4 && q != cover / kBsTile))
         return ECAMD_EINVAL;
-    std::shared_ptr<RsEntry> e;
-    int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
-    if (rc) return rc;
     // whole payloads: the object chunks j*bs are 16-byte aligned; partial cover (objects that do not
     // fill k 16 KiB-multiple payloads): the object side is read with unaligned loads
-    if (!e->map || !(cover == bs ? copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)
-                                 : copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)))
+    if (!(cover == bs ? copy_aligned(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)
+                      : copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs)))
         return ECAMD_EINVAL;
-    for (int j = 0; j < k; j++)
-        if (e->inputs[j] != j) return ECAMD_EINVAL;
-    for (int r = 0; r < m; r++)
-        if (e->outputs[r] != k + r) return ECAMD_EINVAL;
-    const ecamd_map* map = e->map.get();
     ApplyArgs a{};
     a.in_base = static_cast<const uint8_t*>(obj);
     a.in_stride = obj_stride;
@@ -1481,7 +1476,7 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     // objects 1.544 vs 1.542, profiles/r04_cover_ab2.log) and its larger register need spills at
     // some shift patterns (C3 objects 10 bytes long), which then fall back to the codec + CRC pass
     const uint32_t in_records = a.in_records;
-    hipFunction_t fn = bitslice_function(map->device, map->coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
+    hipFunction_t fn = bitslice_function(device, coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
                                          nullptr, m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
@@ -1512,8 +1507,46 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
     // frees a slot, which balances units better than a grid-stride loop over resident workgroups
     const int wgs = static_cast<int>(g_tune.frame_crc_bs_wgs);
     const int grid = static_cast<int>(
-        wgs > 0 ? std::min<int64_t>(units, static_cast<int64_t>(cu_count(map->device)) * wgs) : units);
+        wgs > 0 ? std::min<int64_t>(units, static_cast<int64_t>(cu_count(device)) * wgs) : units);
     return bitslice_launch(fn, b, grid, static_cast<hipStream_t>(stream), hold);
+}
+
+}  // namespace
+
+int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                          int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                          const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos,
+                          int64_t cover)
+{
+    if (!g_tune.bitslice || m > kBsMaxR || k > kBsMaxK) return ECAMD_EINVAL;
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(0, k, m, nullptr, 0, -1, e);
+    if (rc) return rc;
+    if (!e->map) return ECAMD_EINVAL;
+    for (int j = 0; j < k; j++)
+        if (e->inputs[j] != j) return ECAMD_EINVAL;
+    for (int r = 0; r < m; r++)
+        if (e->outputs[r] != k + r) return ECAMD_EINVAL;
+    return encode_copy_crc_bs(e->map->device, e->map->coeff, k, m, obj, obj_stride, payload0, stripe_stride,
+                              frag_stride, bs, nstripes, d_img, d_partial, q, stream, crc_pos, cover);
+}
+
+int xor_encode_copy_crc_bs(const uint32_t* masks, int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                           int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                           const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos,
+                           int64_t cover)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!masks || !g_tune.bitslice || m > kBsMaxR || k > kBsMaxK) return ECAMD_EINVAL;
+    // a flat-XOR code as a GF(2^16) matrix of 0 / 1: the bitsliced network of a coefficient 1 is the
+    // identity on the bit planes, so the network is the parity masks' XORs
+    std::vector<int> coeff(static_cast<size_t>(m) * k, 0);
+    for (int r = 0; r < m; r++)
+        for (int j = 0; j < k; j++) coeff[static_cast<size_t>(r) * k + j] = (masks[r] >> j) & 1u;
+    return encode_copy_crc_bs(dev, coeff, k, m, obj, obj_stride, payload0, stripe_stride, frag_stride, bs, nstripes,
+                              d_img, d_partial, q, stream, crc_pos, cover);
 }
 
 int xor_encode_copy(const uint32_t* masks, int k, int m, const void* obj, int64_t obj_stride, void* payload0,

@@ -514,8 +514,9 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
                      void* stream)
 {
     constexpr int64_t kTile = 16384;
+    const bool xorc = c.backend == kBackendXor;
     if (dev_tune("frame_crc_cover") == 0 || dev_tune("frame_crc_bs") == 0 || dev_tune("frame_crc_fused") == 0 ||
-        c.m > 8 || bs % 2 || nstripes <= 0)
+        c.m > 8 || bs % 2 || nstripes <= 0 || (xorc && !copy_fits32(c.k, fs, bs, static_cast<int64_t>(obj_size))))
         return ECAMD_EINVAL;
     const int64_t last = static_cast<int64_t>(obj_size) - (c.k - 1) * bs;  // bytes of the last data chunk
     const int64_t cover = std::min(bs, last) / kTile * kTile;
@@ -533,15 +534,32 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
     if (npos <= 0) npos = lane && c.m <= 4 ? 1 : 2;
     const bool nib = dev_tune("frame_crc_bs_nib") > 0;
     if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos, nib))) return rc;
-    rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                               partial, q, stream, npos | (lane ? 8 : 0) | (nib ? 16 : 0), cover);
+    unsigned pb[32], db[32];
+    if (xorc) ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db);
+    const int pos = npos | (lane ? 8 : 0) | (nib ? 16 : 0);
+    rc = xorc ? xor_encode_copy_crc_bs(pb, c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                                       partial, q, stream, pos, cover)
+              : rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                                      partial, q, stream, pos, cover);
     if (rc) return rc;
     if (tail) {
         // from here on a failure is an error, not a fallback: part of the payloads is written
-        rc = encode_tail(dev, c, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, stream);
-        if (rc == ECAMD_EINVAL)
-            rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, stream,
-                                static_cast<int64_t>(obj_size), cover);
+        if (xorc) {  // the data payloads' rest by the split, then the XOR of that range
+            rc = split_range(dev, c.k, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, stream);
+            if (rc == 0) {
+                std::vector<int64_t> in_off(c.k), out_off(c.m);
+                for (int j = 0; j < c.k; j++) in_off[j] = j * fs;
+                for (int r = 0; r < c.m; r++) out_off[r] = (c.k + r) * fs;
+                uint8_t* pc = frags + kHeaderBytes + cover;
+                rc = ecamd_xor_apply_strided(pb, c.m, c.k, pc, ss, in_off.data(), pc, ss, out_off.data(), bs - cover,
+                                             nstripes, stream);
+            }
+        } else {
+            rc = encode_tail(dev, c, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, stream);
+            if (rc == ECAMD_EINVAL)
+                rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, stream,
+                                    static_cast<int64_t>(obj_size), cover);
+        }
         if (rc) return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail codec failed") : rc;
         HeaderArgs none{};
         if ((rc = run_crc(dev, legacy, true, frags, ss, fs, kHeaderBytes + cover, nf, tail, nstripes, tail_crc,
@@ -675,6 +693,11 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
         // launch that reads the chunks, writes the data payloads and the parity; the payloads' rest by
         // the streaming split + the XOR of that range; then the CRC pass and headers.  Against split +
         // XOR it moves 26 instead of 36 payload-sized units of HBM traffic per stripe at (10,6).
+        if (checksum == kChksumCrc32) {  // the checksums folded into the codec launch, as for RS
+            rc = encode_crc_cover(dev, c, legacy_crc(), d_obj, obj_stride, obj_size, frags, stripe_stride,
+                                  frag_stride, bs, nstripes, stream);
+            if (rc != ECAMD_EINVAL) return rc;
+        }
         const int64_t last = static_cast<int64_t>(obj_size) - (k - 1) * bs;
         const int64_t cover = last > 0 ? std::min(bs, last) / 4096 * 4096 : 0;
         unsigned pb[32], db[32];

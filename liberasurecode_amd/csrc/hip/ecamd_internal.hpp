@@ -47,6 +47,13 @@ int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payl
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
                    void* stream, int64_t obj_size = -1, int64_t from = 0, int64_t to = -1);
 
+// The same crc variant for a flat-XOR code (parity r = XOR of the data chunks in masks[r], run as a
+// 0 / 1 coefficient matrix through the bitsliced generator).
+int xor_encode_copy_crc_bs(const uint32_t* masks, int k, int m, const void* obj, int64_t obj_stride, void* payload0,
+                           int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
+                           const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos = 1,
+                           int64_t cover = -1);
+
 // Framed flat-XOR encode, copy-through: bytes [0, cover) of every payload (cover a multiple of 4096,
 // every object chunk at least that long) from objects of obj_stride bytes whose chunk j starts at j*bs
 // (unaligned loads when bs % 16 != 0): the data payloads are written as the chunks stream through the

@@ -808,23 +808,34 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
 def test_frame_xor_copy_through_matches_split(F, k, m, hd, ct):
     """Framed flat-XOR encode on the copy-through XOR launch (round 4, knob frame_xor_copy): the whole
     4 KiB tiles every object chunk holds in one pass (object chunks -> data payloads + parity), the
-    rest by the streaming split + the XOR of that range -- fragments equal the split-then-XOR path's and
-    the restated framing, over sizes with bs % 16 != 0 (Swift's segments), chunks shorter than a tile
-    and tiny objects."""
+    rest by the streaming split + the XOR of that range; with CRC32 the bitsliced crc variant over the
+    whole 16 KiB tiles (the code as a 0 / 1 matrix) -- fragments equal the split-then-XOR path's and
+    the restated framing, over sizes with bs % 16 != 0 (Swift's segments), whole tiles, chunks shorter
+    than a tile and tiny objects."""
     from liberasurecode_amd import _lib
     be = ec_api.EC_BACKEND_FLAT_XOR_HD
     S = 3
-    for size in (1 << 20, 10 * 104858 - 3, 777777, k * 4096, k * 4096 + 2, 4096 * 3 + 5, 100, 1):
+    for size in (1 << 20, 10 * 104858 - 3, 777777, k * 4096, k * 4096 + 2, 4096 * 3 + 5, 100, 1,
+                 k * 3 * 16384, 2 * k * 16384 + 6):
         objs = _objects(S, size, k * 31 + m + size)
         out = []
         try:
-            for on in (1, 0):
+            # (frame_xor_copy, bitslice): with CRC32 and bitslice 2 the checksums fold into the bitsliced
+            # crc variant run as a 0 / 1 matrix (launch counter); bitslice 0 the copy-through XOR + CRC
+            # pass; frame_xor_copy 0 the split + XOR path
+            for on, mode in ((1, 2), (1, 0), (0, 1)):
                 _lib.check(_lib.dev().ecamd_tune(b"frame_xor_copy", on), "tune")
+                _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+                n0 = _bs_launches()
                 fb = F.FrameBatch(be, k, m, size, S, hd=hd, checksum=ct)
                 fb.encode(_upload_objects(objs, fb.obj_stride))
                 out.append(fb.fragments())
+                last = size - (k - 1) * fb.blocksize
+                if mode == 2 and ct == ec_api.CHKSUM_CRC32 and last >= 16384 and m <= 8 and fb.blocksize % 2 == 0:
+                    assert _bs_launches() > n0, ("crc variant did not run", size)
         finally:
             _lib.dev().ecamd_tune(b"frame_xor_copy", 1)
-        assert np.array_equal(out[0], out[1]), size
+            _lib.dev().ecamd_tune(b"bitslice", 1)
+        assert all(np.array_equal(o, out[2]) for o in out), size
         want = expected_stripe(be, k, m, hd, objs[S - 1], ct)
         assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m)), size

@@ -22,8 +22,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "dpp":  # round 4: knob frame_copy_dpp o
     SHAPES = [(256, 1, 0), (256, 1, 1), (64, 1, 0), (64, 1, 1), (128, 1, 1), (256, 4, 1)]
 # round 4: the copy-through flat-XOR framed encode (knob frame_xor_copy) -- mode "xorcopy": the XOR
 # encode shapes only, dpp 3 marks frame_xor_copy 0 (split + XOR)
-if len(sys.argv) > 1 and sys.argv[1] == "xorcopy":
-    SHAPES = [(256, 1, 1), (256, 1, 3)]
+if len(sys.argv) > 1 and sys.argv[1] == "xorcopy":  # dp 4: frame_crc_cover 0 (XOR copy-through + CRC pass)
+    SHAPES = [(256, 1, 1), (256, 1, 4), (256, 1, 3)]
 # round 4: join tiles starting on aligned object chunks (knob frame_join_align); dpp 2 marks them
 if len(sys.argv) > 1 and sys.argv[1] == "align":
     SHAPES = [(256, 1, 1), (256, 1, 2), (128, 1, 1), (128, 1, 2)]
@@ -31,6 +31,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "align":
 
 def main(rounds=5, reps=10):
     d = _lib.dev()
+    d.ecamd_tune(b"bitslice", 2)  # run-time compiled kernels ready before the timing
     st = D.Stream()
     cases = [("c3", frame.RS_VAND, 10, 4, 10 << 20, 256),
              ("swift_1MiB_segment", frame.RS_VAND, 10, 4, 1 << 20, 2560),
@@ -60,6 +61,7 @@ def main(rounds=5, reps=10):
             d.ecamd_tune(b"frame_copy_dpp", 1 if dp else 0)
             d.ecamd_tune(b"frame_join_align", 1 if dp == 2 else 0)
             d.ecamd_tune(b"frame_xor_copy", 0 if dp == 3 else 1)
+            d.ecamd_tune(b"frame_crc_cover", 0 if dp == 4 else 1)
             fn()
             st.synchronize()
             got = fb.fragments() if enc else out.download()
@@ -79,6 +81,7 @@ def main(rounds=5, reps=10):
                 d.ecamd_tune(b"frame_copy_dpp", 1 if dp else 0)
                 d.ecamd_tune(b"frame_join_align", 1 if dp == 2 else 0)
                 d.ecamd_tune(b"frame_xor_copy", 0 if dp == 3 else 1)
+                d.ecamd_tune(b"frame_crc_cover", 0 if dp == 4 else 1)
                 fn()
                 a.record(st)
                 for _ in range(reps):
@@ -88,7 +91,7 @@ def main(rounds=5, reps=10):
                 times[(t, u, dp)].append(a.elapsed_ms(b) / reps)
         for (t, u, dp), ts in times.items():
             ms = statistics.median(ts)
-            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": 1 if dp else 0, "aligned_tiles": dp == 2, "xor_copy": dp != 3,
+            rec = {"op": tag, "lanes": t, "chunks_per_lane": u, "dpp": 1 if dp else 0, "aligned_tiles": dp == 2, "xor_copy": dp != 3, "crc_fused": dp not in (3, 4),
                    "tile_bytes": t * u * 16,
                    "ms": round(ms, 4)}
             if not enc:
@@ -102,6 +105,7 @@ def main(rounds=5, reps=10):
     d.ecamd_tune(b"frame_copy_dpp", -1)
     d.ecamd_tune(b"frame_join_align", -1)
     d.ecamd_tune(b"frame_xor_copy", 1)
+    d.ecamd_tune(b"frame_crc_cover", 1)
 
 
 if __name__ == "__main__":

@@ -4,8 +4,8 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_frame.py > gpurun_out/r04_frame_tests_q.log 2>&1 || { echo "TESTS rc=$?"; tail -30 gpurun_out/r04_frame_tests_q.log; exit 1; }
-tail -1 gpurun_out/r04_frame_tests_q.log
-timeout -k 10 300 python tools/copy_shape_ab.py xorcopy > gpurun_out/r04_xor_copy_ab.log 2>&1 || { echo "AB rc=$?"; tail -20 gpurun_out/r04_xor_copy_ab.log; exit 1; }
-cat gpurun_out/r04_xor_copy_ab.log
+timeout -k 10 700 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_frame.py > gpurun_out/r04_frame_tests_q2.log 2>&1 || { echo "TESTS rc=$?"; tail -30 gpurun_out/r04_frame_tests_q2.log; exit 1; }
+tail -1 gpurun_out/r04_frame_tests_q2.log
+timeout -k 10 300 python tools/copy_shape_ab.py xorcopy > gpurun_out/r04_xor_copy_ab2.log 2>&1 || { echo "AB rc=$?"; tail -20 gpurun_out/r04_xor_copy_ab2.log; exit 1; }
+cat gpurun_out/r04_xor_copy_ab2.log
 echo R04_Q_OK
