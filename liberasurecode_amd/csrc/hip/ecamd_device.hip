@@ -258,7 +258,9 @@ struct Tuning {
                                   //   0.754 -> 0.766, C3 + 6 B 0.689 -> 0.792 of 8 TB/s with 4 KiB tiles
                                   //   (profiles/r04_join_align_ab.log); 0 never
     Knob frame_xor_copy{1};       // framed flat-XOR encode: copy-through XOR launch over the whole tiles (object
-                                  //   chunks -> data payloads + parity in one pass); 0 = split + XOR
+                                  //   chunks -> data payloads + parity in one pass); decode with data lost:
+                                  //   the decode-join (lost data straight into the objects); 0 = split + XOR,
+                                  //   decode in place + join
     Knob frame_tail_bs{1};        // framed RS encode of objects that do not fill the payloads: the payloads'
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
@@ -1575,14 +1577,15 @@ int xor_encode_copy(const uint32_t* masks, int k, int m, const void* obj, int64_
                              static_cast<hipStream_t>(stream), copy_off.data());
 }
 
-int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
-                   int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
-                   void* stream, int64_t obj_size)
+namespace {
+
+// The decode-join of a prepared map (rs_decode_join, xor_decode_join): e's outputs are data fragments,
+// computed into their object chunks; its data inputs are copied there as they stream through.
+int decode_join_entry(const RsEntry& e, int k, const void* payload0, int64_t stripe_stride, int64_t frag_stride,
+                      void* obj, int64_t obj_stride, int64_t bs, int nstripes, void* stream, int64_t obj_size)
 {
-    std::shared_ptr<RsEntry> e;
-    int rc = rs_entry(1, k, m, missing, 0, -1, e);
-    if (rc) return rc;
-    if (!e->map || nstripes <= 0 || bs <= 0)
+    const RsEntry* ep = &e;
+    if (!ep->map || nstripes <= 0 || bs <= 0)
         return fail(ECAMD_EINVAL, "decode-join needs at least one missing data fragment");
     if (obj_size < 0) obj_size = k * bs;
     if (obj_size > k * bs || !copy_aligned_payloads(obj, payload0, obj_stride, stripe_stride, frag_stride, bs))
@@ -1592,19 +1595,71 @@ int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64
         return std::max<int64_t>(0, std::min<int64_t>(bs, obj_size - static_cast<int64_t>(j) * bs));
     };
     std::vector<int64_t> in_off, out_off, copy_off, out_len, copy_len;
-    for (int i : e->inputs) {
+    for (int i : ep->inputs) {
         in_off.push_back(static_cast<int64_t>(i) * frag_stride);
         copy_off.push_back(i < k ? static_cast<int64_t>(i) * bs : -1);  // parity is not copied
         copy_len.push_back(i < k ? chunk(i) : bs);
     }
-    for (int o : e->outputs) {
+    for (int o : ep->outputs) {
         out_off.push_back(static_cast<int64_t>(o) * bs);
         out_len.push_back(chunk(o));
     }
     auto* ob = static_cast<uint8_t*>(obj);
-    return map_apply_copy(*e, static_cast<const uint8_t*>(payload0), stripe_stride, in_off, ob,
+    return map_apply_copy(*ep, static_cast<const uint8_t*>(payload0), stripe_stride, in_off, ob,
                           obj_stride, out_off, ob, obj_stride, copy_off, bs, nstripes, stream, nullptr,
                           &out_len, &copy_len);
+}
+
+}  // namespace
+
+int rs_decode_join(int k, int m, const int* missing, const void* payload0, int64_t stripe_stride,
+                   int64_t frag_stride, void* obj, int64_t obj_stride, int64_t bs, int nstripes,
+                   void* stream, int64_t obj_size)
+{
+    std::shared_ptr<RsEntry> e;
+    int rc = rs_entry(1, k, m, missing, 0, -1, e);
+    if (rc) return rc;
+    return decode_join_entry(*e, k, payload0, stripe_stride, frag_stride, obj, obj_stride, bs, nstripes, stream,
+                             obj_size);
+}
+
+int xor_decode_join(int k, const std::vector<int>& inputs, const std::vector<int>& outputs,
+                    const std::vector<int>& coeff, const void* payload0, int64_t stripe_stride, int64_t frag_stride,
+                    void* obj, int64_t obj_stride, int64_t bs, int nstripes, void* stream, int64_t obj_size)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    const size_t R = outputs.size(), K = inputs.size();
+    if (R == 0 || K == 0 || coeff.size() != R * K) return fail(ECAMD_EINVAL, "xor decode-join: bad matrix");
+    for (int o : outputs)
+        if (o < 0 || o >= k) return fail(ECAMD_EINVAL, "xor decode-join: outputs must be data fragments");
+    // cached like the RS maps (kind 3): the map's coefficient tables live on the device
+    std::vector<int> key = {dev, 3, k, static_cast<int>(R), static_cast<int>(K), 0};
+    key.insert(key.end(), inputs.begin(), inputs.end());
+    key.insert(key.end(), outputs.begin(), outputs.end());
+    key.insert(key.end(), coeff.begin(), coeff.end());
+    std::shared_ptr<RsEntry> e;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto it = g_cache.find(key);
+        if (it != g_cache.end()) {
+            g_lru.splice(g_lru.begin(), g_lru, it->second.lru);
+            e = it->second.entry;
+        }
+    }
+    if (!e) {
+        e = std::make_shared<RsEntry>();
+        e->inputs = inputs;
+        e->outputs = outputs;
+        ecamd_map* mp = nullptr;
+        if ((rc = ecamd_map_create(coeff.data(), static_cast<int>(R), static_cast<int>(K), &mp))) return rc;
+        e->map.reset(mp);
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        cache_insert(key, e);
+    }
+    return decode_join_entry(*e, k, payload0, stripe_stride, frag_stride, obj, obj_stride, bs, nstripes, stream,
+                             obj_size);
 }
 
 }  // namespace ecamd

@@ -789,6 +789,40 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
         return rs_decode_join(k, m, missing, p0, stripe_stride, frag_stride, d_obj, obj_stride, bs,
                               nstripes, stream, static_cast<int64_t>(obj_size));
     }
+    if (data_missing && backend == kBackendXor && d_obj && a16(d_obj) && obj_stride % 16 == 0 &&
+        dev_tune("frame_unfused") == 0 && dev_tune("frame_xor_copy") != 0 &&
+        (static_cast<int64_t>(obj_size) == k * bs || dev_tune("frame_copy_padded") != 0)) {
+        // flat XOR, as the RS decode-join: the plan is one 0 / 1 matrix over the surviving fragments
+        // (lost ones count as zero, as in xor_plan_apply), so the lost data go straight into the
+        // objects and the surviving data payloads are copied there by the same launch
+        unsigned pb[32], db[32];
+        ecamd_xor_code_tables(k, m, hd, pb, db);
+        std::vector<int> outs(k + m);
+        std::vector<uint64_t> srcs(k + m);
+        int n = 0;
+        if (ecamd_xor_plan(1, k, m, hd, pb, db, missing, 0, outs.data(), srcs.data(), &n) < 0)
+            return dev_fail(ECAMD_EINVAL, "flat_xor_hd: erasure pattern not recoverable");
+        uint64_t lost = 0;
+        for (int i = 0; missing[i] >= 0; i++) lost |= uint64_t(1) << missing[i];
+        std::vector<int> douts, inputs, coeff;
+        std::vector<uint64_t> dsrc;
+        uint64_t need = 0, got = 0;
+        for (int i = 0; i < n; i++)
+            if (outs[i] < k) {
+                douts.push_back(outs[i]);
+                dsrc.push_back(srcs[i] & ~lost);
+                need |= srcs[i] & ~lost;
+                got |= uint64_t(1) << outs[i];
+            }
+        if (got == (lost & ((uint64_t(1) << k) - 1))) {  // every lost data fragment has its row
+            for (int f = 0; f < k + m; f++)
+                if (!(lost >> f & 1) && (f < k || (need >> f & 1))) inputs.push_back(f);
+            for (uint64_t sm : dsrc)
+                for (int f : inputs) coeff.push_back(static_cast<int>(sm >> f & 1));
+            return xor_decode_join(k, inputs, douts, coeff, p0, stripe_stride, frag_stride, d_obj, obj_stride, bs,
+                                   nstripes, stream, static_cast<int64_t>(obj_size));
+        }
+    }
     if (data_missing) {  // the systematic fast path (src/erasurecode.c:597-607) skips this
         if (backend == kBackendRs)
             rc = ecamd_rs_decode(k, m, missing, 0, p0, stripe_stride, frag_stride, bs, nstripes, stream);

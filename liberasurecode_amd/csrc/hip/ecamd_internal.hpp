@@ -1,5 +1,6 @@
 // ecamd_internal.hpp -- helpers ecamd_device.hip shares with the other launch files.
 #pragma once
+#include <vector>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -46,6 +47,13 @@ int dev_tune(const char* key);                      // current value of an ecamd
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
                    void* stream, int64_t obj_size = -1, int64_t from = 0, int64_t to = -1);
+
+// Framed flat-XOR decode with data lost, straight into the objects: data output r (outputs[r] < k) =
+// XOR of the inputs (fragment indices) whose coeff[r*K + col] is 1; every data input is copied into
+// its object chunk by the same launch (the RS decode-join with a 0 / 1 matrix).
+int xor_decode_join(int k, const std::vector<int>& inputs, const std::vector<int>& outputs,
+                    const std::vector<int>& coeff, const void* payload0, int64_t stripe_stride, int64_t frag_stride,
+                    void* obj, int64_t obj_stride, int64_t bs, int nstripes, void* stream, int64_t obj_size);
 
 // The same crc variant for a flat-XOR code (parity r = XOR of the data chunks in masks[r], run as a
 // 0 / 1 coefficient matrix through the bitsliced generator).

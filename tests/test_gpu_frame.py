@@ -839,3 +839,42 @@ def test_frame_xor_copy_through_matches_split(F, k, m, hd, ct):
         assert all(np.array_equal(o, out[2]) for o in out), size
         want = expected_stripe(be, k, m, hd, objs[S - 1], ct)
         assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m)), size
+
+
+@pytest.mark.parametrize("k,m,hd,missing", [(10, 6, 4, [0, 1, 2]), (10, 6, 4, [3, 11, 14]), (3, 3, 3, [1, 4]),
+                                            (10, 5, 3, [9, 12]), (20, 6, 4, [19, 0, 7]), (12, 6, 4, [5])])
+def test_frame_xor_decode_join_matches(F, k, m, hd, missing):
+    """Framed flat-XOR decode with data lost (round 4, knob frame_xor_copy): the plan's 0 / 1 matrix over
+    the surviving fragments as one decode-join launch (lost data straight into the objects, surviving
+    data copied there) against decode in place + join; objects equal the originals, guard bytes after
+    every object intact, over sizes with unaligned chunks (Swift's segments), whole tiles and tiny
+    objects, on the bitsliced and the LDS-table kernels."""
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import DeviceBuffer
+    be = ec_api.EC_BACKEND_FLAT_XOR_HD
+    S = 3
+    for size in (1 << 20, 10 * 104858 - 3, 777777, k * 3 * 16384, 100, 1):
+        objs = _objects(S, size, k * 29 + m + size)
+        fb = F.FrameBatch(be, k, m, size, S, hd=hd)
+        fb.encode(_upload_objects(objs, fb.obj_stride))
+        bad = fb.fragments()
+        bad[:, missing] = 0x6B
+        fb.upload_fragments(bad)
+        stride = (size + 16 + 15) // 16 * 16
+        got = []
+        try:
+            for on, mode in ((1, 2), (1, 0), (0, 1)):
+                _lib.check(_lib.dev().ecamd_tune(b"frame_xor_copy", on), "tune")
+                _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+                d = DeviceBuffer(S * stride)
+                d.upload(np.full(S * stride, 0xA5, dtype=np.uint8))
+                fb.decode(missing, d, obj_stride=stride)
+                got.append(d.download().reshape(S, stride))
+                fb.upload_fragments(bad)  # the in-place decode rewrites the lost slots
+        finally:
+            _lib.dev().ecamd_tune(b"frame_xor_copy", 1)
+            _lib.dev().ecamd_tune(b"bitslice", 1)
+        for g in got:
+            for s in range(S):
+                assert g[s, :size].tobytes() == objs[s], (size, s)
+                assert (g[s, size:] == 0xA5).all(), (size, s)
