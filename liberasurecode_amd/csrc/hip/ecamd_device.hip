@@ -249,6 +249,8 @@ struct Tuning {
                                   //   previous input's copy stores: C3 framed encode 0.657 -> 0.721, decode-join
                                   //   0.637 -> 0.747 (profiles/r04_frame_wave_pf_ab2.log). Plain maps: neutral
                                   //   (profiles/r04_bs_prefetch_ab.log), so they keep none
+    Knob bs_late_copy{0};         // 16 KiB-tile bitsliced copy-through (5-8 outputs): 1 = each input's copy stores
+                                  //   after its network and the next input's loads (BitsliceStyle prefetch 1)
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
@@ -364,6 +366,7 @@ int dev_tune(const char* key)
     if (k == "frame_xor_copy") return g_tune.frame_xor_copy;
     if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
+    if (k == "bs_late_copy") return g_tune.bs_late_copy;
     if (k == "bs_prefetch") return g_tune.bs_prefetch;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
     if (k == "bitslice_entries") return g_tune.bitslice_entries;
@@ -767,7 +770,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     const uint32_t in_records = realign_records(a, K, cover, copy_off != nullptr, shifts);
     hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, wave ? 0 : static_cast<int>(g_tune.bitslice_depth),
                                          mode == 2, hold, copy_off != nullptr, 0, wave, &shifts,
-                                         wave && copy_off ? static_cast<int>(g_tune.bs_prefetch) : 0);
+                                         !copy_off ? 0 : wave ? static_cast<int>(g_tune.bs_prefetch)
+                                                              : static_cast<int>(g_tune.bs_late_copy));
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1837,6 +1841,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_cover = value;  // 0 off, anything else on
     } else if (k == "bs_prefetch") {
         g_tune.bs_prefetch = value < 0 ? 2 : value == 2 || value == 4 ? value : 0;  // < 0: the default (2)
+    } else if (k == "bs_late_copy") {
+        g_tune.bs_late_copy = value > 0 ? 1 : 0;
     } else if (k == "bs_realign") {
         g_tune.bs_realign = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_unfused") {

@@ -396,7 +396,8 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     copy = copy || crc;
     wave = wave && !crc;
     depth = (copy || wave) ? 0 : bitslice_depth(depth, K);
-    prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch : 0;
+    prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
+               : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
     std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0) | (prefetch << 9)};
     key.insert(key.end(), coeff.begin(), coeff.end());
     std::vector<int> shifts;  // realigned copy-through inputs: their own kernel (and cache entry)

@@ -594,6 +594,37 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             if (any_shift) s << "        v4u xnh[" << PF << "];\n";
             if (pre(0)) load_next(0);
         }
+        // late copy (style.prefetch 1, copy-through, no realigned inputs): input j's copy stores go out
+        // AFTER its network and after input j + 1's loads, from the planes transposed back (tr16 is an
+        // involution; the network leaves P as it found it), so the next loads never wait for them
+        // (vmcnt retires in issue order) and no register outlives the network
+        if (style.prefetch == 1 && style.copy_through && !any_shift) {
+            auto ld4 = [&](int j) {
+                s << "#pragma unroll\n        for (int c = 0; c < 4; c++) xl[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off["
+                  << j << "] + off + c * " << CS << ", 0, 2);\n";
+            };
+            s << "        v4u xl[4];\n";
+            ld4(0);
+            for (int j = 0; j < net.K; j++) {
+                s << "        {  // input " << j << "\n            u32 P[16];\n"
+                  << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
+                  << "                P[4 * c] = xl[c][0]; P[4 * c + 1] = xl[c][1]; P[4 * c + 2] = xl[c][2]; P[4 * c + 3] = xl[c][3];\n"
+                  << "            }\n";
+                network(j);
+                if (j + 1 < net.K) ld4(j + 1);
+                s << "            tr16(P);  // back to the input's own layout\n"
+                  << "#pragma unroll\n            for (int c = 0; c < 4; c++) {\n"
+                  << "                const v4u x = {P[4 * c], P[4 * c + 1], P[4 * c + 2], P[4 * c + 3]};\n"
+                  << "                __builtin_amdgcn_raw_buffer_store_b128(x, rcopy, cofs" << j << " + off + c * " << CS
+                  << ", 0, 2);  // copy-through\n"
+                  << "            }\n"
+                  << "            __builtin_amdgcn_sched_barrier(0);\n"
+                  << "        }\n";
+            }
+            outputs("rout", "off");
+            s << "    }\n}\n";
+            return s.str();
+        }
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
             const int d = shift_of(j);
@@ -742,7 +773,9 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     wave = wave && !crc;
-    const int pf = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch : 0;
+    // 1: the late copy of the 16 KiB-tile copy-through form
+    const int pf = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
+                   : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
     bool shifted = false;
     if (in_shift && (copy || crc))
         for (int j = 0; j < K && j < static_cast<int>(in_shift->size()); j++) shifted = shifted || ((*in_shift)[j] & 15);
@@ -773,7 +806,9 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 2047 || (cp & 12) == 12 || depth != 0))
         return false;  // copy / one-wave tiles: register loads
     const int pf = (cp >> 8) & 7;
-    if ((pf != 0 && pf != 2 && pf != 4) || (pf && !(cp & 64) && !(cp & 2))) return false;  // one-wave / crc forms
+    if ((pf != 0 && pf != 1 && pf != 2 && pf != 4) || (pf > 1 && !(cp & 64) && !(cp & 2)) ||
+        (pf == 1 && (!(cp & 1) || (cp & 66))))
+        return false;  // 2 / 4: one-wave / crc forms; 1 (late copy): the 16 KiB-tile copy-through form
     if (prefetch) *prefetch = pf;
     if (in_shift) in_shift->clear();
     if (version == 3) {  // shifts: copy-through inputs only, at least one non-zero

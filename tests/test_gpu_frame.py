@@ -770,9 +770,11 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
     try:
         # (bitslice, bs_realign): unaligned object chunks (bs % 16 != 0) read as aligned chunks + the
         # neighbour lane's, realigned (default), or with unaligned loads
-        for mode, realign in ((2, 1), (0, 1), (2, 0)):
+        # + bs_late_copy: each input's copy stores after its network and the next input's loads
+        for mode, realign, late in ((2, 1, 0), (0, 1, 0), (2, 0, 0), (2, 1, 1)):
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"bs_late_copy", late), "tune")
             n0 = _bs_launches()
             # no checksum: with CRC32 a one-pass map that fits takes the fused CRC kernel instead
             fb = F.FrameBatch(be, k, m, size, S, checksum=ec_api.CHKSUM_NONE)
@@ -793,11 +795,12 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
     finally:
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"bs_realign", -1)
-    assert np.array_equal(frags[0], frags[1]) and np.array_equal(frags[2], frags[1])
+        _lib.dev().ecamd_tune(b"bs_late_copy", 0)
+    assert all(np.array_equal(f, frags[1]) for f in frags)
     want = expected_stripe(be, k, m, 0, objs[1], ec_api.CHKSUM_NONE)
     assert all(frags[0][1, i].tobytes() == want[i] for i in range(k + m))
     if lost is not None:
-        assert np.array_equal(joined[0], joined[1]) and np.array_equal(joined[2], joined[1])
+        assert all(np.array_equal(j, joined[1]) for j in joined)
         for s in range(S):
             assert joined[0][s, :size].tobytes() == objs[s]
             assert (joined[0][s, size:] == 0xA5).all()
