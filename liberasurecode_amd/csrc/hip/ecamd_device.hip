@@ -249,8 +249,10 @@ struct Tuning {
                                   //   previous input's copy stores: C3 framed encode 0.657 -> 0.721, decode-join
                                   //   0.637 -> 0.747 (profiles/r04_frame_wave_pf_ab2.log). Plain maps: neutral
                                   //   (profiles/r04_bs_prefetch_ab.log), so they keep none
-    Knob bs_late_copy{0};         // 16 KiB-tile bitsliced copy-through (5-8 outputs): 1 = each input's copy stores
-                                  //   after its network and the next input's loads (BitsliceStyle prefetch 1)
+    Knob bs_late_copy{1};         // 16 KiB-tile bitsliced copy-through (5-8 outputs): 1 (default) = each input's copy
+                                  //   stores after its network and the next input's loads, from the planes
+                                  //   transposed back (BitsliceStyle prefetch 1): C5 framed encode 0.660 ->
+                                  //   0.670, decode-join of 8 data 0.629 -> 0.710 (profiles/r04_late_copy_ab.log)
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
@@ -1842,7 +1844,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_prefetch") {
         g_tune.bs_prefetch = value < 0 ? 2 : value == 2 || value == 4 ? value : 0;  // < 0: the default (2)
     } else if (k == "bs_late_copy") {
-        g_tune.bs_late_copy = value > 0 ? 1 : 0;
+        g_tune.bs_late_copy = value < 0 ? 1 : value > 0 ? 1 : 0;  // < 0: the default (1)
     } else if (k == "bs_realign") {
         g_tune.bs_realign = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_unfused") {

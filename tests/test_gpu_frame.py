@@ -795,7 +795,7 @@ def test_frame_bitsliced_copy_through(F, k, m, size, missing):
     finally:
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"bs_realign", -1)
-        _lib.dev().ecamd_tune(b"bs_late_copy", 0)
+        _lib.dev().ecamd_tune(b"bs_late_copy", -1)
     assert all(np.array_equal(f, frags[1]) for f in frags)
     want = expected_stripe(be, k, m, 0, objs[1], ec_api.CHKSUM_NONE)
     assert all(frags[0][1, i].tobytes() == want[i] for i in range(k + m))

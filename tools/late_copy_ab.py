@@ -70,7 +70,7 @@ def main(rounds=5, reps=6):
         obj.free()
         out.free()
         del fb
-    d.ecamd_tune(b"bs_late_copy", 0)
+    d.ecamd_tune(b"bs_late_copy", -1)
     d.ecamd_tune(b"bitslice", 1)
 
 
