@@ -200,6 +200,13 @@ __device__ __forceinline__ u32 bfi(u32 m, u32 x, u32 y)
 // realigned 16-byte window D bytes into the 32-byte pair (lo, the next aligned chunk): the next
 // chunk is the neighbour lane's lo (DPP wave_shl:1); lane 63 has no neighbour and keeps `own`, the
 // chunk it loaded itself (bound_ctrl off: an out-of-range source leaves the old value)
+// lane 0's 16 bytes in every lane (v_readlane: the last lane's next chunk when it is the next
+// 1 KiB chunk's first, one-wave tiles)
+__device__ __forceinline__ v4u lane0(v4u x)
+{
+    return v4u{(u32)__builtin_amdgcn_readlane((int)x[0], 0), (u32)__builtin_amdgcn_readlane((int)x[1], 0),
+               (u32)__builtin_amdgcn_readlane((int)x[2], 0), (u32)__builtin_amdgcn_readlane((int)x[3], 0)};
+}
 template <int D>
 __device__ __forceinline__ v4u rlg(v4u lo, v4u own)
 {
@@ -581,13 +588,16 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         const int PF = (T == 64 && (style.prefetch == 2 || style.prefetch == 4)) ? style.prefetch : 0;
         // (realigned inputs: their aligned chunks into xn[], the last lane's next ones into xnh[])
         auto pre = [&](int j) { return PF > 0 && j < net.K; };
+        // (style.realign_lane: the last lane's next chunk of chunks 0-2 by v_readlane, T = 64 only)
+        const bool rl = style.realign_lane && T == 64;
         auto load_next = [&](int j) {
             const int d = shift_of(j);
             s << "#pragma unroll\n            for (int c = 0; c < " << PF << "; c++) xn[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off["
               << j << "]" << (d ? " - " + std::to_string(d) : std::string()) << " + off + c * " << CS << ", 0, 2);\n";
-            if (d)
-                s << "#pragma unroll\n            for (int c = 0; c < " << PF << "; c++) xnh[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off["
-                  << j << "] - " << d << " + off + c * " << CS << " + 16 : (i32)0x80000000u, 0, 2);\n";
+            if (d && (!rl || PF > 3))
+                s << "#pragma unroll\n            for (int c = " << (rl ? 3 : 0) << "; c < " << PF
+                  << "; c++) xnh[c] = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off[" << j << "] - " << d
+                  << " + off + c * " << CS << " + 16 : (i32)0x80000000u, 0, 2);\n";
         };
         if (PF) {
             s << "        v4u xn[" << PF << "];\n";
@@ -639,11 +649,12 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                 if (pre(j))
                     s << "#pragma unroll\n            for (int c = 0; c < 4; c++) xa[c] = c < " << pfs << " ? xn[c < " << pfs
                       << " ? c : 0] : " << la << ";\n"
-                      << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = c < " << pfs << " ? xnh[c < " << pfs
-                      << " ? c : 0] : " << lh << ";\n";
+                      << "#pragma unroll\n            for (int c = " << (rl ? 3 : 0) << "; c < 4; c++) xh[c] = c < " << pfs
+                      << " ? xnh[c < " << pfs << " ? c : 0] : " << lh << ";\n";
                 else
                     s << "#pragma unroll\n            for (int c = 0; c < 4; c++) xa[c] = " << la << ";\n"
-                      << "#pragma unroll\n            for (int c = 0; c < 4; c++) xh[c] = " << lh << ";\n";
+                      << "#pragma unroll\n            for (int c = " << (rl ? 3 : 0) << "; c < 4; c++) xh[c] = " << lh << ";\n";
+                if (rl) s << "#pragma unroll\n            for (int c = 0; c < 3; c++) xh[c] = lane0(xa[c + 1]);\n";
             }
             const std::string ld = "__builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" + std::to_string(j) +
                                    "] + off + c * " + std::to_string(CS) + ", 0, 2)";

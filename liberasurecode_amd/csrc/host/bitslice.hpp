@@ -86,6 +86,9 @@ struct BitsliceStyle {
     // wave has the next input's loads in flight while it computes (the compiler otherwise issues each
     // input's loads right before its use and waits for them at once)
     int prefetch = 0;
+    // one-wave realigned inputs: the last lane's next chunk for chunks 0-2 is lane 0 of the input's
+    // following chunk (1 KiB on), taken by v_readlane instead of a load; only chunk 3's is loaded
+    bool realign_lane = false;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
