@@ -143,6 +143,39 @@ def test_jitc_builds_realigned_inputs(tmp_path, flags, tag):
         assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2
 
 
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so") or not shutil.which("/opt/rocm/bin/hipcc"),
+                    reason="needs hiprtc and hipcc")
+def test_jitc_realign_lane_experiment(tmp_path):
+    """Experiment flag ECAMD_BS_RLANE (round 4, profiles/r04_rlane_ab.log): the one-wave copy-through
+    form takes the last lane's next chunk of chunks 0-2 from lane 0 of the following chunk by
+    v_readlane and loads only chunk 3's; the kernel builds without scratch and issues fewer loads."""
+    G = orc.generator(10, 4)
+    shifts = [(j * 104858) % 16 for j in range(10)]
+    rows = [" ".join(str(c) for c in G[100 + 10 * r:100 + 10 * (r + 1)]) for r in range(4)]
+    req_text = f"ecamd-bitslice-request 3\n4 10 96 0 {1 | 192 | (2 << 8)}\n" + " ".join(map(str, shifts)) + "\n" + \
+        "\n".join(rows) + "\n"
+    loads = {}
+    for rl in ("0", "1"):
+        req = tmp_path / f"rl{rl}.req"
+        req.write_text(req_text)
+        out = tmp_path / f"rl{rl}.co"
+        env = dict(os.environ, ECAMD_JIT_KEEP_SOURCE="1", ECAMD_BS_RLANE=rl)
+        r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        src = (tmp_path / f"rl{rl}.hip").read_text()
+        assert ("xh[c] = lane0(xa[c + 1]);" in src) == (rl == "1")
+        hip = tmp_path / f"k{rl}.hip"
+        hip.write_text("#include <hip/hip_runtime.h>\n" + src)
+        asm = tmp_path / f"k{rl}.s"
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S",
+                            "-o", str(asm), str(hip)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        text = asm.read_text()
+        assert "ScratchSize: 0" in text
+        loads[rl] = sum(1 for ln in text.splitlines() if ln.strip().startswith("buffer_load"))
+    assert loads["1"] < loads["0"], loads
+
+
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs hiprtc")
 def test_jitc_prefetch_flag(tmp_path):
     """Flag bits 8-10 (round 4): the one-wave form loads the first 2 / 4 chunks of the next input before
