@@ -88,6 +88,52 @@ int scratch(int dev, void* stream, size_t words, uint32_t** out, int slot = 0)
     return 0;
 }
 
+// Per-(device, stream) side stream (knob frame_tail_fork): side_fork makes it wait for everything
+// issued so far to the caller's stream; side_join makes the caller's stream wait for everything
+// issued to it since.  The payload tails of a padded framed encode run there beside the launch over
+// the whole tiles; the two write disjoint bytes.
+struct Side {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::map<std::pair<int, void*>, Side> g_side;
+
+int side_fork(int dev, void* stream, void** side)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    Side& e = g_side[std::make_pair(dev, stream)];
+    if (!e.s) {
+        HIP_TRY(hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&e.fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e.join, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(e.fork, static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamWaitEvent(e.s, e.fork, 0));
+    *side = e.s;
+    return 0;
+}
+
+int side_join(int dev, void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    const Side& e = g_side[std::make_pair(dev, stream)];
+    if (!e.s) return dev_fail(ECAMD_EHIP, "side_join without side_fork");
+    HIP_TRY(hipEventRecord(e.join, e.s));
+    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), e.join, 0));
+    return 0;
+}
+
+// Knob frame_tail_fork: 2 forks every padded framed encode's tail; 1 (default) only the encodes
+// without checksum whose payloads' rest is 1-4 KiB (its codec then one LDS-table launch): Swift
+// segments RS 1.320 -> 1.233 ms, flat XOR 1.340 -> 1.315, 4 MiB objects 1.279 -> 1.266.  A rest that
+// takes a bitsliced tile too (C3 + 10 B: 1.183 -> 1.240) and the CRC32 encodes (LDS-bound side work
+// beside an LDS-bound launch) measured slower (profiles/r04_tail_fork_ab1.log, _ab2.log).
+bool fork_tail(int64_t rest, bool crc)
+{
+    const int knob = dev_tune("frame_tail_fork");
+    return rest > 0 && (knob == 2 || (knob == 1 && !crc && rest >= 1024 && rest < 4096));
+}
+
 struct Code {
     int backend, k, m, hd, w;
 };
@@ -537,34 +583,54 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
     unsigned pb[32], db[32];
     if (xorc) ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db);
     const int pos = npos | (lane ? 8 : 0) | (nib ? 16 : 0);
-    rc = xorc ? xor_encode_copy_crc_bs(pb, c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                                       partial, q, stream, pos, cover)
-              : rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                                      partial, q, stream, pos, cover);
-    if (rc) return rc;
-    if (tail) {
-        // from here on a failure is an error, not a fallback: part of the payloads is written
+    auto whole = [&] {  // the whole tiles [0, cover): codec + copy + CRC partials in one launch
+        return xorc ? xor_encode_copy_crc_bs(pb, c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes,
+                                             img, partial, q, stream, pos, cover)
+                    : rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                                            partial, q, stream, pos, cover);
+    };
+    // the payloads' rest [cover, bs): codec, then the CRC32 of that range on its own; `exact`: no byte
+    // below cover is touched (the side stream runs it beside whole())
+    auto rest = [&](void* st, bool exact) {
+        int r;
         if (xorc) {  // the data payloads' rest by the split, then the XOR of that range
-            rc = split_range(dev, c.k, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, stream);
-            if (rc == 0) {
+            r = split_range(dev, c.k, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, st);
+            if (r == 0) {
                 std::vector<int64_t> in_off(c.k), out_off(c.m);
                 for (int j = 0; j < c.k; j++) in_off[j] = j * fs;
-                for (int r = 0; r < c.m; r++) out_off[r] = (c.k + r) * fs;
+                for (int o = 0; o < c.m; o++) out_off[o] = (c.k + o) * fs;
                 uint8_t* pc = frags + kHeaderBytes + cover;
-                rc = ecamd_xor_apply_strided(pb, c.m, c.k, pc, ss, in_off.data(), pc, ss, out_off.data(), bs - cover,
-                                             nstripes, stream);
+                r = ecamd_xor_apply_strided(pb, c.m, c.k, pc, ss, in_off.data(), pc, ss, out_off.data(), bs - cover,
+                                            nstripes, st);
             }
         } else {
-            rc = encode_tail(dev, c, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, stream);
-            if (rc == ECAMD_EINVAL)
-                rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, stream,
-                                    static_cast<int64_t>(obj_size), cover);
+            // encode_tail re-encodes whole 4 KiB tiles reaching below cover from the payloads: only
+            // after whole() on the same stream
+            r = exact ? ECAMD_EINVAL : encode_tail(dev, c, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, cover, st);
+            if (r == ECAMD_EINVAL)
+                r = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, st,
+                                   static_cast<int64_t>(obj_size), cover);
         }
-        if (rc) return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail codec failed") : rc;
+        if (r) return r == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail codec failed") : r;
         HeaderArgs none{};
-        if ((rc = run_crc(dev, legacy, true, frags, ss, fs, kHeaderBytes + cover, nf, tail, nstripes, tail_crc,
-                          none, stream)))
-            return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail CRC failed") : rc;
+        if ((r = run_crc(dev, legacy, true, frags, ss, fs, kHeaderBytes + cover, nf, tail, nstripes, tail_crc, none,
+                         st)))
+            return r == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail CRC failed") : r;
+        return 0;
+    };
+    if (fork_tail(tail, true)) {
+        void* side = nullptr;
+        if ((rc = side_fork(dev, stream, &side))) return rc;
+        rc = rest(side, true);
+        // whole() may decline (ECAMD_EINVAL: the kernel is still compiling): the caller's fallback then
+        // rewrites every payload after the tails (joined first), byte-identically
+        if (rc == 0) rc = whole();
+        const int rj = side_join(dev, stream);
+        if (rc || rj) return rc ? rc : rj;
+    } else {
+        if ((rc = whole())) return rc;
+        // from here on a failure is an error, not a fallback: part of the payloads is written
+        if (tail && (rc = rest(stream, false))) return rc;
     }
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream, cover,
                            tail_crc);
@@ -663,12 +729,24 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
                                   frag_stride, bs, nstripes, stream);
             if (rc != ECAMD_EINVAL) return rc;
         }
-        // the whole 4 KiB tiles every payload holds on the copy-through launch, the rest by
-        // encode_tail (split + plain encode of the payloads' last tiles)
+        // the whole 4 KiB tiles every payload holds on the copy-through launch; the rest by the
+        // copy-through codec of exactly [cover, bs) on the side stream beside it (knob
+        // frame_tail_fork), or after it by encode_tail (split + plain encode of the payloads' last tiles)
         const int64_t last = static_cast<int64_t>(obj_size) - (k - 1) * bs;
         const int64_t cover = last > 0 ? std::min(bs, last) / 4096 * 4096 : 0;
         rc = ECAMD_EINVAL;
-        if (cover > 0 && cover < bs && dev_tune("frame_tail_bs") != 0) {
+        if (cover > 0 && fork_tail(bs - cover, checksum == kChksumCrc32)) {
+            // the rest [cover, bs) on the side stream, from the objects (exact range), beside the whole tiles
+            void* side = nullptr;
+            if ((rc = side_fork(dev, stream, &side))) return rc;
+            rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, side,
+                                static_cast<int64_t>(obj_size), cover);
+            if (rc == 0)
+                rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, stream,
+                                    static_cast<int64_t>(obj_size), 0, cover);
+            const int rj = side_join(dev, stream);
+            if (rc == 0) rc = rj;
+        } else if (cover > 0 && cover < bs && dev_tune("frame_tail_bs") != 0) {
             if ((rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, stream,
                                      static_cast<int64_t>(obj_size), 0, cover)))
                 return rc;
@@ -702,20 +780,35 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
         const int64_t cover = last > 0 ? std::min(bs, last) / 4096 * 4096 : 0;
         unsigned pb[32], db[32];
         ecamd_xor_code_tables(k, m, hd, pb, db);
-        rc = cover > 0 ? xor_encode_copy(pb, k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, cover,
-                                         nstripes, stream)
-                       : ECAMD_EINVAL;
-        if (rc == 0 && cover < bs) {  // from here on a failure is an error: part of the payloads is written
-            rc = split_range(dev, k, d_obj, obj_stride, obj_size, frags, stripe_stride, frag_stride, bs, nstripes,
-                             cover, stream);
-            if (rc == 0) {
+        // the payloads' rest [cover, bs): split, then the XOR of that range (bytes disjoint from the
+        // copy-through launch: on the side stream beside it, knob frame_tail_fork)
+        auto rest = [&](void* st2) {
+            int r = split_range(dev, k, d_obj, obj_stride, obj_size, frags, stripe_stride, frag_stride, bs, nstripes,
+                                cover, st2);
+            if (r == 0) {
                 std::vector<int64_t> in_off(k), out_off(m);
                 for (int j = 0; j < k; j++) in_off[j] = j * frag_stride;
-                for (int r = 0; r < m; r++) out_off[r] = (k + r) * frag_stride;
-                rc = ecamd_xor_apply_strided(pb, m, k, p0 + cover, stripe_stride, in_off.data(), p0 + cover,
-                                             stripe_stride, out_off.data(), bs - cover, nstripes, stream);
+                for (int o = 0; o < m; o++) out_off[o] = (k + o) * frag_stride;
+                r = ecamd_xor_apply_strided(pb, m, k, p0 + cover, stripe_stride, in_off.data(), p0 + cover,
+                                            stripe_stride, out_off.data(), bs - cover, nstripes, st2);
             }
-            if (rc) return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed xor encode: tail failed") : rc;
+            return r == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed xor encode: tail failed") : r;
+        };
+        if (cover > 0 && fork_tail(bs - cover, checksum == kChksumCrc32)) {
+            void* side = nullptr;
+            if ((rc = side_fork(dev, stream, &side))) return rc;
+            rc = rest(side);
+            if (rc == 0)  // ECAMD_EINVAL (declined): the split path below rewrites every payload after the join
+                rc = xor_encode_copy(pb, k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, cover, nstripes,
+                                     stream);
+            const int rj = side_join(dev, stream);
+            if (rj) return rj;
+        } else {
+            rc = cover > 0 ? xor_encode_copy(pb, k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, cover,
+                                             nstripes, stream)
+                           : ECAMD_EINVAL;
+            // from here on a failure is an error: part of the payloads is written
+            if (rc == 0 && cover < bs && (rc = rest(stream))) return rc;
         }
         if (rc == 0)
             return run_crc(dev, legacy_crc(), checksum == kChksumCrc32, frags, stripe_stride, frag_stride,

@@ -450,10 +450,12 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         # (frame_crc_cover, bs_realign, frame_tail_bs): the crc variant reads the object chunks
         # realigned from aligned loads + the neighbour lane's (default) or with unaligned loads; the
         # payloads' rest by split + plain encode of their last tiles (default) or the LDS-table launch
-        for cover, realign, tail in ((1, 1, 1), (0, 1, 1), (1, 0, 1), (1, 1, 0)):
+        # (+ frame_tail_fork 2: the rest and its CRC32 on the side stream beside the crc variant)
+        for cover, realign, tail, fork in ((1, 1, 1, 1), (0, 1, 1, 1), (1, 0, 1, 1), (1, 1, 0, 1), (1, 1, 1, 2)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_cover", cover), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_tail_fork", fork), "tune")
             n0 = _bs_launches()
             fb = F.FrameBatch(be, k, m, size, S)
             fb.encode(_upload_objects(objs, fb.obj_stride))
@@ -469,6 +471,7 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"bs_realign", -1)
         _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
+        _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
     assert all(np.array_equal(o, out[1]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
     assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
@@ -517,13 +520,15 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         # tiles with realigned loads when the object chunks are unaligned, knob bs_wave_copy 2), on
         # the LDS tables, and the split-then-encode path
         # (+ frame_tail_bs: the payloads' rest past the whole tiles by split + plain encode, or not;
-        # + bs_prefetch: the copy-through kernel's next-input loads ahead of its copy stores, 0 / 2 / 4)
-        for padded, mode, tail, pf in ((1, 2, 1, 2), (1, 0, 1, 2), (0, 1, 1, 2), (1, 2, 0, 2), (1, 2, 1, 0),
-                                       (1, 2, 1, 4)):
+        # + bs_prefetch: the copy-through kernel's next-input loads ahead of its copy stores, 0 / 2 / 4;
+        # + frame_tail_fork: the rest on the side stream by default (1-4 KiB, no checksum), never, always)
+        for padded, mode, tail, pf, fork in ((1, 2, 1, 2, 1), (1, 0, 1, 2, 1), (0, 1, 1, 2, 1), (1, 2, 0, 2, 0),
+                                             (1, 2, 1, 0, 1), (1, 2, 1, 4, 1), (1, 2, 1, 2, 0), (1, 2, 1, 2, 2)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_prefetch", pf), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_tail_fork", fork), "tune")
             fb = F.FrameBatch(be, k, m, size, S, checksum=ct)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
@@ -532,6 +537,7 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
         _lib.dev().ecamd_tune(b"bs_prefetch", -1)
+        _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
     assert all(np.array_equal(o, out[2]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[1], ct)
     assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
@@ -825,10 +831,12 @@ def test_frame_xor_copy_through_matches_split(F, k, m, hd, ct):
         try:
             # (frame_xor_copy, bitslice): with CRC32 and bitslice 2 the checksums fold into the bitsliced
             # crc variant run as a 0 / 1 matrix (launch counter); bitslice 0 the copy-through XOR + CRC
-            # pass; frame_xor_copy 0 the split + XOR path
-            for on, mode in ((1, 2), (1, 0), (0, 1)):
+            # pass; frame_xor_copy 0 the split + XOR path; frame_tail_fork 0 / 2: the payloads' rest after
+            # the whole tiles on the caller's stream / always on the side stream (default: no checksum, 1-4 KiB)
+            for on, mode, fork in ((1, 2, 1), (1, 0, 1), (0, 1, 1), (1, 2, 0), (1, 2, 2)):
                 _lib.check(_lib.dev().ecamd_tune(b"frame_xor_copy", on), "tune")
                 _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
+                _lib.check(_lib.dev().ecamd_tune(b"frame_tail_fork", fork), "tune")
                 n0 = _bs_launches()
                 fb = F.FrameBatch(be, k, m, size, S, hd=hd, checksum=ct)
                 fb.encode(_upload_objects(objs, fb.obj_stride))
@@ -839,6 +847,7 @@ def test_frame_xor_copy_through_matches_split(F, k, m, hd, ct):
         finally:
             _lib.dev().ecamd_tune(b"frame_xor_copy", 1)
             _lib.dev().ecamd_tune(b"bitslice", 1)
+            _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
         assert all(np.array_equal(o, out[2]) for o in out), size
         want = expected_stripe(be, k, m, hd, objs[S - 1], ct)
         assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m)), size
