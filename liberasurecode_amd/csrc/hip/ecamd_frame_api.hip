@@ -124,10 +124,11 @@ int side_join(int dev, void* stream)
 }
 
 // Knob frame_tail_fork: 2 forks every padded framed encode's tail; 1 (default) only the encodes
-// without checksum whose payloads' rest is 1-4 KiB (its codec then one LDS-table launch): Swift
-// segments RS 1.320 -> 1.233 ms, flat XOR 1.340 -> 1.315, 4 MiB objects 1.279 -> 1.266.  A rest that
-// takes a bitsliced tile too (C3 + 10 B: 1.183 -> 1.240) and the CRC32 encodes (LDS-bound side work
-// beside an LDS-bound launch) measured slower (profiles/r04_tail_fork_ab1.log, _ab2.log).
+// without checksum whose payloads' rest is 1-4 KiB (its codec then one LDS-table launch; the headers
+// go to the side stream too): Swift segments RS 1.316 -> 1.225 ms, flat XOR 1.339 -> 1.312, 4 MiB
+// objects 1.276 -> 1.260.  A rest that takes a bitsliced tile too (C3 + 10 B: 1.184 -> 1.232) and the
+// CRC32 encodes (LDS-bound side work beside an LDS-bound launch) measured slower
+// (profiles/r04_tail_fork_ab1.log .. _ab3.log).
 bool fork_tail(int64_t rest, bool crc)
 {
     const int knob = dev_tune("frame_tail_fork");
@@ -741,11 +742,15 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
             if ((rc = side_fork(dev, stream, &side))) return rc;
             rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, side,
                                 static_cast<int64_t>(obj_size), cover);
+            const bool heads = checksum != kChksumCrc32;  // no checksum: the headers read no payload byte
+            if (rc == 0 && heads)
+                rc = run_crc(dev, legacy_crc(), false, frags, stripe_stride, frag_stride, kHeaderBytes, k + m, bs,
+                             nstripes, nullptr, header_args(c, checksum, bs, obj_size, 0), side);
             if (rc == 0)
                 rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, stream,
                                     static_cast<int64_t>(obj_size), 0, cover);
             const int rj = side_join(dev, stream);
-            if (rc == 0) rc = rj;
+            if (rc || rj || heads) return rc ? rc : rj;
         } else if (cover > 0 && cover < bs && dev_tune("frame_tail_bs") != 0) {
             if ((rc = rs_encode_copy(k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, nstripes, stream,
                                      static_cast<int64_t>(obj_size), 0, cover)))
@@ -798,11 +803,16 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
             void* side = nullptr;
             if ((rc = side_fork(dev, stream, &side))) return rc;
             rc = rest(side);
-            if (rc == 0)  // ECAMD_EINVAL (declined): the split path below rewrites every payload after the join
+            const bool heads = checksum != kChksumCrc32;  // no checksum: the headers read no payload byte
+            if (rc == 0 && heads)
+                rc = run_crc(dev, legacy_crc(), false, frags, stripe_stride, frag_stride, kHeaderBytes, k + m, bs,
+                             nstripes, nullptr, header_args(c, checksum, bs, obj_size, 0), side);
+            if (rc == 0)  // ECAMD_EINVAL (declined): the split path below rewrites everything after the join
                 rc = xor_encode_copy(pb, k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, cover, nstripes,
                                      stream);
             const int rj = side_join(dev, stream);
             if (rj) return rj;
+            if (rc == 0 && heads) return 0;
         } else {
             rc = cover > 0 ? xor_encode_copy(pb, k, m, d_obj, obj_stride, p0, stripe_stride, frag_stride, bs, cover,
                                              nstripes, stream)
