@@ -273,7 +273,8 @@ struct Tuning {
                                   //   past the whole tiles (codec, and its CRC32) on a side stream forked from
                                   //   the caller's, beside the launch of the whole tiles, with exact ranges (no
                                   //   byte written by both); 1 = without checksum and a rest of 1-4 KiB, 2 = always,
-                                  //   0 = after it on the caller's stream (ecamd_frame_api.hip fork_tail)
+                                  //   0 = after it on the caller's stream (ecamd_frame_api.hip fork_tail).  The
+                                  //   same for the LDS-table rest of a copy-through map (decode-join): map_apply_copy
     Knob frame_crc_prefetch{0};   // bitsliced crc variant (<= 4 outputs; the 8-output form has no registers left):
                                   //   chunks (0, 2, 4) of the next input loaded before the current input's
                                   //   copy stores (BitsliceStyle::prefetch)
@@ -1190,6 +1191,19 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
     // every input / copy / output fully holds (the first group copying the inputs through); the
     // LDS-table passes of those rows then run on the rest of each fragment only.
     std::vector<int64_t> bs_done(static_cast<size_t>((map->R + 7) / 8), 0);
+    // knob frame_tail_fork: the LDS-table passes over each fragment's rest run on a side stream
+    // beside the bitsliced launch (disjoint bytes) when that rest is 1-4 KiB -- one LDS-table launch
+    // -- or, at 2, any rest; `pst` is the stream the passes go to
+    hipStream_t pst = st;
+    struct Joiner {  // error paths: the caller's stream still ends up after the side stream's work
+        int dev;
+        void* stream;
+        bool on = false;
+        ~Joiner()
+        {
+            if (on) (void)side_join(dev, stream);
+        }
+    } joiner{map->device, stream};
     {
         ApplyArgs b{};
         b.in_base = in_base;
@@ -1232,6 +1246,17 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
             }
             return true;
         };
+        if (g_tune.stream && g_tune.frame_tail_fork != 0) {
+            const int64_t rest = bs - cover_of(0);
+            if (rest > 0 && rest < bs && (g_tune.frame_tail_fork == 2 || (rest >= 1024 && rest < 4096)) &&
+                tail_on_stream(0)) {
+                void* side = nullptr;
+                const int rc = side_fork(map->device, stream, &side);
+                if (rc) return rc;
+                pst = static_cast<hipStream_t>(side);
+                joiner.on = true;
+            }
+        }
         for (int g = 0; g * 8 < map->R && g_tune.stream; g++) {
             if (cover_of(g) < bs && !tail_on_stream(g)) continue;
             int brc = 0;
@@ -1279,7 +1304,7 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         int rc;
         if (g_tune.stream && p.ncols <= 4 * kStreamGroups && stream_offsets(a, pbs) &&
             (p.row0 != 0 || stream_copy_offsets(a, pbs))) {
-            rc = launch_stream_pass(a, map->device, p.bytes, p.width, 1, false, pbs, nstripes, st);
+            rc = launch_stream_pass(a, map->device, p.bytes, p.width, 1, false, pbs, nstripes, pst);
             if (rc) return rc;
             continue;
         }
@@ -1291,18 +1316,22 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         dim3 grid(g.grid), block(g.threads);
         if (p.row0 == 0) {  // the first row group copies the inputs through
             switch (p.width) {
-            case 2: hipLaunchKernelGGL((gf16_copy_apply_kernel<2>), grid, block, g.lds, st, a); break;
-            case 4: hipLaunchKernelGGL((gf16_copy_apply_kernel<4>), grid, block, g.lds, st, a); break;
-            default: hipLaunchKernelGGL((gf16_copy_apply_kernel<8>), grid, block, g.lds, st, a); break;
+            case 2: hipLaunchKernelGGL((gf16_copy_apply_kernel<2>), grid, block, g.lds, pst, a); break;
+            case 4: hipLaunchKernelGGL((gf16_copy_apply_kernel<4>), grid, block, g.lds, pst, a); break;
+            default: hipLaunchKernelGGL((gf16_copy_apply_kernel<8>), grid, block, g.lds, pst, a); break;
             }
         } else {
             switch (p.width) {
-            case 2: hipLaunchKernelGGL((gf16_apply_kernel<2, false, true, false>), grid, block, g.lds, st, a); break;
-            case 4: hipLaunchKernelGGL((gf16_apply_kernel<4, false, true, false>), grid, block, g.lds, st, a); break;
-            default: hipLaunchKernelGGL((gf16_apply_kernel<8, false, true, false>), grid, block, g.lds, st, a); break;
+            case 2: hipLaunchKernelGGL((gf16_apply_kernel<2, false, true, false>), grid, block, g.lds, pst, a); break;
+            case 4: hipLaunchKernelGGL((gf16_apply_kernel<4, false, true, false>), grid, block, g.lds, pst, a); break;
+            default: hipLaunchKernelGGL((gf16_apply_kernel<8, false, true, false>), grid, block, g.lds, pst, a); break;
             }
         }
         HIP_TRY(hipGetLastError());
+    }
+    if (joiner.on) {
+        joiner.on = false;
+        return side_join(map->device, stream);
     }
     return 0;
 }
@@ -1325,6 +1354,44 @@ bool copy_aligned_payloads(const void* obj, const void* payload0, int64_t obj_st
 }
 
 }  // namespace
+
+// Per-(device, stream) side stream (knob frame_tail_fork): side_fork makes it wait for everything
+// issued so far to the caller's stream; side_join makes the caller's stream wait for everything
+// issued to it since.  The payload tails of a padded framed encode, and the LDS-table rest of a
+// copy-through map, run there beside the launch over the whole tiles; the two write disjoint bytes.
+namespace {
+struct Side {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+std::map<std::pair<int, void*>, Side> g_side;
+}  // namespace
+
+int side_fork(int dev, void* stream, void** side)
+{
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    Side& e = g_side[std::make_pair(dev, stream)];
+    if (!e.s) {
+        HIP_TRY(hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&e.fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e.join, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(e.fork, static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipStreamWaitEvent(e.s, e.fork, 0));
+    *side = e.s;
+    return 0;
+}
+
+int side_join(int dev, void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_side_mu);
+    const auto it = g_side.find(std::make_pair(dev, stream));
+    if (it == g_side.end() || !it->second.s) return fail(ECAMD_EHIP, "side_join without side_fork");
+    HIP_TRY(hipEventRecord(it->second.join, it->second.s));
+    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), it->second.join, 0));
+    return 0;
+}
 
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,

@@ -88,41 +88,6 @@ int scratch(int dev, void* stream, size_t words, uint32_t** out, int slot = 0)
     return 0;
 }
 
-// Per-(device, stream) side stream (knob frame_tail_fork): side_fork makes it wait for everything
-// issued so far to the caller's stream; side_join makes the caller's stream wait for everything
-// issued to it since.  The payload tails of a padded framed encode run there beside the launch over
-// the whole tiles; the two write disjoint bytes.
-struct Side {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-std::map<std::pair<int, void*>, Side> g_side;
-
-int side_fork(int dev, void* stream, void** side)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    Side& e = g_side[std::make_pair(dev, stream)];
-    if (!e.s) {
-        HIP_TRY(hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&e.fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&e.join, hipEventDisableTiming));
-    }
-    HIP_TRY(hipEventRecord(e.fork, static_cast<hipStream_t>(stream)));
-    HIP_TRY(hipStreamWaitEvent(e.s, e.fork, 0));
-    *side = e.s;
-    return 0;
-}
-
-int side_join(int dev, void* stream)
-{
-    std::lock_guard<std::mutex> lk(g_mu);
-    const Side& e = g_side[std::make_pair(dev, stream)];
-    if (!e.s) return dev_fail(ECAMD_EHIP, "side_join without side_fork");
-    HIP_TRY(hipEventRecord(e.join, e.s));
-    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), e.join, 0));
-    return 0;
-}
-
 // Knob frame_tail_fork: 2 forks every padded framed encode's tail; 1 (default) only the encodes
 // without checksum whose payloads' rest is 1-4 KiB (its codec then one LDS-table launch; the headers
 // go to the side stream too): Swift segments RS 1.316 -> 1.225 ms, flat XOR 1.339 -> 1.312, 4 MiB

@@ -44,6 +44,12 @@ int dev_tune(const char* key);                      // current value of an ecamd
 // object base / stride and payloads; bs even (the object side may be read unaligned).  from > 0 (a
 // multiple of 16): only bytes [from, bs) of every payload (the rest of a partly fused encode); to > 0:
 // only bytes [from, to).
+// Side stream of (dev, stream) for work beside the caller's launches (knob frame_tail_fork):
+// side_fork orders it after everything issued to `stream` so far, side_join orders `stream` after
+// everything issued to the side stream since.
+int side_fork(int dev, void* stream, void** side);
+int side_join(int dev, void* stream);
+
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
                    void* stream, int64_t obj_size = -1, int64_t from = 0, int64_t to = -1);

@@ -560,11 +560,14 @@ def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
     got = []
     try:
         # (frame_copy_padded, bitslice, bs_prefetch): the one-wave bitsliced decode-join (copy-through,
-        # next input's loads ahead of the copy stores: 2 default, 0, 4), the LDS tables, decode + join
-        for padded, mode, pf in ((1, 2, 2), (1, 2, 0), (1, 2, 4), (1, 0, 2), (0, 1, 2)):
+        # next input's loads ahead of the copy stores: 2 default, 0, 4), the LDS tables, decode + join;
+        # frame_tail_fork: the LDS-table rest beside the bitsliced launch by default (1-4 KiB), never, always
+        for padded, mode, pf, fork in ((1, 2, 2, 1), (1, 2, 0, 1), (1, 2, 4, 1), (1, 0, 2, 1), (1, 2, 2, 0),
+                                       (1, 2, 2, 2), (0, 1, 2, 1)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_prefetch", pf), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_tail_fork", fork), "tune")
             host = np.full(S * stride, 0xA5, dtype=np.uint8)
             d = DeviceBuffer(host.size)
             d.upload(host)
@@ -574,6 +577,7 @@ def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
         _lib.dev().ecamd_tune(b"frame_copy_padded", 1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"bs_prefetch", -1)
+        _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
     assert all(np.array_equal(g, got[-1]) for g in got)
     for s in range(S):
         assert got[0][s, :size].tobytes() == objs[s]

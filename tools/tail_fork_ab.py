@@ -5,7 +5,8 @@ flat XOR (10,6,4), checksum none and CRC32 -- with the payloads' rest past the w
 stream beside the launch over the whole tiles (2: always; 1: default, without checksum and a rest of 1-4 KiB)
 or after it on the caller's stream (0).  Fragments
 checked equal across the variants; interleaved rounds, median ms and fraction of 8 TB/s of the
-algorithmic bytes (objects read + payloads written)."""
+algorithmic bytes (objects read + payloads written; payloads read + objects written for the RS decode-join
+of data {0,1,2,3}, whose LDS-table rest forks the same way)."""
 import json
 import os
 import statistics
@@ -34,15 +35,27 @@ def main(rounds=5, reps=10):
             obj = D.DeviceBuffer(fb.obj_stride * S)
             _lib.check(d.ecamd_fill_splitmix(obj.ptr, fb.obj_stride, 0, 1, size, S, 0, 0x7A, st.handle), "fill")
             nbytes = S * (size + (k + m) * fb.blocksize)
+            # the decode-join of data {0,1,2,3} (RS, no checksum): the LDS-table rest of the copy-through
+            # map forked the same way (map_apply_copy)
+            dj = be == frame.RS_VAND and ck == frame.CHKSUM_NONE
+            out = D.DeviceBuffer(fb.obj_stride * S) if dj else None
+            dbytes = S * ((k + 4) * fb.blocksize - 4 * fb.blocksize + size)
             ref = None
             for v in (0, 1, 2):
                 d.ecamd_tune(b"frame_tail_fork", v)
                 fb.encode(obj, stream=st)
                 st.synchronize()
                 f = fb.fragments()
+                if dj:
+                    fb.decode([0, 1, 2, 3], out, stream=st)
+                    st.synchronize()
+                    f = (f, out.download())
                 if ref is None:
                     ref = f
-                assert (f == ref).all(), (tag, ck, v)
+                if dj:
+                    assert (f[0] == ref[0]).all() and (f[1] == ref[1]).all(), (tag, ck, v)
+                else:
+                    assert (f == ref).all(), (tag, ck, v)
             del ref, f
             for _ in range(20):
                 fb.encode(obj, stream=st)
@@ -58,11 +71,23 @@ def main(rounds=5, reps=10):
                     b.record(st)
                     st.synchronize()
                     times.setdefault(v, []).append(a.elapsed_ms(b) / reps)
+                    if dj:
+                        fb.decode([0, 1, 2, 3], out, stream=st)
+                        a.record(st)
+                        for _ in range(reps):
+                            fb.decode([0, 1, 2, 3], out, stream=st)
+                        b.record(st)
+                        st.synchronize()
+                        times.setdefault(("join_0123", v), []).append(a.elapsed_ms(b) / reps)
             for v, ts in times.items():
                 ms = statistics.median(ts)
-                print(json.dumps({"shape": tag, "checksum": ck, "frame_tail_fork": v, "ms": round(ms, 4),
-                                  "frac": round(nbytes / (ms * 1e-3) / 8e12, 4)}), flush=True)
+                op, v = (v[0], v[1]) if isinstance(v, tuple) else ("encode", v)
+                nb = dbytes if op == "join_0123" else nbytes
+                print(json.dumps({"shape": tag, "op": op, "checksum": ck, "frame_tail_fork": v, "ms": round(ms, 4),
+                                  "frac": round(nb / (ms * 1e-3) / 8e12, 4)}), flush=True)
             obj.free()
+            if out is not None:
+                out.free()
             del fb
     d.ecamd_tune(b"frame_tail_fork", -1)
     d.ecamd_tune(b"bitslice", 1)
