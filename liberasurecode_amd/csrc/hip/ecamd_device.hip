@@ -269,6 +269,8 @@ struct Tuning {
                                   //   rest past the whole tiles by a streaming split + the plain bitsliced
                                   //   encode of their last 4 KiB tiles (ecamd_frame_api.hip encode_tail);
                                   //   0 = the LDS-table copy-through launch
+    Knob frame_tail_tiles{1};     // encode_tail: whole 4 KiB tiles past `from` by the copy-through launch of that
+                                  //   range first (split + re-encoded tiles only for the last partial one); 0 off
     Knob frame_tail_fork{1};      // framed encode of objects that do not fill the payloads: the payloads' rest
                                   //   past the whole tiles (codec, and its CRC32) on a side stream forked from
                                   //   the caller's, beside the launch of the whole tiles, with exact ranges (no
@@ -372,6 +374,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_prefetch") return g_tune.frame_crc_prefetch;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "frame_tail_fork") return g_tune.frame_tail_fork;
+    if (k == "frame_tail_tiles") return g_tune.frame_tail_tiles;
     if (k == "frame_xor_copy") return g_tune.frame_xor_copy;
     if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
@@ -1908,6 +1911,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_join_align = value < 0 ? 2 : std::min(value, 2);  // < 0: the default (2)
     } else if (k == "frame_xor_copy") {
         g_tune.frame_xor_copy = value;  // 0 off, anything else on
+    } else if (k == "frame_tail_tiles") {
+        g_tune.frame_tail_tiles = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_tail_fork") {
         g_tune.frame_tail_fork = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
     } else if (k == "frame_tail_bs") {

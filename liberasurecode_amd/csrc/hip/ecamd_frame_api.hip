@@ -497,18 +497,30 @@ int split_range(int dev, int k, const void* obj, int64_t obj_stride, uint64_t ob
 // most of its time staging 40 KiB of tables per workgroup for ~2.5-6.5 KiB of work per stripe
 // (profiles/r04_swift_prof_*: 0.10-0.17 ms of a 1.3-1.5 ms encode).  ECAMD_EINVAL, nothing
 // launched, when it does not apply (payloads shorter than the tiles, 32-bit offsets, knob
-// frame_tail_bs 0).
+// frame_tail_bs 0).  Whole 4 KiB tiles every object chunk still holds past `from` (the 16 KiB-tile
+// crc variant leaves one on Swift's segments) go first through the copy-through launch of exactly
+// that range, so the split and the re-encoded tiles shrink to the last partial tile (knob
+// frame_tail_tiles, default on).
 int encode_tail(int dev, const Code& c, const void* obj, int64_t obj_stride, uint64_t obj_size, uint8_t* frags,
                 int64_t ss, int64_t fs, int64_t bs, int nstripes, int64_t from, void* stream)
 {
     constexpr int64_t kTile = 4096;
-    const int64_t r16 = (bs + 15) & ~int64_t(15);
-    const int64_t n = (r16 - from + kTile - 1) / kTile;
-    const int64_t t0 = r16 - n * kTile;
-    if (dev_tune("frame_tail_bs") == 0 || from <= 0 || from % 16 || from >= bs || t0 < 0 ||
+    if (dev_tune("frame_tail_bs") == 0 || from <= 0 || from % 16 || from >= bs ||
         !copy_fits32(c.k, fs, bs, static_cast<int64_t>(obj_size)) || dev_tune("frame_copy_stream") == 0)
         return ECAMD_EINVAL;
-    int rc = split_range(dev, c.k, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, from, stream);
+    const int64_t last = static_cast<int64_t>(obj_size) - (c.k - 1) * bs;
+    const int64_t c4 = last > 0 ? std::min(bs, last) / kTile * kTile : 0;  // whole 4 KiB tiles of every chunk
+    const int64_t r16 = (bs + 15) & ~int64_t(15);
+    const int64_t mid = dev_tune("frame_tail_tiles") != 0 && c4 > from && c4 < bs ? c4 : from;
+    const int64_t n = (r16 - mid + kTile - 1) / kTile;
+    const int64_t t0 = r16 - n * kTile;
+    if (t0 < 0) return ECAMD_EINVAL;
+    int rc;
+    if (mid > from && (rc = rs_encode_copy(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes,
+                                           stream, static_cast<int64_t>(obj_size), from, mid)))
+        return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail tiles failed") : rc;
+    from = mid;
+    rc = split_range(dev, c.k, obj, obj_stride, obj_size, frags, ss, fs, bs, nstripes, from, stream);
     if (rc) return rc;
     rc = ecamd_rs_encode(c.k, c.m, frags + kHeaderBytes + t0, ss, fs, n * kTile, nstripes, stream);
     return rc == ECAMD_EINVAL ? dev_fail(ECAMD_EHIP, "framed encode: tail encode failed") : rc;

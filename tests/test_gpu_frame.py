@@ -450,12 +450,15 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         # (frame_crc_cover, bs_realign, frame_tail_bs): the crc variant reads the object chunks
         # realigned from aligned loads + the neighbour lane's (default) or with unaligned loads; the
         # payloads' rest by split + plain encode of their last tiles (default) or the LDS-table launch
-        # (+ frame_tail_fork 2: the rest and its CRC32 on the side stream beside the crc variant)
-        for cover, realign, tail, fork in ((1, 1, 1, 1), (0, 1, 1, 1), (1, 0, 1, 1), (1, 1, 0, 1), (1, 1, 1, 2)):
+        # (+ frame_tail_fork 2: the rest and its CRC32 on the side stream beside the crc variant;
+        # + frame_tail_tiles 0: the rest's whole 4 KiB tiles by the split + re-encode too)
+        for cover, realign, tail, fork, tt in ((1, 1, 1, 1, 1), (0, 1, 1, 1, 1), (1, 0, 1, 1, 1), (1, 1, 0, 1, 1),
+                                               (1, 1, 1, 2, 1), (1, 1, 1, 1, 0)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_cover", cover), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_fork", fork), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_tail_tiles", tt), "tune")
             n0 = _bs_launches()
             fb = F.FrameBatch(be, k, m, size, S)
             fb.encode(_upload_objects(objs, fb.obj_stride))
@@ -472,6 +475,7 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         _lib.dev().ecamd_tune(b"bs_realign", -1)
         _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
         _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
+        _lib.dev().ecamd_tune(b"frame_tail_tiles", -1)
     assert all(np.array_equal(o, out[1]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
     assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the CRC32 pass's span length (knob crc_span_kib; round 4, development tool) on the Swift
+"""A/B of the Swift segment CRC32 encode's tail (round 4, development tool): the CRC32 pass's span length
+(knob crc_span_kib) and grid, and frame_tail_tiles, on the Swift
 segment CRC32 encode (2560 x 1 MiB, bs = 104858), whose serial tail checksums the 6554 bytes past
 the 16 KiB tiles of every payload in a run_crc launch of its own (one 8 KiB span per payload by
 default: 35840 waves of one span each).  Fragments checked equal; interleaved rounds, median ms."""
@@ -15,7 +16,10 @@ import torch  # noqa: E402,F401
 from liberasurecode_amd import _lib, frame  # noqa: E402
 from liberasurecode_amd import device as D  # noqa: E402
 
-VARIANTS = {"auto": (0, 0), "span4": (4, 0), "span4_wgs16": (4, 16), "auto_wgs16": (0, 16)}
+# (crc_span_kib, crc_wgs, frame_tail_tiles): round 4 first run -- span / grid of the tail's CRC pass
+# (profiles/r04_tail_crc_ab.log: the default best); second -- the whole 4 KiB tile past the 16 KiB
+# tiles by the copy-through launch before the split (frame_tail_tiles)
+VARIANTS = {"tail_tiles_off": (0, 0, 0), "tail_tiles_on": (0, 0, 1)}
 
 
 def main(rounds=5, reps=10):
@@ -31,6 +35,7 @@ def main(rounds=5, reps=10):
     def setv(v):
         d.ecamd_tune(b"crc_span_kib", v[0])
         d.ecamd_tune(b"crc_wgs", v[1])
+        d.ecamd_tune(b"frame_tail_tiles", v[2])
 
     ref = None
     for v in VARIANTS.values():
@@ -60,7 +65,7 @@ def main(rounds=5, reps=10):
         ms = statistics.median(ts)
         print(json.dumps({"shape": "swift_1MiB_segment_crc32", "variant": name, "ms": round(ms, 4),
                           "frac": round(nbytes / (ms * 1e-3) / 8e12, 4)}), flush=True)
-    setv((0, 0))
+    setv((0, 0, -1))
     d.ecamd_tune(b"bitslice", 1)
 
 
