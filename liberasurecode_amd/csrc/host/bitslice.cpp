@@ -283,6 +283,18 @@ __device__ __forceinline__ u32 lane_shift(const u32* t, u32 v, u32 lofs)
                      tab_at(t + 5120, (((v >> 20) & 15u) << 8) + lofs));
     return x3(a, b, tab_at(t + 6144, (((v >> 24) & 15u) << 8) + lofs) ^ tab_at(t + 7168, ((v >> 28) << 8) + lofs));
 }
+// XOR of v over the wave, in every lane (BitsliceStyle::dpp_reduce): DPP within each row of 16 (quad
+// swaps, half-row and row mirrors), then the 4 rows' lane 0 by v_readlane -- no LDS instruction,
+// where a ds_bpermute butterfly (__shfl_xor) takes 6 from the LDS the CRC lookups saturate
+__device__ __forceinline__ u32 wave_xor(u32 v)
+{
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);  // row_mirror
+    return (u32)__builtin_amdgcn_readlane((int)v, 0) ^ (u32)__builtin_amdgcn_readlane((int)v, 16) ^
+           (u32)__builtin_amdgcn_readlane((int)v, 32) ^ (u32)__builtin_amdgcn_readlane((int)v, 48);
+}
 // lane F of `held` := lane 0 of v (v_readlane into an SGPR, v_writelane back)
 template <int F>
 __device__ __forceinline__ u32 put_lane(u32 held, u32 v)
@@ -439,10 +451,11 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             }
             if (fold_each)  // each lane's state shifted to the segment end, then an XOR reduction
                 s << "            cs = lane_shift(lanes, cs, lofs);\n"
-                     "#pragma unroll\n"
-                     "            for (int l = 0; l < 6; l++) cs ^= __shfl_xor(cs, 1 << l, 64);\n"
-                     // lane f of `held` keeps fragment f's wave value: no branch inside the network code
-                     "            held = put_lane<" << f << ">(held, cs);\n";
+                  << (style.dpp_reduce ? "            cs = wave_xor(cs);\n"
+                                       : "#pragma unroll\n"
+                                         "            for (int l = 0; l < 6; l++) cs ^= __shfl_xor(cs, 1 << l, 64);\n")
+                  // lane f of `held` keeps fragment f's wave value: no branch inside the network code
+                  << "            held = put_lane<" << f << ">(held, cs);\n";
         };
         const int lds_words = words + (lane_fold ? kBsCrcLaneWords : 0);
         s << "    __shared__ u32 ctab[" << lds_words << "];\n"
@@ -538,9 +551,10 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             s << "#pragma unroll\n"
                  "        for (int f = 0; f < " << NS << "; f++) {\n"
                  "            u32 x = lane_shift(lanes, st[f], lofs);\n"
-                 "#pragma unroll\n"
-                 "            for (int l = 0; l < 6; l++) x ^= __shfl_xor(x, 1 << l, 64);\n"
-                 "            if (lane == 0) xch[wave * " << NS << " + f] = x;\n"
+              << (style.dpp_reduce ? "            x = wave_xor(x);\n"
+                                   : "#pragma unroll\n"
+                                     "            for (int l = 0; l < 6; l++) x ^= __shfl_xor(x, 1 << l, 64);\n")
+              << "            if (lane == 0) xch[wave * " << NS << " + f] = x;\n"
                  "        }\n";
         else
             s << "#pragma unroll\n"

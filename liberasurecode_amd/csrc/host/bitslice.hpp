@@ -89,6 +89,11 @@ struct BitsliceStyle {
     // one-wave realigned inputs: the last lane's next chunk for chunks 0-2 is lane 0 of the input's
     // following chunk (1 KiB on), taken by v_readlane instead of a load; only chunk 3's is loaded
     bool realign_lane = false;
+    // crc variant: the wave XOR reductions of the lane-shift fold by DPP + v_readlane (wave_xor)
+    // instead of a ds_bpermute butterfly, whose 6 LDS instructions per fragment and tile compete with
+    // the CRC lookups: C5 framed CRC32 encode 1.380 -> 1.317 ms (profiles/r04_dppred_ab.log);
+    // ECAMD_BS_DPPRED=0 in ecamd_jitc's environment restores the butterfly (A/B only)
+    bool dpp_reduce = true;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly

@@ -78,6 +78,7 @@ int main(int argc, char** argv)
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_RLANE")) style.realign_lane = std::atoi(v) != 0;
+    if (const char* v = std::getenv("ECAMD_BS_DPPRED")) style.dpp_reduce = std::atoi(v) != 0;  // A/B only
     std::remove(argv[1]);
     const std::string src = ecamd::bitslice_source(ecamd::bitslice_network(coeff, R, K, cap), depth, style);
     std::string out(argv[2]);
