@@ -59,6 +59,13 @@ __device__ __forceinline__ const uint8_t* item_ptr(const CrcArgs& a, int64_t ite
 
 }  // namespace
 
+// lane l takes lane l + N of its row of 16 (DPP row_shl; past the row's end: 0)
+template <int N>
+__device__ __forceinline__ uint32_t row_shl(uint32_t x)
+{
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x100 + N, 0xf, 0xf, false));
+}
+
 template <int MB, int G, bool POS>
 __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
                                                           uint32_t* __restrict__ partial)
@@ -113,12 +120,18 @@ __global__ __launch_bounds__(512) void crc_partial_kernel(const CrcArgs a, const
 #pragma unroll
             for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
         }
-        // Lane l's state sits (63 - l) pieces before the span end: fold pairs, quads, ...
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            const uint32_t right = __shfl_down(st, 1 << t, 64);
-            st = lmap<G>(tab + PIECE + FIELDS * (1 + t), st) ^ right;
-        }
+        // Lane l's state sits (63 - l) pieces before the span end: fold pairs, quads, ... -- inside
+        // each row of 16 lanes by DPP row_shl (lane l takes lane l + 2^t; only the lanes that are
+        // multiples of 2^(t+1) matter), then the 4 row values by v_readlane, folded on uniform values
+        // (no ds_bpermute: the LDS serves the lookups; broadcast lookups do not conflict)
+        st = lmap<G>(tab + PIECE + FIELDS * 1, st) ^ row_shl<1>(st);
+        st = lmap<G>(tab + PIECE + FIELDS * 2, st) ^ row_shl<2>(st);
+        st = lmap<G>(tab + PIECE + FIELDS * 3, st) ^ row_shl<4>(st);
+        st = lmap<G>(tab + PIECE + FIELDS * 4, st) ^ row_shl<8>(st);
+        const uint32_t r0 = __builtin_amdgcn_readlane(st, 0), r1 = __builtin_amdgcn_readlane(st, 16);
+        const uint32_t r2 = __builtin_amdgcn_readlane(st, 32), r3 = __builtin_amdgcn_readlane(st, 48);
+        const uint32_t s0 = lmap<G>(tab + PIECE + FIELDS * 5, r0) ^ r1, s1 = lmap<G>(tab + PIECE + FIELDS * 5, r2) ^ r3;
+        st = lmap<G>(tab + PIECE + FIELDS * 6, s0) ^ s1;
         if (lane == 0) partial[ws] = st;
     }
 }
