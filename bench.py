@@ -337,6 +337,8 @@ def c5_rebuild(D, stream, reps=30, warm=120):
     D.rs_encode(k, m, lay, stream=stream)
     for pat in (lost, MIXED_PATTERNS["c5"]):
         D.rs_decode(k, m, pat, lay, stream=stream)
+    for d in lost:  # single-destination maps (bitsliced when bs_narrow_min_k takes them)
+        D.rs_reconstruct(k, m, lost, d, lay, stream=stream)
     stream.synchronize()
     # per launch: k inputs read + 8 outputs written per stripe (algorithmic bytes)
     algo = S * (k + 8) * F
@@ -518,7 +520,16 @@ def main():
     n0 = bs_count()
     D.rs_encode(k, m, lay, stream=stream)
     stream.synchronize()
-    bs_per_pass = bs_count() - n0
+    bs_enc = bs_count() - n0
+    n0 = bs_count()
+    D.rs_decode(k, m, missing, lay, stream=stream)
+    stream.synchronize()
+    bs_dec = bs_count() - n0
+    # one per-launch figure for both passes only when both run the same form in as many launches
+    if (bs_enc > 0) != (bs_dec > 0) or (bs_enc and bs_enc != bs_dec):
+        raise SystemExit(f"bench.py: encode / decode passes run different kernels or launch counts "
+                         f"(bitsliced launches {bs_enc} / {bs_dec}); the per-launch roofline would be misstated")
+    bs_per_pass = bs_enc
 
     ev = [(D.Event(), D.Event(), D.Event()) for _ in range(args.steps)]
 

@@ -56,6 +56,29 @@ int ecamd_bitslice_entries(void);
 /* Bitsliced kernel launches this process has enqueued (tests pin which kernel ran). */
 long long ecamd_bitslice_launches(void);
 
+/* Which kernel an rs_vand operation's passes run on this process's current device, for fragments
+ * of `blocksize` bytes: encode (missing NULL), decode of the -1 terminated `missing` (dest < 0;
+ * rebuild_parity as ecamd_rs_decode) or single-destination reconstruct of `dest`.  Returns
+ * ECAMD_FORM_TABLES (the LDS-table kernels serve it by shape or knob), ECAMD_FORM_BITSLICED (its
+ * bitsliced kernel is loaded: shipped with the library, cached, or compiled), ECAMD_FORM_COMPILING
+ * (being compiled; the LDS tables serve it meanwhile) or ECAMD_FORM_UNAVAILABLE (it would take the
+ * bitsliced kernel but none can be had -- no shipped code object and no ecamd_jitc / libhiprtc, or
+ * the compile failed: the LDS tables serve it, byte-identically); < 0 on error.  Asking starts the
+ * compile of a map not seen before (knob "bitslice" 2: waits for it), as its first launch would. */
+#define ECAMD_FORM_TABLES 0
+#define ECAMD_FORM_BITSLICED 1
+#define ECAMD_FORM_COMPILING 2
+#define ECAMD_FORM_UNAVAILABLE 3
+int ecamd_rs_kernel_form(int k, int m, const int *missing, int dest, int rebuild_parity, int64_t blocksize);
+
+/* Build time, no GPU needed: compile the bitsliced kernels of one rs_vand operation (arguments as
+ * ecamd_rs_kernel_form) for target `arch` ("gfx950") into `dir` -- the library's jit/ directory,
+ * which the run time searches before the per-user cache -- under the names the run time looks up
+ * with the current knobs.  Returns the number of code objects present (0: the operation takes no
+ * bitsliced kernel), < 0 on error (ecamd_jitc missing or failed). */
+int ecamd_bitslice_prebuild(int k, int m, const int *missing, int dest, int rebuild_parity, const char *arch,
+                            const char *dir);
+
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
 typedef struct ecamd_map ecamd_map;
 
@@ -241,10 +264,14 @@ int ecamd_host_alloc(void **h_ptr, int64_t bytes); /* pinned host memory */
 int ecamd_host_free(void *h_ptr);
 int ecamd_synchronize(void);
 int ecamd_stream_create(void **stream);
+/* Also releases the library's per-stream context of that stream (side stream, scratch). */
 int ecamd_stream_destroy(void *stream);
 int ecamd_stream_synchronize(void *stream);
 /* 0 when all work on stream is complete, 1 while some is pending, ECAMD_EHIP on error. */
 int ecamd_stream_query(void *stream);
+/* Per-(device, stream) contexts the framed calls hold (side stream + events + CRC scratch): bounded --
+ * released by ecamd_stream_destroy, and idle ones of other streams past a cap of 16 (diagnostics). */
+int ecamd_stream_contexts(void);
 /* HIP events for timing work on a stream (elapsed_ms waits for `stop`). */
 int ecamd_event_create(void **ev);
 int ecamd_event_destroy(void *ev);

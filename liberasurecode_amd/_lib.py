@@ -15,7 +15,9 @@ try:  # single HIP runtime per process (see module docstring)
 except Exception:  # pragma: no cover - torch is optional for the C path
     torch = None
 
-LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+# $LIBERASURECODE_AMD_LIBDIR: another directory of the same built libraries (tests run a copy
+# without ecamd_jitc / the shipped jit/ objects there)
+LIBDIR = os.environ.get("LIBERASURECODE_AMD_LIBDIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 
 IP = C.POINTER(C.c_int)
 I64P = C.POINTER(C.c_int64)
@@ -126,6 +128,10 @@ def dev():
         _proto(d, "ecamd_bitslice_available", C.c_int, [])
         _proto(d, "ecamd_bitslice_wait", C.c_int, [])
         _proto(d, "ecamd_bitslice_entries", C.c_int, [])
+        _proto(d, "ecamd_bitslice_launches", C.c_longlong, [])
+        _proto(d, "ecamd_rs_kernel_form", C.c_int, [C.c_int, C.c_int, VP, C.c_int, C.c_int, C.c_int64])
+        _proto(d, "ecamd_bitslice_prebuild", C.c_int,
+               [C.c_int, C.c_int, VP, C.c_int, C.c_int, C.c_char_p, C.c_char_p])
         _proto(d, "ecamd_percall_reset", None, [])
         _proto(d, "ecamd_percall_status", C.c_int, [])
         _proto(d, "ecamd_fault_inject", C.c_int, [C.c_char_p, C.c_int])
@@ -140,6 +146,7 @@ def dev():
         _proto(d, "ecamd_synchronize", C.c_int, [])
         _proto(d, "ecamd_stream_create", C.c_int, [C.POINTER(VP)])
         _proto(d, "ecamd_stream_destroy", C.c_int, [VP])
+        _proto(d, "ecamd_stream_contexts", C.c_int, [])
         _proto(d, "ecamd_stream_synchronize", C.c_int, [VP])
         _proto(d, "ecamd_event_create", C.c_int, [C.POINTER(VP)])
         _proto(d, "ecamd_event_destroy", C.c_int, [VP])

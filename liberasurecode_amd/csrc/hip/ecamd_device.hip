@@ -8,6 +8,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <list>
@@ -58,10 +59,30 @@ std::mutex g_dev_mu;
 int g_ndev = -1;
 std::vector<DeviceInfo> g_dev;
 
+// $ECAMD_TUNE="key=value,key=value": knobs applied once, before the first call touches a device --
+// so a profiler or an A/B can run an unmodified command (bench.py) with other launch shapes.
+void tune_from_env()
+{
+    const char* env = std::getenv("ECAMD_TUNE");
+    if (!env) return;
+    std::string all(env);
+    size_t pos = 0;
+    while (pos < all.size()) {
+        size_t end = all.find(',', pos);
+        if (end == std::string::npos) end = all.size();
+        const std::string kv = all.substr(pos, end - pos);
+        const size_t eq = kv.find('=');
+        if (eq != std::string::npos && eq > 0)
+            (void)ecamd_tune(kv.substr(0, eq).c_str(), std::atoi(kv.c_str() + eq + 1));
+        pos = end + 1;
+    }
+}
+
 int ensure_device(int* dev_out)
 {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     if (g_ndev < 0) {
+        tune_from_env();
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
         g_ndev = n;
@@ -170,6 +191,7 @@ struct Knob {
 
 constexpr int kFrameCrcNibDefault = 0;
 constexpr int kFrameCrcBsDefault = 1;
+constexpr int kBsNarrowMinKDefault = 0;  // 1-2-output maps: LDS tables (A/B pending)
 
 struct Tuning {
     Knob threads{0};     // threads per workgroup of the gf16 kernel
@@ -312,7 +334,11 @@ struct Tuning {
                                   //   rounds (tools/bs_wave_ab.py, profiles/r04_bs_wave_ab1.log): encode
                                   //   0.733 -> 0.746, decode {0,1,2,3} 0.734 -> 0.742, mixed {0,5,10,13}
                                   //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
-    Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (2..4)
+    Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (1..4)
+    Knob bs_narrow_min_k{kBsNarrowMinKDefault};      //   > 0: row groups of 1-2 outputs over at least this many inputs take it too
+    Knob bs_wave_depth{0};        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
+                                  //   deep (the next input's loads in flight during the network, no VGPRs held
+                                  //   for them); 0 = straight into registers
     Knob bs_wave_copy{1};         //   copy-through maps (framed encode / decode-join): 1 (default) too, 2 only
                                   //   when their inputs start at offsets that are not multiples of 16, 0 never.
                                   //   With the prefetch (bs_prefetch) the one-wave form beats the LDS-table
@@ -405,7 +431,9 @@ struct ecamd_map {
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
                                 std::shared_ptr<void>& hold, bool copy = false, int crc = 0, bool wave = false,
-                                const std::vector<int>* in_shift = nullptr, int prefetch = 0);
+                                const std::vector<int>* in_shift = nullptr, int prefetch = 0, int* status = nullptr);
+int bitslice_prebuild(const std::vector<int>& coeff, int R, int K, int depth, bool copy, int crc, bool wave,
+                      const std::vector<int>* in_shift, int prefetch, const std::string& arch, const std::string& dir);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
                     const std::shared_ptr<void>& hold, int threads = 256);
 }  // namespace ecamd
@@ -733,12 +761,40 @@ uint32_t realign_records(const ApplyArgs& a, int K, int64_t cover, bool copy, st
     return static_cast<uint32_t>(end);
 }
 
-bool bs_wave_tiles(int nrows, bool copy, bool* narrow, bool unaligned = false)
+bool bs_wave_tiles(int nrows, int K, bool copy, bool* narrow, bool unaligned = false)
 {
     const bool ok = !copy || g_tune.bs_wave_copy == 1 || (g_tune.bs_wave_copy == 2 && unaligned && g_tune.bs_realign);
-    const bool n = ok && g_tune.bs_wave >= 1 && nrows >= g_tune.bs_wave_min_rows && nrows <= 4;
+    // 1-2 outputs (single-destination reconstruct, 1-2 lost): bitsliced when the map has at least
+    // bs_narrow_min_k inputs (the LDS tables are K x 2 KiB there, and small at C2's k = 4)
+    const bool few = nrows <= 2 && g_tune.bs_narrow_min_k > 0 && K >= g_tune.bs_narrow_min_k;
+    const bool n = ok && g_tune.bs_wave >= 1 && (nrows >= g_tune.bs_wave_min_rows || few) && nrows <= 4;
     if (narrow) *narrow = n;
     return ok && (n || g_tune.bs_wave == 2);
+}
+
+// Whether a row group of nrows outputs over K inputs takes the bitsliced kernel under the current
+// knobs, and in which form (launch_bitslice; ecamd_bitslice_prebuild and ecamd_rs_kernel_form ask
+// the same question without launching).
+struct BsForm {
+    bool wave = false;  // one-wave 4 KiB tiles (else 4-wave 16 KiB tiles)
+    int depth = 0;      // LDS ring depth (0: register loads)
+    int prefetch = 0;   // BitsliceStyle::prefetch (copy-through forms)
+};
+bool bs_form(int nrows, int K, bool copy, bool unaligned, BsForm& f)
+{
+    if (!g_tune.bitslice || nrows <= 0 || nrows > kBsMaxR || K <= 0 || K > kBsMaxK) return false;
+    if (copy && bitslice_depth(g_tune.bitslice_depth, K) != 0) return false;  // ring form: no copy-through
+    // one-wave 4 KiB tiles (knob bs_wave): 3-4-output maps (C3 encode and decodes) run best in the
+    // finest dispatcher-balanced units the 4-chunk transpose allows -- interleaved output slots
+    // ({0,5,10,13}) above all; 5-8-output maps keep the 4-wave 16 KiB tiles
+    bool narrow = false;
+    f.wave = bs_wave_tiles(nrows, K, copy, &narrow, unaligned);
+    if (nrows < g_tune.bitslice_min_rows && !narrow) return false;
+    // LDS ring (depth 2 / 4) or register loads: bs_wave_depth for one-wave plain maps, bitslice_depth
+    // for 16 KiB tiles; copy-through maps always load into registers
+    f.depth = copy ? 0 : static_cast<int>(f.wave ? g_tune.bs_wave_depth : g_tune.bitslice_depth);
+    f.prefetch = !copy ? 0 : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
+    return true;
 }
 
 int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyArgs& base,
@@ -748,22 +804,17 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     *rc = 0;
     const int mode = g_tune.bitslice;
     const int K = map->K;
-    if (!mode || nrows > kBsMaxR || K > kBsMaxK) return 0;
     if (!copy_off && (base.copy_records || base.limited)) return 0;
-    if (copy_off && bitslice_depth(g_tune.bitslice_depth, K) != 0) return 0;  // ring form: no copy-through
+    bool unaligned = false;
+    for (int j = 0; j < K && j < kBsMaxK; j++) unaligned = unaligned || (in_off[j] & 15);
+    BsForm form;
+    if (!bs_form(nrows, K, copy_off != nullptr, unaligned, form)) return 0;
     ApplyArgs a = base;
     a.ncols = K;
     a.nrows = nrows;
     for (int j = 0; j < K; j++) a.in_off[j] = in_off[j];
     for (int r = 0; r < nrows; r++) a.out_off[r] = out_off[row0 + r];
-    // one-wave 4 KiB tiles (knob bs_wave): 3-4-output maps (C3 encode and decodes) run best in the
-    // finest dispatcher-balanced units the 4-chunk transpose allows -- interleaved output slots
-    // ({0,5,10,13}) above all; 5-8-output maps keep the 4-wave 16 KiB tiles
-    bool narrow = false;
-    bool unaligned = false;
-    for (int j = 0; j < K; j++) unaligned = unaligned || (in_off[j] & 15);
-    const bool wave = bs_wave_tiles(nrows, copy_off != nullptr, &narrow, unaligned);
-    if (nrows < g_tune.bitslice_min_rows && !narrow) return 0;
+    const bool wave = form.wave;
     const int64_t tile = wave ? kBsTileWave : kBsTile;
     if (bs < tile) return 0;
     const int64_t cover = (base.limited ? std::min<int64_t>(bs, base.min_len) : bs) / tile * tile;
@@ -780,10 +831,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     std::shared_ptr<void> hold;  // the kernel's module stays loaded until the launch is enqueued
     std::vector<int> shifts;
     const uint32_t in_records = realign_records(a, K, cover, copy_off != nullptr, shifts);
-    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, wave ? 0 : static_cast<int>(g_tune.bitslice_depth),
-                                         mode == 2, hold, copy_off != nullptr, 0, wave, &shifts,
-                                         !copy_off ? 0 : wave ? static_cast<int>(g_tune.bs_prefetch)
-                                                              : static_cast<int>(g_tune.bs_late_copy));
+    hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, form.depth, mode == 2, hold, copy_off != nullptr,
+                                         0, wave, &shifts, form.prefetch);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1230,7 +1279,7 @@ int map_apply_copy(const RsEntry& e, const uint8_t* in_base, int64_t in_stride,
         for (int64_t o : in_off) unaligned = unaligned || (o & 15);
         auto cover_of = [&](int g) {  // bytes the group's bitsliced launch would cover
             const int64_t tile =
-                bs_wave_tiles(std::min(8, map->R - g * 8), true, nullptr, unaligned) ? kBsTileWave : kBsTile;
+                bs_wave_tiles(std::min(8, map->R - g * 8), map->K, true, nullptr, unaligned) ? kBsTileWave : kBsTile;
             return (b.limited ? std::min<int64_t>(bs, b.min_len) : bs) / tile * tile;
         };
         auto tail_on_stream = [&](int g) {
@@ -1358,42 +1407,179 @@ bool copy_aligned_payloads(const void* obj, const void* payload0, int64_t obj_st
 
 }  // namespace
 
-// Per-(device, stream) side stream (knob frame_tail_fork): side_fork makes it wait for everything
-// issued so far to the caller's stream; side_join makes the caller's stream wait for everything
-// issued to it since.  The payload tails of a padded framed encode, and the LDS-table rest of a
-// copy-through map, run there beside the launch over the whole tiles; the two write disjoint bytes.
+// Per-(device, caller stream) context of the framed calls: the side stream (knob frame_tail_fork)
+// with its fork / join events, and the CRC scratch slots of ecamd_frame_api.hip.  side_fork makes
+// the side stream wait for everything issued so far to the caller's stream; side_join makes the
+// caller's stream wait for everything issued to the side stream since.  The payload tails of a
+// padded framed encode, and the LDS-table rest of a copy-through map, run there beside the launch
+// over the whole tiles; the two write disjoint bytes.
+//
+// Callers that create and destroy streams (a proxy's per-request streams) must not grow this map
+// for the life of the process: ecamd_stream_destroy releases the stream's context, and past
+// kStreamCtxMax contexts every new one first releases the IDLE contexts of other streams -- no
+// framed call or fork in progress (busy), and every event recorded for them complete (done: the
+// end of the last framed call, join: the side stream's last work), so neither the side stream nor
+// a scratch slot can still be in use.  Only our own events are queried, never a caller's stream
+// (which may have been destroyed behind our back).
 namespace {
-struct Side {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+struct StreamCtx {
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr, done = nullptr;
+    int busy = 0;  // framed calls (StreamUse) and forks not yet joined
+    uint32_t* scratch[kStreamScratchSlots] = {};
+    size_t scratch_words[kStreamScratchSlots] = {};
 };
-std::mutex g_side_mu;
-std::map<std::pair<int, void*>, Side> g_side;
+constexpr size_t kStreamCtxMax = 16;
+std::mutex g_ctx_mu;
+auto& g_ctx = *new std::map<std::pair<int, void*>, StreamCtx>();  // never destroyed: no HIP call at exit
+
+bool ctx_idle(const StreamCtx& c)
+{
+    if (c.busy) return false;
+    for (hipEvent_t e : {c.join, c.done})
+        if (e && hipEventQuery(e) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+    return true;
+}
+
+// Releases an idle context's resources (the caller holds g_ctx_mu and erases the entry).
+void ctx_release(int dev, StreamCtx& c)
+{
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    if (c.side) (void)hipStreamDestroy(c.side);
+    for (hipEvent_t e : {c.fork, c.join, c.done})
+        if (e) (void)hipEventDestroy(e);
+    for (uint32_t* p : c.scratch)
+        if (p) (void)hipFree(p);
+    if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+    (void)hipGetLastError();
+    c = StreamCtx{};
+}
+
+// The context of (dev, stream), created on first use; g_ctx_mu held.
+StreamCtx& ctx_of(int dev, void* stream)
+{
+    const auto key = std::make_pair(dev, stream);
+    auto it = g_ctx.find(key);
+    if (it != g_ctx.end()) return it->second;
+    if (g_ctx.size() >= kStreamCtxMax)
+        for (auto jt = g_ctx.begin(); jt != g_ctx.end();) {
+            if (ctx_idle(jt->second)) {
+                ctx_release(jt->first.first, jt->second);
+                jt = g_ctx.erase(jt);
+            } else {
+                ++jt;
+            }
+        }
+    return g_ctx[key];
+}
 }  // namespace
+
+int stream_use_begin(int dev, void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    ctx_of(dev, stream).busy++;
+    return 0;
+}
+
+void stream_use_end(int dev, void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    const auto it = g_ctx.find(std::make_pair(dev, stream));
+    if (it == g_ctx.end()) return;
+    StreamCtx& c = it->second;
+    // everything this call enqueued on the caller's stream (scratch reads included) is behind `done`
+    if (!c.done && hipEventCreateWithFlags(&c.done, hipEventDisableTiming) != hipSuccess) c.done = nullptr;
+    if (c.done) (void)hipEventRecord(c.done, static_cast<hipStream_t>(stream));
+    (void)hipGetLastError();
+    if (c.busy > 0) c.busy--;
+}
+
+int stream_scratch(int dev, void* stream, int slot, size_t words, uint32_t** out)
+{
+    if (slot < 0 || slot >= kStreamScratchSlots) return fail(ECAMD_EINVAL, "scratch slot %d", slot);
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    StreamCtx& c = ctx_of(dev, stream);
+    uint32_t*& p = c.scratch[slot];
+    size_t& n = c.scratch_words[slot];
+    if (n < words) {
+        if (p) {  // calls on one stream are ordered: the old slot is free once the stream drains
+            HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+            HIP_TRY(hipFree(p));
+            p = nullptr;
+            n = 0;
+        }
+        HIP_TRY(hipMalloc(&p, std::max<size_t>(words, 1) * sizeof(uint32_t)));
+        n = std::max<size_t>(words, 1);
+    }
+    *out = p;
+    return 0;
+}
 
 int side_fork(int dev, void* stream, void** side)
 {
-    std::lock_guard<std::mutex> lk(g_side_mu);
-    Side& e = g_side[std::make_pair(dev, stream)];
-    if (!e.s) {
-        HIP_TRY(hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&e.fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&e.join, hipEventDisableTiming));
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    StreamCtx& e = ctx_of(dev, stream);
+    if (!e.side) {  // all three or none: a half-made context would record on null events later
+        hipStream_t s = nullptr;
+        hipEvent_t f = nullptr, j = nullptr;
+        hipError_t rc = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (rc == hipSuccess) rc = hipEventCreateWithFlags(&f, hipEventDisableTiming);
+        if (rc == hipSuccess) rc = hipEventCreateWithFlags(&j, hipEventDisableTiming);
+        if (rc != hipSuccess) {
+            if (s) (void)hipStreamDestroy(s);
+            if (f) (void)hipEventDestroy(f);
+            (void)hipGetLastError();
+            return fail(ECAMD_EHIP, "side stream: %s", hipGetErrorString(rc));
+        }
+        e.side = s;
+        e.fork = f;
+        e.join = j;
     }
     HIP_TRY(hipEventRecord(e.fork, static_cast<hipStream_t>(stream)));
-    HIP_TRY(hipStreamWaitEvent(e.s, e.fork, 0));
-    *side = e.s;
+    HIP_TRY(hipStreamWaitEvent(e.side, e.fork, 0));
+    e.busy++;
+    *side = e.side;
     return 0;
 }
 
 int side_join(int dev, void* stream)
 {
-    std::lock_guard<std::mutex> lk(g_side_mu);
-    const auto it = g_side.find(std::make_pair(dev, stream));
-    if (it == g_side.end() || !it->second.s) return fail(ECAMD_EHIP, "side_join without side_fork");
-    HIP_TRY(hipEventRecord(it->second.join, it->second.s));
-    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), it->second.join, 0));
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    const auto it = g_ctx.find(std::make_pair(dev, stream));
+    if (it == g_ctx.end() || !it->second.side) return fail(ECAMD_EHIP, "side_join without side_fork");
+    StreamCtx& e = it->second;
+    if (e.busy > 0) e.busy--;
+    HIP_TRY(hipEventRecord(e.join, e.side));
+    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(stream), e.join, 0));
     return 0;
+}
+
+// ecamd_stream_destroy: the stream's contexts go with it (after its work, which may read them).
+void stream_forget(void* stream)
+{
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    for (auto it = g_ctx.begin(); it != g_ctx.end();) {
+        if (it->first.second == stream && !it->second.busy) {
+            (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
+            if (it->second.side) (void)hipStreamSynchronize(it->second.side);
+            ctx_release(it->first.first, it->second);
+            it = g_ctx.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    (void)hipGetLastError();
+}
+
+int stream_contexts()
+{
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    return static_cast<int>(g_ctx.size());
 }
 
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
@@ -1984,7 +2170,11 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_wave_copy") {
         g_tune.bs_wave_copy = value < 0 ? 1 : std::min(value, 2);  // < 0: the default (1)
     } else if (k == "bs_wave_min_rows") {
-        g_tune.bs_wave_min_rows = value >= 2 && value <= 4 ? value : 3;  // else the default
+        g_tune.bs_wave_min_rows = value >= 1 && value <= 4 ? value : 3;  // else the default
+    } else if (k == "bs_narrow_min_k") {
+        g_tune.bs_narrow_min_k = value < 0 ? kBsNarrowMinKDefault : std::min(value, 33);
+    } else if (k == "bs_wave_depth") {
+        g_tune.bs_wave_depth = value == 2 || value == 4 ? value : 0;
     } else if (k == "bs_tiles_per_slot") {
         g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {
@@ -2481,6 +2671,7 @@ int ecamd_stream_create(void** stream)
 
 int ecamd_stream_destroy(void* stream)
 {
+    ecamd::stream_forget(stream);
     HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
     return 0;
 }
@@ -2497,6 +2688,86 @@ int ecamd_stream_query(void* stream)
     if (e == hipSuccess) return 0;
     if (e == hipErrorNotReady) return 1;
     return ECAMD_EHIP;
+}
+
+int ecamd_stream_contexts(void) { return ecamd::stream_contexts(); }
+
+namespace {
+// The coefficient map of an rs_vand operation: encode (missing NULL), decode (dest < 0) or
+// single-destination reconstruct -- the same host planning rs_entry uses.
+int rs_plan(int k, int m, const int* missing, int dest, int rebuild_parity, FragmentMap& fm)
+{
+    if (k <= 0 || m < 0 || k + m > 65536) return fail(ECAMD_EINVAL, "bad k=%d m=%d", k, m);
+    std::vector<int> miss;
+    if (missing)
+        for (int i = 0; missing[i] > -1; i++) miss.push_back(missing[i]);
+    const std::vector<int> G = rs_generator(k, m);
+    if (G.empty()) return fail(ECAMD_EINVAL, "no generator for k=%d m=%d", k, m);
+    if (!missing)
+        fm = rs_encode_map(G, k, m);
+    else if (dest < 0) {
+        if (rs_decode_map(G, k, m, miss, rebuild_parity != 0, fm) != 0)
+            return fail(ECAMD_EINVAL, "too many missing fragments (%zu > m=%d)", miss.size(), m);
+    } else if (rs_reconstruct_map(G, k, m, miss, dest, fm) != 0)
+        return fail(ECAMD_EINVAL, "cannot reconstruct %d", dest);
+    return 0;
+}
+
+std::vector<int> group_rows(const FragmentMap& fm, int row0, int nrows)
+{
+    const size_t K = fm.inputs.size();
+    return std::vector<int>(fm.coeff.begin() + static_cast<std::ptrdiff_t>(row0 * K),
+                            fm.coeff.begin() + static_cast<std::ptrdiff_t>((row0 + nrows) * K));
+}
+}  // namespace
+
+int ecamd_bitslice_prebuild(int k, int m, const int* missing, int dest, int rebuild_parity, const char* arch,
+                            const char* dir)
+{
+    if (!arch || !dir) return fail(ECAMD_EINVAL, "null arch / dir");
+    FragmentMap fm;
+    int rc = rs_plan(k, m, missing, dest, rebuild_parity, fm);
+    if (rc) return rc;
+    const int R = static_cast<int>(fm.outputs.size()), K = static_cast<int>(fm.inputs.size());
+    int built = 0;
+    for (int row0 = 0; row0 < R && K > 0; row0 += 8) {
+        const int nrows = std::min(8, R - row0);
+        BsForm f;
+        if (!bs_form(nrows, K, false, false, f)) continue;
+        const int r = ecamd::bitslice_prebuild(group_rows(fm, row0, nrows), nrows, K, f.depth, false, 0, f.wave, nullptr,
+                                               f.prefetch, arch, dir);
+        if (r < 0) return fail(ECAMD_EHIP, "bitsliced prebuild failed (%d) for a %dx%d map", r, nrows, K);
+        built += r;
+    }
+    return built;
+}
+
+int ecamd_rs_kernel_form(int k, int m, const int* missing, int dest, int rebuild_parity, int64_t blocksize)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    FragmentMap fm;
+    if ((rc = rs_plan(k, m, missing, dest, rebuild_parity, fm))) return rc;
+    const int R = static_cast<int>(fm.outputs.size()), K = static_cast<int>(fm.inputs.size());
+    // per row group of 8 outputs; the answer is the weakest: unavailable > compiling > bitsliced > tables
+    auto rank = [](int form) { return form == ECAMD_FORM_UNAVAILABLE ? 3 : form == ECAMD_FORM_COMPILING ? 2
+                                                                        : form == ECAMD_FORM_BITSLICED ? 1 : 0; };
+    int form = ECAMD_FORM_TABLES;
+    for (int row0 = 0; row0 < R && K > 0; row0 += 8) {
+        const int nrows = std::min(8, R - row0);
+        BsForm f;
+        int g = ECAMD_FORM_TABLES;
+        if (bs_form(nrows, K, false, false, f) && blocksize >= (f.wave ? kBsTileWave : kBsTile)) {
+            std::shared_ptr<void> hold;
+            int st = -1;
+            (void)bitslice_function(dev, group_rows(fm, row0, nrows), nrows, K, f.depth, g_tune.bitslice == 2, hold,
+                                    false, 0, f.wave, nullptr, f.prefetch, &st);
+            g = st == 1 ? ECAMD_FORM_BITSLICED : st == 0 ? ECAMD_FORM_COMPILING : ECAMD_FORM_UNAVAILABLE;
+        }
+        if (rank(g) > rank(form)) form = g;
+    }
+    return form;
 }
 
 int ecamd_event_create(void** ev)

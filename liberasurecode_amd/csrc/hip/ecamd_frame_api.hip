@@ -49,7 +49,6 @@ struct DevImage {
 
 std::mutex g_mu;
 std::map<std::tuple<int, int, int, int, int, int>, std::unique_ptr<DevImage>> g_images;  // dev, legacy, B, J, G, pos
-std::map<std::tuple<int, void*, int>, std::pair<uint32_t*, size_t>> g_scratch;  // dev, stream, slot
 
 int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** out)
 {
@@ -68,24 +67,10 @@ int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** 
     return 0;
 }
 
-// Per-(device, stream) scratch for span partials; calls on one stream are ordered, so reuse is safe.
-// Slot 1 holds values that must outlive a run_crc on the same stream (its partials use slot 0).
+// Per-(device, stream) scratch for span partials (the stream's context, ecamd_internal.hpp).
 int scratch(int dev, void* stream, size_t words, uint32_t** out, int slot = 0)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto& e = g_scratch[std::make_tuple(dev, stream, slot)];
-    if (e.second < words) {
-        if (e.first) {
-            HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-            HIP_TRY(hipFree(e.first));
-            e.first = nullptr;
-            e.second = 0;
-        }
-        HIP_TRY(hipMalloc(&e.first, std::max<size_t>(words, 1) * sizeof(uint32_t)));
-        e.second = std::max<size_t>(words, 1);
-    }
-    *out = e.first;
-    return 0;
+    return stream_scratch(dev, stream, slot, words, out);
 }
 
 // Knob frame_tail_fork: 2 forks every padded framed encode's tail; 1 (default) only the encodes
@@ -664,6 +649,7 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
     int dev = 0;
     int rc = dev_ensure(&dev);
     if (rc) return rc;
+    const StreamUse use(dev, stream);  // its stream context outlives this call
     const Code c = make_code(backend, k, m, hd);
     if ((rc = check_code(c))) return rc;
     if (obj_size > 0x7fffffffull) return dev_fail(ECAMD_EINVAL, "object larger than INT_MAX");
@@ -846,6 +832,7 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
     int dev = 0;
     int rc = dev_ensure(&dev);
     if (rc) return rc;
+    const StreamUse use(dev, stream);  // its stream context outlives this call
     const Code c = make_code(backend, k, m, hd);
     if ((rc = check_code(c))) return rc;
     if (!missing) return dev_fail(ECAMD_EINVAL, "null missing list");
@@ -944,6 +931,7 @@ int ecamd_frame_reconstruct(int backend, int k, int m, int hd, int checksum, con
     int dev = 0;
     int rc = dev_ensure(&dev);
     if (rc) return rc;
+    const StreamUse use(dev, stream);  // its stream context outlives this call
     const Code c = make_code(backend, k, m, hd);
     if ((rc = check_code(c))) return rc;
     if (!missing || dest < 0 || dest >= k + m) return dev_fail(ECAMD_EINVAL, "bad missing / dest");
@@ -975,6 +963,7 @@ int ecamd_frame_verify(int nfrag, int64_t blocksize, int legacy, const void* d_f
     int dev = 0;
     int rc = dev_ensure(&dev);
     if (rc) return rc;
+    const StreamUse use(dev, stream);  // its stream context outlives this call
     if (nfrag < 1 || nfrag > 64 || blocksize < 0 || !d_status)
         return dev_fail(ECAMD_EINVAL, "bad nfrag / blocksize / status");
     if ((rc = check_frames(d_frags, stripe_stride, frag_stride, blocksize, nfrag, nstripes))) return rc;
@@ -1015,6 +1004,7 @@ int ecamd_crc32(int legacy, const void* d_base, int64_t stripe_stride, int64_t f
     int dev = 0;
     int rc = dev_ensure(&dev);
     if (rc) return rc;
+    const StreamUse use(dev, stream);  // its stream context outlives this call
     if (!d_base || !d_crc || nfrag < 1 || len < 0 || nstripes < 0)
         return dev_fail(ECAMD_EINVAL, "bad crc32 arguments");
     if (!a16(d_base) || stripe_stride % 16 || frag_stride % 16)

@@ -47,8 +47,29 @@ int dev_tune(const char* key);                      // current value of an ecamd
 // Side stream of (dev, stream) for work beside the caller's launches (knob frame_tail_fork):
 // side_fork orders it after everything issued to `stream` so far, side_join orders `stream` after
 // everything issued to the side stream since.
+// The side stream and the scratch slots live in a per-(dev, stream) context (ecamd_device.hip),
+// bounded: ecamd_stream_destroy releases a stream's, and idle ones are released past a small cap.
 int side_fork(int dev, void* stream, void** side);
 int side_join(int dev, void* stream);
+// Device scratch of `words` 32-bit words in slot 0..kStreamScratchSlots-1 of (dev, stream); calls
+// on one stream are ordered, so reuse is safe (slot 1 holds values that must outlive a CRC pass on
+// the same stream, whose partials use slot 0).
+constexpr int kStreamScratchSlots = 3;
+int stream_scratch(int dev, void* stream, int slot, size_t words, uint32_t** out);
+// A framed call in progress on (dev, stream): its context is not released until the call has
+// returned and its work on the stream has completed.
+int stream_use_begin(int dev, void* stream);
+void stream_use_end(int dev, void* stream);
+struct StreamUse {
+    int dev;
+    void* stream;
+    StreamUse(int d, void* s) : dev(d), stream(s) { (void)stream_use_begin(d, s); }
+    ~StreamUse() { stream_use_end(dev, stream); }
+    StreamUse(const StreamUse&) = delete;
+    StreamUse& operator=(const StreamUse&) = delete;
+};
+void stream_forget(void* stream);
+int stream_contexts();
 
 int rs_encode_copy(int k, int m, const void* obj, int64_t obj_stride, void* payload0,
                    int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,

@@ -79,6 +79,29 @@ std::string helper_path()
     return path;
 }
 
+// Code objects shipped with the library (<libdir>/jit, written at build time by
+// ecamd_bitslice_prebuild for the maps the BASELINE configurations run): looked up before the
+// per-user cache, so those maps take the bitsliced kernel at their first launch without a compile
+// -- and without ecamd_jitc or libhiprtc.  Used only if it is a real directory owned by this user
+// or root that nobody else can write (its code objects run on the GPU, like the library beside it).
+std::string shipped_dir()
+{
+    static std::string dir;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        Dl_info info{};
+        if (!dladdr(reinterpret_cast<void*>(&shipped_dir), &info) || !info.dli_fname) return;
+        std::string lib(info.dli_fname);
+        const size_t slash = lib.rfind('/');
+        const std::string d = (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/jit";
+        struct stat st {};
+        if (lstat(d.c_str(), &st) == 0 && S_ISDIR(st.st_mode) && (st.st_uid == getuid() || st.st_uid == 0) &&
+            !(st.st_mode & 022))
+            dir = d;
+    });
+    return dir;
+}
+
 // Keep the disk cache to the newest $ECAMD_JIT_CACHE_MAX (4096) code objects and drop temporaries
 // older than an hour (a compile stopped mid-way): run once per process.
 void prune_cache(const std::string& dir)
@@ -188,6 +211,7 @@ struct BsEntry {
     time_t started = 0;   // when the child was spawned
     int state = 0;        // 0 compiling, 2 waiting for a compiler slot, 1 code object ready, -1 failed
     std::string code;
+    bool shipped = false;  // code object from the library's own jit/ directory
     std::map<int, hipFunction_t> fn;  // per device; nullptr: unusable there
     std::vector<std::pair<int, hipModule_t>> modules;  // (device, module), spilled ones included
     uint64_t last_use = 0;
@@ -258,14 +282,15 @@ const std::string& generator_fingerprint()
         lane.crc_lane = true;
         nib = lane;
         nib.crc_nib = true;
-        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave;
+        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave, wave_ring = wave;
         wave_pf.prefetch = 4;
         shifted.in_shift = {6};
         crc_shifted.in_shift = {10};
         fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
              bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + bitslice_source(tiny, 0, shifted) +
-             bitslice_source(tiny, 0, crc_shifted) + bitslice_source(tiny5, 0, wave_pf) + kBsNetworkVersion;
+             bitslice_source(tiny, 0, crc_shifted) + bitslice_source(tiny5, 0, wave_pf) +
+             bitslice_source(tiny, 2, wave_ring) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -283,26 +308,46 @@ void stop_children_at_exit()
     g_jit_mu.unlock();
 }
 
-// Start (or skip, when cached) the build of e's kernel at kCaps[e.cap_index]; queue it (state 2)
-// while max_jobs() compilers run, unless `force`.  Caller holds the lock.
+// The compile request of e's kernel at kCaps[e.cap_index], and the name of its code object (a hash
+// of the request, the target and the generator: the same in the shipped and the per-user cache).
+std::string request_of(const BsEntry& e)
+{
+    return bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
+                            e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0, e.wave, &e.shifts,
+                            e.prefetch);
+}
+std::string object_name(const BsEntry& e)
+{
+    char name[40];
+    std::snprintf(name, sizeof(name), "bs_%016llx",
+                  static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + request_of(e))));
+    return name;
+}
+
+// Start (or skip, when shipped or cached) the build of e's kernel at kCaps[e.cap_index]; queue it
+// (state 2) while max_jobs() compilers run, unless `force`.  Caller holds the lock.
 void start_compile(const std::shared_ptr<BsEntry>& ep, bool force)
 {
     BsEntry& e = *ep;
-    const std::string req = bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
-                                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0,
-                                             e.wave, &e.shifts, e.prefetch);
-    char name[32];
-    std::snprintf(name, sizeof(name), "%016llx",
-                  static_cast<unsigned long long>(fnv1a(generator_fingerprint() + "arch " + e.arch + "\n" + req)));
+    const std::string req = request_of(e);
+    const std::string name = object_name(e);
+    e.pid = -1;
+    e.code.clear();
+    const std::string shipped = shipped_dir();
+    if (!shipped.empty() && read_file(shipped + "/" + name + ".co", e.code)) {  // built with the library
+        e.co_path = shipped + "/" + name + ".co";
+        e.state = 1;
+        e.shipped = true;
+        return;
+    }
+    e.shipped = false;
     const std::string dir = cache_dir();
     if (dir.empty()) {  // no usable cache directory: the LDS tables serve this matrix
         e.state = -1;
         return;
     }
-    const std::string base = dir + "/bs_" + name;
+    const std::string base = dir + "/" + name;
     e.co_path = base + ".co";
-    e.pid = -1;
-    e.code.clear();
     if (read_file(e.co_path, e.code)) {  // compiled before, here or by another process
         e.state = 1;
         return;
@@ -379,28 +424,23 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
     }
 }
 
-}  // namespace
-
-// Kernel for the R x K matrix on `dev`: nullptr while compiling (wait = false) or when the
-// bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
-// keeps the kernel's module loaded until the caller has enqueued its launch.
-hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
-                                std::shared_ptr<void>& hold, bool copy, int crc, bool wave,
-                                const std::vector<int>* in_shift, int prefetch)
+// The canonical parameters of a request (and the entry's key): whatever the caller asked, equal
+// kernels get equal requests.  Returns the key.
+std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& depth, bool& copy, int& crc,
+                           bool& wave, const std::vector<int>* in_shift, int& prefetch, std::vector<int>& shifts)
 {
-    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || helper_path().empty()) return nullptr;
     if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
         const int pos = crc & 7;
         crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (crc & 24);
     }
     copy = copy || crc;
     wave = wave && !crc;
-    depth = (copy || wave) ? 0 : bitslice_depth(depth, K);
+    depth = copy ? 0 : bitslice_depth(depth, K);  // one-wave tiles: the LDS ring only in plain maps
     prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
                : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
     std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0) | (prefetch << 9)};
     key.insert(key.end(), coeff.begin(), coeff.end());
-    std::vector<int> shifts;  // realigned copy-through inputs: their own kernel (and cache entry)
+    shifts.clear();  // realigned copy-through inputs: their own kernel (and cache entry)
     if (copy && in_shift)
         for (int j = 0; j < K; j++) {
             const int v = j < static_cast<int>(in_shift->size()) ? ((*in_shift)[static_cast<size_t>(j)] & 15) : 0;
@@ -411,6 +451,101 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         key.push_back(-1);
         key.insert(key.end(), shifts.begin(), shifts.end());
     }
+    return key;
+}
+
+// First kCaps index of a new entry: the 4-waves-per-SIMD build of maps with up to 4 outputs (16 KiB
+// tiles) has half the registers, so it starts at 40 temporaries.
+int first_cap(int R, int crc, bool wave)
+{
+    return std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 && !wave ? 2 : 0);
+}
+
+// The code object's private segment (scratch) size from its metadata note (msgpack: the key string
+// ".private_segment_fixed_size" followed by an unsigned integer): > 0 means the network spilled.
+long code_object_scratch(const std::string& code)
+{
+    static const std::string key = ".private_segment_fixed_size";
+    size_t pos = code.find(key);
+    if (pos == std::string::npos) return -1;
+    pos += key.size();
+    if (pos >= code.size()) return -1;
+    const auto b = [&](size_t i) { return static_cast<unsigned char>(code[i]); };
+    const unsigned char t = b(pos);
+    if (t < 0x80) return t;
+    if (t == 0xcc && pos + 1 < code.size()) return b(pos + 1);
+    if (t == 0xcd && pos + 2 < code.size()) return (b(pos + 1) << 8) | b(pos + 2);
+    if (t == 0xce && pos + 4 < code.size())
+        return static_cast<long>((static_cast<unsigned long>(b(pos + 1)) << 24) | (b(pos + 2) << 16) |
+                                 (b(pos + 3) << 8) | b(pos + 4));
+    return -1;
+}
+
+}  // namespace
+
+// Build time (no GPU): the code object of one map into `dir` (the library's jit/ directory), under the
+// name the run-time lookup computes, through ecamd_jitc run synchronously; a network that spills is
+// built again at the next cap, as the run time would ask for it.  1: present (built now or before),
+// 0: this form never takes a bitsliced kernel, < 0: the helper is missing or failed.
+int bitslice_prebuild(const std::vector<int>& coeff, int R, int K, int depth, bool copy, int crc, bool wave,
+                      const std::vector<int>* in_shift, int prefetch, const std::string& arch, const std::string& dir)
+{
+    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK) return 0;
+    const std::string helper = helper_path();
+    if (helper.empty()) return -1;
+    BsEntry e;
+    std::vector<int> shifts;
+    normalize(coeff, R, K, depth, copy, crc, wave, in_shift, prefetch, shifts);
+    e.coeff = coeff;
+    e.R = R;
+    e.K = K;
+    e.depth = depth;
+    e.copy = copy;
+    e.crc = crc;
+    e.wave = wave;
+    e.shifts = shifts;
+    e.prefetch = prefetch;
+    e.arch = arch;
+    for (e.cap_index = first_cap(R, crc, wave); e.cap_index < kNumCaps; e.cap_index++) {
+        const std::string co = dir + "/" + object_name(e) + ".co";
+        std::string code;
+        if (!read_file(co, code)) {
+            const std::string req_path = co + ".req." + std::to_string(getpid());
+            {
+                std::ofstream f(req_path);
+                f << request_of(e);
+                if (!f) return -2;
+            }
+            const char* argv[] = {helper.c_str(), req_path.c_str(), co.c_str(), arch.c_str(), nullptr};
+            pid_t pid = -1;
+            int status = 0;
+            if (posix_spawn(&pid, helper.c_str(), nullptr, nullptr, const_cast<char* const*>(argv), environ) != 0)
+                return -3;
+            while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+            }
+            std::remove(req_path.c_str());
+            if (!WIFEXITED(status) || WEXITSTATUS(status) != 0 || !read_file(co, code)) return -4;
+        }
+        const long scratch = code_object_scratch(code);
+        if (scratch == 0) return 1;
+        if (scratch < 0) return -5;
+    }
+    return -6;  // every cap spills: the run time keeps the LDS tables for this map
+}
+
+// Kernel for the R x K matrix on `dev`: nullptr while compiling (wait = false) or when the
+// bitsliced form is unavailable; starts the compile the first time the matrix is seen.  `hold`
+// keeps the kernel's module loaded until the caller has enqueued its launch.  `status` (optional):
+// 1 the kernel is loaded, 0 compiling or queued, -1 unavailable (no code object can be had).
+hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
+                                std::shared_ptr<void>& hold, bool copy, int crc, bool wave,
+                                const std::vector<int>* in_shift, int prefetch, int* status)
+{
+    if (status) *status = -1;
+    if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || (helper_path().empty() && shipped_dir().empty()))
+        return nullptr;
+    std::vector<int> shifts;
+    const std::vector<int> key = normalize(coeff, R, K, depth, copy, crc, wave, in_shift, prefetch, shifts);
     std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
     std::unique_lock<std::mutex> lk(g_jit_mu);
     for (size_t i = 0; i < g_running.size();) {  // reap finished compilers, freeing their slots
@@ -441,8 +576,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->shifts = shifts;
         slot->prefetch = prefetch;
         slot->arch = device_arch(dev);
-        // the 4-waves-per-SIMD build of maps with up to 4 outputs has half the registers: start at 40
-        slot->cap_index = std::max(first_cap_index(), bitslice_waves_per_simd(R, crc > 0) > 2 && !wave ? 2 : 0);
+        slot->cap_index = first_cap(R, crc, wave);
         start_compile(slot, wait);
     }
     const std::shared_ptr<BsEntry> ep = slot;
@@ -451,13 +585,22 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
     hold = ep;
     for (;;) {
         auto it = e.fn.find(dev);
-        if (it != e.fn.end()) return it->second;
+        if (it != e.fn.end()) {
+            if (status) *status = it->second ? 1 : -1;
+            return it->second;
+        }
         if (wait)
             wait_compile(lk, ep);
         else
             poll_compile(ep, false);
-        if (e.state == 0 || e.state == 2) return nullptr;
-        if ((it = e.fn.find(dev)) != e.fn.end()) return it->second;  // loaded while unlocked
+        if (e.state == 0 || e.state == 2) {
+            if (status) *status = 0;
+            return nullptr;
+        }
+        if ((it = e.fn.find(dev)) != e.fn.end()) {  // loaded while unlocked
+            if (status) *status = it->second ? 1 : -1;
+            return it->second;
+        }
         hipFunction_t fn = nullptr;
         int spill = 0;
         if (e.state == 1) {
@@ -483,6 +626,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
             continue;
         }
         e.fn[dev] = fn;
+        if (status) *status = fn ? 1 : -1;
         return fn;
     }
 }

@@ -319,6 +319,12 @@ __device__ __forceinline__ u32 piece_r0n(const u32* t, u32 a, u32 b, u32 c, u32 
 
 int bitslice_waves_per_simd(int R, bool crc) { return R <= 4 ? (crc ? 3 : 4) : 2; }
 
+// One-wave tiles: a budget of 2 waves per SIMD lets the compiler keep the dense 3-4-output decode
+// networks in ~128 VGPRs without spilling (a budget of exactly 128 spills them); smaller maps get a
+// tighter budget, which the compiler's scheduler otherwise fills by hoisting (an R = 1 LDS-ring
+// network: 165 VGPRs at 2 waves, 37 at 8; R = 2: 62-83 at 4).
+int bitslice_wave_budget(int R) { return R <= 1 ? 8 : R == 2 ? 4 : 2; }
+
 int bitslice_depth(int depth, int K)
 {
     if (depth < 2) return 0;
@@ -338,8 +344,8 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     if (style.crc) s << kPreludeCrc;
     const int wpe = (!style.crc && style.waves >= 1 && style.waves <= 8) ? style.waves
                                                                         : bitslice_waves_per_simd(net.R, style.crc);
-    // one-wave tiles only in the plain / copy-through register form
-    const int T = (!style.crc && !D && style.threads == 64) ? 64 : 256;
+    // one-wave tiles: the plain / copy-through register form, and the plain LDS-ring form
+    const int T = (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64 : 256;
     const int CS = T * 16;  // bytes between a lane's 4 chunks of one fragment
     const int TILE = T * 64;
     s << "extern \"C\" __global__ void __launch_bounds__(" << T << ") __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
@@ -707,6 +713,59 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         s << "    }\n}\n";
         return s.str();
     }
+    if (T == 64) {
+        // One-wave LDS ring: the wave streams the 4 KiB of each input of its tile (4 chunks of 1 KiB, one
+        // LDS-DMA load each: lane l's 16 bytes land at slot + c*1024 + l*16) into a ring of D slots,
+        // D - 1 inputs ahead of the network, so the next input's loads are in flight while the current
+        // network runs -- without the 16 VGPRs per input a register prefetch holds across it.  The
+        // code is straight-line per tile, so each wait is exact: before input j's reads at most
+        // 4*min(D - 1, K - 1 - j) loads may still be outstanding (vmcnt retires in issue order; the
+        // previous tile's output stores, issued earlier, are retired by the same wait).  A slot is
+        // refilled only after the reads of its previous input returned (lgkmcnt(0) before each network).
+        s << "    __shared__ __attribute__((aligned(16))) u8 ring[" << D << " * 4096];\n"
+             "    typedef __attribute__((address_space(3))) u8 lds_u8;\n"
+             "    const u32 wring = (u32)(unsigned long)(lds_u8*)ring;\n"
+             "    const u32 lane = threadIdx.x * 16u;\n"
+             "    for (u32 t = blockIdx.x; t < a.ntiles; t += gridDim.x) {\n"
+             "        const u32 sl = t / a.tiles_per_stripe;\n"
+             "        const u32 s = a.stripe_list ? (u32)a.stripe_list[sl] : sl;\n"
+             "        const i32 off = (i32)(t - sl * a.tiles_per_stripe) * "
+          << kBsTileWave
+          << " + (i32)threadIdx.x * 16;\n"
+             "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
+             "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n";
+        auto issue1 = [&](int j) {
+            for (int c = 0; c < 4; c++)
+                s << "        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (__attribute__((address_space(3))) void*)(unsigned "
+                     "long)(wring + "
+                  << (j % D) * 4096 + c * 1024 << "u), 16, a.in_off[" << j << "] + off + " << c * 1024 << ", 0, 0, 2);\n";
+        };
+        acc_init();
+        for (int q = 0; q < D - 1 && q < net.K; q++) issue1(q);
+        for (int j = 0; j < net.K; j++) {
+            s << "        {  // input " << j << "\n";
+            if (j + D - 1 < net.K) issue1(j + D - 1);
+            s << "            asm volatile(\"s_waitcnt vmcnt(" << 4 * std::min(D - 1, net.K - 1 - j) << ")\" ::: \"memory\");\n"
+              << "            const u32 rd = wring + " << (j % D) * 4096 << "u + lane;\n"
+              << "            v4u q0, q1, q2, q3;\n"
+              << "            asm volatile(\"ds_read_b128 %0, %1\" : \"=v\"(q0) : \"v\"(rd) : \"memory\");\n"
+              << "            asm volatile(\"ds_read_b128 %0, %1 offset:1024\" : \"=v\"(q1) : \"v\"(rd) : \"memory\");\n"
+              << "            asm volatile(\"ds_read_b128 %0, %1 offset:2048\" : \"=v\"(q2) : \"v\"(rd) : \"memory\");\n"
+              << "            asm volatile(\"ds_read_b128 %0, %1 offset:3072\" : \"=v\"(q3) : \"v\"(rd) : \"memory\");\n"
+              << "            asm volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(q0), \"+v\"(q1), \"+v\"(q2), \"+v\"(q3));\n"
+              << "            u32 P[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],\n"
+              << "                         q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3]};\n";
+            network(j);
+            s << "        }\n";
+        }
+        outputs("rout", "off");
+        s << "    }\n"
+             "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
+             "}\n";
+        return s.str();
+    }
     // LDS ring: each wave streams its 1 KiB share of the tile's four 4 KiB chunks of every input into
     // a ring of D slots by LDS-DMA loads (no VGPRs), D - 1 inputs ahead of the network -- across the
     // tile boundary too -- and reads its own 64 B per lane back (conflict-free ds_read_b128).  Loads
@@ -795,7 +854,8 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // bit 7 the register budget of 2 waves per SIMD (set with bit 6: the compiler then keeps the
     // dense decode networks of <= 4 outputs in ~128 VGPRs without spilling, which a 4-wave budget
     // of exactly 128 does not -- the occupancy follows the registers actually used), bits 8-10 the
-    // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch)
+    // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch), bits 11-12 the one-wave form's
+    // register budget instead of bit 7's 2 waves per SIMD: 1 = 4 waves, 2 = 8 (bitslice_wave_budget)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     wave = wave && !crc;
     // 1: the late copy of the 16 KiB-tile copy-through form
@@ -807,7 +867,8 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     if (copy || crc || wave) {
         s << "ecamd-bitslice-request " << (shifted ? 3 : 2) << "\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
-              (crc && crc_nib ? 32 : 0) | (wave ? 64 | 128 : 0) | (pf << 8))
+              (crc && crc_nib ? 32 : 0) | (pf << 8) |
+              (!wave ? 0 : bitslice_wave_budget(R) == 8 ? 64 | (2 << 11) : bitslice_wave_budget(R) == 4 ? 64 | (1 << 11) : 64 | 128))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -820,7 +881,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib,
-                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch)
+                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch, int* wave_budget)
 {
     std::istringstream s(text);
     std::string magic;
@@ -828,8 +889,13 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 2047 || (cp & 12) == 12 || depth != 0))
-        return false;  // copy / one-wave tiles: register loads
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 8191 || (cp & 12) == 12))
+        return false;
+    const int wb = (cp >> 11) & 3;  // one-wave register budget: 0 = bit 7's, 1 = 4 waves, 2 = 8
+    if (wb == 3 || (wb && ((cp & 128) || !(cp & 64)))) return false;
+    if (version >= 2 && depth != 0 && ((cp & ~(128 | (3 << 11))) != 64 || (depth != 2 && depth != 4)))
+        return false;  // copy / crc: register loads; plain one-wave tiles: registers or an LDS ring
+    if (wave_budget) *wave_budget = wb == 1 ? 4 : wb == 2 ? 8 : 0;
     const int pf = (cp >> 8) & 7;
     if ((pf != 0 && pf != 1 && pf != 2 && pf != 4) || (pf > 1 && !(cp & 64) && !(cp & 2)) ||
         (pf == 1 && (!(cp & 1) || (cp & 66))))

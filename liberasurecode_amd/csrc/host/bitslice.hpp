@@ -107,6 +107,7 @@ int bitslice_depth(int depth, int K);
 // in <= 256 VGPRs) for 5..8 outputs, 4 (<= 128 VGPRs) for up to 4; the crc variant (up to 4
 // outputs) 3 (its K + R CRC states need more than 128).
 int bitslice_waves_per_simd(int R, bool crc = false);
+int bitslice_wave_budget(int R);  // waves per SIMD the one-wave form of an R-output map is built for
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
 // in_shift (copy-through only): per-input byte shifts of BitsliceStyle::in_shift; any non-zero makes
@@ -118,7 +119,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
                             bool* crc_lane = nullptr, bool* crc_nib = nullptr, bool* wave = nullptr,
                             bool* budget2 = nullptr, std::vector<int>* in_shift = nullptr,
-                            int* prefetch = nullptr);
+                            int* prefetch = nullptr, int* wave_budget = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

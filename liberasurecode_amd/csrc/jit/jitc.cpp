@@ -58,9 +58,9 @@ int main(int argc, char** argv)
     bool copy = false, crc = false, crc_lane = false, crc_nib = false, wave = false, budget2 = false;
     int crc_pos = 1;
     std::vector<int> shifts;
-    int prefetch = 0;
+    int prefetch = 0, wave_budget = 0;
     if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy, &crc, &crc_pos, &crc_lane,
-                                       &crc_nib, &wave, &budget2, &shifts, &prefetch)) {
+                                       &crc_nib, &wave, &budget2, &shifts, &prefetch, &wave_budget)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
@@ -71,7 +71,7 @@ int main(int argc, char** argv)
     style.crc_lane = crc_lane;
     style.crc_nib = crc_nib;
     style.threads = wave ? 64 : 256;
-    style.waves = budget2 ? 2 : 0;
+    style.waves = wave_budget ? wave_budget : budget2 ? 2 : 0;
     style.in_shift = shifts;
     style.prefetch = prefetch;
     if (const char* v = std::getenv("ECAMD_BS_WPE")) style.waves = std::atoi(v);  // experiment only

@@ -58,6 +58,12 @@ class Stream:
     def synchronize(self):
         check(dev().ecamd_stream_synchronize(self.handle), "stream sync")
 
+    def destroy(self):
+        """ecamd_stream_destroy: the stream and the library's context for it."""
+        if self.handle:
+            check(dev().ecamd_stream_destroy(self.handle), "stream destroy")
+            self.handle = None
+
 
 class Event:
     def __init__(self):

@@ -898,3 +898,40 @@ def test_frame_xor_decode_join_matches(F, k, m, hd, missing):
             for s in range(S):
                 assert g[s, :size].tobytes() == objs[s], (size, s)
                 assert (g[s, size:] == 0xA5).all(), (size, s)
+
+
+def test_stream_contexts_bounded(F):
+    """A caller that creates and destroys a stream per request (a proxy) must not grow the library's
+    per-stream contexts (side stream + events + CRC scratch, ecamd_device.hip StreamCtx): 1000 streams,
+    each used once by a Swift-shaped framed encode (1 MiB segment, k=10: bs = 104858, the payloads'
+    rest forked to the side stream without checksum; CRC32 scratch with it), half destroyed through
+    ecamd_stream_destroy, half behind the library's back by hipStreamDestroy.  The context count stays
+    at the cap and every sampled stripe is byte-exact against the restated framing."""
+    import ctypes
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import Stream
+    hip = ctypes.CDLL("libamdhip64.so")
+    d = _lib.dev()
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    k, m, size = 10, 4, 1 << 20
+    objs = _objects(1, size, 4242)
+    fbs = {ct: F.FrameBatch(be, k, m, size, 1, checksum=ct) for ct in (ec_api.CHKSUM_NONE, ec_api.CHKSUM_CRC32)}
+    want = {ct: expected_stripe(be, k, m, 0, objs[0], ct) for ct in fbs}
+    d_obj = _upload_objects(objs, fbs[ec_api.CHKSUM_NONE].obj_stride)
+    peak = 0
+    for i in range(1000):
+        ct = ec_api.CHKSUM_CRC32 if i % 3 == 2 else ec_api.CHKSUM_NONE
+        s = Stream()
+        fbs[ct].encode(d_obj, stream=s)
+        if i % 50 in (0, 2):
+            s.synchronize()
+            got = fbs[ct].fragments()
+            assert all(got[0, f].tobytes() == want[ct][f] for f in range(k + m)), (i, ct)
+        if i % 2:
+            s.destroy()
+        else:
+            s.synchronize()
+            assert hip.hipStreamDestroy(ctypes.c_void_p(s.handle)) == 0
+            s.handle = None
+        peak = max(peak, d.ecamd_stream_contexts())
+    assert peak <= 17, peak  # the cap (16) + the context being created

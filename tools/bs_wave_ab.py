@@ -30,6 +30,12 @@ from liberasurecode_amd import device as D  # noqa: E402
 C3 = (10, 4, 1 << 20, 256, {"encode": None, "decode": [0, 1, 2, 3], "decode_mixed": [0, 5, 10, 13]})
 C5 = (20, 8, 4 << 20, 32, {"rebuild_data": list(range(8)), "rebuild_mixed": [0, 2, 4, 6, 20, 22, 24, 26]})
 C2 = (4, 2, 64 << 10, 4096, {"encode": None, "decode": [0, 1], "decode_mixed": [0, 4]})
+# round 5: 1-2-output maps (knob bs_narrow_min_k) -- single-destination reconstruct (Swift's
+# reconstructor), 1-2 lost -- and the one-wave LDS-DMA ring (bs_wave_depth)
+C3N = (10, 4, 1 << 20, 256, {"rec_data": ("rec", [3], 3), "rec_parity": ("rec", [12], 12),
+                             "decode_1": [0], "decode_2": [0, 11]})
+C5N = (20, 8, 4 << 20, 32, {"rec_x8_d5": ("rec", list(range(8)), 5),
+                            "rec_mixed_d22": ("rec", [0, 2, 4, 6, 20, 22, 24, 26], 22)})
 # round 4, first run (profiles/r04_bs_wave_ab1.log): bs_wave 0 (tables), 1 = then only outputs that are
 # not consecutive slots, 2 + bitslice_min_rows 4 = every C3 pass, bitslice_min_rows 4 alone = 4-wave
 # 16 KiB tiles (decodes spilled there and fell back to the tables).  Now bs_wave 1 is the default
@@ -39,8 +45,16 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
             # neutral here, profiles/r04_bs_prefetch_ab.log, so the library now applies it to copy-through maps only)
             "c3pf": {"wave1": {}, "pf2": {"bs_prefetch": 2}, "pf4": {"bs_prefetch": 4}},
             "c2": {"tables": {}, "wave_2rows": {"bs_wave_min_rows": 2}},
-            "c5": {"wave0": {}, "wave2": {"bs_wave": 2}}}
-DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1}
+            "c5": {"wave0": {}, "wave2": {"bs_wave": 2}},
+            "c3ring": {"wave1": {}, "ring2": {"bs_wave_depth": 2}, "ring4": {"bs_wave_depth": 4}},
+            "c3n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
+                    "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}},
+            "c5n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
+                    "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}},
+            "c2n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
+                    "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}}}
+DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
+            "bs_narrow_min_k": -1, "bs_wave_depth": 0}
 
 
 def launches():
@@ -57,7 +71,8 @@ def apply(d, knobs):
 
 
 def run(cfg, rounds=3, n=30, skip=10):
-    K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5}[cfg]
+    K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
+                       "c2n": C2}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)
@@ -70,7 +85,12 @@ def run(cfg, rounds=3, n=30, skip=10):
     def op_fn(pat):
         if pat is None:
             return lambda: D.rs_encode(K, M, lay, stream=st)
+        if isinstance(pat, tuple):  # ("rec", missing, dest): one destination
+            return lambda: D.rs_reconstruct(K, M, pat[1], pat[2], lay, stream=st)
         return lambda: D.rs_decode(K, M, pat, lay, stream=st)
+
+    def n_out(pat):
+        return M if pat is None else 1 if isinstance(pat, tuple) else len(pat)
 
     # exactness and which kernel runs: every variant rebuilds every op from the same fragments
     ran = {}
@@ -92,7 +112,7 @@ def run(cfg, rounds=3, n=30, skip=10):
             apply(d, knobs)
             for op, pat in ops.items():
                 fn = op_fn(pat)
-                outs = M if pat is None else len(pat)
+                outs = n_out(pat)
                 algo = S * (K + outs) * F
                 ev = [D.Event() for _ in range(n + 1)]
                 ev[0].record(st)
