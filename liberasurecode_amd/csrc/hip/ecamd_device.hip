@@ -336,7 +336,17 @@ struct Tuning {
                                   //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
     Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (1..4)
     Knob bs_narrow_min_k{kBsNarrowMinKDefault};      //   > 0: row groups of 1-2 outputs over at least this many inputs take it too
-    Knob bs_wave_depth{0};        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
+    Knob bs_wave_wmin{0};         //   one-wave forms: amdgpu_waves_per_eu min / max and a scheduling barrier after
+    Knob bs_wave_wmax{0};         //   each input's network (BsOcc, host/bitslice.hpp); 0 / < 0: by R (wave_occ)
+    Knob bs_wave_barrier{-1};
+    Knob bs_wave_per_cu{7};       //   one-wave plain maps: > 0 caps the resident workgroups per CU (a dynamic LDS
+                                  //   share of 160 KiB / N each, per_cu_lds) below the 8 the registers allow:
+                                  //   C3 encode / decode / mixed 0.749 / 0.746 / 0.756 -> 0.812 / 0.796 / 0.783 of
+                                  //   8 TB/s at 7, 0.70 / 0.67 / 0.66 at 6 (tools/bs_wave_ab.py c3cap c3cap2,
+                                  //   profiles/r05_ab_cap.log, r05_ab_cap2.log)
+    Knob bs_copy_per_cu{0};       //   the same for one-wave copy-through maps (framed encode, decode-join)
+    Knob bs_wave_depth{0};
+    Knob xor_per_cu{0};           // xor_stream_kernel: > 0 caps its resident workgroups per CU (per_cu_lds)        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
                                   //   deep (the next input's loads in flight during the network, no VGPRs held
                                   //   for them); 0 = straight into registers
     Knob bs_wave_copy{1};         //   copy-through maps (framed encode / decode-join): 1 (default) too, 2 only
@@ -431,11 +441,13 @@ struct ecamd_map {
 namespace ecamd {
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
                                 std::shared_ptr<void>& hold, bool copy = false, int crc = 0, bool wave = false,
-                                const std::vector<int>* in_shift = nullptr, int prefetch = 0, int* status = nullptr);
+                                const std::vector<int>* in_shift = nullptr, int prefetch = 0, int* status = nullptr,
+                                const BsOcc* occ = nullptr);
 int bitslice_prebuild(const std::vector<int>& coeff, int R, int K, int depth, bool copy, int crc, bool wave,
-                      const std::vector<int>* in_shift, int prefetch, const std::string& arch, const std::string& dir);
+                      const std::vector<int>* in_shift, int prefetch, const BsOcc& occ, const std::string& arch,
+                      const std::string& dir);
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
-                    const std::shared_ptr<void>& hold, int threads = 256);
+                    const std::shared_ptr<void>& hold, int threads = 256, unsigned lds = 0);
 }  // namespace ecamd
 
 namespace {
@@ -772,6 +784,35 @@ bool bs_wave_tiles(int nrows, int K, bool copy, bool* narrow, bool unaligned = f
     return ok && (n || g_tune.bs_wave == 2);
 }
 
+// The one-wave form's occupancy for an R-output map (BsOcc, host/bitslice.hpp): knobs bs_wave_wmin /
+// bs_wave_wmax (0: the policy below) and bs_wave_barrier (< 0: the policy).
+BsOcc wave_occ(int R, bool copy)
+{
+    // 2 waves per SIMD: the register budget the dense 3-4-output decode networks need without
+    // spilling, and an occupancy cap (descriptor VGPRs padded to 176) -- which is also the rate's
+    // optimum: more resident waves run SLOWER (C3 encode 0.745 at 2 per SIMD, 0.717 at 3, 0.711 at 4,
+    // 0.68 at 1; profiles/r05_ab_occ.log, r05_ab_occ2.log), and the resident workgroups per CU are
+    // then trimmed further (bs_wave_per_cu).  Plain maps close each input's network with a scheduling
+    // barrier (the next input's loads are not hoisted into it: fewer live registers, and 0.5-1%
+    // faster at the same occupancy, r05_ab_occ2.log w22b); copy-through forms order their loads and
+    // stores themselves (bs_prefetch).
+    BsOcc o;
+    o.wmin = 2;
+    o.wmax = 2;
+    o.barrier = !copy;
+    if (g_tune.bs_wave_wmin > 0) o.wmin = g_tune.bs_wave_wmin;
+    if (g_tune.bs_wave_wmax > 0) o.wmax = g_tune.bs_wave_wmax;
+    if (g_tune.bs_wave_barrier >= 0) o.barrier = g_tune.bs_wave_barrier != 0;
+    o.wmax = std::max(o.wmax, o.wmin);
+    return o;
+}
+
+// Dynamic LDS per workgroup that caps the resident workgroups of a launch at n per CU (0: none).  The
+// streaming kernels are HBM-pattern bound, and their rate peaks at a concurrency below what their
+// registers allow: C3's one-wave bitsliced kernel runs 0.75 of 8 TB/s at 8 one-wave workgroups per
+// CU, 0.81 at 7, 0.70 at 6 (tools/bs_wave_ab.py c3cap2, profiles/r05_ab_cap2.log).
+size_t per_cu_lds(int n) { return n > 0 ? (kLdsBytes / static_cast<size_t>(n)) & ~size_t(511) : 0; }
+
 // Whether a row group of nrows outputs over K inputs takes the bitsliced kernel under the current
 // knobs, and in which form (launch_bitslice; ecamd_bitslice_prebuild and ecamd_rs_kernel_form ask
 // the same question without launching).
@@ -779,6 +820,7 @@ struct BsForm {
     bool wave = false;  // one-wave 4 KiB tiles (else 4-wave 16 KiB tiles)
     int depth = 0;      // LDS ring depth (0: register loads)
     int prefetch = 0;   // BitsliceStyle::prefetch (copy-through forms)
+    BsOcc occ;          // one-wave forms: occupancy (knobs bs_wave_wmin / bs_wave_wmax / bs_wave_barrier)
 };
 bool bs_form(int nrows, int K, bool copy, bool unaligned, BsForm& f)
 {
@@ -794,6 +836,7 @@ bool bs_form(int nrows, int K, bool copy, bool unaligned, BsForm& f)
     // for 16 KiB tiles; copy-through maps always load into registers
     f.depth = copy ? 0 : static_cast<int>(f.wave ? g_tune.bs_wave_depth : g_tune.bitslice_depth);
     f.prefetch = !copy ? 0 : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
+    f.occ = wave_occ(nrows, copy);
     return true;
 }
 
@@ -832,7 +875,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     std::vector<int> shifts;
     const uint32_t in_records = realign_records(a, K, cover, copy_off != nullptr, shifts);
     hipFunction_t fn = bitslice_function(map->device, sub, nrows, K, form.depth, mode == 2, hold, copy_off != nullptr,
-                                         0, wave, &shifts, form.prefetch);
+                                         0, wave, &shifts, form.prefetch, nullptr, &form.occ);
     if (!fn) return 0;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -889,7 +932,11 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
         // bs_grid 1: one workgroup per tile (the dispatcher balances the tiles); 0: the resident slots
         const int64_t grid = g_tune.bs_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots);
-        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256);
+        // knob bs_wave_per_cu: one-wave workgroups resident per CU capped by a dynamic LDS share each
+        const unsigned lds = wave && form.depth == 0
+                                 ? static_cast<unsigned>(per_cu_lds(copy_off ? g_tune.bs_copy_per_cu : g_tune.bs_wave_per_cu))
+                                 : 0u;
+        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256, lds);
     }
     return *rc ? 0 : cover;
 }
@@ -1069,21 +1116,22 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                     const dim3 grid(static_cast<int>(std::max<int64_t>(
                         1, g_tune.xor_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots)))),
                         block(g.threads);
+                    const size_t lds = per_cu_lds(g_tune.xor_per_cu);  // resident workgroups per CU cap
                     if (copy) {  // (for_each_launch advanced copy_base with the stripes)
                         switch ((c.ncols + 3) / 4) {
-                        case 1: hipLaunchKernelGGL((xor_stream_kernel<1, true>), grid, block, 0, st, c); break;
-                        case 2: hipLaunchKernelGGL((xor_stream_kernel<2, true>), grid, block, 0, st, c); break;
-                        case 3: hipLaunchKernelGGL((xor_stream_kernel<3, true>), grid, block, 0, st, c); break;
-                        case 4: hipLaunchKernelGGL((xor_stream_kernel<4, true>), grid, block, 0, st, c); break;
-                        default: hipLaunchKernelGGL((xor_stream_kernel<8, true>), grid, block, 0, st, c); break;
+                        case 1: hipLaunchKernelGGL((xor_stream_kernel<1, true>), grid, block, lds, st, c); break;
+                        case 2: hipLaunchKernelGGL((xor_stream_kernel<2, true>), grid, block, lds, st, c); break;
+                        case 3: hipLaunchKernelGGL((xor_stream_kernel<3, true>), grid, block, lds, st, c); break;
+                        case 4: hipLaunchKernelGGL((xor_stream_kernel<4, true>), grid, block, lds, st, c); break;
+                        default: hipLaunchKernelGGL((xor_stream_kernel<8, true>), grid, block, lds, st, c); break;
                         }
                     } else {
                         switch ((c.ncols + 3) / 4) {
-                        case 1: hipLaunchKernelGGL((xor_stream_kernel<1, false>), grid, block, 0, st, c); break;
-                        case 2: hipLaunchKernelGGL((xor_stream_kernel<2, false>), grid, block, 0, st, c); break;
-                        case 3: hipLaunchKernelGGL((xor_stream_kernel<3, false>), grid, block, 0, st, c); break;
-                        case 4: hipLaunchKernelGGL((xor_stream_kernel<4, false>), grid, block, 0, st, c); break;
-                        default: hipLaunchKernelGGL((xor_stream_kernel<8, false>), grid, block, 0, st, c); break;
+                        case 1: hipLaunchKernelGGL((xor_stream_kernel<1, false>), grid, block, lds, st, c); break;
+                        case 2: hipLaunchKernelGGL((xor_stream_kernel<2, false>), grid, block, lds, st, c); break;
+                        case 3: hipLaunchKernelGGL((xor_stream_kernel<3, false>), grid, block, lds, st, c); break;
+                        case 4: hipLaunchKernelGGL((xor_stream_kernel<4, false>), grid, block, lds, st, c); break;
+                        default: hipLaunchKernelGGL((xor_stream_kernel<8, false>), grid, block, lds, st, c); break;
                         }
                     }
                     HIP_TRY(hipGetLastError());
@@ -2173,6 +2221,18 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_wave_min_rows = value >= 1 && value <= 4 ? value : 3;  // else the default
     } else if (k == "bs_narrow_min_k") {
         g_tune.bs_narrow_min_k = value < 0 ? kBsNarrowMinKDefault : std::min(value, 33);
+    } else if (k == "bs_wave_wmin") {
+        g_tune.bs_wave_wmin = value >= 1 && value <= 8 ? value : 0;
+    } else if (k == "bs_wave_wmax") {
+        g_tune.bs_wave_wmax = value >= 1 && value <= 8 ? value : 0;
+    } else if (k == "bs_wave_barrier") {
+        g_tune.bs_wave_barrier = value < 0 ? -1 : value != 0;
+    } else if (k == "bs_wave_per_cu") {
+        g_tune.bs_wave_per_cu = value < 0 ? 7 : value <= 32 ? value : 0;  // < 0: the default
+    } else if (k == "bs_copy_per_cu") {
+        g_tune.bs_copy_per_cu = value >= 1 && value <= 32 ? value : 0;
+    } else if (k == "xor_per_cu") {
+        g_tune.xor_per_cu = value >= 1 && value <= 32 ? value : 0;
     } else if (k == "bs_wave_depth") {
         g_tune.bs_wave_depth = value == 2 || value == 4 ? value : 0;
     } else if (k == "bs_tiles_per_slot") {
@@ -2735,7 +2795,7 @@ int ecamd_bitslice_prebuild(int k, int m, const int* missing, int dest, int rebu
         BsForm f;
         if (!bs_form(nrows, K, false, false, f)) continue;
         const int r = ecamd::bitslice_prebuild(group_rows(fm, row0, nrows), nrows, K, f.depth, false, 0, f.wave, nullptr,
-                                               f.prefetch, arch, dir);
+                                               f.prefetch, f.occ, arch, dir);
         if (r < 0) return fail(ECAMD_EHIP, "bitsliced prebuild failed (%d) for a %dx%d map", r, nrows, K);
         built += r;
     }
@@ -2762,7 +2822,7 @@ int ecamd_rs_kernel_form(int k, int m, const int* missing, int dest, int rebuild
             std::shared_ptr<void> hold;
             int st = -1;
             (void)bitslice_function(dev, group_rows(fm, row0, nrows), nrows, K, f.depth, g_tune.bitslice == 2, hold,
-                                    false, 0, f.wave, nullptr, f.prefetch, &st);
+                                    false, 0, f.wave, nullptr, f.prefetch, &st, &f.occ);
             g = st == 1 ? ECAMD_FORM_BITSLICED : st == 0 ? ECAMD_FORM_COMPILING : ECAMD_FORM_UNAVAILABLE;
         }
         if (rank(g) > rank(form)) form = g;

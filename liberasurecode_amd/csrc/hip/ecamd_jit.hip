@@ -204,6 +204,7 @@ struct BsEntry {
     bool wave = false;    // one-wave workgroups, 4 KiB tiles (BitsliceStyle::threads 64)
     std::vector<int> shifts;  // copy-through inputs' byte shifts (BitsliceStyle::in_shift), empty: none
     int prefetch = 0;         // one-wave form: chunks of the next input loaded ahead (BitsliceStyle::prefetch)
+    BsOcc occ;                // one-wave form: amdgpu_waves_per_eu and input barrier (bitslice.hpp)
     int cap_index = 0;    // into kCaps: shared temporaries allowed (fewer: fewer registers)
     std::string arch;     // target of the code object (the requesting device's gcnArchName)
     std::string co_path;  // cache file of the code object
@@ -282,7 +283,9 @@ const std::string& generator_fingerprint()
         lane.crc_lane = true;
         nib = lane;
         nib.crc_nib = true;
-        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave, wave_ring = wave;
+        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave, wave_ring = wave, wave_occ = wave;
+        wave_occ.waves_max = 8;
+        wave_occ.input_barrier = true;
         wave_pf.prefetch = 4;
         shifted.in_shift = {6};
         crc_shifted.in_shift = {10};
@@ -290,7 +293,7 @@ const std::string& generator_fingerprint()
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
              bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + bitslice_source(tiny, 0, shifted) +
              bitslice_source(tiny, 0, crc_shifted) + bitslice_source(tiny5, 0, wave_pf) +
-             bitslice_source(tiny, 2, wave_ring) + kBsNetworkVersion;
+             bitslice_source(tiny, 2, wave_ring) + bitslice_source(tiny, 0, wave_occ) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -314,7 +317,7 @@ std::string request_of(const BsEntry& e)
 {
     return bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0, e.wave, &e.shifts,
-                            e.prefetch);
+                            e.prefetch, e.wave ? &e.occ : nullptr);
 }
 std::string object_name(const BsEntry& e)
 {
@@ -427,7 +430,8 @@ void wait_compile(std::unique_lock<std::mutex>& lk, const std::shared_ptr<BsEntr
 // The canonical parameters of a request (and the entry's key): whatever the caller asked, equal
 // kernels get equal requests.  Returns the key.
 std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& depth, bool& copy, int& crc,
-                           bool& wave, const std::vector<int>* in_shift, int& prefetch, std::vector<int>& shifts)
+                           bool& wave, const std::vector<int>* in_shift, int& prefetch, std::vector<int>& shifts,
+                           BsOcc& occ)
 {
     if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
         const int pos = crc & 7;
@@ -438,7 +442,11 @@ std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& dep
     depth = copy ? 0 : bitslice_depth(depth, K);  // one-wave tiles: the LDS ring only in plain maps
     prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
                : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
-    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0) | (prefetch << 9)};
+    if (!wave) occ = BsOcc{};
+    occ.wmin = std::clamp(occ.wmin, 1, 8);
+    occ.wmax = std::clamp(occ.wmax, occ.wmin, 8);
+    std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0) | (prefetch << 9),
+                            occ.wmin, occ.wmax, occ.barrier ? 1 : 0};
     key.insert(key.end(), coeff.begin(), coeff.end());
     shifts.clear();  // realigned copy-through inputs: their own kernel (and cache entry)
     if (copy && in_shift)
@@ -488,14 +496,17 @@ long code_object_scratch(const std::string& code)
 // built again at the next cap, as the run time would ask for it.  1: present (built now or before),
 // 0: this form never takes a bitsliced kernel, < 0: the helper is missing or failed.
 int bitslice_prebuild(const std::vector<int>& coeff, int R, int K, int depth, bool copy, int crc, bool wave,
-                      const std::vector<int>* in_shift, int prefetch, const std::string& arch, const std::string& dir)
+                      const std::vector<int>* in_shift, int prefetch, const BsOcc& occ_in, const std::string& arch,
+                      const std::string& dir)
 {
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK) return 0;
     const std::string helper = helper_path();
     if (helper.empty()) return -1;
     BsEntry e;
     std::vector<int> shifts;
-    normalize(coeff, R, K, depth, copy, crc, wave, in_shift, prefetch, shifts);
+    BsOcc occ = occ_in;
+    normalize(coeff, R, K, depth, copy, crc, wave, in_shift, prefetch, shifts, occ);
+    e.occ = occ;
     e.coeff = coeff;
     e.R = R;
     e.K = K;
@@ -539,13 +550,14 @@ int bitslice_prebuild(const std::vector<int>& coeff, int R, int K, int depth, bo
 // 1 the kernel is loaded, 0 compiling or queued, -1 unavailable (no code object can be had).
 hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, int K, int depth, bool wait,
                                 std::shared_ptr<void>& hold, bool copy, int crc, bool wave,
-                                const std::vector<int>* in_shift, int prefetch, int* status)
+                                const std::vector<int>* in_shift, int prefetch, int* status, const BsOcc* occ_in)
 {
     if (status) *status = -1;
     if (R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || (helper_path().empty() && shipped_dir().empty()))
         return nullptr;
     std::vector<int> shifts;
-    const std::vector<int> key = normalize(coeff, R, K, depth, copy, crc, wave, in_shift, prefetch, shifts);
+    BsOcc occ = occ_in ? *occ_in : BsOcc{};
+    const std::vector<int> key = normalize(coeff, R, K, depth, copy, crc, wave, in_shift, prefetch, shifts, occ);
     std::vector<std::shared_ptr<BsEntry>> evicted;  // released after the lock (declared before it)
     std::unique_lock<std::mutex> lk(g_jit_mu);
     for (size_t i = 0; i < g_running.size();) {  // reap finished compilers, freeing their slots
@@ -575,6 +587,7 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
         slot->wave = wave;
         slot->shifts = shifts;
         slot->prefetch = prefetch;
+        slot->occ = occ;
         slot->arch = device_arch(dev);
         slot->cap_index = first_cap(R, crc, wave);
         start_compile(slot, wait);
@@ -632,12 +645,12 @@ hipFunction_t bitslice_function(int dev, const std::vector<int>& coeff, int R, i
 }
 
 int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t st,
-                    const std::shared_ptr<void>& hold, int threads)
+                    const std::shared_ptr<void>& hold, int threads, unsigned lds)
 {
     BsArgs a = args;
     void* params[] = {&a};
     const hipError_t e = hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1,
-                                               static_cast<unsigned>(threads == 64 ? 64 : 256), 1, 1, 0, st,
+                                               static_cast<unsigned>(threads == 64 ? 64 : 256), 1, 1, lds, st,
                                                params, nullptr);
     if (e != hipSuccess)
         return dev_fail(ECAMD_EHIP, "hipModuleLaunchKernel(bitslice): %s", hipGetErrorString(e));

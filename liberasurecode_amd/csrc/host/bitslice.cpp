@@ -319,11 +319,6 @@ __device__ __forceinline__ u32 piece_r0n(const u32* t, u32 a, u32 b, u32 c, u32 
 
 int bitslice_waves_per_simd(int R, bool crc) { return R <= 4 ? (crc ? 3 : 4) : 2; }
 
-// One-wave tiles: a budget of 2 waves per SIMD lets the compiler keep the dense 3-4-output decode
-// networks in ~128 VGPRs without spilling (a budget of exactly 128 spills them); smaller maps get a
-// tighter budget, which the compiler's scheduler otherwise fills by hoisting (an R = 1 LDS-ring
-// network: 165 VGPRs at 2 waves, 37 at 8; R = 2: 62-83 at 4).
-int bitslice_wave_budget(int R) { return R <= 1 ? 8 : R == 2 ? 4 : 2; }
 
 int bitslice_depth(int depth, int K)
 {
@@ -348,8 +343,12 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     const int T = (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64 : 256;
     const int CS = T * 16;  // bytes between a lane's 4 chunks of one fragment
     const int TILE = T * 64;
+    // amdgpu_waves_per_eu(min, max): min sets the register budget (512 / min VGPRs); max is an
+    // occupancy CAP -- the compiler raises the kernel descriptor's VGPR count until no more than max
+    // waves fit (max 2: 176 VGPRs whatever the code uses).  style.waves_max 0: max = min.
+    const int wmax = style.waves_max > 0 ? std::max(style.waves_max, wpe) : wpe;
     s << "extern \"C\" __global__ void __launch_bounds__(" << T << ") __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
-      << wpe << ")))\n"
+      << wmax << ")))\n"
          "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
     auto shift_of = [&](int j) {
         return j < static_cast<int>(style.in_shift.size()) ? (style.in_shift[static_cast<size_t>(j)] & 15) : 0;
@@ -707,6 +706,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             if (style.copy_through || pre(j + 1))
                 s << "            __builtin_amdgcn_sched_barrier(0);  // loads / stores leave before the network\n";
             network(j);
+            if (style.input_barrier) s << "            __builtin_amdgcn_sched_barrier(0);\n";
             s << "        }\n";
         }
         outputs("rout", "off");
@@ -846,7 +846,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
                              bool crc, int crc_pos, bool crc_lane, bool crc_nib, bool wave,
-                             const std::vector<int>* in_shift, int prefetch)
+                             const std::vector<int>* in_shift, int prefetch, const BsOcc* occ)
 {
     std::ostringstream s;
     // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
@@ -854,9 +854,10 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // bit 7 the register budget of 2 waves per SIMD (set with bit 6: the compiler then keeps the
     // dense decode networks of <= 4 outputs in ~128 VGPRs without spilling, which a 4-wave budget
     // of exactly 128 does not -- the occupancy follows the registers actually used), bits 8-10 the
-    // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch), bits 11-12 the one-wave form's
-    // register budget instead of bit 7's 2 waves per SIMD: 1 = 4 waves, 2 = 8 (bitslice_wave_budget)
+    // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch); one-wave forms: bits 11-14
+    // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
+    const BsOcc o = occ ? *occ : BsOcc{};
     wave = wave && !crc;
     // 1: the late copy of the 16 KiB-tile copy-through form
     const int pf = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
@@ -868,7 +869,8 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
         s << "ecamd-bitslice-request " << (shifted ? 3 : 2) << "\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
               (crc && crc_nib ? 32 : 0) | (pf << 8) |
-              (!wave ? 0 : bitslice_wave_budget(R) == 8 ? 64 | (2 << 11) : bitslice_wave_budget(R) == 4 ? 64 | (1 << 11) : 64 | 128))
+              (!wave ? 0 : 64 | (std::clamp(o.wmin, 1, 8) << 11) | (std::clamp(o.wmax, o.wmin, 8) << 15) |
+                               (o.barrier ? 1 << 19 : 0)))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -881,7 +883,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib,
-                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch, int* wave_budget)
+                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch, BsOcc* occ)
 {
     std::istringstream s(text);
     std::string magic;
@@ -889,13 +891,18 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp > 8191 || (cp & 12) == 12))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 20) || (cp & 12) == 12))
         return false;
-    const int wb = (cp >> 11) & 3;  // one-wave register budget: 0 = bit 7's, 1 = 4 waves, 2 = 8
-    if (wb == 3 || (wb && ((cp & 128) || !(cp & 64)))) return false;
-    if (version >= 2 && depth != 0 && ((cp & ~(128 | (3 << 11))) != 64 || (depth != 2 && depth != 4)))
+    const int wmin = (cp >> 11) & 15, wmax = (cp >> 15) & 15;  // one-wave occupancy (0: bit 7 / by R)
+    if (wmin > 8 || wmax > 8 || (wmax && wmax < wmin) || ((wmin || wmax || (cp >> 19)) && (!(cp & 64) || (cp & 128))))
+        return false;
+    if (version >= 2 && depth != 0 && ((cp & ~(128 | (511 << 11))) != 64 || (depth != 2 && depth != 4)))
         return false;  // copy / crc: register loads; plain one-wave tiles: registers or an LDS ring
-    if (wave_budget) *wave_budget = wb == 1 ? 4 : wb == 2 ? 8 : 0;
+    if (occ) {
+        occ->wmin = wmin ? wmin : (cp & 128) ? 2 : 0;
+        occ->wmax = wmax ? wmax : occ->wmin;
+        occ->barrier = (cp >> 19) & 1;
+    }
     const int pf = (cp >> 8) & 7;
     if ((pf != 0 && pf != 1 && pf != 2 && pf != 4) || (pf > 1 && !(cp & 64) && !(cp & 2)) ||
         (pf == 1 && (!(cp & 1) || (cp & 66))))

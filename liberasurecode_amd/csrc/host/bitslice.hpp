@@ -76,6 +76,9 @@ struct BitsliceStyle {
     // waves per SIMD the plain / copy-through form is built for (its register budget); 0: by R
     // (bitslice_waves_per_simd)
     int waves = 0;
+    // the occupancy cap of amdgpu_waves_per_eu (0: = waves, which makes the compiler pad the VGPR
+    // count of the kernel descriptor so that exactly `waves` fit, whatever the code uses)
+    int waves_max = 0;
     // copy-through forms: input j's bytes start in_shift[j] (0..15) past a 16-byte boundary (object
     // chunks at j*bs when bs % 16 != 0).  Non-zero: each lane loads the ALIGNED chunk under its
     // window, takes the next one from its neighbour lane (DPP wave_shl:1; the wave's last lane loads
@@ -107,19 +110,29 @@ int bitslice_depth(int depth, int K);
 // in <= 256 VGPRs) for 5..8 outputs, 4 (<= 128 VGPRs) for up to 4; the crc variant (up to 4
 // outputs) 3 (its K + R CRC states need more than 128).
 int bitslice_waves_per_simd(int R, bool crc = false);
-int bitslice_wave_budget(int R);  // waves per SIMD the one-wave form of an R-output map is built for
+// One-wave forms: the kernel's amdgpu_waves_per_eu(wmin, wmax) and whether a scheduling barrier
+// closes every input's network.  wmin sets the register budget (512 / wmin VGPRs); wmax caps the
+// occupancy (the compiler pads the descriptor's VGPR count so no more waves fit: (2, 2) means 176
+// VGPRs, 2 waves per SIMD, whatever the code uses); the barrier keeps the compiler from hoisting the
+// next input's loads into the network, which is what holds the extra registers.
+struct BsOcc {
+    int wmin = 2;
+    int wmax = 2;
+    bool barrier = false;
+};
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.
 // in_shift (copy-through only): per-input byte shifts of BitsliceStyle::in_shift; any non-zero makes
 // a version-3 request (a line of K shifts after the flags).
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
                              bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false,
-                             bool wave = false, const std::vector<int>* in_shift = nullptr, int prefetch = 0);
+                             bool wave = false, const std::vector<int>* in_shift = nullptr, int prefetch = 0,
+                             const BsOcc* occ = nullptr);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
                             bool* crc_lane = nullptr, bool* crc_nib = nullptr, bool* wave = nullptr,
                             bool* budget2 = nullptr, std::vector<int>* in_shift = nullptr,
-                            int* prefetch = nullptr, int* wave_budget = nullptr);
+                            int* prefetch = nullptr, BsOcc* occ = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

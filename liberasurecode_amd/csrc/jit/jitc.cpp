@@ -58,9 +58,10 @@ int main(int argc, char** argv)
     bool copy = false, crc = false, crc_lane = false, crc_nib = false, wave = false, budget2 = false;
     int crc_pos = 1;
     std::vector<int> shifts;
-    int prefetch = 0, wave_budget = 0;
+    int prefetch = 0;
+    ecamd::BsOcc occ;
     if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy, &crc, &crc_pos, &crc_lane,
-                                       &crc_nib, &wave, &budget2, &shifts, &prefetch, &wave_budget)) {
+                                       &crc_nib, &wave, &budget2, &shifts, &prefetch, &occ)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
@@ -71,10 +72,13 @@ int main(int argc, char** argv)
     style.crc_lane = crc_lane;
     style.crc_nib = crc_nib;
     style.threads = wave ? 64 : 256;
-    style.waves = wave_budget ? wave_budget : budget2 ? 2 : 0;
+    style.waves = wave ? occ.wmin : 0;  // one-wave forms: the request's occupancy (0: by R)
+    style.waves_max = wave ? occ.wmax : 0;
+    style.input_barrier = wave && occ.barrier;
     style.in_shift = shifts;
     style.prefetch = prefetch;
     if (const char* v = std::getenv("ECAMD_BS_WPE")) style.waves = std::atoi(v);  // experiment only
+    if (const char* v = std::getenv("ECAMD_BS_WPE_MAX")) style.waves_max = std::atoi(v);  // experiment only
     if (const char* v = std::getenv("ECAMD_BS_LAZY")) style.lazy_temps = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_BARRIER")) style.input_barrier = std::atoi(v) != 0;
     if (const char* v = std::getenv("ECAMD_BS_RLANE")) style.realign_lane = std::atoi(v) != 0;

@@ -43,6 +43,9 @@ def prebuild(arch="gfx950", jobs=8, verbose=False):
     lib.ecamd_bitslice_prebuild.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_char_p]
     lib.ecamd_last_error.restype = C.c_char_p
     os.makedirs(JIT_DIR, exist_ok=True)
+    for name in os.listdir(JIT_DIR):  # objects of an earlier generator or knob set are never looked up
+        if name.startswith("bs_"):
+            os.remove(os.path.join(JIT_DIR, name))
     # the run time uses this directory only if nobody but its owner can write it
     os.chmod(JIT_DIR, stat.S_IRWXU | stat.S_IRGRP | stat.S_IXGRP | stat.S_IROTH | stat.S_IXOTH)
 

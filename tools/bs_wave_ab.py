@@ -51,10 +51,58 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}},
             "c5n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}},
+            # round 5: amdgpu_waves_per_eu(2, 2) capped the one-wave kernel at 2 waves per SIMD (descriptor
+            # VGPRs padded to 176); occupancy variants (knobs bs_wave_wmin / wmax / barrier / depth)
+            "c3occ": {"w22": {"bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_barrier": 0},
+                      "w28": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_barrier": 0},
+                      "w28b": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_barrier": 1},
+                      "w58b": {"bs_wave_wmin": 5, "bs_wave_wmax": 8, "bs_wave_barrier": 1},
+                      "ring2_w28": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_depth": 2}},
+            # measured: more waves per SIMD run SLOWER (w22 0.742 / w28 0.717 / w28b 0.711, r05_ab_occ.log)
+            "c3occ2": {"w22": {"bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_barrier": 0},
+                       "w11": {"bs_wave_wmin": 1, "bs_wave_wmax": 1, "bs_wave_barrier": 0},
+                       "w22b": {"bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_barrier": 1}},
+            # resident one-wave workgroups per CU between the register-set occupancies (knob bs_wave_per_cu over
+            # a 4-wave-per-SIMD build: (2, 8) + barrier)
+            "c3cap": {"w22b": {"bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_barrier": 1},
+                      **{f"cap{n}": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_barrier": 1, "bs_wave_per_cu": n}
+                         for n in (6, 7, 8, 9, 10, 12)}},
+            "c5ncap": {"w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2},
+                       **{f"cap{n}": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8, "bs_wave_per_cu": n}
+                          for n in (6, 7, 8, 9, 10, 12)}},
+            # finer: the cap-7 optimum (r05_ab_cap.log: C3 encode 0.80) against w22, on both builds
+            "c3cap2": {"w22b": {"bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_barrier": 1},
+                       "cap7": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_barrier": 1, "bs_wave_per_cu": 7},
+                       "cap7_w22b": {"bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_barrier": 1, "bs_wave_per_cu": 7},
+                       "cap7_w28": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_barrier": 0, "bs_wave_per_cu": 7},
+                       "cap5": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_barrier": 1, "bs_wave_per_cu": 5},
+                       "cap7_ring2": {"bs_wave_wmin": 2, "bs_wave_wmax": 8, "bs_wave_depth": 2, "bs_wave_per_cu": 7}},
+            "c5cap": {"tiles16k": {},
+                      "wave_cap7": {"bs_wave": 2, "bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_per_cu": 7},
+                      "wave_cap6": {"bs_wave": 2, "bs_wave_wmin": 2, "bs_wave_wmax": 2, "bs_wave_per_cu": 6},
+                      "wave_w22": {"bs_wave": 2, "bs_wave_wmin": 2, "bs_wave_wmax": 2}},
+            # round 5 defaults: (2, 2) + barrier, 7 one-wave workgroups per CU; 1-2-output maps
+            "c3ncap": {"tables": {"bs_narrow_min_k": 0},
+                       "w22b_cap7": {"bs_narrow_min_k": 1},
+                       "w22_cap7": {"bs_narrow_min_k": 1, "bs_wave_barrier": 0},
+                       "w88_cap7": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8, "bs_wave_barrier": 0},
+                       "w22b_cap8": {"bs_narrow_min_k": 1, "bs_wave_per_cu": 8}},
+            "c5ncap2": {"tables": {"bs_narrow_min_k": 0},
+                        "w22b_cap7": {"bs_narrow_min_k": 1},
+                        "w22_cap7": {"bs_narrow_min_k": 1, "bs_wave_barrier": 0},
+                        "w88_cap7": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8, "bs_wave_barrier": 0},
+                        "w22b_cap8": {"bs_narrow_min_k": 1, "bs_wave_per_cu": 8}},
+            "c5nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
+                       "w44": {"bs_narrow_min_k": 1, "bs_wave_wmin": 4, "bs_wave_wmax": 4},
+                       "w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2},
+                       "w11": {"bs_narrow_min_k": 1, "bs_wave_wmin": 1, "bs_wave_wmax": 1}},
+            "c3nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
+                       "w44": {"bs_narrow_min_k": 1, "bs_wave_wmin": 4, "bs_wave_wmax": 4},
+                       "w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2}},
             "c2n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}}}
-DEFAULTS = {"bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
-            "bs_narrow_min_k": -1, "bs_wave_depth": 0}
+DEFAULTS = {"bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
+            "bs_narrow_min_k": -1, "bs_wave_depth": 0, "bs_wave_wmin": 0, "bs_wave_wmax": 0, "bs_wave_barrier": -1}
 
 
 def launches():
@@ -72,7 +120,8 @@ def apply(d, knobs):
 
 def run(cfg, rounds=3, n=30, skip=10):
     K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
-                       "c2n": C2}[cfg]
+                       "c2n": C2, "c3occ": C3, "c3occ2": C3, "c5nocc": C5N, "c3nocc": C3N,
+                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)

@@ -3,7 +3,9 @@
 threads (4 / 2 / 1 KiB of every fragment; knob xor_threads) -- the codec-shaped probe ran the C3
 pattern at 0.73 / 0.76 with 4 KiB / 1 KiB one-wave tiles (profiles/r03_geom_probe3.log).  Encode and
 decode of (10,6,4) and (10,5,3) at 1 MiB x 256 stripes and (3,3,3) at 4 KiB x 131072 stripes,
-interleaved rounds, median; every variant's bytes checked equal to the default's."""
+interleaved rounds, median; every variant's bytes checked equal to the default's.
+Round 5: `xor_threads_ab.py KNOB v1,v2,...` A/Bs any knob the same way (e.g. xor_per_cu 0,7,8,12:
+resident workgroups per CU)."""
 import json
 import os
 import statistics
@@ -18,7 +20,9 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 SHAPES = [(10, 6, 4, 1 << 20, 256, [0, 1, 2]), (10, 5, 3, 1 << 20, 256, [0, 1]), (3, 3, 3, 4096, 131072, [0, 1]),
           (3, 3, 3, 1 << 20, 1024, [0, 1]), (10, 6, 4, 64 << 10, 4096, [0, 1, 2]), (10, 6, 4, 16 << 10, 16384, [0, 1, 2])]
-THREADS = [256, 128, 64, 0]  # 0: the library default (by fragment size)
+KNOB = sys.argv[1].encode() if len(sys.argv) > 2 else b"xor_threads"
+THREADS = ([int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2
+           else [256, 128, 64, 0])  # xor_threads 0: the library default (by fragment size)
 
 
 def timed(fn, st, n=14, skip=4):
@@ -41,7 +45,7 @@ def main(rounds=3):
                "decode": (lambda: D.xor_decode(k, m, hd, lost, lay, stream=st), None)}
         refs = {}
         for t in THREADS:
-            d.ecamd_tune(b"xor_threads", t)
+            d.ecamd_tune(KNOB, t)
             for op, (fn, _) in ops.items():
                 fn()
                 st.synchronize()
@@ -55,17 +59,17 @@ def main(rounds=3):
         res = {}
         for _ in range(rounds):
             for t in THREADS:
-                d.ecamd_tune(b"xor_threads", t)
+                d.ecamd_tune(KNOB, t)
                 for op, (fn, _) in ops.items():
                     res.setdefault((t, op), []).append(timed(fn, st))
         for (t, op), ts in res.items():
             ms = statistics.median(ts)
             algo = ops[op][1]
             print(json.dumps({"code": f"({k},{m},{hd})", "F": F, "stripes": S, "op": op,
-                              "threads": t or "default", "ms": round(ms, 4),
+                              KNOB.decode(): t, "ms": round(ms, 4),
                               "frac": round(algo / (ms * 1e-3) / 8e12, 4) if algo else None}), flush=True)
         lay.buf.free()
-    d.ecamd_tune(b"xor_threads", 0)
+    d.ecamd_tune(KNOB, 0)
 
 
 if __name__ == "__main__":
