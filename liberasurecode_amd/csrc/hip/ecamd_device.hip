@@ -191,7 +191,12 @@ struct Knob {
 
 constexpr int kFrameCrcNibDefault = 0;
 constexpr int kFrameCrcBsDefault = 1;
-constexpr int kBsNarrowMinKDefault = 0;  // 1-2-output maps: LDS tables (A/B pending)
+// 1-2-output maps of at least 8 inputs take the one-wave bitsliced kernel: C3 (k = 10) single
+// reconstruct of a data / parity fragment 0.685 / 0.690 -> 0.750 / 0.774 of 8 TB/s, decode of 1 / 2
+// lost 0.687 / 0.688 -> 0.770 / 0.750; C5 (k = 20) reconstruct 0.692 -> 0.806; C2 (k = 4) keeps its
+// 8 KiB tables (0.80 against 0.70 bitsliced) (tools/bs_wave_ab.py c3ncap c5ncap2 c2n,
+// profiles/r05_ab_ncap.log, r05_ab_narrow.log)
+constexpr int kBsNarrowMinKDefault = 8;
 
 struct Tuning {
     Knob threads{0};     // threads per workgroup of the gf16 kernel
@@ -346,7 +351,8 @@ struct Tuning {
                                   //   profiles/r05_ab_cap.log, r05_ab_cap2.log)
     Knob bs_copy_per_cu{0};       //   the same for one-wave copy-through maps (framed encode, decode-join)
     Knob bs_wave_depth{0};
-    Knob xor_per_cu{0};           // xor_stream_kernel: > 0 caps its resident workgroups per CU (per_cu_lds)        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
+    Knob xor_per_cu{-1};          // xor_stream_kernel: > 0 caps its resident workgroups per CU (per_cu_lds), 0 off,
+                                  //   < 0 by shape (launch_xor)        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
                                   //   deep (the next input's loads in flight during the network, no VGPRs held
                                   //   for them); 0 = straight into registers
     Knob bs_wave_copy{1};         //   copy-through maps (framed encode / decode-join): 1 (default) too, 2 only
@@ -933,9 +939,10 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         // bs_grid 1: one workgroup per tile (the dispatcher balances the tiles); 0: the resident slots
         const int64_t grid = g_tune.bs_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots);
         // knob bs_wave_per_cu: one-wave workgroups resident per CU capped by a dynamic LDS share each
-        const unsigned lds = wave && form.depth == 0
-                                 ? static_cast<unsigned>(per_cu_lds(copy_off ? g_tune.bs_copy_per_cu : g_tune.bs_wave_per_cu))
-                                 : 0u;
+        // (the LDS-ring form holds depth x 4 KiB of static LDS: the dynamic share tops it up)
+        const size_t cap = per_cu_lds(copy_off ? g_tune.bs_copy_per_cu : g_tune.bs_wave_per_cu);
+        const size_t ring = wave ? static_cast<size_t>(bitslice_depth(form.depth, K)) * 4096 : 0;
+        const unsigned lds = wave && cap > ring ? static_cast<unsigned>(cap - ring) : 0u;
         *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256, lds);
     }
     return *rc ? 0 : cover;
@@ -1116,7 +1123,12 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                     const dim3 grid(static_cast<int>(std::max<int64_t>(
                         1, g_tune.xor_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots)))),
                         block(g.threads);
-                    const size_t lds = per_cu_lds(g_tune.xor_per_cu);  // resident workgroups per CU cap
+                    // resident workgroups per CU: knob xor_per_cu (< 0: 6 for 4 KiB tiles of more than 4
+                    // inputs -- (10,6,4) at 64 KiB 0.754 -> 0.791, at 16 KiB 0.751 -> 0.758; one-wave tiles
+                    // and small codes lose with any cap, tools/xor_threads_ab.py, profiles/r05_ab_xorcap.log)
+                    const int xcap = g_tune.xor_per_cu >= 0 ? static_cast<int>(g_tune.xor_per_cu)
+                                                            : (g.threads == 256 && c.ncols > 4 ? 6 : 0);
+                    const size_t lds = per_cu_lds(xcap);
                     if (copy) {  // (for_each_launch advanced copy_base with the stripes)
                         switch ((c.ncols + 3) / 4) {
                         case 1: hipLaunchKernelGGL((xor_stream_kernel<1, true>), grid, block, lds, st, c); break;
@@ -2232,7 +2244,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_copy_per_cu") {
         g_tune.bs_copy_per_cu = value >= 1 && value <= 32 ? value : 0;
     } else if (k == "xor_per_cu") {
-        g_tune.xor_per_cu = value >= 1 && value <= 32 ? value : 0;
+        g_tune.xor_per_cu = value < 0 ? -1 : std::min(value, 32);
     } else if (k == "bs_wave_depth") {
         g_tune.bs_wave_depth = value == 2 || value == 4 ? value : 0;
     } else if (k == "bs_tiles_per_slot") {

@@ -191,6 +191,12 @@ __device__ __forceinline__ u32 x3(u32 a, u32 b, u32 c)
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+__device__ __forceinline__ u32 x2(u32 a, u32 b)
+{
+    u32 r;
+    asm("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ u32 bfi(u32 m, u32 x, u32 y)
 {
     u32 r;
@@ -364,6 +370,10 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             std::snprintf(b, sizeof(b), "t%d", v);
         return std::string(b);
     };
+    // The one-wave LDS-ring form accumulates single terms through an asm XOR too: with plain `^=` the
+    // compiler re-associates the sum of a 1-output map over the inputs (a tree over all 20 inputs'
+    // planes at K = 20: 256 VGPRs + scratch), which the ring's inline-asm reads leave it free to do.
+    const bool opaque_xor = D != 0 && T == 64;
     // the network of input j on P[16] (bit planes), accumulated into acc
     auto network = [&](int j) {
         const auto& in = net.inputs[static_cast<size_t>(j)];
@@ -402,7 +412,12 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             for (; q + 1 < terms.size(); q += 2)
                 s << "            " << dst << " = x3(" << dst << ", " << ref(terms[q]) << ", "
                   << ref(terms[q + 1]) << ");\n";
-            if (q < terms.size()) s << "            " << dst << " ^= " << ref(terms[q]) << ";\n";
+            if (q < terms.size()) {
+                if (opaque_xor)  // an asm XOR: the compiler cannot re-associate the sum across inputs
+                    s << "            " << dst << " = x2(" << dst << ", " << ref(terms[q]) << ");\n";
+                else
+                    s << "            " << dst << " ^= " << ref(terms[q]) << ";\n";
+            }
         }
     };
     auto acc_init = [&]() {
@@ -736,11 +751,13 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
              "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
              "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n";
+        // (the chunk's byte offset goes into the scalar offset: the instruction's immediate offset
+        // would move the LDS destination too)
         auto issue1 = [&](int j) {
             for (int c = 0; c < 4; c++)
                 s << "        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (__attribute__((address_space(3))) void*)(unsigned "
                      "long)(wring + "
-                  << (j % D) * 4096 + c * 1024 << "u), 16, a.in_off[" << j << "] + off + " << c * 1024 << ", 0, 0, 2);\n";
+                  << (j % D) * 4096 + c * 1024 << "u), 16, off, a.in_off[" << j << "] + " << c * 1024 << ", 0, 2);\n";
         };
         acc_init();
         for (int q = 0; q < D - 1 && q < net.K; q++) issue1(q);
@@ -758,7 +775,10 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
               << "            u32 P[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],\n"
               << "                         q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3]};\n";
             network(j);
-            s << "        }\n";
+            // every network completes before the next input's reads: without it the compiler sinks
+            // the networks below later reads and keeps many inputs' planes live (R = 1, K = 20:
+            // 256 VGPRs + scratch)
+            s << "            __builtin_amdgcn_sched_barrier(0);\n        }\n";
         }
         outputs("rout", "off");
         s << "    }\n"

@@ -22,6 +22,21 @@ from liberasurecode_amd import device as D  # noqa: E402
 # before the current input's copy stores
 VARIANTS = {"lds_tables_stream": (0, 0), "bitsliced_wave": (1, 0), "bitsliced_wave_pf2": (1, 2),
             "bitsliced_wave_pf4": (1, 4)}
+# round 5 (`frame_wave_ab.py cap`): resident one-wave workgroups per CU of the copy-through form (knob
+# bs_copy_per_cu; the plain maps run best at 7, profiles/r05_ab_cap2.log), defaults otherwise
+KNOBSETS = {"cap": {"copy_cap0": {"bs_copy_per_cu": 0}, "copy_cap6": {"bs_copy_per_cu": 6},
+                    "copy_cap7": {"bs_copy_per_cu": 7}, "copy_cap8": {"bs_copy_per_cu": 8}}}
+if len(sys.argv) > 1:
+    VARIANTS = KNOBSETS[sys.argv[1]]
+
+
+def apply(d, v):
+    if isinstance(v, dict):
+        for key, val in v.items():
+            d.ecamd_tune(key.encode(), val)
+    else:
+        d.ecamd_tune(b"bs_wave_copy", v[0])
+        d.ecamd_tune(b"bs_prefetch", v[1])
 
 
 def main(rounds=3, reps=10):
@@ -39,8 +54,7 @@ def main(rounds=3, reps=10):
                "join_0123": (lambda: fb.decode([0, 1, 2, 3], out, stream=st), S * ((k + 4) * bs - 4 * bs + size))}
         ref = {}
         for vname, v in VARIANTS.items():
-            d.ecamd_tune(b"bs_wave_copy", v[0])
-            d.ecamd_tune(b"bs_prefetch", v[1])
+            apply(d, v)
             fb.encode(obj, stream=st)
             st.synchronize()
             frags = fb.fragments()
@@ -57,8 +71,7 @@ def main(rounds=3, reps=10):
         a, b = D.Event(), D.Event()
         for _ in range(rounds):
             for vname, v in VARIANTS.items():
-                d.ecamd_tune(b"bs_wave_copy", v[0])
-                d.ecamd_tune(b"bs_prefetch", v[1])
+                apply(d, v)
                 for op, (fn, _) in ops.items():
                     fn()
                     a.record(st)
@@ -76,6 +89,7 @@ def main(rounds=3, reps=10):
         del fb
     d.ecamd_tune(b"bs_wave_copy", -1)
     d.ecamd_tune(b"bs_prefetch", -1)
+    d.ecamd_tune(b"bs_copy_per_cu", 0)
     d.ecamd_tune(b"bitslice", 1)
 
 
