@@ -39,7 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # second decode pattern per config, data and parity mixed
 MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}
 GIB = float(1 << 30)
-ROUND = "r04"  # profiles/<round>_* written by tools/gpu_prof.sh for this bench
+ROUND = "r05"  # profiles/<round>_* written by tools/gpu_prof.sh for this bench
 
 CONFIGS = {
     # name: (k, m, fragment bytes, stripes per GPU, decode erasures, description)

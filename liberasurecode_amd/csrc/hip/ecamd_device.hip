@@ -349,7 +349,11 @@ struct Tuning {
                                   //   C3 encode / decode / mixed 0.749 / 0.746 / 0.756 -> 0.812 / 0.796 / 0.783 of
                                   //   8 TB/s at 7, 0.70 / 0.67 / 0.66 at 6 (tools/bs_wave_ab.py c3cap c3cap2,
                                   //   profiles/r05_ab_cap.log, r05_ab_cap2.log)
-    Knob bs_copy_per_cu{0};       //   the same for one-wave copy-through maps (framed encode, decode-join)
+    Knob bs_copy_per_cu{6};       //   the same for one-wave copy-through maps whose inputs are aligned: C3 framed
+                                  //   encode 0.708 -> 0.758, decode-join 0.734 -> 0.783 at 6 (7: 0.725 / 0.746;
+                                  //   Swift segments' decode-join 0.636 -> 0.651; tools/frame_wave_ab.py cap,
+                                  //   profiles/r05_ab_copycap.log)
+    Knob bs_copy_realign_per_cu{0};  //   ... and realigned inputs (Swift's segment encode: 0.664 uncapped, 0.652 at 6)
     Knob bs_wave_depth{0};
     Knob xor_per_cu{-1};          // xor_stream_kernel: > 0 caps its resident workgroups per CU (per_cu_lds), 0 off,
                                   //   < 0 by shape (launch_xor)        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
@@ -940,7 +944,10 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         const int64_t grid = g_tune.bs_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots);
         // knob bs_wave_per_cu: one-wave workgroups resident per CU capped by a dynamic LDS share each
         // (the LDS-ring form holds depth x 4 KiB of static LDS: the dynamic share tops it up)
-        const size_t cap = per_cu_lds(copy_off ? g_tune.bs_copy_per_cu : g_tune.bs_wave_per_cu);
+        // copy-through maps: bs_copy_per_cu when every input is read aligned (C3 objects, decode-joins),
+        // bs_copy_realign_per_cu when inputs are realigned in registers (Swift's segments)
+        const size_t cap = per_cu_lds(!copy_off ? g_tune.bs_wave_per_cu
+                                                : shifts.empty() ? g_tune.bs_copy_per_cu : g_tune.bs_copy_realign_per_cu);
         const size_t ring = wave ? static_cast<size_t>(bitslice_depth(form.depth, K)) * 4096 : 0;
         const unsigned lds = wave && cap > ring ? static_cast<unsigned>(cap - ring) : 0u;
         *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256, lds);
@@ -2242,7 +2249,9 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_wave_per_cu") {
         g_tune.bs_wave_per_cu = value < 0 ? 7 : value <= 32 ? value : 0;  // < 0: the default
     } else if (k == "bs_copy_per_cu") {
-        g_tune.bs_copy_per_cu = value >= 1 && value <= 32 ? value : 0;
+        g_tune.bs_copy_per_cu = value < 0 ? 6 : std::min(value, 32);  // < 0: the default
+    } else if (k == "bs_copy_realign_per_cu") {
+        g_tune.bs_copy_realign_per_cu = value < 0 ? 0 : std::min(value, 32);
     } else if (k == "xor_per_cu") {
         g_tune.xor_per_cu = value < 0 ? -1 : std::min(value, 32);
     } else if (k == "bs_wave_depth") {

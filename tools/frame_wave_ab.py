@@ -25,7 +25,11 @@ VARIANTS = {"lds_tables_stream": (0, 0), "bitsliced_wave": (1, 0), "bitsliced_wa
 # round 5 (`frame_wave_ab.py cap`): resident one-wave workgroups per CU of the copy-through form (knob
 # bs_copy_per_cu; the plain maps run best at 7, profiles/r05_ab_cap2.log), defaults otherwise
 KNOBSETS = {"cap": {"copy_cap0": {"bs_copy_per_cu": 0}, "copy_cap6": {"bs_copy_per_cu": 6},
-                    "copy_cap7": {"bs_copy_per_cu": 7}, "copy_cap8": {"bs_copy_per_cu": 8}}}
+                    "copy_cap7": {"bs_copy_per_cu": 7}, "copy_cap8": {"bs_copy_per_cu": 8}},
+            "cap2": {"copy_cap6": {"bs_copy_per_cu": 6, "bs_copy_realign_per_cu": 0},
+                     "copy_cap5": {"bs_copy_per_cu": 5, "bs_copy_realign_per_cu": 0},
+                     "realign_cap7": {"bs_copy_per_cu": 6, "bs_copy_realign_per_cu": 7},
+                     "realign_cap10": {"bs_copy_per_cu": 6, "bs_copy_realign_per_cu": 10}}}
 if len(sys.argv) > 1:
     VARIANTS = KNOBSETS[sys.argv[1]]
 
@@ -89,7 +93,8 @@ def main(rounds=3, reps=10):
         del fb
     d.ecamd_tune(b"bs_wave_copy", -1)
     d.ecamd_tune(b"bs_prefetch", -1)
-    d.ecamd_tune(b"bs_copy_per_cu", 0)
+    d.ecamd_tune(b"bs_copy_per_cu", -1)
+    d.ecamd_tune(b"bs_copy_realign_per_cu", -1)
     d.ecamd_tune(b"bitslice", 1)
 
 
