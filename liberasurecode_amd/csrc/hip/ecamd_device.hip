@@ -340,25 +340,28 @@ struct Tuning {
                                   //   0.733 -> 0.746, decode {0,1,2,3} 0.734 -> 0.742, mixed {0,5,10,13}
                                   //   0.700 -> 0.753 of 8 TB/s against the LDS-table stream kernel
     Knob bs_wave_min_rows{3};     //   fewest outputs of a row group that bs_wave 1 moves (1..4)
-    Knob bs_narrow_min_k{kBsNarrowMinKDefault};      //   > 0: row groups of 1-2 outputs over at least this many inputs take it too
+    Knob bs_narrow_min_k{kBsNarrowMinKDefault};  //   > 0: row groups of 1-2 outputs over at least this many inputs
+                                                 //   take it too
     Knob bs_wave_wmin{0};         //   one-wave forms: amdgpu_waves_per_eu min / max and a scheduling barrier after
     Knob bs_wave_wmax{0};         //   each input's network (BsOcc, host/bitslice.hpp); 0 / < 0: by R (wave_occ)
     Knob bs_wave_barrier{-1};
-    Knob bs_wave_per_cu{7};       //   one-wave plain maps: > 0 caps the resident workgroups per CU (a dynamic LDS
-                                  //   share of 160 KiB / N each, per_cu_lds) below the 8 the registers allow:
-                                  //   C3 encode / decode / mixed 0.749 / 0.746 / 0.756 -> 0.812 / 0.796 / 0.783 of
-                                  //   8 TB/s at 7, 0.70 / 0.67 / 0.66 at 6 (tools/bs_wave_ab.py c3cap c3cap2,
-                                  //   profiles/r05_ab_cap.log, r05_ab_cap2.log)
-    Knob bs_copy_per_cu{6};       //   the same for one-wave copy-through maps whose inputs are aligned: C3 framed
-                                  //   encode 0.708 -> 0.758, decode-join 0.734 -> 0.783 at 6 (7: 0.725 / 0.746;
-                                  //   Swift segments' decode-join 0.636 -> 0.651; tools/frame_wave_ab.py cap,
+    Knob bs_wave_depth{0};        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
+                                  //   deep (the next input's loads in flight during the network, no VGPRs held
+                                  //   for them); 0 = straight into registers (the ring measured 1-4% slower)
+    // Resident workgroups per CU (> 0: a cap below what the registers allow, by a dynamic LDS share that
+    // tops the kernel's own LDS up to 160 KiB / N, cap_lds; 0: none):
+    Knob bs_wave_per_cu{7};       //   one-wave plain maps: C3 encode / decode / mixed 0.749 / 0.746 / 0.756 ->
+                                  //   0.812 / 0.796 / 0.783 of 8 TB/s at 7, 0.70 / 0.67 / 0.66 at 6, 0.73-0.75
+                                  //   at 8 (tools/bs_wave_ab.py c3cap c3cap2, profiles/r05_ab_cap.log,
+                                  //   r05_ab_cap2.log)
+    Knob bs_copy_per_cu{6};       //   one-wave copy-through maps whose inputs are aligned: C3 framed encode
+                                  //   0.708 -> 0.758, decode-join 0.734 -> 0.783 at 6 (7: 0.725 / 0.746; Swift
+                                  //   segments' decode-join 0.636 -> 0.651; tools/frame_wave_ab.py cap,
                                   //   profiles/r05_ab_copycap.log)
     Knob bs_copy_realign_per_cu{0};  //   ... and realigned inputs (Swift's segment encode: 0.664 uncapped, 0.652 at 6)
-    Knob bs_wave_depth{0};
-    Knob xor_per_cu{-1};          // xor_stream_kernel: > 0 caps its resident workgroups per CU (per_cu_lds), 0 off,
-                                  //   < 0 by shape (launch_xor)        //   one-wave plain maps: inputs by LDS-DMA through a per-wave ring 2 / 4 inputs
-                                  //   deep (the next input's loads in flight during the network, no VGPRs held
-                                  //   for them); 0 = straight into registers
+    Knob bs_tile_per_cu{0};       //   ecamd_bs_kernel in 16 KiB tiles (5-8 outputs)
+    Knob frame_crc_per_cu{0};     //   the bitsliced crc variant (framed CRC32 encode)
+    Knob xor_per_cu{-1};          //   xor_stream_kernel: < 0 by shape (launch_xor)
     Knob bs_wave_copy{1};         //   copy-through maps (framed encode / decode-join): 1 (default) too, 2 only
                                   //   when their inputs start at offsets that are not multiples of 16, 0 never.
                                   //   With the prefetch (bs_prefetch) the one-wave form beats the LDS-table
@@ -823,6 +826,20 @@ BsOcc wave_occ(int R, bool copy)
 // CU, 0.81 at 7, 0.70 at 6 (tools/bs_wave_ab.py c3cap2, profiles/r05_ab_cap2.log).
 size_t per_cu_lds(int n) { return n > 0 ? (kLdsBytes / static_cast<size_t>(n)) & ~size_t(511) : 0; }
 
+// The dynamic LDS a launch of the module kernel fn adds so that its workgroup's LDS (static + dynamic)
+// is per_cu_lds(n): 0 when n is 0 or the static share is already that large.
+unsigned cap_lds(hipFunction_t fn, int n)
+{
+    const size_t want = per_cu_lds(n);
+    if (!want || !fn) return 0;
+    int stat = 0;
+    if (hipFuncGetAttribute(&stat, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, fn) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return want > static_cast<size_t>(stat) ? static_cast<unsigned>(want - static_cast<size_t>(stat)) : 0u;
+}
+
 // Whether a row group of nrows outputs over K inputs takes the bitsliced kernel under the current
 // knobs, and in which form (launch_bitslice; ecamd_bitslice_prebuild and ecamd_rs_kernel_form ask
 // the same question without launching).
@@ -942,14 +959,14 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         c.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(n);
         // bs_grid 1: one workgroup per tile (the dispatcher balances the tiles); 0: the resident slots
         const int64_t grid = g_tune.bs_grid ? static_cast<int64_t>(c.ntiles) : std::min<int64_t>(c.ntiles, slots);
-        // knob bs_wave_per_cu: one-wave workgroups resident per CU capped by a dynamic LDS share each
-        // (the LDS-ring form holds depth x 4 KiB of static LDS: the dynamic share tops it up)
-        // copy-through maps: bs_copy_per_cu when every input is read aligned (C3 objects, decode-joins),
-        // bs_copy_realign_per_cu when inputs are realigned in registers (Swift's segments)
-        const size_t cap = per_cu_lds(!copy_off ? g_tune.bs_wave_per_cu
-                                                : shifts.empty() ? g_tune.bs_copy_per_cu : g_tune.bs_copy_realign_per_cu);
-        const size_t ring = wave ? static_cast<size_t>(bitslice_depth(form.depth, K)) * 4096 : 0;
-        const unsigned lds = wave && cap > ring ? static_cast<unsigned>(cap - ring) : 0u;
+        // resident workgroups per CU: one-wave plain maps bs_wave_per_cu; copy-through maps bs_copy_per_cu
+        // when every input is read aligned (C3 objects, decode-joins), bs_copy_realign_per_cu when inputs
+        // are realigned in registers (Swift's segments); 16 KiB tiles bs_tile_per_cu
+        const int wg_cap = !wave ? static_cast<int>(g_tune.bs_tile_per_cu)
+                        : !copy_off ? static_cast<int>(g_tune.bs_wave_per_cu)
+                        : shifts.empty() ? static_cast<int>(g_tune.bs_copy_per_cu)
+                                         : static_cast<int>(g_tune.bs_copy_realign_per_cu);
+        const unsigned lds = cap_lds(fn, wg_cap);
         *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256, lds);
     }
     return *rc ? 0 : cover;
@@ -1845,7 +1862,8 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     const int wgs = static_cast<int>(g_tune.frame_crc_bs_wgs);
     const int grid = static_cast<int>(
         wgs > 0 ? std::min<int64_t>(units, static_cast<int64_t>(cu_count(device)) * wgs) : units);
-    return bitslice_launch(fn, b, grid, static_cast<hipStream_t>(stream), hold);
+    return bitslice_launch(fn, b, grid, static_cast<hipStream_t>(stream), hold, 256,
+                           cap_lds(fn, static_cast<int>(g_tune.frame_crc_per_cu)));
 }
 
 }  // namespace
@@ -2250,6 +2268,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_wave_per_cu = value < 0 ? 7 : value <= 32 ? value : 0;  // < 0: the default
     } else if (k == "bs_copy_per_cu") {
         g_tune.bs_copy_per_cu = value < 0 ? 6 : std::min(value, 32);  // < 0: the default
+    } else if (k == "bs_tile_per_cu") {
+        g_tune.bs_tile_per_cu = value < 0 ? 0 : std::min(value, 32);
+    } else if (k == "frame_crc_per_cu") {
+        g_tune.frame_crc_per_cu = value < 0 ? 0 : std::min(value, 32);
     } else if (k == "bs_copy_realign_per_cu") {
         g_tune.bs_copy_realign_per_cu = value < 0 ? 0 : std::min(value, 32);
     } else if (k == "xor_per_cu") {
