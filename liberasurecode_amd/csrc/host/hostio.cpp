@@ -109,6 +109,24 @@ int64_t chunk_target()
 // blocking, while 4-16 MiB objects gained 15% with it (tools/latency_ab.py,
 // profiles/r03_latency_ab2.log).
 constexpr int64_t kSpinMinBytes = 64 << 10;
+// off by default: the kernel's own PCIe reads / writes cost MORE than the two DMAs at small sizes
+// (4 KiB RS(10,4) encode 35.5 -> 45.5 us, one thread, tools/latency_bench.py,
+// profiles/r05_lat_zc0.log, r05_lat_zc256.log); 256 KiB - 1 MiB gain 5-14% (r05_lat_zc4096.log)
+constexpr long kZeroCopyKibDefault = 0;
+
+// ECAMD_PERCALL_ZEROCOPY_KIB: a call whose fragments fit one chunk of at most this many KiB (all
+// fragments) skips both DMAs -- the kernel reads its inputs from, and writes its outputs to, the pinned
+// slab itself over PCIe (hipHostMalloc memory is device-accessible and coherent), so the call costs
+// one launch and one wait instead of three queued operations ("Small objects").
+int64_t zerocopy_bytes()
+{
+    static const int64_t v = [] {
+        const char* env = std::getenv("ECAMD_PERCALL_ZEROCOPY_KIB");
+        const long kib = env ? std::atol(env) : kZeroCopyKibDefault;
+        return static_cast<int64_t>(std::max(0L, kib)) << 10;
+    }();
+    return v;
+}
 
 int spin_us()
 {
@@ -303,6 +321,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     const int64_t crc_off = st->cap - 256;
     std::vector<uint32_t> crc(want_crc ? nfr : 0, 0u);
     const int64_t nchunks = (bs + chunk - 1) / chunk;
+    const bool zero_copy = nchunks == 1 && chunk * nfr <= zerocopy_bytes();
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
     std::vector<void*> cdst(static_cast<size_t>(nfr));
     std::vector<const void*> csrc(static_cast<size_t>(nfr));
@@ -368,16 +387,18 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         // One DMA each way per chunk (the slabs are [K inputs | R outputs] x chunk, contiguous):
         // for small fragments the per-call cost is API latency, not bytes.  A short last chunk
         // also moves the stale tail of each slot, which the kernel and the unpack never read.
-        rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
-        if (rc == 0) rc = launch(ctx, sl.d_buf, chunk, n, sl.stream);
-        if (rc == 0)
+        // zero_copy: the kernels work on the pinned slab itself (no DMA either way)
+        char* const work = zero_copy ? sl.h_pin : sl.d_buf;
+        if (!zero_copy) rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
+        if (rc == 0) rc = launch(ctx, work, chunk, n, sl.stream);
+        if (rc == 0 && !zero_copy)
             rc = ecamd_memcpy_async(sl.h_pin + K * chunk, sl.d_buf + K * chunk,
                                     (R - 1) * chunk + n, 1, sl.stream);
         if (rc == 0 && want_crc) {
-            auto* d_crc = reinterpret_cast<uint32_t*>(sl.d_buf + crc_off);
-            rc = ecamd_crc32(t_crc.legacy ? 1 : 0, sl.d_buf, 0, chunk, static_cast<int>(nfr), n,
+            auto* d_crc = reinterpret_cast<uint32_t*>(work + crc_off);
+            rc = ecamd_crc32(t_crc.legacy ? 1 : 0, work, 0, chunk, static_cast<int>(nfr), n,
                              1, d_crc, sl.stream);
-            if (rc == 0)
+            if (rc == 0 && !zero_copy)
                 rc = ecamd_memcpy_async(sl.h_pin + crc_off, d_crc, nfr * 4, 1, sl.stream);
         }
         pending[s] = c;
