@@ -92,6 +92,13 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
                         "w22_cap7": {"bs_narrow_min_k": 1, "bs_wave_barrier": 0},
                         "w88_cap7": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8, "bs_wave_barrier": 0},
                         "w22b_cap8": {"bs_narrow_min_k": 1, "bs_wave_per_cu": 8}},
+            # the LDS ring at capped residency: fewer waves, each with its next input in flight
+            "c3ringcap": {"regs_cap7": {},
+                          "ring2_cap7": {"bs_wave_depth": 2},
+                          "ring2_cap6": {"bs_wave_depth": 2, "bs_wave_per_cu": 6},
+                          "ring2_cap5": {"bs_wave_depth": 2, "bs_wave_per_cu": 5},
+                          "ring4_cap6": {"bs_wave_depth": 4, "bs_wave_per_cu": 6}},
+            "c2wgs": {"wgs0": {"wgs_per_cu": 0}, "wgs2": {"wgs_per_cu": 2}, "wgs3": {"wgs_per_cu": 3}},
             "c5tile": {"cap0": {"bs_tile_per_cu": 0}, "cap1": {"bs_tile_per_cu": 1}},
             "c5nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
                        "w44": {"bs_narrow_min_k": 1, "bs_wave_wmin": 4, "bs_wave_wmax": 4},
@@ -102,7 +109,7 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
                        "w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2}},
             "c2n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}}}
-DEFAULTS = {"bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
+DEFAULTS = {"wgs_per_cu": 0, "bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
             "bs_narrow_min_k": -1, "bs_wave_depth": 0, "bs_wave_wmin": 0, "bs_wave_wmax": 0, "bs_wave_barrier": -1}
 
 
@@ -122,7 +129,7 @@ def apply(d, knobs):
 def run(cfg, rounds=3, n=30, skip=10):
     K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
                        "c2n": C2, "c3occ": C3, "c3occ2": C3, "c5nocc": C5N, "c3nocc": C3N,
-                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5}[cfg]
+                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)
