@@ -359,6 +359,8 @@ struct Tuning {
                                   //   segments' decode-join 0.636 -> 0.651; tools/frame_wave_ab.py cap,
                                   //   profiles/r05_ab_copycap.log)
     Knob bs_copy_realign_per_cu{0};  //   ... and realigned inputs (Swift's segment encode: 0.664 uncapped, 0.652 at 6)
+    Knob bs_tile_threads{256};    //   ecamd_bs_kernel, plain 5-8-output maps: lanes per workgroup (128 / 256 / 512:
+                                  //   8 / 16 / 32 KiB tiles)
     Knob bs_tile_per_cu{0};       //   ecamd_bs_kernel in 16 KiB tiles (5-8 outputs)
     Knob frame_crc_per_cu{0};     //   the bitsliced crc variant (framed CRC32 encode)
     Knob xor_per_cu{-1};          //   xor_stream_kernel: < 0 by shape (launch_xor)
@@ -864,8 +866,16 @@ bool bs_form(int nrows, int K, bool copy, bool unaligned, BsForm& f)
     f.depth = copy ? 0 : static_cast<int>(f.wave ? g_tune.bs_wave_depth : g_tune.bitslice_depth);
     f.prefetch = !copy ? 0 : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
     f.occ = wave_occ(nrows, copy);
+    if (!f.wave) {  // multi-wave form: its workgroup size (plain register form only; bs_tile_threads)
+        f.occ = BsOcc{};
+        const int t = static_cast<int>(g_tune.bs_tile_threads);
+        if (!copy && f.depth == 0 && (t == 128 || t == 512)) f.occ.threads = t;
+    }
     return true;
 }
+
+// Lanes per workgroup and bytes of each fragment per tile of a form.
+int bs_threads(const BsForm& f) { return f.wave ? 64 : f.occ.threads ? f.occ.threads : 256; }
 
 int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyArgs& base,
                         const int64_t* in_off, const int64_t* out_off, int64_t bs, int nstripes,
@@ -885,7 +895,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     for (int j = 0; j < K; j++) a.in_off[j] = in_off[j];
     for (int r = 0; r < nrows; r++) a.out_off[r] = out_off[row0 + r];
     const bool wave = form.wave;
-    const int64_t tile = wave ? kBsTileWave : kBsTile;
+    const int threads = bs_threads(form);
+    const int64_t tile = static_cast<int64_t>(threads) * 64;  // kBsTileWave / kBsTile at 64 / 256 lanes
     if (bs < tile) return 0;
     const int64_t cover = (base.limited ? std::min<int64_t>(bs, base.min_len) : bs) / tile * tile;
     if (cover < tile) return 0;
@@ -938,7 +949,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
     // 2 workgroups of 4 waves per CU: the network's ~240 VGPRs allow 2 waves per SIMD
     // one 4-wave workgroup per wave per SIMD the kernel is built for (2 for 5..8 outputs)
     // (one-wave workgroups: 4 per such slot, so a launch keeps its bytes)
-    const int64_t slots = static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows) * (wave ? 4 : 1);
+    const int64_t slots = static_cast<int64_t>(cu_count(map->device)) * bitslice_waves_per_simd(nrows) * 4 * 64 / threads;
     // long passes as several launches (bs_tiles_per_slot; as launch_stream_pass)
     const uint64_t limit = static_cast<uint64_t>(std::max(0, static_cast<int>(g_tune.bs_tiles_per_slot)));
     int per = nstripes;
@@ -967,7 +978,7 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
                         : shifts.empty() ? static_cast<int>(g_tune.bs_copy_per_cu)
                                          : static_cast<int>(g_tune.bs_copy_realign_per_cu);
         const unsigned lds = cap_lds(fn, wg_cap);
-        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, wave ? 64 : 256, lds);
+        *rc = bitslice_launch(fn, c, static_cast<int>(grid), st, hold, threads, lds);
     }
     return *rc ? 0 : cover;
 }
@@ -2268,6 +2279,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_wave_per_cu = value < 0 ? 7 : value <= 32 ? value : 0;  // < 0: the default
     } else if (k == "bs_copy_per_cu") {
         g_tune.bs_copy_per_cu = value < 0 ? 6 : std::min(value, 32);  // < 0: the default
+    } else if (k == "bs_tile_threads") {
+        g_tune.bs_tile_threads = value == 128 || value == 512 ? value : 256;
     } else if (k == "bs_tile_per_cu") {
         g_tune.bs_tile_per_cu = value < 0 ? 0 : std::min(value, 32);
     } else if (k == "frame_crc_per_cu") {
@@ -2861,7 +2874,7 @@ int ecamd_rs_kernel_form(int k, int m, const int* missing, int dest, int rebuild
         const int nrows = std::min(8, R - row0);
         BsForm f;
         int g = ECAMD_FORM_TABLES;
-        if (bs_form(nrows, K, false, false, f) && blocksize >= (f.wave ? kBsTileWave : kBsTile)) {
+        if (bs_form(nrows, K, false, false, f) && blocksize >= static_cast<int64_t>(bs_threads(f)) * 64) {
             std::shared_ptr<void> hold;
             int st = -1;
             (void)bitslice_function(dev, group_rows(fm, row0, nrows), nrows, K, f.depth, g_tune.bitslice == 2, hold,

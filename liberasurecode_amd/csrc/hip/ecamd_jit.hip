@@ -317,7 +317,7 @@ std::string request_of(const BsEntry& e)
 {
     return bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0, e.wave, &e.shifts,
-                            e.prefetch, e.wave ? &e.occ : nullptr);
+                            e.prefetch, e.wave || e.occ.threads ? &e.occ : nullptr);
 }
 std::string object_name(const BsEntry& e)
 {
@@ -442,11 +442,15 @@ std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& dep
     depth = copy ? 0 : bitslice_depth(depth, K);  // one-wave tiles: the LDS ring only in plain maps
     prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
                : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
-    if (!wave) occ = BsOcc{};
+    if (!wave) {  // the multi-wave forms: only the plain register form's workgroup size
+        const int th = occ.threads;
+        occ = BsOcc{};
+        if (!copy && !crc && depth == 0 && (th == 128 || th == 512)) occ.threads = th;
+    }
     occ.wmin = std::clamp(occ.wmin, 1, 8);
     occ.wmax = std::clamp(occ.wmax, occ.wmin, 8);
     std::vector<int> key = {R, K, depth, (copy ? 1 : 0) | (crc << 1) | (wave ? 256 : 0) | (prefetch << 9),
-                            occ.wmin, occ.wmax, occ.barrier ? 1 : 0};
+                            occ.wmin, occ.wmax, occ.barrier ? 1 : 0, occ.threads};
     key.insert(key.end(), coeff.begin(), coeff.end());
     shifts.clear();  // realigned copy-through inputs: their own kernel (and cache entry)
     if (copy && in_shift)
@@ -650,7 +654,9 @@ int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t 
     BsArgs a = args;
     void* params[] = {&a};
     const hipError_t e = hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1,
-                                               static_cast<unsigned>(threads == 64 ? 64 : 256), 1, 1, lds, st,
+                                               static_cast<unsigned>(threads == 64 || threads == 128 || threads == 512
+                                                                         ? threads : 256),
+                                               1, 1, lds, st,
                                                params, nullptr);
     if (e != hipSuccess)
         return dev_fail(ECAMD_EHIP, "hipModuleLaunchKernel(bitslice): %s", hipGetErrorString(e));

@@ -346,7 +346,10 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     const int wpe = (!style.crc && style.waves >= 1 && style.waves <= 8) ? style.waves
                                                                         : bitslice_waves_per_simd(net.R, style.crc);
     // one-wave tiles: the plain / copy-through register form, and the plain LDS-ring form
-    const int T = (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64 : 256;
+    const int T = (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64
+                  : (!style.crc && !D && !style.copy_through && (style.threads == 128 || style.threads == 512))
+                      ? style.threads
+                      : 256;
     const int CS = T * 16;  // bytes between a lane's 4 chunks of one fragment
     const int TILE = T * 64;
     // amdgpu_waves_per_eu(min, max): min sets the register budget (512 / min VGPRs); max is an
@@ -875,9 +878,11 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // dense decode networks of <= 4 outputs in ~128 VGPRs without spilling, which a 4-wave budget
     // of exactly 128 does not -- the occupancy follows the registers actually used), bits 8-10 the
     // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch); one-wave forms: bits 11-14
-    // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused)
+    // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused); plain maps in
+    // the multi-wave form, bits 20-21: lanes per workgroup (1 = 128, 2 = 512; 0 = 256)
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     const BsOcc o = occ ? *occ : BsOcc{};
+    const int tcode = !wave && !copy && !crc && depth == 0 ? (o.threads == 128 ? 1 : o.threads == 512 ? 2 : 0) : 0;
     wave = wave && !crc;
     // 1: the late copy of the 16 KiB-tile copy-through form
     const int pf = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
@@ -885,12 +890,12 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     bool shifted = false;
     if (in_shift && (copy || crc))
         for (int j = 0; j < K && j < static_cast<int>(in_shift->size()); j++) shifted = shifted || ((*in_shift)[j] & 15);
-    if (copy || crc || wave) {
+    if (copy || crc || wave || tcode) {
         s << "ecamd-bitslice-request " << (shifted ? 3 : 2) << "\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
               (crc && crc_nib ? 32 : 0) | (pf << 8) |
               (!wave ? 0 : 64 | (std::clamp(o.wmin, 1, 8) << 11) | (std::clamp(o.wmax, o.wmin, 8) << 15) |
-                               (o.barrier ? 1 << 19 : 0)))
+                               (o.barrier ? 1 << 19 : 0)) | (tcode << 20))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -911,10 +916,13 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 20) || (cp & 12) == 12))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 22) || (cp & 12) == 12))
         return false;
+    const int tcode = (cp >> 20) & 3;  // lanes per workgroup of the multi-wave plain form
+    if (tcode == 3 || (tcode && ((cp & (1 | 2 | 64)) || depth != 0))) return false;
     const int wmin = (cp >> 11) & 15, wmax = (cp >> 15) & 15;  // one-wave occupancy (0: bit 7 / by R)
-    if (wmin > 8 || wmax > 8 || (wmax && wmax < wmin) || ((wmin || wmax || (cp >> 19)) && (!(cp & 64) || (cp & 128))))
+    if (wmin > 8 || wmax > 8 || (wmax && wmax < wmin) ||
+        ((wmin || wmax || ((cp >> 19) & 1)) && (!(cp & 64) || (cp & 128))))
         return false;
     if (version >= 2 && depth != 0 && ((cp & ~(128 | (511 << 11))) != 64 || (depth != 2 && depth != 4)))
         return false;  // copy / crc: register loads; plain one-wave tiles: registers or an LDS ring
@@ -922,6 +930,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
         occ->wmin = wmin ? wmin : (cp & 128) ? 2 : 0;
         occ->wmax = wmax ? wmax : occ->wmin;
         occ->barrier = (cp >> 19) & 1;
+        occ->threads = tcode == 1 ? 128 : tcode == 2 ? 512 : 0;
     }
     const int pf = (cp >> 8) & 7;
     if ((pf != 0 && pf != 1 && pf != 2 && pf != 4) || (pf > 1 && !(cp & 64) && !(cp & 2)) ||

@@ -119,6 +119,9 @@ struct BsOcc {
     int wmin = 2;
     int wmax = 2;
     bool barrier = false;
+    // plain maps in the multi-wave register form only: lanes per workgroup 128 / 512 (8 / 32 KiB tiles)
+    // instead of 256 (16 KiB); 0 = 256
+    int threads = 0;
 };
 
 // A compile request (R, K, cap, depth, coefficients) as the text ecamd_jitc reads, and back.

@@ -71,7 +71,7 @@ int main(int argc, char** argv)
     style.crc_pos = crc_pos;
     style.crc_lane = crc_lane;
     style.crc_nib = crc_nib;
-    style.threads = wave ? 64 : 256;
+    style.threads = wave ? 64 : occ.threads ? occ.threads : 256;
     style.waves = wave ? occ.wmin : 0;  // one-wave forms: the request's occupancy (0: by R)
     style.waves_max = wave ? occ.wmax : 0;
     style.input_barrier = wave && occ.barrier;

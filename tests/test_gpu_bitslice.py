@@ -207,3 +207,25 @@ def test_few_output_builds_exact(sync_compile, k, m, bs, rows):
         assert (lay.download_stripes() == want).all()
     finally:
         d.ecamd_tune(b"bitslice_min_rows", 0)
+
+
+@pytest.mark.parametrize("threads", [128, 512])
+@pytest.mark.parametrize("k,m,lost", [(20, 8, None), (20, 8, [0, 2, 4, 6, 20, 22, 24, 26]), (10, 6, [0, 1, 2, 3, 4, 5])])
+def test_tile_threads_exact(sync_compile, threads, k, m, lost):
+    """The multi-wave form with 128 / 512 lanes per workgroup (8 / 32 KiB tiles, knob bs_tile_threads)
+    against the oracle, fragments with a ragged tail (the LDS tables take the rest)."""
+    d = sync_compile
+    d.ecamd_tune(b"bs_tile_threads", threads)
+    try:
+        bs = 32768 * 3 + 4096 + 10
+        lay, want = _batch(k, m, bs, 3, seed=51)
+        if lost is None:
+            D.rs_encode(k, m, lay)
+        else:
+            host = want.copy()
+            host[:, lost] = 0x6B
+            lay.upload_stripes(host)
+            D.rs_decode(k, m, lost, lay)
+        assert (lay.download_stripes() == want).all()
+    finally:
+        d.ecamd_tune(b"bs_tile_threads", 256)

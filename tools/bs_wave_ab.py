@@ -29,6 +29,7 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 C3 = (10, 4, 1 << 20, 256, {"encode": None, "decode": [0, 1, 2, 3], "decode_mixed": [0, 5, 10, 13]})
 C5 = (20, 8, 4 << 20, 32, {"rebuild_data": list(range(8)), "rebuild_mixed": [0, 2, 4, 6, 20, 22, 24, 26]})
+C5E = (20, 8, 4 << 20, 32, {"encode": None, "rebuild_data": list(range(8)), "rebuild_mixed": [0, 2, 4, 6, 20, 22, 24, 26]})
 C2 = (4, 2, 64 << 10, 4096, {"encode": None, "decode": [0, 1], "decode_mixed": [0, 4]})
 # round 5: 1-2-output maps (knob bs_narrow_min_k) -- single-destination reconstruct (Swift's
 # reconstructor), 1-2 lost -- and the one-wave LDS-DMA ring (bs_wave_depth)
@@ -99,6 +100,11 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
                           "ring2_cap5": {"bs_wave_depth": 2, "bs_wave_per_cu": 5},
                           "ring4_cap6": {"bs_wave_depth": 4, "bs_wave_per_cu": 6}},
             "c2wgs": {"wgs0": {"wgs_per_cu": 0}, "wgs2": {"wgs_per_cu": 2}, "wgs3": {"wgs_per_cu": 3}},
+            # round 5: lanes per workgroup of the 16 KiB-tile form (8 / 16 / 32 KiB tiles)
+            # the default build ((2, 2) + barrier) at 6 / 7 / 8 resident workgroups per CU, per pattern
+            "c3cap3": {"cap6": {"bs_wave_per_cu": 6}, "cap7": {}, "cap8": {"bs_wave_per_cu": 8}},
+            "c5ncap3": {"cap6": {"bs_wave_per_cu": 6}, "cap7": {}, "cap8": {"bs_wave_per_cu": 8}},
+            "c5tt": {"t256": {}, "t128": {"bs_tile_threads": 128}, "t512": {"bs_tile_threads": 512}},
             "c5tile": {"cap0": {"bs_tile_per_cu": 0}, "cap1": {"bs_tile_per_cu": 1}},
             "c5nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
                        "w44": {"bs_narrow_min_k": 1, "bs_wave_wmin": 4, "bs_wave_wmax": 4},
@@ -109,7 +115,7 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
                        "w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2}},
             "c2n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}}}
-DEFAULTS = {"wgs_per_cu": 0, "bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
+DEFAULTS = {"bs_tile_threads": 256, "wgs_per_cu": 0, "bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
             "bs_narrow_min_k": -1, "bs_wave_depth": 0, "bs_wave_wmin": 0, "bs_wave_wmax": 0, "bs_wave_barrier": -1}
 
 
@@ -129,7 +135,7 @@ def apply(d, knobs):
 def run(cfg, rounds=3, n=30, skip=10):
     K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
                        "c2n": C2, "c3occ": C3, "c3occ2": C3, "c5nocc": C5N, "c3nocc": C3N,
-                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2}[cfg]
+                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)

@@ -5,6 +5,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "gpurun_out/r05_$name.log" 2>&1; local rc=$?; tail -2 "gpurun_out/r05_$name.log" | cut -c1-400; [ $rc -eq 0 ] || { echo "STEP $name FAILED rc=$rc"; exit 1; }; }
-step ab_ringcap 700 python -u tools/bs_wave_ab.py c3ringcap c2wgs
-grep summary gpurun_out/r05_ab_ringcap.log
+
+step ab_cap3 700 python -u tools/bs_wave_ab.py c3cap3 c5ncap3
+grep summary gpurun_out/r05_ab_cap3.log
 echo ALL_OK
