@@ -350,10 +350,12 @@ struct Tuning {
                                   //   for them); 0 = straight into registers (the ring measured 1-4% slower)
     // Resident workgroups per CU (> 0: a cap below what the registers allow, by a dynamic LDS share that
     // tops the kernel's own LDS up to 160 KiB / N, cap_lds; 0: none):
-    Knob bs_wave_per_cu{7};       //   one-wave plain maps: C3 encode / decode / mixed 0.749 / 0.746 / 0.756 ->
-                                  //   0.812 / 0.796 / 0.783 of 8 TB/s at 7, 0.70 / 0.67 / 0.66 at 6, 0.73-0.75
-                                  //   at 8 (tools/bs_wave_ab.py c3cap c3cap2, profiles/r05_ab_cap.log,
-                                  //   r05_ab_cap2.log)
+    Knob bs_wave_per_cu{-1};      //   one-wave plain maps (< 0: 7 below 20 fragments per tile, else none): C3 encode /
+                                  //   decode / mixed 0.749 / 0.746 / 0.756 -> 0.812 / 0.796 / 0.783 of 8 TB/s at
+                                  //   7, 0.70 / 0.67 / 0.66 at 6, 0.73-0.75 at 8 (tools/bs_wave_ab.py c3cap c3cap2
+                                  //   c3cap3, profiles/r05_ab_cap.log, r05_ab_cap2.log, r05_ab_cap3.log); a
+                                  //   21-fragment tile (C5 single reconstruct) runs best uncapped at 8: 0.813 /
+                                  //   0.822 against 0.799 / 0.806 at 7 (r05_ab_cap3.log, r05_ab_ncap.log)
     Knob bs_copy_per_cu{6};       //   one-wave copy-through maps whose inputs are aligned: C3 framed encode
                                   //   0.708 -> 0.758, decode-join 0.734 -> 0.783 at 6 (7: 0.725 / 0.746; Swift
                                   //   segments' decode-join 0.636 -> 0.651; tools/frame_wave_ab.py cap,
@@ -974,7 +976,8 @@ int64_t launch_bitslice(const ecamd_map* map, int row0, int nrows, const ApplyAr
         // when every input is read aligned (C3 objects, decode-joins), bs_copy_realign_per_cu when inputs
         // are realigned in registers (Swift's segments); 16 KiB tiles bs_tile_per_cu
         const int wg_cap = !wave ? static_cast<int>(g_tune.bs_tile_per_cu)
-                        : !copy_off ? static_cast<int>(g_tune.bs_wave_per_cu)
+                        : !copy_off ? (g_tune.bs_wave_per_cu >= 0 ? static_cast<int>(g_tune.bs_wave_per_cu)
+                                                                   : K + nrows >= 20 ? 0 : 7)
                         : shifts.empty() ? static_cast<int>(g_tune.bs_copy_per_cu)
                                          : static_cast<int>(g_tune.bs_copy_realign_per_cu);
         const unsigned lds = cap_lds(fn, wg_cap);
@@ -2276,7 +2279,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "bs_wave_barrier") {
         g_tune.bs_wave_barrier = value < 0 ? -1 : value != 0;
     } else if (k == "bs_wave_per_cu") {
-        g_tune.bs_wave_per_cu = value < 0 ? 7 : value <= 32 ? value : 0;  // < 0: the default
+        g_tune.bs_wave_per_cu = value < 0 ? -1 : std::min(value, 32);  // < 0: by shape
     } else if (k == "bs_copy_per_cu") {
         g_tune.bs_copy_per_cu = value < 0 ? 6 : std::min(value, 32);  // < 0: the default
     } else if (k == "bs_tile_threads") {
