@@ -365,6 +365,8 @@ struct Tuning {
                                   //   8 / 16 / 32 KiB tiles)
     Knob bs_tile_per_cu{0};       //   ecamd_bs_kernel in 16 KiB tiles (5-8 outputs)
     Knob frame_crc_per_cu{0};     //   the bitsliced crc variant (framed CRC32 encode)
+    Knob bs_plain_prefetch{0};    //   one-wave plain maps: chunks (0 / 2 / 4) of the next input loaded before each network
+    Knob frame_copy_per_cu{0};    //   framed split / join streaming kernels (copy_lds, ecamd_frame_api.hip)
     Knob xor_per_cu{-1};          //   xor_stream_kernel: < 0 by shape (launch_xor)
     Knob bs_wave_copy{1};         //   copy-through maps (framed encode / decode-join): 1 (default) too, 2 only
                                   //   when their inputs start at offsets that are not multiples of 16, 0 never.
@@ -405,6 +407,7 @@ int dev_tune(const char* key)
     if (k == "crc_bits") return g_tune.crc_bits;
     if (k == "crc_wgs") return g_tune.crc_wgs;
     if (k == "frame_copy_grid") return g_tune.frame_copy_grid;
+    if (k == "frame_copy_per_cu") return g_tune.frame_copy_per_cu;
     if (k == "frame_copy_dpp") return g_tune.frame_copy_dpp;
     if (k == "frame_crc_lane") return g_tune.frame_crc_lane;
     if (k == "frame_crc_bs_nib") return g_tune.frame_crc_bs_nib;
@@ -866,7 +869,8 @@ bool bs_form(int nrows, int K, bool copy, bool unaligned, BsForm& f)
     // LDS ring (depth 2 / 4) or register loads: bs_wave_depth for one-wave plain maps, bitslice_depth
     // for 16 KiB tiles; copy-through maps always load into registers
     f.depth = copy ? 0 : static_cast<int>(f.wave ? g_tune.bs_wave_depth : g_tune.bitslice_depth);
-    f.prefetch = !copy ? 0 : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
+    f.prefetch = !copy ? (f.wave && f.depth == 0 ? static_cast<int>(g_tune.bs_plain_prefetch) : 0)
+                       : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
     f.occ = wave_occ(nrows, copy);
     if (!f.wave) {  // multi-wave form: its workgroup size (plain register form only; bs_tile_threads)
         f.occ = BsOcc{};
@@ -2282,6 +2286,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_wave_per_cu = value < 0 ? -1 : std::min(value, 32);  // < 0: by shape
     } else if (k == "bs_copy_per_cu") {
         g_tune.bs_copy_per_cu = value < 0 ? 6 : std::min(value, 32);  // < 0: the default
+    } else if (k == "bs_plain_prefetch") {
+        g_tune.bs_plain_prefetch = value == 2 || value == 4 ? value : 0;
+    } else if (k == "frame_copy_per_cu") {
+        g_tune.frame_copy_per_cu = value < 0 ? 0 : std::min(value, 32);
     } else if (k == "bs_tile_threads") {
         g_tune.bs_tile_threads = value == 128 || value == 512 ? value : 256;
     } else if (k == "bs_tile_per_cu") {

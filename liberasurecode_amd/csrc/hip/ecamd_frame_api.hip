@@ -67,6 +67,14 @@ int image(int dev, bool legacy, int B, int J, int G, bool pos, const DevImage** 
     return 0;
 }
 
+// Knob frame_copy_per_cu: resident workgroups per CU of the streaming split / join kernels (a dynamic
+// LDS share of 160 KiB / N; 0 = none).
+size_t copy_lds()
+{
+    const int n = dev_tune("frame_copy_per_cu");
+    return n > 0 ? (size_t(163840) / static_cast<size_t>(n)) & ~size_t(511) : 0;
+}
+
 // Per-(device, stream) scratch for span partials (the stream's context, ecamd_internal.hpp).
 int scratch(int dev, void* stream, size_t words, uint32_t** out, int slot = 0)
 {
@@ -465,10 +473,10 @@ int split_range(int dev, int k, const void* obj, int64_t obj_stride, uint64_t ob
     const bool dpp = dev_tune("frame_copy_dpp") != 0;
     if (cs.u == 1)
         hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<1, true> : frame_split_stream_kernel<1, false>), grid, block,
-                           0, st, sa);
+                           copy_lds(), st, sa);
     else
         hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<4, true> : frame_split_stream_kernel<4, false>), grid, block,
-                           0, st, sa);
+                           copy_lds(), st, sa);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -797,10 +805,10 @@ int ecamd_frame_encode(int backend, int k, int m, int hd, int checksum, const vo
         const bool dpp = dev_tune("frame_copy_dpp") != 0;
         if (cs.u == 1)
             hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<1, true> : frame_split_stream_kernel<1, false>), grid,
-                               block, 0, st, sa);
+                               block, copy_lds(), st, sa);
         else
             hipLaunchKernelGGL((dpp ? frame_split_stream_kernel<4, true> : frame_split_stream_kernel<4, false>), grid,
-                               block, 0, st, sa);
+                               block, copy_lds(), st, sa);
     } else
         hipLaunchKernelGGL(frame_split_kernel, dim3(grid_for(dev, ((bs + 15) / 16) * k * nstripes)),
                            dim3(256), 0, st, sa);
@@ -912,10 +920,10 @@ int ecamd_frame_decode(int backend, int k, int m, int hd, const int* missing, vo
         const bool dpp = dev_tune("frame_copy_dpp") != 0;
         if (cs.u == 1)
             hipLaunchKernelGGL((dpp ? frame_join_stream_kernel<1, true> : frame_join_stream_kernel<1, false>), grid,
-                               block, 0, static_cast<hipStream_t>(stream), ja, k, align);
+                               block, copy_lds(), static_cast<hipStream_t>(stream), ja, k, align);
         else
             hipLaunchKernelGGL((dpp ? frame_join_stream_kernel<4, true> : frame_join_stream_kernel<4, false>), grid,
-                               block, 0, static_cast<hipStream_t>(stream), ja, k, align);
+                               block, copy_lds(), static_cast<hipStream_t>(stream), ja, k, align);
     } else
         hipLaunchKernelGGL(frame_join_kernel,
                            dim3(grid_for(dev, ((static_cast<int64_t>(obj_size) + 15) / 16) * nstripes)),

@@ -104,6 +104,7 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
             # the default build ((2, 2) + barrier) at 6 / 7 / 8 resident workgroups per CU, per pattern
             "c3cap3": {"cap6": {"bs_wave_per_cu": 6}, "cap7": {}, "cap8": {"bs_wave_per_cu": 8}},
             "c5ncap3": {"cap6": {"bs_wave_per_cu": 6}, "cap7": {}, "cap8": {"bs_wave_per_cu": 8}},
+            "c3pf5": {"pf0": {}, "pf2": {"bs_plain_prefetch": 2}, "pf4": {"bs_plain_prefetch": 4}},
             "c5tt": {"t256": {}, "t128": {"bs_tile_threads": 128}, "t512": {"bs_tile_threads": 512}},
             "c5tile": {"cap0": {"bs_tile_per_cu": 0}, "cap1": {"bs_tile_per_cu": 1}},
             "c5nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
@@ -115,7 +116,7 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
                        "w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2}},
             "c2n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}}}
-DEFAULTS = {"bs_tile_threads": 256, "wgs_per_cu": 0, "bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
+DEFAULTS = {"bs_plain_prefetch": 0, "bs_tile_threads": 256, "wgs_per_cu": 0, "bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
             "bs_narrow_min_k": -1, "bs_wave_depth": 0, "bs_wave_wmin": 0, "bs_wave_wmax": 0, "bs_wave_barrier": -1}
 
 
@@ -135,7 +136,7 @@ def apply(d, knobs):
 def run(cfg, rounds=3, n=30, skip=10):
     K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
                        "c2n": C2, "c3occ": C3, "c3occ2": C3, "c5nocc": C5N, "c3nocc": C3N,
-                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N}[cfg]
+                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N, "c3pf5": C3}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)

@@ -5,7 +5,6 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "gpurun_out/r05_$name.log" 2>&1; local rc=$?; tail -2 "gpurun_out/r05_$name.log" | cut -c1-600; [ $rc -eq 0 ] || { echo "STEP $name FAILED rc=$rc"; exit 1; }; }
-step gpu_tests 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 300 python3 bench.py
+step ab_pf5 600 python -u tools/bs_wave_ab.py c3pf5
+grep summary gpurun_out/r05_ab_pf5.log
 echo ALL_OK
