@@ -109,21 +109,34 @@ int64_t chunk_target()
 // blocking, while 4-16 MiB objects gained 15% with it (tools/latency_ab.py,
 // profiles/r03_latency_ab2.log).
 constexpr int64_t kSpinMinBytes = 64 << 10;
-// off by default: the kernel's own PCIe reads / writes cost MORE than the two DMAs at small sizes
-// (4 KiB RS(10,4) encode 35.5 -> 45.5 us, one thread, tools/latency_bench.py,
-// profiles/r05_lat_zc0.log, r05_lat_zc256.log); 256 KiB - 1 MiB gain 5-14% (r05_lat_zc4096.log)
-constexpr long kZeroCopyKibDefault = 0;
+// Default: one-chunk calls (up to 8 MiB of fragments) let the kernel write its outputs straight into the
+// pinned slab (mode 2), saving the D2H DMA and its queue round trip; the inputs still arrive by DMA -- a
+// kernel READING pinned host memory over PCIe costs more than the DMA (mode 1 / 3: 4 KiB RS(10,4) encode
+// 36.9 -> 49.1 us).  One thread, RS(10,4), two interleaved passes (tools/latency_bench.py,
+// profiles/r05_lat_m{0,1,2,3}{a,b}.log): encode 4 KiB 36.9 -> 35.0 us, 64 KiB 69.7 -> 62.8, 256 KiB
+// 82.7 -> 74.5, 1 MiB 135 -> 126; with CRC32 64 KiB 100.6 -> 79, 256 KiB 122 -> 101.
+constexpr long kZeroCopyKibDefault = 8192;
+constexpr int kZeroCopyModeDefault = 2;
 
 // ECAMD_PERCALL_ZEROCOPY_KIB: a call whose fragments fit one chunk of at most this many KiB (all
-// fragments) skips both DMAs -- the kernel reads its inputs from, and writes its outputs to, the pinned
-// slab itself over PCIe (hipHostMalloc memory is device-accessible and coherent), so the call costs
-// one launch and one wait instead of three queued operations ("Small objects").
+// fragments) lets the kernel work on the pinned slab itself over PCIe (hipHostMalloc memory is
+// device-accessible and coherent) instead of a DMA: its outputs (ECAMD_PERCALL_ZEROCOPY_MODE bit 1,
+// default) and / or its inputs (bit 0) -- one queued operation fewer per direction.
 int64_t zerocopy_bytes()
 {
     static const int64_t v = [] {
         const char* env = std::getenv("ECAMD_PERCALL_ZEROCOPY_KIB");
         const long kib = env ? std::atol(env) : kZeroCopyKibDefault;
         return static_cast<int64_t>(std::max(0L, kib)) << 10;
+    }();
+    return v;
+}
+
+int zerocopy_mode()
+{
+    static const int v = [] {
+        const char* env = std::getenv("ECAMD_PERCALL_ZEROCOPY_MODE");
+        return env ? std::atoi(env) & 3 : kZeroCopyModeDefault;
     }();
     return v;
 }
@@ -301,7 +314,8 @@ void release(Staging* st)
 }
 
 // Kernel launcher for one chunk: inputs at d + j*pitch, outputs at d + (K+r)*pitch.
-using Launch = int (*)(const void* ctx, char* d, int64_t pitch, int64_t bytes, void* stream);
+// Inputs at din + j*pitch, outputs at dout + (K+r)*pitch.
+using Launch = int (*)(const void* ctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream);
 
 int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, int64_t bs,
                 const void* ctx, Launch launch)
@@ -322,6 +336,8 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     std::vector<uint32_t> crc(want_crc ? nfr : 0, 0u);
     const int64_t nchunks = (bs + chunk - 1) / chunk;
     const bool zero_copy = nchunks == 1 && chunk * nfr <= zerocopy_bytes();
+    // which side works on the pinned slab itself (ECAMD_PERCALL_ZEROCOPY_MODE, bit 0 inputs, bit 1 outputs)
+    const bool zc_in = zero_copy && (zerocopy_mode() & 1), zc_out = zero_copy && (zerocopy_mode() & 2);
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
     std::vector<void*> cdst(static_cast<size_t>(nfr));
     std::vector<const void*> csrc(static_cast<size_t>(nfr));
@@ -387,18 +403,21 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         // One DMA each way per chunk (the slabs are [K inputs | R outputs] x chunk, contiguous):
         // for small fragments the per-call cost is API latency, not bytes.  A short last chunk
         // also moves the stale tail of each slot, which the kernel and the unpack never read.
-        // zero_copy: the kernels work on the pinned slab itself (no DMA either way)
-        char* const work = zero_copy ? sl.h_pin : sl.d_buf;
-        if (!zero_copy) rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
-        if (rc == 0) rc = launch(ctx, work, chunk, n, sl.stream);
-        if (rc == 0 && !zero_copy)
+        // zero copy: the kernel reads its inputs from / writes its outputs to the pinned slab itself
+        char* const win = zc_in ? sl.h_pin : sl.d_buf;
+        char* const work = zc_out ? sl.h_pin : sl.d_buf;  // outputs (and the CRC pass)
+        if (!zc_in) rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
+        if (rc == 0) rc = launch(ctx, win, work, chunk, n, sl.stream);
+        if (rc == 0 && want_crc && zc_in && !zc_out)  // the CRC pass reads every fragment from the device slab
+            rc = ecamd_memcpy_async(work, win, K * chunk, 0, sl.stream);
+        if (rc == 0 && !zc_out)
             rc = ecamd_memcpy_async(sl.h_pin + K * chunk, sl.d_buf + K * chunk,
                                     (R - 1) * chunk + n, 1, sl.stream);
         if (rc == 0 && want_crc) {
             auto* d_crc = reinterpret_cast<uint32_t*>(work + crc_off);
             rc = ecamd_crc32(t_crc.legacy ? 1 : 0, work, 0, chunk, static_cast<int>(nfr), n,
                              1, d_crc, sl.stream);
-            if (rc == 0 && !zero_copy)
+            if (rc == 0 && !zc_out)
                 rc = ecamd_memcpy_async(sl.h_pin + crc_off, d_crc, nfr * 4, 1, sl.stream);
         }
         pending[s] = c;
@@ -420,13 +439,13 @@ struct MapCtx {
     int K, R;
 };
 
-int launch_map(const void* vctx, char* d, int64_t pitch, int64_t bytes, void* stream)
+int launch_map(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream)
 {
     const MapCtx* c = static_cast<const MapCtx*>(vctx);
     std::vector<int64_t> io(c->K), oo(c->R);
     for (int j = 0; j < c->K; j++) io[j] = j * pitch;
     for (int r = 0; r < c->R; r++) oo[r] = (c->K + r) * pitch;
-    return ecamd_map_apply_strided(c->map, d, 0, io.data(), d, 0, oo.data(), bytes, 1, stream);
+    return ecamd_map_apply_strided(c->map, din, 0, io.data(), dout, 0, oo.data(), bytes, 1, stream);
 }
 
 struct XorCtx {
@@ -434,13 +453,13 @@ struct XorCtx {
     int K, R;
 };
 
-int launch_xor(const void* vctx, char* d, int64_t pitch, int64_t bytes, void* stream)
+int launch_xor(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream)
 {
     const XorCtx* c = static_cast<const XorCtx*>(vctx);
     std::vector<int64_t> io(c->K), oo(c->R);
     for (int j = 0; j < c->K; j++) io[j] = j * pitch;
     for (int r = 0; r < c->R; r++) oo[r] = (c->K + r) * pitch;
-    return ecamd_xor_apply_strided(c->masks.data(), c->R, c->K, d, 0, io.data(), d, 0, oo.data(),
+    return ecamd_xor_apply_strided(c->masks.data(), c->R, c->K, din, 0, io.data(), dout, 0, oo.data(),
                                    bytes, 1, stream);
 }
 
