@@ -254,6 +254,10 @@ int ecamd_fill_splitmix(void *base, int64_t stripe_stride, int64_t frag_stride, 
 
 /* ---- device memory helpers for C / ctypes callers ---- */
 int ecamd_malloc(void **d_ptr, int64_t bytes);
+/* Device memory the host may also write directly (the same address, through the PCIe BAR), uncached on the
+ * GPU side; ECAMD_EINVAL where the platform does not map device memory for the host.  The per-call path
+ * packs small calls' inputs there instead of staging them through a DMA. */
+int ecamd_malloc_host_writable(void **d_ptr, int64_t bytes);
 int ecamd_free(void *d_ptr);
 int ecamd_memcpy_h2d(void *d_dst, const void *h_src, int64_t bytes);
 int ecamd_memcpy_d2h(void *h_dst, const void *d_src, int64_t bytes);

@@ -2731,6 +2731,24 @@ int ecamd_malloc(void** d_ptr, int64_t bytes)
     return 0;
 }
 
+int ecamd_malloc_host_writable(void** d_ptr, int64_t bytes)
+{
+    int rc = ensure_device(nullptr);
+    if (rc) return rc;
+    if (!d_ptr || bytes <= 0) return fail(ECAMD_EINVAL, "bad host-writable allocation");
+    void* p = nullptr;
+    // uncached on the GPU side: the kernel always sees what the host wrote last, no stale cache lines
+    HIP_TRY(hipExtMallocWithFlags(&p, static_cast<size_t>(bytes), hipDeviceMallocUncached));
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess || attr.hostPointer != p) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        return fail(ECAMD_EINVAL, "device memory is not host-accessible here (no large BAR)");
+    }
+    *d_ptr = p;
+    return 0;
+}
+
 int ecamd_free(void* d_ptr)
 {
     HIP_TRY(hipFree(d_ptr));

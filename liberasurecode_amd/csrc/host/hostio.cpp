@@ -117,6 +117,10 @@ constexpr int64_t kSpinMinBytes = 64 << 10;
 // 82.7 -> 74.5, 1 MiB 135 -> 126; with CRC32 64 KiB 100.6 -> 79, 256 KiB 122 -> 101.
 constexpr long kZeroCopyKibDefault = 8192;
 constexpr int kZeroCopyModeDefault = 2;
+// off by default: measured neutral (4 KiB encode 33.6-34.5 -> 33.2-33.4 us, 16 KiB 43.3 -> 42.2 us; the
+// DMA is queued ahead of the launch and overlaps it -- the floor is the launch and its completion;
+// profiles/r05_lat3_{def,bar}{a,b}.log)
+constexpr long kBarKibDefault = 0;
 
 // ECAMD_PERCALL_ZEROCOPY_KIB: a call whose fragments fit one chunk of at most this many KiB (all
 // fragments) lets the kernel work on the pinned slab itself over PCIe (hipHostMalloc memory is
@@ -140,6 +144,23 @@ int zerocopy_mode()
     }();
     return v;
 }
+
+// ECAMD_PERCALL_BAR_KIB: a one-chunk call whose inputs are at most this many KiB packs them straight
+// into host-writable device memory (ecamd_malloc_host_writable: the PCIe BAR, no DMA) -- a 4 KiB
+// hipMemcpyAsync + wait costs ~13.5 us, the host's own 4 KiB write through the BAR ~0.7 us
+// (tools/bar_probe.py) -- while the kernel writes its outputs into the pinned slab (zero copy, mode
+// bit 1): the call is then one launch and one wait.  0 = off; platforms without a large BAR fall
+// back to the DMA by themselves.
+int64_t bar_bytes()
+{
+    static const int64_t v = [] {
+        const char* env = std::getenv("ECAMD_PERCALL_BAR_KIB");
+        const long kib = env ? std::atol(env) : kBarKibDefault;
+        return static_cast<int64_t>(std::max(0L, kib)) << 10;
+    }();
+    return v;
+}
+std::atomic<int> g_bar_ok{1};  // 0 once an allocation found no host-visible device memory
 
 int spin_us()
 {
@@ -191,6 +212,7 @@ struct Slot {
     void* event = nullptr;
     char* h_pin = nullptr;
     char* d_buf = nullptr;
+    char* d_bar = nullptr;  // host-writable device memory for small calls' inputs (bar_bytes())
 };
 
 struct Staging {
@@ -202,9 +224,24 @@ struct Staging {
         for (auto& s : slot) {
             if (s.h_pin) ecamd_host_free(s.h_pin);
             if (s.d_buf) ecamd_free(s.d_buf);
+            if (s.d_bar) ecamd_free(s.d_bar);
         }
     }
 };
+
+// The slot's host-writable input slab (kBarSlabBytes), allocated on first use; null when unavailable.
+constexpr int64_t kBarSlabBytes = 1 << 20;
+char* bar_slab(Slot& s)
+{
+    if (!s.d_bar && g_bar_ok.load(std::memory_order_relaxed)) {
+        void* p = nullptr;
+        if (ecamd_malloc_host_writable(&p, kBarSlabBytes) == 0)
+            s.d_bar = static_cast<char*>(p);
+        else
+            g_bar_ok.store(0, std::memory_order_relaxed);
+    }
+    return s.d_bar;
+}
 
 // One pool of staging contexts per device; calls go round-robin over the planned devices
 // (ecamd_percall_device_plan), so concurrent callers on an 8-GPU node use 8 PCIe links.
@@ -338,6 +375,8 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     const bool zero_copy = nchunks == 1 && chunk * nfr <= zerocopy_bytes();
     // which side works on the pinned slab itself (ECAMD_PERCALL_ZEROCOPY_MODE, bit 0 inputs, bit 1 outputs)
     const bool zc_in = zero_copy && (zerocopy_mode() & 1), zc_out = zero_copy && (zerocopy_mode() & 2);
+    // inputs packed straight into host-writable device memory (no H2D DMA), outputs into the pinned slab
+    const bool bar = zc_out && !zc_in && !want_crc && nchunks == 1 && K * chunk <= std::min(bar_bytes(), kBarSlabBytes);
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
     std::vector<void*> cdst(static_cast<size_t>(nfr));
     std::vector<const void*> csrc(static_cast<size_t>(nfr));
@@ -370,9 +409,12 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         if ((rc = drain(s))) break;
         const int64_t off = c * chunk;
         const int64_t n = std::min(chunk, bs - off);
+        // the pack's destination: the pinned slab, or (small calls) host-writable device memory
+        char* const bar_in = bar ? bar_slab(sl) : nullptr;
+        char* const pack = bar_in ? bar_in : sl.h_pin;
         if (t_tee.empty()) {
             for (int j = 0; j < K; j++) {
-                cdst[j] = sl.h_pin + j * chunk;
+                cdst[j] = pack + j * chunk;
                 csrc[j] = in[j] + off;
                 clen[j] = n;
             }
@@ -389,7 +431,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
                 plen.push_back(len);
             };
             for (int j = 0; j < K; j++) {
-                char* d = sl.h_pin + j * chunk;
+                char* d = pack + j * chunk;
                 Tee* te = find_tee(in[j]);
                 const int64_t a = te && off < te->len ? std::min(n, te->len - off) : 0;
                 if (a > 0) {
@@ -404,9 +446,12 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         // for small fragments the per-call cost is API latency, not bytes.  A short last chunk
         // also moves the stale tail of each slot, which the kernel and the unpack never read.
         // zero copy: the kernel reads its inputs from / writes its outputs to the pinned slab itself
-        char* const win = zc_in ? sl.h_pin : sl.d_buf;
+        char* const win = bar_in ? bar_in : zc_in ? sl.h_pin : sl.d_buf;
         char* const work = zc_out ? sl.h_pin : sl.d_buf;  // outputs (and the CRC pass)
-        if (!zc_in) rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
+        if (bar_in)  // the host's writes through the BAR reach the device before the launch's doorbell
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+        else if (!zc_in)
+            rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
         if (rc == 0) rc = launch(ctx, win, work, chunk, n, sl.stream);
         if (rc == 0 && want_crc && zc_in && !zc_out)  // the CRC pass reads every fragment from the device slab
             rc = ecamd_memcpy_async(work, win, K * chunk, 0, sl.stream);
