@@ -935,3 +935,46 @@ def test_stream_contexts_bounded(F):
             s.handle = None
         peak = max(peak, d.ecamd_stream_contexts())
     assert peak <= 17, peak  # the cap (16) + the context being created
+
+
+def test_stream_contexts_threaded(F):
+    """Stream contexts under concurrency: 8 threads, each creating a stream per request, running a Swift-shaped
+    framed encode (side-stream fork, CRC32 scratch on every third request) into its own fragments, checking the
+    bytes and destroying the stream -- contexts are created, evicted and released while other threads' calls are
+    in flight (busy contexts are never released).  The count stays bounded."""
+    import threading
+    from liberasurecode_amd import _lib
+    from liberasurecode_amd.device import Stream
+    d = _lib.dev()
+    be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
+    k, m, size = 10, 4, 1 << 20
+    objs = _objects(1, size, 777)
+    want = {ct: expected_stripe(be, k, m, 0, objs[0], ct) for ct in (ec_api.CHKSUM_NONE, ec_api.CHKSUM_CRC32)}
+    errors, peak = [], [0]
+    lock = threading.Lock()
+
+    def worker(tid):
+        try:
+            fbs = {ct: F.FrameBatch(be, k, m, size, 1, checksum=ct) for ct in want}
+            d_obj = _upload_objects(objs, fbs[ec_api.CHKSUM_NONE].obj_stride)
+            for i in range(40):
+                ct = ec_api.CHKSUM_CRC32 if (i + tid) % 3 == 0 else ec_api.CHKSUM_NONE
+                s = Stream()
+                fbs[ct].encode(d_obj, stream=s)
+                s.synchronize()
+                got = fbs[ct].fragments()
+                if not all(got[0, f].tobytes() == want[ct][f] for f in range(k + m)):
+                    errors.append((tid, i, ct))
+                s.destroy()
+                with lock:
+                    peak[0] = max(peak[0], d.ecamd_stream_contexts())
+        except Exception as e:  # noqa: BLE001
+            errors.append((tid, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:5]
+    assert peak[0] <= 16 + 8, peak[0]
