@@ -105,6 +105,10 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
             "c3cap3": {"cap6": {"bs_wave_per_cu": 6}, "cap7": {}, "cap8": {"bs_wave_per_cu": 8}},
             "c5ncap3": {"cap6": {"bs_wave_per_cu": 6}, "cap7": {}, "cap8": {"bs_wave_per_cu": 8}},
             "c3pf5": {"pf0": {}, "pf2": {"bs_plain_prefetch": 2}, "pf4": {"bs_plain_prefetch": 4}},
+            # robustness of the cap across batch sizes and fragment sizes
+            "c3s64": {"cap7": {}, "cap8": {"bs_wave_per_cu": 8}, "cap6": {"bs_wave_per_cu": 6}},
+            "c3s1024": {"cap7": {}, "cap8": {"bs_wave_per_cu": 8}, "cap6": {"bs_wave_per_cu": 6}},
+            "c3f256k": {"cap7": {}, "cap8": {"bs_wave_per_cu": 8}, "cap6": {"bs_wave_per_cu": 6}},
             "c5tt": {"t256": {}, "t128": {"bs_tile_threads": 128}, "t512": {"bs_tile_threads": 512}},
             "c5tile": {"cap0": {"bs_tile_per_cu": 0}, "cap1": {"bs_tile_per_cu": 1}},
             "c5nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
@@ -136,7 +140,9 @@ def apply(d, knobs):
 def run(cfg, rounds=3, n=30, skip=10):
     K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
                        "c2n": C2, "c3occ": C3, "c3occ2": C3, "c5nocc": C5N, "c3nocc": C3N,
-                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N, "c3pf5": C3}[cfg]
+                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N, "c3pf5": C3,
+                       "c3s64": (10, 4, 1 << 20, 64, C3[4]), "c3s1024": (10, 4, 1 << 20, 1024, C3[4]),
+                       "c3f256k": (10, 4, 256 << 10, 1024, C3[4])}[cfg]
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)
     lay = D.Layout.alloc(K + M, F, S)

@@ -5,5 +5,6 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "gpurun_out/r05_$name.log" 2>&1; local rc=$?; tail -1 "gpurun_out/r05_$name.log" | cut -c1-300; [ $rc -eq 0 ] || { echo "STEP $name FAILED rc=$rc"; tail -30 "gpurun_out/r05_$name.log"; exit 1; }; }
-step tests_ctx 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_frame.py -k "stream_contexts"
+step ab_capsize 900 python -u tools/bs_wave_ab.py c3s64 c3s1024 c3f256k
+grep summary gpurun_out/r05_ab_capsize.log
 echo ALL_OK
