@@ -379,6 +379,14 @@ struct Tuning {
     Knob xor_tiles_per_slot{32};  // xor_stream_kernel: the same for flat XOR passes (0: one launch;
                                   //   32 measured best with the 12-wave geometry, (3,3,3) C1 +2%,
                                   //   tools/xor_geom_sweep.py; 64 before)
+    // framed CRC32 encode on the crc variant in one-wave 4 KiB tiles (bitslice.cpp CW form): waves per
+    // workgroup (0: the 16 KiB-tile crc variant), position sets (1 / 2 / 4), tiles per wave, waves
+    // per SIMD of its register budget (0: 3)
+    Knob frame_crc_wave{0};
+    Knob frame_crc_wave_pos{2};
+    Knob frame_crc_wave_per{4};
+    Knob frame_crc_wave_wpe{0};
+    Knob frame_crc_wave_strict{0};  // tests: a framed CRC32 encode the one-wave crc form declines fails
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
                             //   peers (0), for every destination incl. local ones (1, exercises the
                             //   fork / join on one-GPU boxes), or none: all on the caller's stream (2)
@@ -428,6 +436,9 @@ int dev_tune(const char* key)
     if (k == "frame_crc_bs") return g_tune.frame_crc_bs;
     if (k == "frame_crc_cover") return g_tune.frame_crc_cover;
     if (k == "frame_crc_prefetch") return g_tune.frame_crc_prefetch;
+    if (k == "frame_crc_wave") return g_tune.frame_crc_wave;
+    if (k == "frame_crc_wave_pos") return g_tune.frame_crc_wave_pos;
+    if (k == "frame_crc_wave_strict") return g_tune.frame_crc_wave_strict;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "frame_tail_fork") return g_tune.frame_tail_fork;
     if (k == "frame_tail_tiles") return g_tune.frame_tail_tiles;
@@ -1816,9 +1827,13 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
 {
     const int mode = g_tune.bitslice;
     if (cover < 0) cover = bs;
-    // more than 4 outputs: the kernel folds every tile on its own (bitslice.cpp fold_each), q = tiles
-    if (!mode || m > kBsMaxR || k > kBsMaxK || cover % kBsTile || cover <= 0 || cover > bs || nstripes <= 0 ||
-        q <= 0 || (cover / kBsTile) % q || (m > 4 && q != cover / kBsTile))
+    // crc_pos & 32: one-wave 4 KiB tiles in workgroups of (crc_pos >> 6) waves, per-tile partials
+    // (tile-major, q unused); else more than 4 outputs fold every 16 KiB tile on its own
+    // (bitslice.cpp fold_each), q = tiles
+    const int cw = (crc_pos & 32) ? (crc_pos >> 6) & 15 : 0;
+    const int64_t tile = cw ? kBsTileWave : kBsTile;
+    if (!mode || m > kBsMaxR || k > kBsMaxK || cover % tile || cover <= 0 || cover > bs || nstripes <= 0 ||
+        (!cw && (q <= 0 || (cover / kBsTile) % q || (m > 4 && q != cover / kBsTile))) || (cw && m > 4))
         return ECAMD_EINVAL;
     // whole payloads: the object chunks j*bs are 16-byte aligned; partial cover (objects that do not
     // fill k 16 KiB-multiple payloads): the object side is read with unaligned loads
@@ -1848,8 +1863,14 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     // objects 1.544 vs 1.542, profiles/r04_cover_ab2.log) and its larger register need spills at
     // some shift patterns (C3 objects 10 bytes long), which then fall back to the codec + CRC pass
     const uint32_t in_records = a.in_records;
+    BsOcc occ{};
+    if (cw) {
+        occ.wmin = g_tune.frame_crc_wave_wpe > 0 ? static_cast<int>(g_tune.frame_crc_wave_wpe) : 3;
+        occ.wmax = occ.wmin;
+    }
     hipFunction_t fn = bitslice_function(device, coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
-                                         nullptr, m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0);
+                                         nullptr, m <= 4 && !cw ? static_cast<int>(g_tune.frame_crc_prefetch) : 0,
+                                         nullptr, cw ? &occ : nullptr);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -1858,7 +1879,7 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     b.out_stride = a.out_stride;
     b.in_records = in_records;
     b.out_records = a.out_records;
-    b.tiles_per_stripe = static_cast<uint32_t>(cover / kBsTile);
+    b.tiles_per_stripe = static_cast<uint32_t>(cover / tile);
     b.ntiles = b.tiles_per_stripe * static_cast<uint32_t>(nstripes);
     for (int j = 0; j < k; j++) {
         b.in_off[j] = a.in_off32[j];
@@ -1872,8 +1893,16 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     b.crc_img = d_img;
     b.crc_partial = d_partial;
     b.crc_q = q;
-    b.crc_per = static_cast<int32_t>(cover / kBsTile / q);
+    b.crc_per = cw ? 0 : static_cast<int32_t>(cover / kBsTile / q);
     b.crc_nfrag = k + m;
+    if (cw) {  // workgroup b's waves: tiles (b * per + i) * cw + wave, i < per
+        const int64_t per = g_tune.frame_crc_wave_per;
+        b.crc_q = 0;
+        b.crc_per = static_cast<int32_t>(per);
+        const int64_t grid = (static_cast<int64_t>(b.ntiles) + cw * per - 1) / (cw * per);
+        return bitslice_launch(fn, b, static_cast<int>(grid), static_cast<hipStream_t>(stream), hold, 64 * cw,
+                               cap_lds(fn, static_cast<int>(g_tune.frame_crc_per_cu)));
+    }
     const int64_t units = static_cast<int64_t>(nstripes) * q;
     // one work unit per workgroup by default: the dispatcher hands the next unit to whichever CU
     // frees a slot, which balances units better than a grid-stride loop over resident workgroups
@@ -2306,6 +2335,16 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {
         g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 32;
+    } else if (k == "frame_crc_wave") {
+        g_tune.frame_crc_wave = value < 0 ? 0 : std::min(value, 15);
+    } else if (k == "frame_crc_wave_pos") {
+        g_tune.frame_crc_wave_pos = value >= 4 ? 4 : value >= 2 ? 2 : 1;
+    } else if (k == "frame_crc_wave_per") {
+        g_tune.frame_crc_wave_per = std::max(1, std::min(value, 1 << 16));
+    } else if (k == "frame_crc_wave_strict") {
+        g_tune.frame_crc_wave_strict = value > 0 ? 1 : 0;
+    } else if (k == "frame_crc_wave_wpe") {
+        g_tune.frame_crc_wave_wpe = std::max(0, std::min(value, 8));
     } else if (k == "scatter_lanes") {
         g_tune.scatter_lanes = std::max(0, std::min(value, 2));
     } else {

@@ -228,6 +228,24 @@ __global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict_
     }
 }
 
+__global__ void crc_combine_kernel(const uint32_t* __restrict__ tiles, uint32_t* __restrict__ out,
+                                   const uint32_t* __restrict__ span, int64_t items, int nf, int tps, int g)
+{
+    const int q = tps / g;
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;  // item * q + r
+    if (i >= items * q) return;
+    const int64_t item = i / q;
+    const int r = static_cast<int>(i - item * q);
+    const int64_t s = item / nf;
+    const int f = static_cast<int>(item - s * nf);
+    const uint32_t* p = tiles + (s * tps + static_cast<int64_t>(r) * g) * nf + f;
+    uint32_t acc = 0;
+    for (int t = 0; t < g; ++t)
+        acc = span[acc & 0xff] ^ span[256 + ((acc >> 8) & 0xff)] ^ span[512 + ((acc >> 16) & 0xff)] ^
+              span[768 + (acc >> 24)] ^ p[static_cast<int64_t>(t) * nf];
+    out[i] = acc;
+}
+
 // prepare_fragments_for_encode: data payload j of stripe s = object bytes [j*bs, (j+1)*bs), zero
 // padded past the object's end (and through the 16-byte slack after the payload).
 __global__ void frame_split_kernel(const SplitArgs a)

@@ -90,6 +90,12 @@ __global__ void crc_partial_kernel(const CrcArgs a, const uint32_t* __restrict__
 __global__ void crc_finalize_kernel(const CrcArgs a, const uint32_t* __restrict__ img,
                                     const uint32_t* __restrict__ partial,
                                     uint32_t* __restrict__ crc_out, const HeaderArgs h);
+// The crc variant in one-wave tiles writes r0 of every fragment's 4 KiB tile, tile-major:
+// tiles[(s * tps + t) * nf + f].  Range r of g consecutive tiles of payload item = s * nf + f:
+// out[item * (tps / g) + r] = Horner over its tiles with A^4096 (span: its byte tables) -- the
+// layout crc_finalize_kernel reads.
+__global__ void crc_combine_kernel(const uint32_t* __restrict__ tiles, uint32_t* __restrict__ out,
+                                   const uint32_t* __restrict__ span, int64_t items, int nf, int tps, int g);
 __global__ void frame_split_kernel(const SplitArgs a);
 __global__ void frame_join_kernel(const JoinArgs a);
 // 32-bit-offset streaming forms (objects < 2 GiB, stripes < 2 GiB): tiles of 4 x 256 x 16 B

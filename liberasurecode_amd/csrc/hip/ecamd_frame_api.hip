@@ -430,6 +430,37 @@ int finalize_ranges(int dev, const Code& c, bool legacy, uint64_t obj_size, uint
     return 0;
 }
 
+// The crc variant in one-wave 4 KiB tiles (knob frame_crc_wave = its waves per workgroup, maps of up
+// to 4 outputs): its per-tile partials go to scratch slot 3, crc_combine_kernel folds them into q
+// ranges of g tiles per payload (g the largest divisor of the tile count up to 16) in `partial`, and
+// finalize_ranges takes those.  crc_wave_form: the crc_pos flags of the form (0: not this form).
+int crc_wave_form(const Code& c, int64_t cover)
+{
+    const int cw = dev_tune("frame_crc_wave");
+    if (cw <= 0 || c.m > 4 || cover <= 0 || cover % 4096) return 0;
+    return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6);
+}
+int crc_wave_groups(int64_t tps)
+{
+    int g = 1;
+    for (int d = 2; d <= 16; d++)
+        if (tps % d == 0) g = d;
+    return g;
+}
+int crc_wave_combine(int dev, bool legacy, const uint32_t* tiles, int64_t items, int nf, int64_t tps, int g,
+                     uint32_t* partial, void* stream)
+{
+    const DevImage* di = nullptr;
+    int rc = image(dev, legacy, 5, 4, 8, false, &di);  // span tables: A^4096
+    if (rc) return rc;
+    const int64_t n = items * (tps / g);
+    hipLaunchKernelGGL(crc_combine_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), tiles, partial, di->d + di->img.span_off, items, nf,
+                       static_cast<int>(tps), g);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 // The same framed encode on the bitsliced kernel's crc variant (no codec tables: the LDS serves
 // only the CRC lookups) for maps of up to 4 outputs over whole 16 KiB tiles.  ECAMD_EINVAL when it
 // does not apply or its kernel is still compiling (knob bitslice 1): the caller runs the LDS-table
@@ -438,7 +469,30 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
                          uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs,
                          int nstripes, void* stream)
 {
-    if (dev_tune("frame_crc_bs") == 0 || c.m > 8 || bs % 16384 || nstripes <= 0) return ECAMD_EINVAL;
+    if (dev_tune("frame_crc_bs") == 0 || c.m > 8 || nstripes <= 0) return ECAMD_EINVAL;
+    if (const int wf = crc_wave_form(c, bs)) {
+        const int nf = c.k + c.m;
+        const int64_t tps = bs / 4096;
+        const int g = crc_wave_groups(tps);
+        uint32_t *tiles = nullptr, *partial = nullptr;
+        int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * static_cast<size_t>(tps) * nf, &tiles, 3);
+        if (rc || (rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * static_cast<size_t>(tps / g),
+                                &partial)))
+            return rc;
+        const uint32_t* img = nullptr;
+        if ((rc = fused_image(dev, legacy, 4, &img, 1024, wf & 7, false))) return rc;
+        if ((rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
+                                        tiles, 0, stream, wf)))
+            return rc == ECAMD_EINVAL && dev_tune("frame_crc_wave_strict")
+                       ? dev_fail(ECAMD_EHIP, "framed encode: the one-wave crc form declined")
+                       : rc;
+        if ((rc = crc_wave_combine(dev, legacy, tiles, static_cast<int64_t>(nstripes) * nf, nf, tps, g, partial,
+                                   stream)))
+            return rc;
+        return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial,
+                               static_cast<int>(tps / g), stream);
+    }
+    if (bs % 16384) return ECAMD_EINVAL;
     // one 16 KiB tile per work unit at C3 (64 units per CU, one per workgroup): the dispatcher
     // balances them (32 / 16 per CU measured 3 / 6% slower, profiles/r03_fused_sweep_pos.log);
     // maps of 5-8 outputs fold every tile on its own (one range per tile)
@@ -530,35 +584,48 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
                      uint64_t obj_size, uint8_t* frags, int64_t ss, int64_t fs, int64_t bs, int nstripes,
                      void* stream)
 {
-    constexpr int64_t kTile = 16384;
     const bool xorc = c.backend == kBackendXor;
     if (dev_tune("frame_crc_cover") == 0 || dev_tune("frame_crc_bs") == 0 || dev_tune("frame_crc_fused") == 0 ||
         c.m > 8 || bs % 2 || nstripes <= 0 || (xorc && !copy_fits32(c.k, fs, bs, static_cast<int64_t>(obj_size))))
         return ECAMD_EINVAL;
     const int64_t last = static_cast<int64_t>(obj_size) - (c.k - 1) * bs;  // bytes of the last data chunk
-    const int64_t cover = std::min(bs, last) / kTile * kTile;
+    // the one-wave crc form covers whole 4 KiB tiles, the 16 KiB-tile crc variant whole 16 KiB tiles
+    const int wf = last > 0 ? crc_wave_form(c, std::min(bs, last) / 4096 * 4096) : 0;
+    const int64_t kTile = wf ? 4096 : 16384;
+    const int64_t cover = last > 0 ? std::min(bs, last) / kTile * kTile : 0;
     if (last <= 0 || cover < kTile) return ECAMD_EINVAL;
     const int64_t tail = bs - cover;
     const int nf = c.k + c.m;
-    const int q = c.m > 4 ? static_cast<int>(cover / kTile) : fused_ranges(dev, cover / kTile, nstripes, 64);
-    uint32_t *partial = nullptr, *tail_crc = nullptr;
+    const int64_t tps = cover / kTile;
+    const int g = wf ? crc_wave_groups(tps) : 1;
+    const int q = wf ? static_cast<int>(tps / g)
+                     : c.m > 4 ? static_cast<int>(tps) : fused_ranges(dev, tps, nstripes, 64);
+    uint32_t *partial = nullptr, *tail_crc = nullptr, *tiles = nullptr;
     int rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf * q, &partial, 1);
     if (rc) return rc;
     if (tail && (rc = scratch(dev, stream, static_cast<size_t>(nstripes) * nf, &tail_crc, 2))) return rc;
+    if (wf && (rc = scratch(dev, stream, static_cast<size_t>(nstripes) * static_cast<size_t>(tps) * nf, &tiles, 3)))
+        return rc;
     const uint32_t* img = nullptr;
     const bool lane = c.m > 4 || dev_tune("frame_crc_lane") != 0;
     int npos = dev_tune("frame_crc_pos");
     if (npos <= 0) npos = lane && c.m <= 4 ? 1 : 2;
     const bool nib = dev_tune("frame_crc_bs_nib") > 0;
-    if ((rc = fused_image(dev, legacy, 4, &img, 4096, npos, nib))) return rc;
+    if ((rc = wf ? fused_image(dev, legacy, 4, &img, 1024, wf & 7, false)
+                 : fused_image(dev, legacy, 4, &img, 4096, npos, nib)))
+        return rc;
     unsigned pb[32], db[32];
     if (xorc) ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db);
-    const int pos = npos | (lane ? 8 : 0) | (nib ? 16 : 0);
+    const int pos = wf ? wf : npos | (lane ? 8 : 0) | (nib ? 16 : 0);
+    uint32_t* out = wf ? tiles : partial;  // (one-wave form: per-tile partials, combined below)
     auto whole = [&] {  // the whole tiles [0, cover): codec + copy + CRC partials in one launch
-        return xorc ? xor_encode_copy_crc_bs(pb, c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes,
-                                             img, partial, q, stream, pos, cover)
-                    : rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
-                                            partial, q, stream, pos, cover);
+        const int r = xorc ? xor_encode_copy_crc_bs(pb, c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs,
+                                                    nstripes, img, out, q, stream, pos, cover)
+                           : rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes,
+                                                   img, out, q, stream, pos, cover);
+        return r == ECAMD_EINVAL && wf && dev_tune("frame_crc_wave_strict")
+                   ? dev_fail(ECAMD_EHIP, "framed encode: the one-wave crc form declined")
+                   : r;
     };
     // the payloads' rest [cover, bs): codec, then the CRC32 of that range on its own; `exact`: no byte
     // below cover is touched (the side stream runs it beside whole())
@@ -603,6 +670,9 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
         // from here on a failure is an error, not a fallback: part of the payloads is written
         if (tail && (rc = rest(stream, false))) return rc;
     }
+    if (wf && (rc = crc_wave_combine(dev, legacy, tiles, static_cast<int64_t>(nstripes) * nf, nf, tps, g, partial,
+                                     stream)))
+        return rc;
     return finalize_ranges(dev, c, legacy, obj_size, frags, ss, fs, bs, nstripes, partial, q, stream, cover,
                            tail_crc);
 }

@@ -283,7 +283,11 @@ const std::string& generator_fingerprint()
         lane.crc_lane = true;
         nib = lane;
         nib.crc_nib = true;
-        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave, wave_ring = wave, wave_occ = wave;
+        BitsliceStyle shifted = copy, crc_shifted = lane, wave_pf = wave, wave_ring = wave, wave_occ = wave,
+                      crc_wave = lane;
+        crc_wave.crc_wave = 6;
+        crc_wave.crc_pos = 2;
+        crc_wave.waves = 3;
         wave_occ.waves_max = 8;
         wave_occ.input_barrier = true;
         wave_pf.prefetch = 4;
@@ -293,7 +297,8 @@ const std::string& generator_fingerprint()
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
              bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + bitslice_source(tiny, 0, shifted) +
              bitslice_source(tiny, 0, crc_shifted) + bitslice_source(tiny5, 0, wave_pf) +
-             bitslice_source(tiny, 2, wave_ring) + bitslice_source(tiny, 0, wave_occ) + kBsNetworkVersion;
+             bitslice_source(tiny, 2, wave_ring) + bitslice_source(tiny, 0, wave_occ) +
+             bitslice_source(tiny, 0, crc_wave) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -315,9 +320,10 @@ void stop_children_at_exit()
 // of the request, the target and the generator: the same in the shipped and the per-user cache).
 std::string request_of(const BsEntry& e)
 {
+    const int cw = (e.crc & 32) ? (e.crc >> 6) & 15 : 0;
     return bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0, e.wave, &e.shifts,
-                            e.prefetch, e.wave || e.occ.threads ? &e.occ : nullptr);
+                            e.prefetch, e.wave || e.occ.threads || cw ? &e.occ : nullptr, cw);
 }
 std::string object_name(const BsEntry& e)
 {
@@ -433,16 +439,20 @@ std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& dep
                            bool& wave, const std::vector<int>* in_shift, int& prefetch, std::vector<int>& shifts,
                            BsOcc& occ)
 {
-    if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables
+    if (crc) {  // position sets 1 / 2 / 4, + 8 for the lane-shift fold, + 16 for nibble piece tables;
+        // + 32 for one-wave tiles (with the lane fold, byte tables) in workgroups of (crc >> 6) waves
         const int pos = crc & 7;
-        crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (crc & 24);
+        const int cw = (crc & 32) ? std::clamp((crc >> 6) & 15, 1, 15) : 0;
+        crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (cw ? 8 | 32 | (cw << 6) : crc & 24);
     }
     copy = copy || crc;
     wave = wave && !crc;
     depth = copy ? 0 : bitslice_depth(depth, K);  // one-wave tiles: the LDS ring only in plain maps
-    prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
+    prefetch = (wave || (crc && !(crc & 32))) && (prefetch == 2 || prefetch == 4) ? prefetch
                : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
-    if (!wave) {  // the multi-wave forms: only the plain register form's workgroup size
+    if (crc & 32) {  // the one-wave crc form keeps its occupancy (waves per SIMD, cap, barrier)
+        occ.threads = 0;
+    } else if (!wave) {  // the multi-wave forms: only the plain register form's workgroup size
         const int th = occ.threads;
         occ = BsOcc{};
         if (!copy && !crc && depth == 0 && (th == 128 || th == 512)) occ.threads = th;
@@ -653,10 +663,10 @@ int bitslice_launch(hipFunction_t fn, const BsArgs& args, int grid, hipStream_t 
 {
     BsArgs a = args;
     void* params[] = {&a};
+    // 64 / 128 / 256 / 512 lanes, or whole waves up to 1024 (the one-wave crc form's workgroups)
+    const bool ok = threads > 0 && threads <= 1024 && threads % 64 == 0;
     const hipError_t e = hipModuleLaunchKernel(fn, static_cast<unsigned>(grid), 1, 1,
-                                               static_cast<unsigned>(threads == 64 || threads == 128 || threads == 512
-                                                                         ? threads : 256),
-                                               1, 1, lds, st,
+                                               static_cast<unsigned>(ok ? threads : 256), 1, 1, lds, st,
                                                params, nullptr);
     if (e != hipSuccess)
         return dev_fail(ECAMD_EHIP, "hipModuleLaunchKernel(bitslice): %s", hipGetErrorString(e));

@@ -343,10 +343,12 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
       << (D ? "LDS ring of " + std::to_string(D) + " inputs per wave" : std::string("register loads")) << "\n";
     s << kPrelude;
     if (style.crc) s << kPreludeCrc;
-    const int wpe = (!style.crc && style.waves >= 1 && style.waves <= 8) ? style.waves
-                                                                        : bitslice_waves_per_simd(net.R, style.crc);
+    const int CW = style.crc ? std::clamp(style.crc_wave, 0, 16) : 0;  // one-wave crc form: waves per workgroup
+    const int wpe = ((!style.crc || CW) && style.waves >= 1 && style.waves <= 8) ? style.waves
+                                                                                : bitslice_waves_per_simd(net.R, style.crc);
     // one-wave tiles: the plain / copy-through register form, and the plain LDS-ring form
-    const int T = (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64
+    const int T = CW ? 64 * CW
+                  : (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64
                   : (!style.crc && !D && !style.copy_through && (style.threads == 128 || style.threads == 512))
                       ? style.threads
                       : 256;
@@ -441,6 +443,108 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "            }\n"
              "        }\n";
     };
+    if (CW) {
+        // crc variant in one-wave tiles: every wave of a workgroup streams 4 KiB tiles on its own -- lane
+        // l's 4 pieces of a fragment at l*16 + c*1024 -- and the workgroup shares one copy of the tables.
+        // Piece c goes through position set c % NP (r0 shifted by A^(1024 (NP - 1 - c % NP)) to the
+        // group's last chunk), so a fragment's 4 pieces take 4 / NP - 1 gap steps (A^(1024 NP)); the
+        // lane-shift tables move each lane's sum to the tile end, an XOR reduction over the wave gives r0
+        // of the fragment's 4 KiB, parked in lane f of `held`, and one store per tile writes the K + R
+        // values (crc_partial[t * (K + R) + f]).  Workgroup b's waves take tiles (b * crc_per + i) * CW +
+        // wave, i < crc_per: consecutive waves on neighbouring tiles, and no barrier after the table fill.
+        const int NS = net.K + net.R;
+        const int NP = style.crc_pos >= 4 ? 4 : style.crc_pos >= 2 ? 2 : 1;
+        const int words = bs_crc_words(NP) + kBsCrcLaneWords;
+        constexpr int CS1 = kBsCrcWaveStep;
+        auto crc1 = [&](int f, const char* x) {
+            s << "            {\n";
+            for (int c0 = 0; c0 < 4; c0 += NP) {
+                s << "                " << (c0 ? "cs = lmap4(gap, cs)" : "u32 cs = 0u");
+                for (int c = c0; c < c0 + NP; c++)
+                    s << " ^ piece_r0(ctab + " << (c % NP) * 4096 << ", " << x << c << "[0], " << x << c << "[1], " << x
+                      << c << "[2], " << x << c << "[3])";
+                s << ";\n";
+            }
+            s << "                cs = wave_xor(lane_shift(lanes, cs, lofs));\n"
+              << "                held = put_lane<" << f << ">(held, cs);\n"
+              << "            }\n";
+        };
+        s << "    __shared__ __attribute__((aligned(16))) u32 ctab[" << words << "];\n"
+          << "    for (int i = (int)threadIdx.x * 4; i < " << words << "; i += " << 4 * T
+          << ") *(v4u*)(ctab + i) = *(const v4u*)(a.crc_img + i);\n"
+             "    __syncthreads();\n"
+             "    const u32* gap = ctab + "
+          << NP * 4096
+          << ";\n"
+             "    const u32* lanes = ctab + "
+          << bs_crc_words(NP)
+          << ";\n"
+             "    const u32 lane = threadIdx.x & 63u;\n"
+             "    const u32 lofs = lane * 4u;\n"
+             "    const u32 wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
+             "    for (i32 i = 0; i < a.crc_per; i++) {\n"
+             "        const u32 t = (blockIdx.x * (u32)a.crc_per + (u32)i) * "
+          << CW
+          << "u + wv;\n"
+             "        if (t >= a.ntiles) break;\n"
+             "        const u32 s = t / a.tiles_per_stripe;\n"
+             "        const i32 off = (i32)(t - s * a.tiles_per_stripe) * "
+          << kBsTileWave
+          << " + (i32)lane * 16;\n"
+             "        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
+             "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n"
+             "        const __amdgpu_buffer_rsrc_t rcopy = __builtin_amdgcn_make_buffer_rsrc(\n"
+             "            (void*)(a.copy_base + (i64)s * a.copy_stride), 0, (int)a.copy_records, 0x00020000);\n";
+        for (int j = 0; j < net.K; j++)
+            s << "        const i32 cofs" << j << " = a.copy_idx[" << j << "] == 0xff ? (i32)0x80000000u : (i32)(a.copy_idx["
+              << j << "] * a.copy_step);\n";
+        acc_init();
+        s << "        u32 held = 0u;\n";
+        for (int j = 0; j < net.K; j++) {
+            s << "        {  // input " << j << "\n            u32 P[16];\n";
+            if (const int d = shift_of(j)) {  // aligned chunk + the neighbour's, realigned
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xa" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                      << "] - " << d << " + off + " << c * CS1 << ", 0, 2);\n";
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xh" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, l63 ? a.in_off[" << j
+                      << "] - " << d << " + off + " << c * CS1 + 16 << " : (i32)0x80000000u, 0, 2);\n";
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xq" << c << " = rlg<" << d << ">(xa" << c << ", xh" << c << ");\n";
+            } else {
+                for (int c = 0; c < 4; c++)
+                    s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                      << "] + off + " << c * CS1 << ", 0, 2);\n";
+            }
+            for (int c = 0; c < 4; c++)
+                s << "            __builtin_amdgcn_raw_buffer_store_b128(xq" << c << ", rcopy, cofs" << j << " + off + "
+                  << c * CS1 << ", 0, 2);  // copy-through\n";
+            crc1(j, "xq");
+            for (int c = 0; c < 4; c++)
+                s << "            P[" << 4 * c << "] = xq" << c << "[0]; P[" << 4 * c + 1 << "] = xq" << c << "[1]; P["
+                  << 4 * c + 2 << "] = xq" << c << "[2]; P[" << 4 * c + 3 << "] = xq" << c << "[3];\n";
+            s << "            __builtin_amdgcn_sched_barrier(0);\n";
+            network(j);
+            if (style.input_barrier) s << "            __builtin_amdgcn_sched_barrier(0);\n";
+            s << "        }\n";
+        }
+        for (int r = 0; r < net.R; r++) {
+            s << "        {  // output " << r << "\n            tr16(acc[" << r << "]);\n";
+            for (int c = 0; c < 4; c++)
+                s << "            const v4u vq" << c << " = {acc[" << r << "][" << 4 * c << "], acc[" << r << "][" << 4 * c + 1
+                  << "], acc[" << r << "][" << 4 * c + 2 << "], acc[" << r << "][" << 4 * c + 3 << "]};\n"
+                  << "            __builtin_amdgcn_raw_buffer_store_b128(vq" << c << ", rout, a.out_off[" << r << "] + off + "
+                  << c * CS1 << ", 0, 2);\n";
+            crc1(net.K + r, "vq");
+            s << "        }\n";
+        }
+        s << "        if (lane < " << NS << "u) a.crc_partial[(i64)t * " << NS << " + lane] = held;\n"
+             "    }\n"
+             "}\n";
+        return s.str();
+    }
     if (style.crc) {
         // Work unit u = (stripe, range of crc_per consecutive tiles).  Lane l's pieces of one fragment
         // sit at tile*16384 + c*4096 + l*16, c = 0..3: consecutive pieces are 4096 bytes apart across
@@ -869,7 +973,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
 
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy,
                              bool crc, int crc_pos, bool crc_lane, bool crc_nib, bool wave,
-                             const std::vector<int>* in_shift, int prefetch, const BsOcc* occ)
+                             const std::vector<int>* in_shift, int prefetch, const BsOcc* occ, int crc_wave)
 {
     std::ostringstream s;
     // flags: bit 0 copy-through, bit 1 crc (which copies too), bits 2-3 log2 of the crc position
@@ -879,7 +983,14 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // of exactly 128 does not -- the occupancy follows the registers actually used), bits 8-10 the
     // one-wave form's prefetch chunks (0, 2, 4; BitsliceStyle::prefetch); one-wave forms: bits 11-14
     // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused); plain maps in
-    // the multi-wave form, bits 20-21: lanes per workgroup (1 = 128, 2 = 512; 0 = 256)
+    // the multi-wave form, bits 20-21: lanes per workgroup (1 = 128, 2 = 512; 0 = 256); bit 22 the
+    // crc variant in one-wave tiles (with the lane fold; bits 11-19 its occupancy as for bit 6), bits
+    // 23-26 its waves per workgroup
+    const int cw = crc ? std::clamp(crc_wave, 0, 15) : 0;
+    if (cw) {  // (the one-wave crc form always folds with the lane tables, on byte piece tables)
+        crc_lane = true;
+        crc_nib = false;
+    }
     const int pcode = crc ? (crc_pos >= 4 ? 2 : crc_pos >= 2 ? 1 : 0) : 0;
     const BsOcc o = occ ? *occ : BsOcc{};
     const int tcode = !wave && !copy && !crc && depth == 0 ? (o.threads == 128 ? 1 : o.threads == 512 ? 2 : 0) : 0;
@@ -894,8 +1005,9 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
         s << "ecamd-bitslice-request " << (shifted ? 3 : 2) << "\n" << R << " " << K << " " << cap << " " << depth << " "
           << ((copy || crc ? 1 : 0) | (crc ? 2 : 0) | (pcode << 2) | (crc && crc_lane ? 16 : 0) |
               (crc && crc_nib ? 32 : 0) | (pf << 8) |
-              (!wave ? 0 : 64 | (std::clamp(o.wmin, 1, 8) << 11) | (std::clamp(o.wmax, o.wmin, 8) << 15) |
-                               (o.barrier ? 1 << 19 : 0)) | (tcode << 20))
+              (!wave && !cw ? 0 : (wave ? 64 : 0) | (std::clamp(o.wmin, 1, 8) << 11) |
+                                      (std::clamp(o.wmax, o.wmin, 8) << 15) | (o.barrier ? 1 << 19 : 0)) |
+              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) : 0))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -908,7 +1020,8 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
 
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy, bool* crc, int* crc_pos, bool* crc_lane, bool* crc_nib,
-                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch, BsOcc* occ)
+                            bool* wave, bool* budget2, std::vector<int>* in_shift, int* prefetch, BsOcc* occ,
+                            int* crc_wave)
 {
     std::istringstream s(text);
     std::string magic;
@@ -916,16 +1029,21 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 22) || (cp & 12) == 12))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 27) || (cp & 12) == 12))
         return false;
+    const int cw = (cp >> 22) & 1 ? (cp >> 23) & 15 : 0;  // one-wave crc form: waves per workgroup
+    if (((cp >> 22) & 1) ? (!cw || (cp & (1 | 2 | 16 | 32)) != (1 | 2 | 16)) : (cp >> 23) != 0)
+        return false;
+    if (crc_wave) *crc_wave = cw;
     const int tcode = (cp >> 20) & 3;  // lanes per workgroup of the multi-wave plain form
     if (tcode == 3 || (tcode && ((cp & (1 | 2 | 64)) || depth != 0))) return false;
     const int wmin = (cp >> 11) & 15, wmax = (cp >> 15) & 15;  // one-wave occupancy (0: bit 7 / by R)
     if (wmin > 8 || wmax > 8 || (wmax && wmax < wmin) ||
-        ((wmin || wmax || ((cp >> 19) & 1)) && (!(cp & 64) || (cp & 128))))
+        ((wmin || wmax || ((cp >> 19) & 1)) && ((!(cp & 64) && !cw) || (cp & 128))))
         return false;
-    if (version >= 2 && depth != 0 && ((cp & ~(128 | (511 << 11))) != 64 || (depth != 2 && depth != 4)))
+    if (version >= 2 && depth != 0 && ((cp & ~(128 | (511 << 11))) != 64 || (depth != 2 && depth != 4) || cw))
         return false;  // copy / crc: register loads; plain one-wave tiles: registers or an LDS ring
+    if (tcode && cw) return false;
     if (occ) {
         occ->wmin = wmin ? wmin : (cp & 128) ? 2 : 0;
         occ->wmax = wmax ? wmax : occ->wmin;

@@ -97,6 +97,11 @@ struct BitsliceStyle {
     // the CRC lookups: C5 framed CRC32 encode 1.380 -> 1.317 ms (profiles/r04_dppred_ab.log);
     // ECAMD_BS_DPPRED=0 in ecamd_jitc's environment restores the butterfly (A/B only)
     bool dpp_reduce = true;
+    // crc variant in one-wave 4 KiB tiles (round 5): 0 = off; W > 0 = workgroups of W waves sharing
+    // one copy of the tables (crc_pos position sets for pieces 1 KiB apart + the lane-shift tables);
+    // workgroup b's waves take tiles (b * crc_per + i) * W + wave, i < crc_per, each on its own (no
+    // barrier after the table fill), and write r0 of each fragment's 4 KiB to crc_partial[t * (K + R) + f]
+    int crc_wave = 0;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
@@ -104,6 +109,7 @@ struct BitsliceStyle {
 constexpr int bs_crc_words(int npos, bool nib = false) { return npos * (nib ? 512 : 4 * 1024) + 8 * 128; }
 constexpr int kBsCrcStep = 4096;  // bytes between a lane's consecutive pieces of one fragment
 constexpr int kBsCrcLaneWords = 8 * 16 * 64;  // lane-shift tables after bs_crc_words (fold-each form)
+constexpr int kBsCrcWaveStep = 1024;  // one-wave crc form: bytes between a lane's pieces of one fragment
 std::string bitslice_source(const BitsliceNet& net, int depth = 0, BitsliceStyle style = {});
 int bitslice_depth(int depth, int K);
 // Waves per SIMD the kernel of an R-output map is built for: 2 (16 R accumulators + the network
@@ -130,12 +136,12 @@ struct BsOcc {
 std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int cap, int depth, bool copy = false,
                              bool crc = false, int crc_pos = 1, bool crc_lane = false, bool crc_nib = false,
                              bool wave = false, const std::vector<int>* in_shift = nullptr, int prefetch = 0,
-                             const BsOcc* occ = nullptr);
+                             const BsOcc* occ = nullptr, int crc_wave = 0);
 bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, int& R, int& K, int& cap,
                             int& depth, bool* copy = nullptr, bool* crc = nullptr, int* crc_pos = nullptr,
                             bool* crc_lane = nullptr, bool* crc_nib = nullptr, bool* wave = nullptr,
                             bool* budget2 = nullptr, std::vector<int>* in_shift = nullptr,
-                            int* prefetch = nullptr, BsOcc* occ = nullptr);
+                            int* prefetch = nullptr, BsOcc* occ = nullptr, int* crc_wave = nullptr);
 
 // Kernel arguments (layout shared by the generated source and the launcher).
 constexpr int kBsTile = 16384;  // bytes of each fragment per workgroup tile (256 lanes x 64 B)

@@ -60,8 +60,9 @@ int main(int argc, char** argv)
     std::vector<int> shifts;
     int prefetch = 0;
     ecamd::BsOcc occ;
+    int crc_wave = 0;
     if (!ecamd::bitslice_parse_request(ss.str(), coeff, R, K, cap, depth, &copy, &crc, &crc_pos, &crc_lane,
-                                       &crc_nib, &wave, &budget2, &shifts, &prefetch, &occ)) {
+                                       &crc_nib, &wave, &budget2, &shifts, &prefetch, &occ, &crc_wave)) {
         std::fprintf(stderr, "ecamd_jitc: bad request %s\n", argv[1]);
         return 2;
     }
@@ -72,9 +73,10 @@ int main(int argc, char** argv)
     style.crc_lane = crc_lane;
     style.crc_nib = crc_nib;
     style.threads = wave ? 64 : occ.threads ? occ.threads : 256;
-    style.waves = wave ? occ.wmin : 0;  // one-wave forms: the request's occupancy (0: by R)
-    style.waves_max = wave ? occ.wmax : 0;
-    style.input_barrier = wave && occ.barrier;
+    style.crc_wave = crc_wave;
+    style.waves = wave || crc_wave ? occ.wmin : 0;  // one-wave forms: the request's occupancy (0: by R)
+    style.waves_max = wave || crc_wave ? occ.wmax : 0;
+    style.input_barrier = (wave || crc_wave) && occ.barrier;
     style.in_shift = shifts;
     style.prefetch = prefetch;
     if (const char* v = std::getenv("ECAMD_BS_WPE")) style.waves = std::atoi(v);  // experiment only

@@ -978,3 +978,45 @@ def test_stream_contexts_threaded(F):
         t.join()
     assert not errors, errors[:5]
     assert peak[0] <= 16 + 8, peak[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("be,k,m,size", [
+    ("rs", 10, 4, 10 << 20), ("rs", 10, 4, 10 * 104858 - 4), ("rs", 4, 2, 4 * 65536 + 6), ("rs", 3, 2, 3 * 4096 * 5),
+    ("rs", 6, 3, 6 * 16384 + 6 * 100), ("rs", 10, 4, 10 * (4096 + 16)), ("xor", 3, 3, 3 * 65536),
+    ("xor", 3, 3, 3 * 104858 - 4)])
+@pytest.mark.parametrize("form", [(6, 2, 4), (4, 1, 1), (12, 4, 3), (6, 2, 1)])
+@pytest.mark.parametrize("legacy", [False, True])
+def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypatch):
+    """CHKSUM_CRC32 framed encode on the crc variant in one-wave 4 KiB tiles (knobs frame_crc_wave =
+    waves per workgroup, frame_crc_wave_pos = position sets, frame_crc_wave_per = tiles per wave;
+    bitslice.cpp CW form, crc_combine_kernel) against the 16 KiB-tile crc variant / the codec + CRC
+    pass, and the restated reference framing for the last stripe.  frame_crc_wave_strict makes a
+    declined form an error, so the new kernel is the one that ran."""
+    from liberasurecode_amd import _lib
+    if legacy:
+        monkeypatch.setenv("LIBERASURECODE_WRITE_LEGACY_CRC", "1")
+    code = (ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND if be == "rs" else ec_api.EC_BACKEND_FLAT_XOR_HD)
+    hd = 3 if m == 3 else 4
+    S = 3
+    objs = _objects(S, size, k * 13 + m + size)
+    d = _lib.dev()
+    out = []
+    _lib.check(d.ecamd_tune(b"bitslice", 2), "tune")
+    try:
+        for w in (0, form[0]):
+            _lib.check(d.ecamd_tune(b"frame_crc_wave", w), "tune")
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_pos", form[1]), "tune")
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_per", form[2]), "tune")
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_strict", 1 if w else 0), "tune")
+            fb = F.FrameBatch(code, k, m, size, S, hd=hd)
+            fb.encode(_upload_objects(objs, fb.obj_stride))
+            out.append(fb.fragments())
+    finally:
+        for kn in (b"frame_crc_wave", b"frame_crc_wave_pos", b"frame_crc_wave_per", b"frame_crc_wave_strict"):
+            d.ecamd_tune(kn, -1 if kn != b"frame_crc_wave_per" else 4)
+        d.ecamd_tune(b"frame_crc_wave_pos", 2)
+        d.ecamd_tune(b"bitslice", 1)
+    assert np.array_equal(out[0], out[1])
+    want = expected_stripe(code, k, m, hd if be == "xor" else 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
+    assert all(out[1][S - 1, i].tobytes() == want[i] for i in range(k + m))
