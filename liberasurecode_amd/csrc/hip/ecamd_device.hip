@@ -198,6 +198,16 @@ constexpr int kFrameCrcBsDefault = 1;
 // profiles/r05_ab_ncap.log, r05_ab_narrow.log)
 constexpr int kBsNarrowMinKDefault = 8;
 
+// Defaults of the one-wave crc form's knobs (frame_crc_wave*).
+struct CrcWaveDefaults {
+    int w, pos, per, pf;
+};
+// 4 waves per workgroup, 2 position sets (68 KiB of LDS: 2 workgroups, 8 waves per CU), one tile per
+// wave, the next input's 4 chunks prefetched: against the 16 KiB-tile crc variant in the same runs
+// C3 0.687 -> 0.704, Swift segments 0.591 -> 0.638, C5 0.599 -> 0.674 (profiles/r05_ab_crcwave_c5b.log;
+// 12 waves per CU, 1 or 4 position sets and longer runs per wave all lose: r05_ab_crcwave_*.log)
+constexpr CrcWaveDefaults kCrcWave{4, 2, 1, 4};
+
 struct Tuning {
     Knob threads{0};     // threads per workgroup of the gf16 kernel
     Knob wgs_per_cu{0};  // resident workgroups per CU the grid is sized for
@@ -381,11 +391,12 @@ struct Tuning {
                                   //   tools/xor_geom_sweep.py; 64 before)
     // framed CRC32 encode on the crc variant in one-wave 4 KiB tiles (bitslice.cpp CW form): waves per
     // workgroup (0: the 16 KiB-tile crc variant), position sets (1 / 2 / 4), tiles per wave, waves
-    // per SIMD of its register budget (0: 3)
-    Knob frame_crc_wave{0};
-    Knob frame_crc_wave_pos{2};
-    Knob frame_crc_wave_per{4};
+    // per SIMD of its register budget (0: 3), chunks (0 / 2 / 4) of the next input loaded with each input's
+    Knob frame_crc_wave{kCrcWave.w};
+    Knob frame_crc_wave_pos{kCrcWave.pos};
+    Knob frame_crc_wave_per{kCrcWave.per};
     Knob frame_crc_wave_wpe{0};
+    Knob frame_crc_wave_pf{kCrcWave.pf};
     Knob frame_crc_wave_strict{0};  // tests: a framed CRC32 encode the one-wave crc form declines fails
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
                             //   peers (0), for every destination incl. local ones (1, exercises the
@@ -1833,7 +1844,7 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     const int cw = (crc_pos & 32) ? (crc_pos >> 6) & 15 : 0;
     const int64_t tile = cw ? kBsTileWave : kBsTile;
     if (!mode || m > kBsMaxR || k > kBsMaxK || cover % tile || cover <= 0 || cover > bs || nstripes <= 0 ||
-        (!cw && (q <= 0 || (cover / kBsTile) % q || (m > 4 && q != cover / kBsTile))) || (cw && m > 4))
+        (!cw && (q <= 0 || (cover / kBsTile) % q || (m > 4 && q != cover / kBsTile))))
         return ECAMD_EINVAL;
     // whole payloads: the object chunks j*bs are 16-byte aligned; partial cover (objects that do not
     // fill k 16 KiB-multiple payloads): the object side is read with unaligned loads
@@ -1865,11 +1876,13 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     const uint32_t in_records = a.in_records;
     BsOcc occ{};
     if (cw) {
-        occ.wmin = g_tune.frame_crc_wave_wpe > 0 ? static_cast<int>(g_tune.frame_crc_wave_wpe) : 3;
+        occ.wmin = g_tune.frame_crc_wave_wpe > 0 ? static_cast<int>(g_tune.frame_crc_wave_wpe) : m > 4 ? 2 : 3;
         occ.wmax = occ.wmin;
     }
     hipFunction_t fn = bitslice_function(device, coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
-                                         nullptr, m <= 4 && !cw ? static_cast<int>(g_tune.frame_crc_prefetch) : 0,
+                                         nullptr,
+                                         cw ? static_cast<int>(g_tune.frame_crc_wave_pf)
+                                            : m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0,
                                          nullptr, cw ? &occ : nullptr);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
@@ -2335,12 +2348,14 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 16;
     } else if (k == "xor_tiles_per_slot") {
         g_tune.xor_tiles_per_slot = value >= 0 && value <= (1 << 20) ? value : 32;
-    } else if (k == "frame_crc_wave") {
-        g_tune.frame_crc_wave = value < 0 ? 0 : std::min(value, 15);
+    } else if (k == "frame_crc_wave") {  // (negative: the defaults)
+        g_tune.frame_crc_wave = value < 0 ? kCrcWave.w : std::min(value, 15);
     } else if (k == "frame_crc_wave_pos") {
-        g_tune.frame_crc_wave_pos = value >= 4 ? 4 : value >= 2 ? 2 : 1;
+        g_tune.frame_crc_wave_pos = value <= 0 ? kCrcWave.pos : value >= 4 ? 4 : value >= 2 ? 2 : 1;
     } else if (k == "frame_crc_wave_per") {
-        g_tune.frame_crc_wave_per = std::max(1, std::min(value, 1 << 16));
+        g_tune.frame_crc_wave_per = value <= 0 ? kCrcWave.per : std::min(value, 1 << 16);
+    } else if (k == "frame_crc_wave_pf") {
+        g_tune.frame_crc_wave_pf = value < 0 ? kCrcWave.pf : value == 2 || value == 4 ? value : 0;
     } else if (k == "frame_crc_wave_strict") {
         g_tune.frame_crc_wave_strict = value > 0 ? 1 : 0;
     } else if (k == "frame_crc_wave_wpe") {

@@ -436,8 +436,9 @@ int finalize_ranges(int dev, const Code& c, bool legacy, uint64_t obj_size, uint
 // finalize_ranges takes those.  crc_wave_form: the crc_pos flags of the form (0: not this form).
 int crc_wave_form(const Code& c, int64_t cover)
 {
-    const int cw = dev_tune("frame_crc_wave");
-    if (cw <= 0 || c.m > 4 || cover <= 0 || cover % 4096) return 0;
+    int cw = dev_tune("frame_crc_wave");
+    if (cw <= 0 || cover <= 0 || cover % 4096) return 0;
+    if (c.m > 4) cw = std::min(cw, 8);  // (5-8 outputs: built for 2 waves per SIMD)
     return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6);
 }
 int crc_wave_groups(int64_t tps)

@@ -502,6 +502,19 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
               << j << "] * a.copy_step);\n";
         acc_init();
         s << "        u32 held = 0u;\n";
+        // prefetch (style.prefetch 2 / 4): the next unrealigned input's first PFc chunks are loaded with
+        // this input's, before its copy stores, CRC lookups and network
+        const int PFc = (style.prefetch == 2 || style.prefetch == 4) ? style.prefetch : 0;
+        auto cpre = [&](int j) { return PFc > 0 && j < net.K && shift_of(j) == 0; };
+        auto cload_next = [&](int j) {
+            for (int c = 0; c < PFc; c++)
+                s << "            xn[" << c << "] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j << "] + off + "
+                  << c * CS1 << ", 0, 2);\n";
+        };
+        if (PFc) {
+            s << "        v4u xn[" << PFc << "];\n";
+            if (cpre(0)) cload_next(0);
+        }
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
             if (const int d = shift_of(j)) {  // aligned chunk + the neighbour's, realigned
@@ -514,10 +527,18 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                 for (int c = 0; c < 4; c++)
                     s << "            const v4u xq" << c << " = rlg<" << d << ">(xa" << c << ", xh" << c << ");\n";
             } else {
-                for (int c = 0; c < 4; c++)
-                    s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
-                      << "] + off + " << c * CS1 << ", 0, 2);\n";
+                for (int c = 0; c < 4; c++) {
+                    if (cpre(j) && c < PFc)
+                        s << "            const v4u xq" << c << " = xn[" << c << "];\n";
+                    else
+                        s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                          << "] + off + " << c * CS1 << ", 0, 2);\n";
+                }
             }
+            if (cpre(j + 1)) cload_next(j + 1);
+            // the 4 loads leave together (without the barrier the compiler consumes the first two
+            // before issuing the rest, and each wait then also retires the previous copy stores)
+            s << "            __builtin_amdgcn_sched_barrier(0);\n";
             for (int c = 0; c < 4; c++)
                 s << "            __builtin_amdgcn_raw_buffer_store_b128(xq" << c << ", rcopy, cofs" << j << " + off + "
                   << c * CS1 << ", 0, 2);  // copy-through\n";

@@ -378,7 +378,7 @@ def test_percall_crc_handoff(F, bs, legacy):
                                       (8, 4, 64 * 8192, 2), (3, 2, 40 * 8192, 9), (12, 6, 16384, 4),
                                       (20, 8, 4 * 8192, 3)])
 @pytest.mark.parametrize("legacy", [False, True])
-@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4", "bsl", "bsn", "bsn4"])
+@pytest.mark.parametrize("mb", [1, 4, "nib", "nib1", "bs", "bs2", "bs4", "bsl", "bsn", "bsn4", "bsw"])
 def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkeypatch):
     """CHKSUM_CRC32 framed encode of objects that fill the payloads: the fused launch (codec +
     copy-through + payload checksums folded per range) against the copy-through encode + separate
@@ -391,9 +391,11 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
     objs = _objects(S, size, k * 7 + m + bs)
     out = []
     bsv = str(mb).startswith("bs")
-    # the bitsliced crc variant takes whole 16 KiB tiles (5-8 outputs: its fold-each form); other
+    # the bitsliced crc variant: bsw its one-wave form (the default, knob frame_crc_wave) over whole
+    # 4 KiB tiles, the other bs* the 16 KiB-tile form (frame_crc_wave 0) over whole 16 KiB tiles; other
     # payload sizes fall back to the LDS-table fused kernel or the copy-through encode + CRC pass
-    bs_fits = m <= 8 and bs % 16384 == 0
+    bs_fits = m <= 8 and bs % (4096 if mb == "bsw" else 16384) == 0
+    _lib.check(_lib.dev().ecamd_tune(b"frame_crc_wave", -1 if mb == "bsw" else 0), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_mb", {"nib": 4, "nib1": 1}.get(mb, 4 if bsv else mb)), "tune")
     _lib.check(_lib.dev().ecamd_tune(b"frame_crc_pos", {"bs2": 2, "bs4": 4, "bsl": 0, "bsn": 0, "bsn4": 4}.get(mb, 1)),
                "tune")
@@ -422,6 +424,7 @@ def test_frame_encode_fused_crc_matches_split(F, k, m, bs, S, legacy, mb, monkey
         _lib.dev().ecamd_tune(b"frame_crc_pos", -1)
         _lib.dev().ecamd_tune(b"frame_crc_lane", -1)
         _lib.dev().ecamd_tune(b"frame_crc_bs_nib", -1)
+        _lib.dev().ecamd_tune(b"frame_crc_wave", -1)
         _lib.dev().ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
     if bs <= (1 << 16):
@@ -452,9 +455,12 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         # payloads' rest by split + plain encode of their last tiles (default) or the LDS-table launch
         # (+ frame_tail_fork 2: the rest and its CRC32 on the side stream beside the crc variant;
         # + frame_tail_tiles 0: the rest's whole 4 KiB tiles by the split + re-encode too)
-        for cover, realign, tail, fork, tt in ((1, 1, 1, 1, 1), (0, 1, 1, 1, 1), (1, 0, 1, 1, 1), (1, 1, 0, 1, 1),
-                                               (1, 1, 1, 2, 1), (1, 1, 1, 1, 0)):
+        # + wave 0: the 16 KiB-tile crc variant instead of its one-wave form (knob frame_crc_wave)
+        for cover, realign, tail, fork, tt, wave in ((1, 1, 1, 1, 1, 1), (0, 1, 1, 1, 1, 1), (1, 0, 1, 1, 1, 1),
+                                                     (1, 1, 0, 1, 1, 1), (1, 1, 1, 2, 1, 1), (1, 1, 1, 1, 0, 1),
+                                                     (1, 1, 1, 1, 1, 0), (1, 0, 0, 2, 1, 0)):
             _lib.check(_lib.dev().ecamd_tune(b"frame_crc_cover", cover), "tune")
+            _lib.check(_lib.dev().ecamd_tune(b"frame_crc_wave", -1 if wave else 0), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_realign", realign), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_fork", fork), "tune")
@@ -465,7 +471,8 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
             out.append(fb.fragments())
             bs = fb.blocksize
             last = size - (k - 1) * bs
-            if cover and last >= 16384:
+            # (the one-wave crc form, knob frame_crc_wave, covers whole 4 KiB tiles)
+            if cover and last >= (4096 if wave else 16384):
                 assert _bs_launches() > n0, "the bitsliced crc variant did not run"
             elif cover:
                 assert _bs_launches() == n0, "a bitsliced kernel ran on a shape it does not take"
@@ -476,6 +483,7 @@ def test_frame_encode_cover_crc_matches(F, k, m, size, legacy, monkeypatch):
         _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
         _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
         _lib.dev().ecamd_tune(b"frame_tail_tiles", -1)
+        _lib.dev().ecamd_tune(b"frame_crc_wave", -1)
     assert all(np.array_equal(o, out[1]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
     assert all(out[0][S - 1, i].tobytes() == want[i] for i in range(k + m))
@@ -984,12 +992,13 @@ def test_stream_contexts_threaded(F):
 @pytest.mark.parametrize("be,k,m,size", [
     ("rs", 10, 4, 10 << 20), ("rs", 10, 4, 10 * 104858 - 4), ("rs", 4, 2, 4 * 65536 + 6), ("rs", 3, 2, 3 * 4096 * 5),
     ("rs", 6, 3, 6 * 16384 + 6 * 100), ("rs", 10, 4, 10 * (4096 + 16)), ("xor", 3, 3, 3 * 65536),
-    ("xor", 3, 3, 3 * 104858 - 4)])
-@pytest.mark.parametrize("form", [(6, 2, 4), (4, 1, 1), (12, 4, 3), (6, 2, 1)])
+    ("xor", 3, 3, 3 * 104858 - 4), ("rs", 20, 8, 20 * 40000), ("rs", 12, 6, 12 * 65536)])
+@pytest.mark.parametrize("form", [(6, 2, 4, 0), (4, 1, 1, 2), (12, 4, 3, 0), (6, 2, 1, 4)])
 @pytest.mark.parametrize("legacy", [False, True])
 def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypatch):
     """CHKSUM_CRC32 framed encode on the crc variant in one-wave 4 KiB tiles (knobs frame_crc_wave =
-    waves per workgroup, frame_crc_wave_pos = position sets, frame_crc_wave_per = tiles per wave;
+    waves per workgroup, frame_crc_wave_pos = position sets, frame_crc_wave_per = tiles per wave,
+    frame_crc_wave_pf = chunks of the next input prefetched;
     bitslice.cpp CW form, crc_combine_kernel) against the 16 KiB-tile crc variant / the codec + CRC
     pass, and the restated reference framing for the last stripe.  frame_crc_wave_strict makes a
     declined form an error, so the new kernel is the one that ran."""
@@ -1008,14 +1017,15 @@ def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypa
             _lib.check(d.ecamd_tune(b"frame_crc_wave", w), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_pos", form[1]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_per", form[2]), "tune")
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_pf", form[3]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_strict", 1 if w else 0), "tune")
             fb = F.FrameBatch(code, k, m, size, S, hd=hd)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
     finally:
-        for kn in (b"frame_crc_wave", b"frame_crc_wave_pos", b"frame_crc_wave_per", b"frame_crc_wave_strict"):
-            d.ecamd_tune(kn, -1 if kn != b"frame_crc_wave_per" else 4)
-        d.ecamd_tune(b"frame_crc_wave_pos", 2)
+        for kn in (b"frame_crc_wave", b"frame_crc_wave_pos", b"frame_crc_wave_per", b"frame_crc_wave_pf",
+                   b"frame_crc_wave_strict"):
+            d.ecamd_tune(kn, -1)
         d.ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
     want = expected_stripe(code, k, m, hd if be == "xor" else 0, objs[S - 1], ec_api.CHKSUM_CRC32, legacy=legacy)
