@@ -200,13 +200,13 @@ constexpr int kBsNarrowMinKDefault = 8;
 
 // Defaults of the one-wave crc form's knobs (frame_crc_wave*).
 struct CrcWaveDefaults {
-    int w, pos, per, pf;
+    int w, pos, per, pf, big;
 };
 // 4 waves per workgroup, 2 position sets (68 KiB of LDS: 2 workgroups, 8 waves per CU), one tile per
 // wave, the next input's 4 chunks prefetched: against the 16 KiB-tile crc variant in the same runs
 // C3 0.687 -> 0.704, Swift segments 0.591 -> 0.638, C5 0.599 -> 0.674 (profiles/r05_ab_crcwave_c5b.log;
 // 12 waves per CU, 1 or 4 position sets and longer runs per wave all lose: r05_ab_crcwave_*.log)
-constexpr CrcWaveDefaults kCrcWave{4, 2, 1, 4};
+constexpr CrcWaveDefaults kCrcWave{4, 2, 1, 4, 0};
 
 struct Tuning {
     Knob threads{0};     // threads per workgroup of the gf16 kernel
@@ -396,6 +396,7 @@ struct Tuning {
     Knob frame_crc_wave_pos{kCrcWave.pos};
     Knob frame_crc_wave_per{kCrcWave.per};
     Knob frame_crc_wave_wpe{0};
+    Knob frame_crc_wave_big{kCrcWave.big};  //   % of the tiles in runs of frame_crc_wave_per per wave
     Knob frame_crc_wave_pf{kCrcWave.pf};
     Knob frame_crc_wave_strict{0};  // tests: a framed CRC32 encode the one-wave crc form declines fails
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
@@ -1908,11 +1909,14 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     b.crc_q = q;
     b.crc_per = cw ? 0 : static_cast<int32_t>(cover / kBsTile / q);
     b.crc_nfrag = k + m;
-    if (cw) {  // workgroup b's waves: tiles (b * per + i) * cw + wave, i < per
-        const int64_t per = g_tune.frame_crc_wave_per;
-        b.crc_q = 0;
+    if (cw) {  // the first `big` workgroups: per tiles per wave, covering ~frame_crc_wave_big % of the
+        // tiles; the rest one tile per wave
+        const int64_t per = std::max<int64_t>(1, g_tune.frame_crc_wave_per);
+        const int64_t big = per > 1 ? static_cast<int64_t>(b.ntiles) * g_tune.frame_crc_wave_big / 100 / (cw * per) : 0;
+        b.crc_q = static_cast<int32_t>(big);
         b.crc_per = static_cast<int32_t>(per);
-        const int64_t grid = (static_cast<int64_t>(b.ntiles) + cw * per - 1) / (cw * per);
+        const int64_t rest = static_cast<int64_t>(b.ntiles) - big * per * cw;
+        const int64_t grid = big + (rest + cw - 1) / cw;
         return bitslice_launch(fn, b, static_cast<int>(grid), static_cast<hipStream_t>(stream), hold, 64 * cw,
                                cap_lds(fn, static_cast<int>(g_tune.frame_crc_per_cu)));
     }
@@ -2354,6 +2358,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_wave_pos = value <= 0 ? kCrcWave.pos : value >= 4 ? 4 : value >= 2 ? 2 : 1;
     } else if (k == "frame_crc_wave_per") {
         g_tune.frame_crc_wave_per = value <= 0 ? kCrcWave.per : std::min(value, 1 << 16);
+    } else if (k == "frame_crc_wave_big") {
+        g_tune.frame_crc_wave_big = value < 0 ? kCrcWave.big : std::min(value, 100);
     } else if (k == "frame_crc_wave_pf") {
         g_tune.frame_crc_wave_pf = value < 0 ? kCrcWave.pf : value == 2 || value == 4 ? value : 0;
     } else if (k == "frame_crc_wave_strict") {

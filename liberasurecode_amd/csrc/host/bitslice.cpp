@@ -450,8 +450,9 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         // group's last chunk), so a fragment's 4 pieces take 4 / NP - 1 gap steps (A^(1024 NP)); the
         // lane-shift tables move each lane's sum to the tile end, an XOR reduction over the wave gives r0
         // of the fragment's 4 KiB, parked in lane f of `held`, and one store per tile writes the K + R
-        // values (crc_partial[t * (K + R) + f]).  Workgroup b's waves take tiles (b * crc_per + i) * CW +
-        // wave, i < crc_per: consecutive waves on neighbouring tiles, and no barrier after the table fill.
+        // values (crc_partial[t * (K + R) + f]).  The first crc_q workgroups' waves take tiles (b * crc_per
+        // + i) * CW + wave, i < crc_per, the later ones one tile each (consecutive waves on neighbouring
+        // tiles); no barrier after the table fill.
         const int NS = net.K + net.R;
         const int NP = style.crc_pos >= 4 ? 4 : style.crc_pos >= 2 ? 2 : 1;
         const int words = bs_crc_words(NP) + kBsCrcLaneWords;
@@ -482,10 +483,17 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "    const u32 lane = threadIdx.x & 63u;\n"
              "    const u32 lofs = lane * 4u;\n"
              "    const u32 wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
-             "    for (i32 i = 0; i < a.crc_per; i++) {\n"
-             "        const u32 t = (blockIdx.x * (u32)a.crc_per + (u32)i) * "
+             // the first crc_q workgroups take crc_per tiles per wave, the rest one: long runs (one
+             // table fill each) first, single tiles for an even finish
+             "    const u32 big = (u32)a.crc_q, per = (u32)a.crc_per;\n"
+             "    const u32 nper = blockIdx.x < big ? per : 1u;\n"
+             "    const u32 t0 = (blockIdx.x < big ? blockIdx.x * per : big * per + (blockIdx.x - big)) * "
           << CW
           << "u + wv;\n"
+             "    for (u32 i = 0; i < nper; i++) {\n"
+             "        const u32 t = t0 + i * "
+          << CW
+          << "u;\n"
              "        if (t >= a.ntiles) break;\n"
              "        const u32 s = t / a.tiles_per_stripe;\n"
              "        const i32 off = (i32)(t - s * a.tiles_per_stripe) * "

@@ -99,8 +99,9 @@ struct BitsliceStyle {
     bool dpp_reduce = true;
     // crc variant in one-wave 4 KiB tiles (round 5): 0 = off; W > 0 = workgroups of W waves sharing
     // one copy of the tables (crc_pos position sets for pieces 1 KiB apart + the lane-shift tables);
-    // workgroup b's waves take tiles (b * crc_per + i) * W + wave, i < crc_per, each on its own (no
-    // barrier after the table fill), and write r0 of each fragment's 4 KiB to crc_partial[t * (K + R) + f]
+    // the first crc_q workgroups' waves take tiles (b * crc_per + i) * W + wave, i < crc_per, the rest
+    // one tile each, each wave on its own (no barrier after the table fill), and write r0 of each
+    // fragment's 4 KiB to crc_partial[t * (K + R) + f]
     int crc_wave = 0;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte

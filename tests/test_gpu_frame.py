@@ -998,7 +998,8 @@ def test_stream_contexts_threaded(F):
 def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypatch):
     """CHKSUM_CRC32 framed encode on the crc variant in one-wave 4 KiB tiles (knobs frame_crc_wave =
     waves per workgroup, frame_crc_wave_pos = position sets, frame_crc_wave_per = tiles per wave,
-    frame_crc_wave_pf = chunks of the next input prefetched;
+    frame_crc_wave_pf = chunks of the next input prefetched, 60% of the tiles in those runs when
+    longer than one;
     bitslice.cpp CW form, crc_combine_kernel) against the 16 KiB-tile crc variant / the codec + CRC
     pass, and the restated reference framing for the last stripe.  frame_crc_wave_strict makes a
     declined form an error, so the new kernel is the one that ran."""
@@ -1018,13 +1019,14 @@ def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypa
             _lib.check(d.ecamd_tune(b"frame_crc_wave_pos", form[1]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_per", form[2]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_pf", form[3]), "tune")
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_big", 60 if form[2] > 1 else 0), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_strict", 1 if w else 0), "tune")
             fb = F.FrameBatch(code, k, m, size, S, hd=hd)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
     finally:
         for kn in (b"frame_crc_wave", b"frame_crc_wave_pos", b"frame_crc_wave_per", b"frame_crc_wave_pf",
-                   b"frame_crc_wave_strict"):
+                   b"frame_crc_wave_big", b"frame_crc_wave_strict"):
             d.ecamd_tune(kn, -1)
         d.ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])

@@ -4,8 +4,8 @@
 timed launches), 5 warm-up then `reps` encodes, and the same on the LDS-table fused kernel
 (frame_crc_bs 0) after it.  Prints one JSON line per kernel path with the HIP-event time per encode
 and the algorithmic bytes (10 MiB read + 14 MiB written per stripe).  Paths (argv, default
-bitsliced_crc lds_fused): bitsliced_crc (16 KiB tiles), wave_crc (one-wave 4 KiB tiles: knobs
-frame_crc_wave 4, frame_crc_wave_pos 1, frame_crc_wave_per 1), lds_fused."""
+bitsliced_crc lds_fused): bitsliced_crc (16 KiB tiles), wave_crc (one-wave 4 KiB tiles, the default
+form: knob frame_crc_wave), lds_fused."""
 import json
 import os
 import sys
@@ -19,7 +19,7 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 
 PATHS = {"bitsliced_crc": {"frame_crc_bs": 1, "frame_crc_wave": 0},
-         "wave_crc": {"frame_crc_bs": 1, "frame_crc_wave": 4, "frame_crc_wave_pos": 1, "frame_crc_wave_per": 1},
+         "wave_crc": {"frame_crc_bs": 1, "frame_crc_wave": -1},  # the default form
          "lds_fused": {"frame_crc_bs": 0, "frame_crc_wave": 0}}
 
 
@@ -47,7 +47,7 @@ def main(paths, reps=20):
         print(json.dumps({"path": path, "ms_per_encode": round(ms, 4), "algorithmic_bytes": algo,
                           "frac": round(algo / ms / 1e6 / 8000, 4)}), flush=True)
     d.ecamd_tune(b"frame_crc_bs", -1)
-    d.ecamd_tune(b"frame_crc_wave", 0)
+    d.ecamd_tune(b"frame_crc_wave", -1)
     d.ecamd_tune(b"bitslice", 1)
 
 
