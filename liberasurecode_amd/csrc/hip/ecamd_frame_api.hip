@@ -439,7 +439,7 @@ int crc_wave_form(const Code& c, int64_t cover)
     int cw = dev_tune("frame_crc_wave");
     if (cw <= 0 || cover <= 0 || cover % 4096) return 0;
     if (c.m > 4) cw = std::min(cw, 8);  // (5-8 outputs: built for 2 waves per SIMD)
-    return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6);
+    return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6) | (dev_tune("frame_crc_wave_mix") ? 1024 : 0);
 }
 int crc_wave_groups(int64_t tps)
 {

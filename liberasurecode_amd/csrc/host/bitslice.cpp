@@ -554,7 +554,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             for (int c = 0; c < 4; c++)
                 s << "            P[" << 4 * c << "] = xq" << c << "[0]; P[" << 4 * c + 1 << "] = xq" << c << "[1]; P["
                   << 4 * c + 2 << "] = xq" << c << "[2]; P[" << 4 * c + 3 << "] = xq" << c << "[3];\n";
-            s << "            __builtin_amdgcn_sched_barrier(0);\n";
+            if (!style.crc_mix) s << "            __builtin_amdgcn_sched_barrier(0);\n";
             network(j);
             if (style.input_barrier) s << "            __builtin_amdgcn_sched_barrier(0);\n";
             s << "        }\n";
@@ -1014,8 +1014,9 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused); plain maps in
     // the multi-wave form, bits 20-21: lanes per workgroup (1 = 128, 2 = 512; 0 = 256); bit 22 the
     // crc variant in one-wave tiles (with the lane fold; bits 11-19 its occupancy as for bit 6), bits
-    // 23-26 its waves per workgroup
-    const int cw = crc ? std::clamp(crc_wave, 0, 15) : 0;
+    // 23-26 its waves per workgroup, bit 27 its crc_mix
+    const int cw = crc ? std::clamp(crc_wave & 15, 0, 15) : 0;  // (+ 16: crc_mix)
+    const int cmix = cw && (crc_wave & 16) ? 1 : 0;
     if (cw) {  // (the one-wave crc form always folds with the lane tables, on byte piece tables)
         crc_lane = true;
         crc_nib = false;
@@ -1036,7 +1037,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
               (crc && crc_nib ? 32 : 0) | (pf << 8) |
               (!wave && !cw ? 0 : (wave ? 64 : 0) | (std::clamp(o.wmin, 1, 8) << 11) |
                                       (std::clamp(o.wmax, o.wmin, 8) << 15) | (o.barrier ? 1 << 19 : 0)) |
-              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) : 0))
+              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) | (cmix << 27) : 0))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -1058,12 +1059,12 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 27) || (cp & 12) == 12))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 28) || (cp & 12) == 12))
         return false;
     const int cw = (cp >> 22) & 1 ? (cp >> 23) & 15 : 0;  // one-wave crc form: waves per workgroup
     if (((cp >> 22) & 1) ? (!cw || (cp & (1 | 2 | 16 | 32)) != (1 | 2 | 16)) : (cp >> 23) != 0)
         return false;
-    if (crc_wave) *crc_wave = cw;
+    if (crc_wave) *crc_wave = cw | (((cp >> 27) & 1) << 4);
     const int tcode = (cp >> 20) & 3;  // lanes per workgroup of the multi-wave plain form
     if (tcode == 3 || (tcode && ((cp & (1 | 2 | 64)) || depth != 0))) return false;
     const int wmin = (cp >> 11) & 15, wmax = (cp >> 15) & 15;  // one-wave occupancy (0: bit 7 / by R)

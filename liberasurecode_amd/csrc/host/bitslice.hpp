@@ -103,6 +103,9 @@ struct BitsliceStyle {
     // one tile each, each wave on its own (no barrier after the table fill), and write r0 of each
     // fragment's 4 KiB to crc_partial[t * (K + R) + f]
     int crc_wave = 0;
+    // one-wave crc form: no scheduling barrier between an input's CRC lookups and its network, so the
+    // compiler may interleave the LDS lookups with the network's XORs
+    bool crc_mix = false;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly
