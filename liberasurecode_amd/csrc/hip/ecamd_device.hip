@@ -398,6 +398,7 @@ struct Tuning {
     Knob frame_crc_wave_wpe{0};
     Knob frame_crc_wave_big{kCrcWave.big};  //   % of the tiles in runs of frame_crc_wave_per per wave
     Knob frame_crc_wave_pf{kCrcWave.pf};
+    Knob frame_crc_wave_mb{4};      //   piece dwords on byte tables (the rest on nibble tables)
     Knob frame_crc_wave_mix{0};     //   no scheduling barrier between an input's CRC lookups and its network
     Knob frame_crc_wave_strict{0};  // tests: a framed CRC32 encode the one-wave crc form declines fails
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
@@ -453,6 +454,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_wave_pos") return g_tune.frame_crc_wave_pos;
     if (k == "frame_crc_wave_strict") return g_tune.frame_crc_wave_strict;
     if (k == "frame_crc_wave_mix") return g_tune.frame_crc_wave_mix;
+    if (k == "frame_crc_wave_mb") return g_tune.frame_crc_wave_mb;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "frame_tail_fork") return g_tune.frame_tail_fork;
     if (k == "frame_tail_tiles") return g_tune.frame_tail_tiles;
@@ -2364,6 +2366,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_wave_big = value < 0 ? kCrcWave.big : std::min(value, 100);
     } else if (k == "frame_crc_wave_pf") {
         g_tune.frame_crc_wave_pf = value < 0 ? kCrcWave.pf : value == 2 || value == 4 ? value : 0;
+    } else if (k == "frame_crc_wave_mb") {
+        g_tune.frame_crc_wave_mb = value <= 0 ? 4 : std::min(value, 4);
     } else if (k == "frame_crc_wave_mix") {
         g_tune.frame_crc_wave_mix = value > 0 ? 1 : 0;
     } else if (k == "frame_crc_wave_strict") {

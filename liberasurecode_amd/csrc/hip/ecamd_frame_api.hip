@@ -358,7 +358,7 @@ int fused_image(int dev, bool legacy, int mb, const uint32_t** out, int tile = 8
     if (it == g_fused_images.end()) {
         // npos > 0: the bitsliced crc variant's image (position sets of byte or nibble tables, step = tile)
         const std::vector<uint32_t> w =
-            npos ? build_fused_crc_image_pos(CrcMachine(legacy), static_cast<uint64_t>(tile), npos, nib)
+            npos ? build_fused_crc_image_pos(CrcMachine(legacy), static_cast<uint64_t>(tile), npos, nib, mb)
                  : build_fused_crc_image(CrcMachine(legacy), static_cast<uint64_t>(tile), mb);
         uint32_t* d = nullptr;
         HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
@@ -439,8 +439,11 @@ int crc_wave_form(const Code& c, int64_t cover)
     int cw = dev_tune("frame_crc_wave");
     if (cw <= 0 || cover <= 0 || cover % 4096) return 0;
     if (c.m > 4) cw = std::min(cw, 8);  // (5-8 outputs: built for 2 waves per SIMD)
-    return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6) | (dev_tune("frame_crc_wave_mix") ? 1024 : 0);
+    const int nibw = 4 - std::clamp(dev_tune("frame_crc_wave_mb"), 1, 4);  // piece dwords on nibble tables
+    return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6) | (dev_tune("frame_crc_wave_mix") ? 1024 : 0) |
+           (nibw << 11);
 }
+int crc_wave_mb(int wf) { return 4 - ((wf >> 11) & 3); }  // byte-table dwords per piece of the form wf
 int crc_wave_groups(int64_t tps)
 {
     int g = 1;
@@ -481,7 +484,7 @@ int encode_crc_bitsliced(int dev, const Code& c, bool legacy, const void* obj, i
                                 &partial)))
             return rc;
         const uint32_t* img = nullptr;
-        if ((rc = fused_image(dev, legacy, 4, &img, 1024, wf & 7, false))) return rc;
+        if ((rc = fused_image(dev, legacy, crc_wave_mb(wf), &img, 1024, wf & 7, false))) return rc;
         if ((rc = rs_encode_copy_crc_bs(c.k, c.m, obj, obj_stride, frags + kHeaderBytes, ss, fs, bs, nstripes, img,
                                         tiles, 0, stream, wf)))
             return rc == ECAMD_EINVAL && dev_tune("frame_crc_wave_strict")
@@ -612,7 +615,7 @@ int encode_crc_cover(int dev, const Code& c, bool legacy, const void* obj, int64
     int npos = dev_tune("frame_crc_pos");
     if (npos <= 0) npos = lane && c.m <= 4 ? 1 : 2;
     const bool nib = dev_tune("frame_crc_bs_nib") > 0;
-    if ((rc = wf ? fused_image(dev, legacy, 4, &img, 1024, wf & 7, false)
+    if ((rc = wf ? fused_image(dev, legacy, crc_wave_mb(wf), &img, 1024, wf & 7, false)
                  : fused_image(dev, legacy, 4, &img, 4096, npos, nib)))
         return rc;
     unsigned pb[32], db[32];

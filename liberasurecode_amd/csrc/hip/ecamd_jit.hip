@@ -321,7 +321,8 @@ void stop_children_at_exit()
 // of the request, the target and the generator: the same in the shipped and the per-user cache).
 std::string request_of(const BsEntry& e)
 {
-    const int cw = (e.crc & 32) ? ((e.crc >> 6) & 15) | ((e.crc & 1024) ? 16 : 0) : 0;  // (+ 16: crc_mix)
+    // (+ 16: crc_mix, + 32 * dwords of a piece on nibble tables)
+    const int cw = (e.crc & 32) ? ((e.crc >> 6) & 15) | ((e.crc & 1024) ? 16 : 0) | (((e.crc >> 11) & 3) << 5) : 0;
     return bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0, e.wave, &e.shifts,
                             e.prefetch, e.wave || e.occ.threads || cw ? &e.occ : nullptr, cw);
@@ -444,7 +445,7 @@ std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& dep
         // + 32 for one-wave tiles (with the lane fold, byte tables) in workgroups of (crc >> 6) waves
         const int pos = crc & 7;
         const int cw = (crc & 32) ? std::clamp((crc >> 6) & 15, 1, 15) : 0;
-        crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (cw ? 8 | 32 | (cw << 6) | (crc & 1024) : crc & 24);
+        crc = (pos >= 4 ? 4 : pos >= 2 ? 2 : 1) | (cw ? 8 | 32 | (cw << 6) | (crc & (1024 | 6144)) : crc & 24);
     }
     copy = copy || crc;
     wave = wave && !crc;

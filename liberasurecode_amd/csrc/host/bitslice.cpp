@@ -314,6 +314,17 @@ __device__ __forceinline__ u32 piece_r0(const u32* t, u32 a, u32 b, u32 c, u32 d
 {
     return x3(lmap8(t, a), lmap8(t + 1024, b), lmap8(t + 2048, c)) ^ lmap8(t + 3072, d);
 }
+// byte tables for the first MB dwords (tab + 1024 w), nibble tables for the rest (tab + 1024 MB + 128 (w - MB))
+template <int MB>
+__device__ __forceinline__ u32 piece_r0m(const u32* t, u32 a, u32 b, u32 c, u32 d)
+{
+    const u32* n = t + 1024 * MB;
+    const u32 ra = lmap8(t, a);
+    const u32 rb = MB > 1 ? lmap8(t + 1024, b) : lmap4(n, b);
+    const u32 rc = MB > 2 ? lmap8(t + 2048, c) : lmap4(n + 128 * (2 - MB), c);
+    const u32 rd = lmap4(n + 128 * (3 - MB), d);
+    return x3(ra, rb, rc) ^ rd;
+}
 // the same through nibble tables: dword w's 8 fields at tab + 128 w (conflict-free 16-entry tables)
 __device__ __forceinline__ u32 piece_r0n(const u32* t, u32 a, u32 b, u32 c, u32 d)
 {
@@ -455,14 +466,18 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         // tiles); no barrier after the table fill.
         const int NS = net.K + net.R;
         const int NP = style.crc_pos >= 4 ? 4 : style.crc_pos >= 2 ? 2 : 1;
-        const int words = bs_crc_words(NP) + kBsCrcLaneWords;
+        const int MB = std::clamp(style.crc_mb, 1, 4);  // piece dwords on byte tables
+        const int PW = MB * 1024 + (4 - MB) * 128;        // piece-table words per position set
+        const int maps = NP * PW;                         // gap, levels, A^1024, then the lane tables
+        const int words = maps + 8 * 128 + kBsCrcLaneWords;
         constexpr int CS1 = kBsCrcWaveStep;
+        const std::string pfn = MB == 4 ? std::string("piece_r0") : "piece_r0m<" + std::to_string(MB) + ">";
         auto crc1 = [&](int f, const char* x) {
             s << "            {\n";
             for (int c0 = 0; c0 < 4; c0 += NP) {
                 s << "                " << (c0 ? "cs = lmap4(gap, cs)" : "u32 cs = 0u");
                 for (int c = c0; c < c0 + NP; c++)
-                    s << " ^ piece_r0(ctab + " << (c % NP) * 4096 << ", " << x << c << "[0], " << x << c << "[1], " << x
+                    s << " ^ " << pfn << "(ctab + " << (c % NP) * PW << ", " << x << c << "[0], " << x << c << "[1], " << x
                       << c << "[2], " << x << c << "[3])";
                 s << ";\n";
             }
@@ -475,10 +490,10 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
           << ") *(v4u*)(ctab + i) = *(const v4u*)(a.crc_img + i);\n"
              "    __syncthreads();\n"
              "    const u32* gap = ctab + "
-          << NP * 4096
+          << maps
           << ";\n"
              "    const u32* lanes = ctab + "
-          << bs_crc_words(NP)
+          << maps + 8 * 128
           << ";\n"
              "    const u32 lane = threadIdx.x & 63u;\n"
              "    const u32 lofs = lane * 4u;\n"
@@ -1014,9 +1029,10 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused); plain maps in
     // the multi-wave form, bits 20-21: lanes per workgroup (1 = 128, 2 = 512; 0 = 256); bit 22 the
     // crc variant in one-wave tiles (with the lane fold; bits 11-19 its occupancy as for bit 6), bits
-    // 23-26 its waves per workgroup, bit 27 its crc_mix
-    const int cw = crc ? std::clamp(crc_wave & 15, 0, 15) : 0;  // (+ 16: crc_mix)
+    // 23-26 its waves per workgroup, bit 27 its crc_mix, bits 28-29 its piece dwords on nibble tables
+    const int cw = crc ? std::clamp(crc_wave & 15, 0, 15) : 0;  // (+ 16: crc_mix, + 32 * nibble dwords)
     const int cmix = cw && (crc_wave & 16) ? 1 : 0;
+    const int cnib = cw ? (crc_wave >> 5) & 3 : 0;
     if (cw) {  // (the one-wave crc form always folds with the lane tables, on byte piece tables)
         crc_lane = true;
         crc_nib = false;
@@ -1037,7 +1053,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
               (crc && crc_nib ? 32 : 0) | (pf << 8) |
               (!wave && !cw ? 0 : (wave ? 64 : 0) | (std::clamp(o.wmin, 1, 8) << 11) |
                                       (std::clamp(o.wmax, o.wmin, 8) << 15) | (o.barrier ? 1 << 19 : 0)) |
-              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) | (cmix << 27) : 0))
+              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) | (cmix << 27) | (cnib << 28) : 0))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -1059,12 +1075,13 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 28) || (cp & 12) == 12))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 30) || (cp & 12) == 12))
         return false;
     const int cw = (cp >> 22) & 1 ? (cp >> 23) & 15 : 0;  // one-wave crc form: waves per workgroup
     if (((cp >> 22) & 1) ? (!cw || (cp & (1 | 2 | 16 | 32)) != (1 | 2 | 16)) : (cp >> 23) != 0)
         return false;
-    if (crc_wave) *crc_wave = cw | (((cp >> 27) & 1) << 4);
+    if (!cw && (cp >> 27)) return false;
+    if (crc_wave) *crc_wave = cw | (((cp >> 27) & 1) << 4) | (((cp >> 28) & 3) << 5);
     const int tcode = (cp >> 20) & 3;  // lanes per workgroup of the multi-wave plain form
     if (tcode == 3 || (tcode && ((cp & (1 | 2 | 64)) || depth != 0))) return false;
     const int wmin = (cp >> 11) & 15, wmax = (cp >> 15) & 15;  // one-wave occupancy (0: bit 7 / by R)

@@ -106,6 +106,9 @@ struct BitsliceStyle {
     // one-wave crc form: no scheduling barrier between an input's CRC lookups and its network, so the
     // compiler may interleave the LDS lookups with the network's XORs
     bool crc_mix = false;
+    // one-wave crc form: a piece's first crc_mb dwords through byte tables, the rest through
+    // conflict-free nibble tables (build_fused_crc_image_pos mb)
+    int crc_mb = 4;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly

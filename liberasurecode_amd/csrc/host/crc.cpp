@@ -89,13 +89,15 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos)
     return img;
 }
 
-std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos, bool nib)
+std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos, bool nib, int mb)
 {
-    // npos sets of all-byte (or all-nibble) piece tables, set u shifted to the group's last piece
-    // (A^(step*(npos-1-u)) folded in), then the gap map A^(step*npos) and the 6 butterfly levels
-    // and A^1024 of build_fused_crc_image, then the lane-shift tables
-    const CrcImage pieces = build_crc_image(m, nib ? 4 : 8, 4, 4, false);
-    const size_t pw = nib ? 4 * 8 * 16 : 4 * 4 * 256;
+    // npos sets of all-byte (or all-nibble, or byte for the first mb dwords) piece tables, set u
+    // shifted to the group's last piece (A^(step*(npos-1-u)) folded in), then the gap map
+    // A^(step*npos) and the 6 butterfly levels and A^1024 of build_fused_crc_image, then the
+    // lane-shift tables
+    mb = nib ? 0 : std::clamp(mb, 0, 4);
+    const CrcImage pieces = build_crc_image(m, mb == 4 ? 8 : 4 + mb, 4, 4, false);
+    const size_t pw = static_cast<size_t>(mb) * 4 * 256 + static_cast<size_t>(4 - mb) * 8 * 16;
     std::vector<uint32_t> w(static_cast<size_t>(npos) * pw + 8 * 128, 0);
     for (int u = 0; u < npos; u++) {
         const Mat32 sh = zero_shift(m, step * static_cast<uint64_t>(npos - 1 - u));

@@ -83,7 +83,10 @@ CrcImage build_crc_image(const CrcMachine& m, int B, int J, int G, bool pos = fa
 std::vector<uint32_t> build_fused_crc_image(const CrcMachine& m, uint64_t tile_bytes, int mb = 1);
 // The bitsliced crc variant's image: npos position sets of byte piece tables (pieces `step` bytes
 // apart, each set shifted to the group's last piece) + gap A^(step*npos) + butterfly levels + A^1024,
-// then the lane-shift tables; nib: the piece tables as 16-entry nibble fields (512 words per set).
-std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos, bool nib = false);
+// then the lane-shift tables; nib: the piece tables as 16-entry nibble fields (512 words per set);
+// mb < 4 (not with nib): byte tables for a piece's first mb dwords, nibble tables for the rest
+// (mb * 1024 + (4 - mb) * 128 words per set).
+std::vector<uint32_t> build_fused_crc_image_pos(const CrcMachine& m, uint64_t step, int npos, bool nib = false,
+                                                int mb = 4);
 
 }  // namespace ecamd

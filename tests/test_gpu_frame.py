@@ -993,13 +993,13 @@ def test_stream_contexts_threaded(F):
     ("rs", 10, 4, 10 << 20), ("rs", 10, 4, 10 * 104858 - 4), ("rs", 4, 2, 4 * 65536 + 6), ("rs", 3, 2, 3 * 4096 * 5),
     ("rs", 6, 3, 6 * 16384 + 6 * 100), ("rs", 10, 4, 10 * (4096 + 16)), ("xor", 3, 3, 3 * 65536),
     ("xor", 3, 3, 3 * 104858 - 4), ("rs", 20, 8, 20 * 40000), ("rs", 12, 6, 12 * 65536)])
-@pytest.mark.parametrize("form", [(6, 2, 4, 0), (4, 1, 1, 2), (12, 4, 3, 0), (6, 2, 1, 4)])
+@pytest.mark.parametrize("form", [(6, 2, 4, 0, 4), (4, 1, 1, 2, 3), (12, 4, 3, 0, 4), (6, 2, 1, 4, 2), (4, 2, 1, 4, 1)])
 @pytest.mark.parametrize("legacy", [False, True])
 def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypatch):
     """CHKSUM_CRC32 framed encode on the crc variant in one-wave 4 KiB tiles (knobs frame_crc_wave =
     waves per workgroup, frame_crc_wave_pos = position sets, frame_crc_wave_per = tiles per wave,
     frame_crc_wave_pf = chunks of the next input prefetched, 60% of the tiles in those runs when
-    longer than one;
+    longer than one, frame_crc_wave_mb = piece dwords on byte tables (the rest on nibble tables);
     bitslice.cpp CW form, crc_combine_kernel) against the 16 KiB-tile crc variant / the codec + CRC
     pass, and the restated reference framing for the last stripe.  frame_crc_wave_strict makes a
     declined form an error, so the new kernel is the one that ran."""
@@ -1020,13 +1020,14 @@ def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypa
             _lib.check(d.ecamd_tune(b"frame_crc_wave_per", form[2]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_pf", form[3]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_big", 60 if form[2] > 1 else 0), "tune")
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_mb", form[4]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_strict", 1 if w else 0), "tune")
             fb = F.FrameBatch(code, k, m, size, S, hd=hd)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
     finally:
         for kn in (b"frame_crc_wave", b"frame_crc_wave_pos", b"frame_crc_wave_per", b"frame_crc_wave_pf",
-                   b"frame_crc_wave_big", b"frame_crc_wave_strict"):
+                   b"frame_crc_wave_big", b"frame_crc_wave_mb", b"frame_crc_wave_strict"):
             d.ecamd_tune(kn, -1)
         d.ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])
