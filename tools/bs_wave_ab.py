@@ -111,6 +111,8 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
             "c3f256k": {"cap7": {}, "cap8": {"bs_wave_per_cu": 8}, "cap6": {"bs_wave_per_cu": 6}},
             "c5tt": {"t256": {}, "t128": {"bs_tile_threads": 128}, "t512": {"bs_tile_threads": 512}},
             "c5tile": {"cap0": {"bs_tile_per_cu": 0}, "cap1": {"bs_tile_per_cu": 1}},
+            # the 16 KiB-tile form's LDS-DMA ring (inputs ahead of the network in LDS, not registers)
+            "c5depth": {"d0": {}, "d2": {"bitslice_depth": 2}, "d4": {"bitslice_depth": 4}},
             "c5nocc": {"w88": {"bs_narrow_min_k": 1, "bs_wave_wmin": 8, "bs_wave_wmax": 8},
                        "w44": {"bs_narrow_min_k": 1, "bs_wave_wmin": 4, "bs_wave_wmax": 4},
                        "w22": {"bs_narrow_min_k": 1, "bs_wave_wmin": 2, "bs_wave_wmax": 2},
@@ -121,7 +123,8 @@ VARIANTS = {"c3": {"tables": {"bs_wave": 0}, "wave1": {}, "bs4_16k": {"bs_wave":
             "c2n": {"tables": {"bs_narrow_min_k": 0}, "narrow": {"bs_narrow_min_k": 1},
                     "narrow_ring2": {"bs_narrow_min_k": 1, "bs_wave_depth": 2}}}
 DEFAULTS = {"bs_plain_prefetch": 0, "bs_tile_threads": 256, "wgs_per_cu": 0, "bs_tile_per_cu": 0, "bs_wave_per_cu": -1, "bs_copy_per_cu": 0, "xor_per_cu": 0, "bs_wave": -1, "bitslice_min_rows": 0, "bs_wave_min_rows": 0, "bs_prefetch": -1,
-            "bs_narrow_min_k": -1, "bs_wave_depth": 0, "bs_wave_wmin": 0, "bs_wave_wmax": 0, "bs_wave_barrier": -1}
+            "bs_narrow_min_k": -1, "bs_wave_depth": 0, "bs_wave_wmin": 0, "bs_wave_wmax": 0, "bs_wave_barrier": -1,
+            "bitslice_depth": 0}
 
 
 def launches():
@@ -140,7 +143,7 @@ def apply(d, knobs):
 def run(cfg, rounds=3, n=30, skip=10):
     K, M, F, S, ops = {"c3": C3, "c3pf": C3, "c2": C2, "c5": C5, "c3ring": C3, "c3n": C3N, "c5n": C5N,
                        "c2n": C2, "c3occ": C3, "c3occ2": C3, "c5nocc": C5N, "c3nocc": C3N,
-                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N, "c3pf5": C3,
+                       "c3cap": C3, "c5ncap": C5N, "c3cap2": C3, "c5cap": C5, "c3ncap": C3N, "c5ncap2": C5N, "c5tile": C5, "c5depth": C5, "c3ringcap": C3, "c2wgs": C2, "c5tt": C5E, "c3cap3": C3, "c5ncap3": C5N, "c3pf5": C3,
                        "c3s64": (10, 4, 1 << 20, 64, C3[4]), "c3s1024": (10, 4, 1 << 20, 1024, C3[4]),
                        "c3f256k": (10, 4, 256 << 10, 1024, C3[4])}[cfg]
     d = _lib.dev()
