@@ -1886,7 +1886,8 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     }
     hipFunction_t fn = bitslice_function(device, coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
                                          nullptr,
-                                         cw ? static_cast<int>(g_tune.frame_crc_wave_pf)
+                                         // (5-8 outputs: no registers for a second input ahead)
+                                         cw ? (m > 4 && g_tune.frame_crc_wave_pf == 3 ? 4 : static_cast<int>(g_tune.frame_crc_wave_pf))
                                             : m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0,
                                          nullptr, cw ? &occ : nullptr);
     if (!fn) return ECAMD_EINVAL;
@@ -2365,7 +2366,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "frame_crc_wave_big") {
         g_tune.frame_crc_wave_big = value < 0 ? kCrcWave.big : std::min(value, 100);
     } else if (k == "frame_crc_wave_pf") {
-        g_tune.frame_crc_wave_pf = value < 0 ? kCrcWave.pf : value == 2 || value == 4 ? value : 0;
+        g_tune.frame_crc_wave_pf = value < 0 ? kCrcWave.pf : value >= 2 && value <= 4 ? value : 0;  // (3: 2 inputs ahead)
     } else if (k == "frame_crc_wave_mb") {
         g_tune.frame_crc_wave_mb = value <= 0 ? 4 : std::min(value, 4);
     } else if (k == "frame_crc_wave_mix") {

@@ -451,6 +451,7 @@ std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& dep
     wave = wave && !crc;
     depth = copy ? 0 : bitslice_depth(depth, K);  // one-wave tiles: the LDS ring only in plain maps
     prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
+               : (crc & 32) && prefetch == 3 ? 3  // the one-wave crc form: two inputs ahead
                : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
     if (crc & 32) {  // the one-wave crc form keeps its occupancy (waves per SIMD, cap, barrier)
         occ.threads = 0;

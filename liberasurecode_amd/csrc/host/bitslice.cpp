@@ -526,17 +526,20 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         acc_init();
         s << "        u32 held = 0u;\n";
         // prefetch (style.prefetch 2 / 4): the next unrealigned input's first PFc chunks are loaded with
-        // this input's, before its copy stores, CRC lookups and network
-        const int PFc = (style.prefetch == 2 || style.prefetch == 4) ? style.prefetch : 0;
+        // this input's, before its copy stores, CRC lookups and network; 3: all 4 chunks of the input
+        // two ahead (PD = 2 register sets)
+        const int PD = style.prefetch == 3 ? 2 : 1;
+        const int PFc = style.prefetch == 3 ? 4 : (style.prefetch == 2 || style.prefetch == 4) ? style.prefetch : 0;
         auto cpre = [&](int j) { return PFc > 0 && j < net.K && shift_of(j) == 0; };
         auto cload_next = [&](int j) {
             for (int c = 0; c < PFc; c++)
-                s << "            xn[" << c << "] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j << "] + off + "
-                  << c * CS1 << ", 0, 2);\n";
+                s << "            xn" << j % PD << "[" << c << "] = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
+                  << "] + off + " << c * CS1 << ", 0, 2);\n";
         };
         if (PFc) {
-            s << "        v4u xn[" << PFc << "];\n";
-            if (cpre(0)) cload_next(0);
+            for (int q = 0; q < PD; q++) s << "        v4u xn" << q << "[" << PFc << "];\n";
+            for (int q = 0; q < PD; q++)
+                if (cpre(q)) cload_next(q);
         }
         for (int j = 0; j < net.K; j++) {
             s << "        {  // input " << j << "\n            u32 P[16];\n";
@@ -552,13 +555,13 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
             } else {
                 for (int c = 0; c < 4; c++) {
                     if (cpre(j) && c < PFc)
-                        s << "            const v4u xq" << c << " = xn[" << c << "];\n";
+                        s << "            const v4u xq" << c << " = xn" << j % PD << "[" << c << "];\n";
                     else
                         s << "            const v4u xq" << c << " = __builtin_amdgcn_raw_buffer_load_b128(rin, a.in_off[" << j
                           << "] + off + " << c * CS1 << ", 0, 2);\n";
                 }
             }
-            if (cpre(j + 1)) cload_next(j + 1);
+            if (cpre(j + PD)) cload_next(j + PD);
             // the 4 loads leave together (without the barrier the compiler consumes the first two
             // before issuing the rest, and each wait then also retires the previous copy stores)
             s << "            __builtin_amdgcn_sched_barrier(0);\n";
@@ -1043,6 +1046,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     wave = wave && !crc;
     // 1: the late copy of the 16 KiB-tile copy-through form
     const int pf = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
+                   : cw && prefetch == 3 ? 3
                    : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
     bool shifted = false;
     if (in_shift && (copy || crc))
@@ -1098,7 +1102,7 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
         occ->threads = tcode == 1 ? 128 : tcode == 2 ? 512 : 0;
     }
     const int pf = (cp >> 8) & 7;
-    if ((pf != 0 && pf != 1 && pf != 2 && pf != 4) || (pf > 1 && !(cp & 64) && !(cp & 2)) ||
+    if ((pf != 0 && pf != 1 && pf != 2 && pf != 4 && !(pf == 3 && cw)) || (pf > 1 && !(cp & 64) && !(cp & 2)) ||
         (pf == 1 && (!(cp & 1) || (cp & 66))))
         return false;  // 2 / 4: one-wave / crc forms; 1 (late copy): the 16 KiB-tile copy-through form
     if (prefetch) *prefetch = pf;

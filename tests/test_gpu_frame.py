@@ -992,8 +992,10 @@ def test_stream_contexts_threaded(F):
 @pytest.mark.parametrize("be,k,m,size", [
     ("rs", 10, 4, 10 << 20), ("rs", 10, 4, 10 * 104858 - 4), ("rs", 4, 2, 4 * 65536 + 6), ("rs", 3, 2, 3 * 4096 * 5),
     ("rs", 6, 3, 6 * 16384 + 6 * 100), ("rs", 10, 4, 10 * (4096 + 16)), ("xor", 3, 3, 3 * 65536),
-    ("xor", 3, 3, 3 * 104858 - 4), ("rs", 20, 8, 20 * 40000), ("rs", 12, 6, 12 * 65536)])
-@pytest.mark.parametrize("form", [(6, 2, 4, 0, 4), (4, 1, 1, 2, 3), (12, 4, 3, 0, 4), (6, 2, 1, 4, 2), (4, 2, 1, 4, 1)])
+    ("xor", 3, 3, 3 * 104858 - 4), ("rs", 20, 8, 20 * 40000), ("rs", 12, 6, 12 * 65536),
+    ("rs", 10, 4, 10 * 23 * 4096), ("rs", 4, 2, 4 * 4096)])
+@pytest.mark.parametrize("form", [(6, 2, 4, 0, 4), (4, 1, 1, 2, 3), (12, 4, 3, 0, 4), (6, 2, 1, 4, 2), (4, 2, 1, 4, 1),
+                                  (4, 2, 1, 3, 4)])
 @pytest.mark.parametrize("legacy", [False, True])
 def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypatch):
     """CHKSUM_CRC32 framed encode on the crc variant in one-wave 4 KiB tiles (knobs frame_crc_wave =
