@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Framed RS(10,4) encode / systematic join across object sizes (development tool, round 5):
 
-  frame_shape_ab.py size[,size...]
+  frame_shape_ab.py size[,size...] [--only op:checksum]   (e.g. --only encode:1, for a profiler run)
 
 Each size gets S = round(2.5 GiB / size) objects; prints the median (3 interleaved rounds of 5) of the
 framed encode without checksum, with CRC32, and the systematic join, as the fraction of 8 TB/s of the
@@ -22,6 +22,7 @@ from liberasurecode_amd import device as D  # noqa: E402
 
 def main():
     sizes = [int(v) for v in sys.argv[1].split(",")]
+    only = sys.argv[sys.argv.index("--only") + 1].split(":") if "--only" in sys.argv else None
     k, m = 10, 4
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)  # every bitsliced kernel compiled before its first launch
@@ -43,6 +44,8 @@ def main():
             if ct == frame.CHKSUM_NONE:
                 fb.encode(obj, stream=st)
                 cases[(size, S, bs, ct, "join")] = (lambda fb=fb, out=out: fb.decode([], out, stream=st), S * (k * bs + size))
+    if only:
+        cases = {key: v for key, v in cases.items() if key[4] == only[0] and key[3] == int(only[1])}
     times = {}
     a, b = D.Event(), D.Event()
     for _ in range(3):
