@@ -4,9 +4,9 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-for i in 1 2; do for RL in 0 1; do
-  rm -rf /tmp/jc_$RL; mkdir -p /tmp/jc_$RL
-  ECAMD_JIT_CACHE=/tmp/jc_$RL ECAMD_BS_RLANE=$RL timeout -k 10 300 python -u tools/frame_shape_ab.py 1048572,4194300 > gpurun_out/r05_rlane_${RL}_$i.log 2>&1 || { echo "RUN FAILED"; tail -20 gpurun_out/r05_rlane_${RL}_$i.log; exit 1; }
-  sed "s/^/rl$RL /" gpurun_out/r05_rlane_${RL}_$i.log | grep frac
-done; done
+step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "gpurun_out/r05_$name.log" 2>&1; local rc=$?; tail -1 "gpurun_out/r05_$name.log" | cut -c1-300; [ $rc -eq 0 ] || { echo "STEP $name FAILED rc=$rc"; tail -30 "gpurun_out/r05_$name.log"; exit 1; }; }
+step crcwave_tests 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_frame.py -k crc_wave
+step ab_crcwave_dma 600 python -u tools/frame_knob_ab.py frame_crc_wave_dma 0,1 --ct crc --ops encode
+step ab_crcwave_dma2 600 python -u tools/frame_knob_ab.py frame_crc_wave_dma 0,1 --ct crc --ops encode
+grep frac gpurun_out/r05_ab_crcwave_dma.log gpurun_out/r05_ab_crcwave_dma2.log
 echo ALL_OK
