@@ -430,8 +430,8 @@ int finalize_ranges(int dev, const Code& c, bool legacy, uint64_t obj_size, uint
     return 0;
 }
 
-// The crc variant in one-wave 4 KiB tiles (knob frame_crc_wave = its waves per workgroup, maps of up
-// to 4 outputs): its per-tile partials go to scratch slot 3, crc_combine_kernel folds them into q
+// The crc variant in one-wave 4 KiB tiles (knob frame_crc_wave = its waves per workgroup, 4 by default;
+// maps of up to 8 outputs): its per-tile partials go to scratch slot 3, crc_combine_kernel folds them into q
 // ranges of g tiles per payload (g the largest divisor of the tile count up to 16) in `partial`, and
 // finalize_ranges takes those.  crc_wave_form: the crc_pos flags of the form (0: not this form).
 int crc_wave_form(const Code& c, int64_t cover)
