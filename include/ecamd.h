@@ -78,6 +78,10 @@ int ecamd_rs_kernel_form(int k, int m, const int *missing, int dest, int rebuild
  * bitsliced kernel), < 0 on error (ecamd_jitc missing or failed). */
 int ecamd_bitslice_prebuild(int k, int m, const int *missing, int dest, int rebuild_parity, const char *arch,
                             const char *dir);
+/* The same for the CHKSUM_CRC32 framed encode (ecamd_frame_encode) of a code (backend 6 rs_vand or 3
+ * flat_xor_hd): its bitsliced codec-and-checksum kernel, one per code whatever the object size.
+ * Returns 1 when present, 0 when that encode takes no bitsliced kernel, < 0 on error. */
+int ecamd_frame_prebuild(int backend, int k, int m, int hd, const char *arch, const char *dir);
 
 /* ---- GF(2^16) fragment maps: outputs[r] = sum_j coeff[r*K+j] * inputs[j] (16-bit LE words) ---- */
 typedef struct ecamd_map ecamd_map;

@@ -132,6 +132,7 @@ def dev():
         _proto(d, "ecamd_rs_kernel_form", C.c_int, [C.c_int, C.c_int, VP, C.c_int, C.c_int, C.c_int64])
         _proto(d, "ecamd_bitslice_prebuild", C.c_int,
                [C.c_int, C.c_int, VP, C.c_int, C.c_int, C.c_char_p, C.c_char_p])
+        _proto(d, "ecamd_frame_prebuild", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_char_p])
         _proto(d, "ecamd_percall_reset", None, [])
         _proto(d, "ecamd_percall_status", C.c_int, [])
         _proto(d, "ecamd_fault_inject", C.c_int, [C.c_char_p, C.c_int])

@@ -1835,6 +1835,18 @@ int rs_encode_copy_crc(int k, int m, const void* obj, int64_t obj_stride, void* 
 
 namespace {
 
+// The crc variant's prefetch and (one-wave form) occupancy for an m-output encode map with crc_pos
+// flags -- shared by the launch and the build-time prebuild, so both name the same code object.
+int crc_form_args(int m, int crc_pos, BsOcc& occ)
+{
+    occ = BsOcc{};
+    if (!(crc_pos & 32)) return m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0;
+    occ.wmin = g_tune.frame_crc_wave_wpe > 0 ? static_cast<int>(g_tune.frame_crc_wave_wpe) : m > 4 ? 2 : 3;
+    occ.wmax = occ.wmin;
+    // (5-8 outputs: no registers for a second input ahead)
+    return m > 4 && g_tune.frame_crc_wave_pf == 3 ? 4 : static_cast<int>(g_tune.frame_crc_wave_pf);
+}
+
 // The crc variant of the bitsliced kernel for the encode map `coeff` (m x k, row-major; RS
 // generator rows or a flat-XOR code's 0/1 parity masks) on `device`: see rs_encode_copy_crc_bs.
 int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, const void* obj, int64_t obj_stride,
@@ -1880,16 +1892,9 @@ int encode_copy_crc_bs(int device, const std::vector<int>& coeff, int k, int m, 
     // some shift patterns (C3 objects 10 bytes long), which then fall back to the codec + CRC pass
     const uint32_t in_records = a.in_records;
     BsOcc occ{};
-    if (cw) {
-        occ.wmin = g_tune.frame_crc_wave_wpe > 0 ? static_cast<int>(g_tune.frame_crc_wave_wpe) : m > 4 ? 2 : 3;
-        occ.wmax = occ.wmin;
-    }
+    const int prefetch = crc_form_args(m, crc_pos, occ);
     hipFunction_t fn = bitslice_function(device, coeff, m, k, 0, mode == 2, hold, true, crc_pos, false,
-                                         nullptr,
-                                         // (5-8 outputs: no registers for a second input ahead)
-                                         cw ? (m > 4 && g_tune.frame_crc_wave_pf == 3 ? 4 : static_cast<int>(g_tune.frame_crc_wave_pf))
-                                            : m <= 4 ? static_cast<int>(g_tune.frame_crc_prefetch) : 0,
-                                         nullptr, cw ? &occ : nullptr);
+                                         nullptr, prefetch, nullptr, cw ? &occ : nullptr);
     if (!fn) return ECAMD_EINVAL;
     BsArgs b{};
     b.in_base = a.in_base;
@@ -2955,6 +2960,27 @@ int ecamd_bitslice_prebuild(int k, int m, const int* missing, int dest, int rebu
     }
     return built;
 }
+
+extern "C++" {
+namespace ecamd {
+int crc_encode_prebuild(int k, int m, const uint32_t* masks, int crc_pos, const char* arch, const char* dir)
+{
+    if (!arch || !dir || k <= 0 || m <= 0 || m > kBsMaxR || k > kBsMaxK) return 0;
+    std::vector<int> coeff(static_cast<size_t>(m) * k, 0);
+    if (masks) {  // flat XOR: the 0 / 1 matrix of xor_encode_copy_crc_bs
+        for (int r = 0; r < m; r++)
+            for (int j = 0; j < k; j++) coeff[static_cast<size_t>(r) * k + j] = (masks[r] >> j) & 1u;
+    } else {  // rs_vand: the generator's parity rows, as the encode map (rs_plan, no missing)
+        FragmentMap fm;
+        if (rs_plan(k, m, nullptr, -1, 0, fm)) return -1;
+        coeff = group_rows(fm, 0, m);
+    }
+    BsOcc occ{};
+    const int prefetch = crc_form_args(m, crc_pos, occ);
+    return bitslice_prebuild(coeff, m, k, 0, true, crc_pos, false, nullptr, prefetch, occ, arch, dir);
+}
+}  // namespace ecamd
+}  // extern "C++"
 
 int ecamd_rs_kernel_form(int k, int m, const int* missing, int dest, int rebuild_parity, int64_t blocksize)
 {

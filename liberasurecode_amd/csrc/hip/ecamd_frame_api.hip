@@ -711,6 +711,24 @@ int encode_crc_fused(int dev, const Code& c, bool legacy, const void* obj, int64
 
 extern "C" {
 
+// Build time (no GPU): the CRC32 framed encode's bitsliced kernel for a code, into the library's jit/
+// directory (prebuild.py) -- the kernel does not depend on the object size (object chunks at offsets
+// that are not multiples of 16 take unaligned loads), so one per code serves whole objects and Swift's
+// segments alike.  1 present, 0 not a bitsliced form under the current knobs, < 0 failed.
+int ecamd_frame_prebuild(int backend, int k, int m, int hd, const char* arch, const char* dir)
+{
+    const Code c = make_code(backend, k, m, hd);
+    const int rc = check_code(c);
+    if (rc) return rc;
+    if (!arch || !dir) return dev_fail(ECAMD_EINVAL, "null arch / dir");
+    const int wf = crc_wave_form(c, 4096);
+    if (!wf || c.m > 8) return 0;
+    unsigned pb[32], db[32];
+    if (c.backend == kBackendXor) ecamd_xor_code_tables(c.k, c.m, c.hd, pb, db);
+    const int r = crc_encode_prebuild(c.k, c.m, c.backend == kBackendXor ? pb : nullptr, wf, arch, dir);
+    return r < 0 ? dev_fail(ECAMD_EHIP, "framed CRC32 prebuild failed (%d)", r) : r;
+}
+
 int ecamd_frame_geometry(int backend, int k, int m, int hd, uint64_t obj_size, int64_t* blocksize,
                          int64_t* fragment_len)
 {

@@ -121,6 +121,11 @@ int rs_encode_copy_crc_bs(int k, int m, const void* obj, int64_t obj_stride, voi
                           int64_t stripe_stride, int64_t frag_stride, int64_t bs, int nstripes,
                           const uint32_t* d_img, uint32_t* d_partial, int q, void* stream, int crc_pos = 1,
                           int64_t cover = -1);  // cover: the first `cover` bytes of each payload only
+// Build time (no GPU): the code object the CRC32 framed encode's crc variant (crc_pos flags as
+// rs_encode_copy_crc_bs takes them) will ask for, for the rs_vand code (k, m) (masks null) or the
+// flat-XOR code with parity masks `masks`, into `dir` (ecamd_frame_prebuild).  1: present, 0: this
+// form takes no bitsliced kernel, < 0: failed.
+int crc_encode_prebuild(int k, int m, const uint32_t* masks, int crc_pos, const char* arch, const char* dir);
 // fused image words with byte tables for the first mb dwords of a piece, nibble tables after
 constexpr int crc_fused_words(int mb = 1) { return mb * 1024 + (4 - mb) * 128 + 8 * 128; }
 

@@ -6,6 +6,7 @@ runs that map on the LDS-table kernels.  `build()` calls `prebui
 maps of C2 / C3 / C5 -- encode, the decodes the bench times, single-destination reconstructs -- are
 already in `lib/jit/`, which libecamd searches before the per-user cache: a fresh process takes the
 bitsliced kernel at their first launch, with or without `ecamd_jitc` / libhiprtc on the machine.
+The CHKSUM_CRC32 framed encode's kernels (one per code, ecamd_frame_prebuild) ship the same way.
 Every object is named by the run time's own key (request text, target, generator fingerprint), so
 a map whose knobs or generator differ simply is not found there and compiles as before.
 
@@ -31,6 +32,10 @@ OPS = (
     + [(20, 8, None, -1, 1)] + [(20, 8, p, -1, 1) for p in C5_LOST]  # C5
     + [(20, 8, C5_LOST[0], d, 0) for d in C5_LOST[0]]  # C5: 8 single-destination reconstructs
 )
+# (backend, k, m, hd): the CHKSUM_CRC32 framed encode's codec-and-checksum kernel, one per code whatever
+# the object size -- Swift's default rs_vand (10, 4) (whole objects and 1 MiB segments alike), the
+# other BASELINE codes, and flat_xor_hd (3, 3, 3)
+FRAME_CODES = [(6, 10, 4, 0), (6, 4, 2, 0), (6, 20, 8, 0), (3, 3, 3, 3)]
 
 
 def _ints(v):
@@ -41,6 +46,8 @@ def prebuild(arch="gfx950", jobs=8, verbose=False):
     lib = C.CDLL(os.path.join(HERE, "lib", "libecamd.so"))
     lib.ecamd_bitslice_prebuild.restype = C.c_int
     lib.ecamd_bitslice_prebuild.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_char_p]
+    lib.ecamd_frame_prebuild.restype = C.c_int
+    lib.ecamd_frame_prebuild.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_char_p]
     lib.ecamd_last_error.restype = C.c_char_p
     os.makedirs(JIT_DIR, exist_ok=True)
     for name in os.listdir(JIT_DIR):  # objects of an earlier generator or knob set are never looked up
@@ -50,6 +57,9 @@ def prebuild(arch="gfx950", jobs=8, verbose=False):
     os.chmod(JIT_DIR, stat.S_IRWXU | stat.S_IRGRP | stat.S_IXGRP | stat.S_IROTH | stat.S_IXOTH)
 
     def one(op):
+        if op[0] == "frame":
+            _, backend, k, m, hd = op
+            return op, lib.ecamd_frame_prebuild(backend, k, m, hd, arch.encode(), JIT_DIR.encode())
         k, m, miss, dest, rebuild = op
         arr = _ints(miss) if miss is not None else None
         rc = lib.ecamd_bitslice_prebuild(k, m, C.cast(arr, C.c_void_p) if arr is not None else None, dest, rebuild,
@@ -57,7 +67,7 @@ def prebuild(arch="gfx950", jobs=8, verbose=False):
         return op, rc
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        results = list(ex.map(one, OPS))
+        results = list(ex.map(one, list(OPS) + [("frame",) + c for c in FRAME_CODES]))
     bad = [(op, rc) for op, rc in results if rc < 0]
     if verbose:
         for op, rc in results:

@@ -63,6 +63,7 @@ def test_fresh_process_runs_shipped_bitsliced_at_first_launch(tmp_path):
     assert out["decode_shipped_form"] == BITSLICED and out["decode_shipped_bitsliced_launches"] > 0, out
     assert out["decode_other_form"] == COMPILING and out["decode_other_bitsliced_launches"] == 0, out
     assert out["encode_exact"] and out["decode_shipped_exact"] and out["decode_other_exact"], out
+    assert out["frame_bitsliced_launches"] > 0 and out["frame_exact"], out  # ecamd_frame_prebuild
 
 
 def test_without_helper_shipped_maps_still_bitsliced(tmp_path):
@@ -72,10 +73,14 @@ def test_without_helper_shipped_maps_still_bitsliced(tmp_path):
     assert out["decode_shipped_form"] == BITSLICED and out["decode_shipped_bitsliced_launches"] > 0, out
     assert out["decode_other_form"] == UNAVAILABLE and out["decode_other_bitsliced_launches"] == 0, out
     assert out["encode_exact"] and out["decode_shipped_exact"] and out["decode_other_exact"], out
+    assert out["frame_bitsliced_launches"] > 0 and out["frame_exact"], out
 
 
 def test_without_helper_or_shipped_objects_tables_serve(tmp_path):
     out = _run(tmp_path, _copy_libs(tmp_path, False))
+    for name in ("encode", "decode_shipped", "decode_other", "frame"):
+        assert out[name + "_bitsliced_launches"] == 0, out
     for name in ("encode", "decode_shipped", "decode_other"):
-        assert out[name + "_form"] == UNAVAILABLE and out[name + "_bitsliced_launches"] == 0, out
+        assert out[name + "_form"] == UNAVAILABLE, out
         assert out[name + "_exact"], out
+    assert out["frame_exact"], out
