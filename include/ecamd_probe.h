@@ -38,6 +38,10 @@ int ecamd_probe_mix(int lp, int sp, int ch, int threads, int wgs_per_cu, void *d
  * (mode 0), from global memory through the vector L1 (1) or half each (2); grid = CUs x wgs_per_cu
  * workgroups of 256 lanes, iters x 4 lookups per lane. */
 int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void *d_table, void *stream);
+/* One workgroup of 256 threads: mode 0 a single store, 1 / 2 first stage `bytes` of d_src into LDS
+ * (one / eight 16-byte loads in flight per thread), 3 / 4 1024 / 4096 straight-line VALU steps
+ * (a long kernel body).  Kernel-trace durations give a small launch's fixed costs. */
+int ecamd_probe_launch(int mode, const void *d_src, int bytes, void *stream);
 /* The same with the tile order (0 grid-stride, 1 a contiguous tile range per workgroup, 2 grid-stride
  * with each tile's fragment order rotated by the tile index) and the
  * chunk layout (wave_contig 1: a wave's ch chunks are 1 KiB apart, contiguous) as parameters. */

@@ -171,6 +171,7 @@ def probe():
         _proto(p, "ecamd_probe_bw", C.c_int,
                [C.c_int, C.c_int, C.c_int, VP, VP, C.c_int64, VP])
         _proto(p, "ecamd_probe_copy_tiles", C.c_int, [C.c_int, VP, VP, C.c_int64, VP])
+        _proto(p, "ecamd_probe_launch", C.c_int, [C.c_int, VP, C.c_int, VP])
         _proto(p, "ecamd_probe_lookup", C.c_int, [C.c_int, C.c_int, C.c_int, VP, VP])
         _proto(p, "ecamd_probe_mix", C.c_int,
                [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int, C.c_int,

@@ -31,6 +31,9 @@ __global__ void mix_probe_kernel(MixArgs a);
 template <int MODE>
 __global__ void lookup_probe_kernel(const uint4* __restrict__ table, int iters, uint32_t* sink);
 
+template <int STAGE, int CODE>
+__global__ void launch_probe_kernel(uint32_t* sink, const uint8_t* src, int bytes);
+
 template <int U>
 __global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int kind,
                                 uint32_t* sink);

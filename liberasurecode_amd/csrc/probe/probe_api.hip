@@ -133,6 +133,28 @@ int ecamd_probe_lookup(int mode, int wgs_per_cu, int iters, const void* d_table,
     return 0;
 }
 
+int ecamd_probe_launch(int mode, const void* d_src, int bytes, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (bytes < 0 || bytes > 64 * 1024 || bytes % 16) return fail(-22, "launch probe: bytes 0..64 KiB, multiple of 16");
+    static uint32_t* sink = nullptr;
+    if (!sink) HIP_TRY(hipMalloc(&sink, 64));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const auto* s = static_cast<const uint8_t*>(d_src);
+    const size_t lds = static_cast<size_t>(bytes);
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((launch_probe_kernel<0, 0>), dim3(1), dim3(256), 0, st, sink, s, bytes); break;
+    case 1: hipLaunchKernelGGL((launch_probe_kernel<1, 0>), dim3(1), dim3(256), lds, st, sink, s, bytes); break;
+    case 2: hipLaunchKernelGGL((launch_probe_kernel<2, 0>), dim3(1), dim3(256), lds, st, sink, s, bytes); break;
+    case 3: hipLaunchKernelGGL((launch_probe_kernel<0, 1024>), dim3(1), dim3(256), 0, st, sink, s, bytes); break;
+    default: hipLaunchKernelGGL((launch_probe_kernel<0, 4096>), dim3(1), dim3(256), 0, st, sink, s, bytes); break;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 int ecamd_probe_mix(int lp, int sp, int ch, int threads, int wgs_per_cu, void* base,
                           int64_t bs, int K, int R, int nstripes, void* stream)
 {

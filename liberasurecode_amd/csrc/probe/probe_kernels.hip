@@ -368,4 +368,39 @@ template __global__ void unaligned_probe_kernel<3>(uint8_t*, const uint8_t*, int
 template __global__ void unaligned_probe_kernel<4>(uint8_t*, const uint8_t*, int64_t, int);
 template __global__ void unaligned_probe_kernel<5>(uint8_t*, const uint8_t*, int64_t, int);
 
+// One workgroup's fixed cost (per-call objects of a few KiB run one workgroup): STAGE 0 none,
+// 1 `bytes` of a device buffer into LDS one 16-byte load per thread and round, 2 the same with 8
+// loads in flight; CODE straight-line dependent VALU steps (≈8 bytes of code each) before the
+// single store -- the cost of fetching a long kernel body into a cold instruction cache.
+template <int STAGE, int CODE>
+__global__ void __launch_bounds__(256) launch_probe_kernel(uint32_t* sink, const uint8_t* src, int bytes)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int tid = static_cast<int>(threadIdx.x);
+    if constexpr (STAGE == 1) {
+        for (int o = tid * 16; o < bytes; o += 256 * 16)
+            *reinterpret_cast<uint4*>(lds + o) = *reinterpret_cast<const uint4*>(src + o);
+    } else if constexpr (STAGE == 2) {
+        for (int o0 = tid * 16; o0 < bytes; o0 += 8 * 4096) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (o0 + u * 4096 < bytes) v[u] = *reinterpret_cast<const uint4*>(src + o0 + u * 4096);
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (o0 + u * 4096 < bytes) *reinterpret_cast<uint4*>(lds + o0 + u * 4096) = v[u];
+        }
+    }
+    if constexpr (STAGE) __syncthreads();
+    uint32_t x = STAGE ? *reinterpret_cast<const uint32_t*>(lds + tid * 4) : static_cast<uint32_t>(tid);
+#pragma unroll
+    for (int i = 0; i < CODE; i++) x = __builtin_amdgcn_alignbit(x, x ^ (0x9e3779b9u + i), i & 31) + (i * 0x85ebca6bu);
+    if (tid == 0) sink[blockIdx.x] = x;
+}
+template __global__ void launch_probe_kernel<0, 0>(uint32_t*, const uint8_t*, int);
+template __global__ void launch_probe_kernel<1, 0>(uint32_t*, const uint8_t*, int);
+template __global__ void launch_probe_kernel<2, 0>(uint32_t*, const uint8_t*, int);
+template __global__ void launch_probe_kernel<0, 1024>(uint32_t*, const uint8_t*, int);
+template __global__ void launch_probe_kernel<0, 4096>(uint32_t*, const uint8_t*, int);
+
 }  // namespace ecamd

@@ -4,6 +4,10 @@ set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > "gpurun_out/r05_$name.log" 2>&1; local rc=$?; tail -1 "gpurun_out/r05_$name.log" | cut -c1-300; [ $rc -eq 0 ] || { echo "STEP $name FAILED rc=$rc"; tail -30 "gpurun_out/r05_$name.log"; exit 1; }; }
-step jit_shipped_frame 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_jit_shipped.py
+export SKP_LAUNCH=1
+for v in 0 1; do
+  if [ $v = 1 ]; then export SKP_H2D=1; fi
+  timeout -k 10 150 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_skh$v" -o run --output-format csv -- python3 tools/small_kernel_probe.py 416 300 > gpurun_out/r05_skh$v.log 2>&1 || { echo FAILED; tail -20 gpurun_out/r05_skh$v.log; exit 1; }
+  grep case gpurun_out/r05_skh$v.log
+done
 echo ALL_OK
