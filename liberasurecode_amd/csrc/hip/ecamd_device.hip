@@ -178,6 +178,10 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // measured best on MI355X ("Tuning").
 // A launch knob: written by ecamd_tune from any thread, read by launches on others (each launch
 // reads each knob once; every setting gives bit-identical results, only the launch shape changes).
+// gf16_small_kernel for launches up to 1024 chunks (16 KiB per fragment, one stripe):
+// DESIGN.md §6 (per-call objects of a few KiB).
+constexpr int kSmallChunksDefault = 1024;
+
 struct Knob {
     std::atomic<int> v;
     explicit Knob(int x) : v(x) {}
@@ -238,6 +242,9 @@ struct Tuning {
     Knob crc_pos{1};        // CRC32 kernel: position-specific piece tables (one gap step per 4 pieces)
     Knob stream{1};         // strided gf16 launches: gf16_stream_kernel (buffer loads, pipelined)
     Knob stream_ch{1};      //   16-byte chunks per lane (1, 2; W = 8 always 1)
+    Knob small_chunks{kSmallChunksDefault};  // strided launches of at most this many 16-byte chunks
+                            //   per output row at a uniform pitch: gf16_small_kernel (0 = never)
+    Knob small_lane{4};     //   gf16_small_kernel: bytes per lane (2, 4 or 16)
     Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = by shape, see
                             // launch_xor)
     Knob grid_mult{0};      // stream launches: workgroups per resident slot (0: 2 for 4-output
@@ -593,6 +600,65 @@ bool stream_copy_offsets(ApplyArgs& a, int64_t bs)
         a.copy_off32[j] = a.copy_off[j] < 0 ? -1 : static_cast<int32_t>(a.copy_off[j]);
     a.copy_records = static_cast<uint32_t>(std::max<int64_t>(mx, 16));
     return true;
+}
+
+// A pass small enough for gf16_small_kernel: at most small_chunks 16-byte chunks in all, plain
+// strided fragments (no copy-through, padding limits or stripe list) at one 16-byte aligned pitch
+// per side.
+bool small_launch(const ApplyArgs& a, int64_t bs, int nstripes)
+{
+    const int64_t chunks = (bs + 15) / 16 * nstripes;
+    if (chunks <= 0 || chunks > g_tune.small_chunks || a.limited || a.copy_base || a.stripe_list ||
+        a.ncols < 1 || a.nrows < 1)
+        return false;
+    auto uniform = [nstripes](const uint8_t* base, int64_t stride, const int64_t* off, int n) {
+        const int64_t pitch = n > 1 ? off[1] - off[0] : 16;
+        for (int j = 0; j < n; j++)
+            if (off[j] != off[0] + j * pitch) return false;
+        return ((reinterpret_cast<uintptr_t>(base) + off[0]) & 15) == 0 && (pitch & 15) == 0 &&
+               (nstripes == 1 || (stride & 15) == 0);
+    };
+    return uniform(a.in_base, a.in_stride, a.in_off, a.ncols) &&
+           uniform(a.out_base, a.out_stride, a.out_off, a.nrows);
+}
+
+int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
+                 hipStream_t st)
+{
+    const int lane = g_tune.small_lane;
+    const int width = p.width;
+    SmallArgs s{};
+    s.tables = tables + p.offset;
+    s.in = a.in_base + a.in_off[0];
+    s.out = a.out_base + a.out_off[0];
+    s.in_stride = a.in_stride;
+    s.out_stride = a.out_stride;
+    s.in_pitch = a.ncols > 1 ? a.in_off[1] - a.in_off[0] : 0;
+    s.out_pitch = a.nrows > 1 ? a.out_off[1] - a.out_off[0] : 0;
+    s.bs = bs;
+    s.cpf = (bs + lane - 1) / lane;
+    s.nchunks = s.cpf * nstripes;
+    s.ncols = a.ncols;
+    s.nrows = a.nrows;
+    s.accumulate = a.accumulate;
+    const dim3 grid(static_cast<unsigned>((s.nchunks + 255) / 256)), block(256);
+    const size_t lds = p.bytes;
+#define SMALL_(W)                                                                                 \
+    switch (lane) {                                                                               \
+    case 2: hipLaunchKernelGGL((gf16_small_kernel<W, 2>), grid, block, lds, st, s); break;          \
+    case 16: hipLaunchKernelGGL((gf16_small_kernel<W, 16>), grid, block, lds, st, s); break;        \
+    default: hipLaunchKernelGGL((gf16_small_kernel<W, 4>), grid, block, lds, st, s); break;         \
+    }
+    if (width == 2) {
+        SMALL_(2)
+    } else if (width == 4) {
+        SMALL_(4)
+    } else {
+        SMALL_(8)
+    }
+#undef SMALL_
+    HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 template <int W, int CH, bool PF, bool NIB = false>
@@ -1051,6 +1117,11 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
                 bs -= done;
                 a.bs = bs;
             }
+        }
+        if (!PTRS && small_launch(a, bs, nstripes)) {
+            int rc = launch_small(a, p, bs, nstripes, map->d_tables, st);
+            if (rc) return rc;
+            continue;
         }
         Geometry g;
         int rc = geometry(map->device, p.bytes, bs, nstripes, g, 1);
@@ -2276,6 +2347,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_unfused = value != 0;
     } else if (k == "stream") {
         g_tune.stream = value != 0;
+    } else if (k == "small_lane") {
+        g_tune.small_lane = value == 16 ? 16 : value == 2 ? 2 : 4;
+    } else if (k == "small_chunks") {
+        g_tune.small_chunks = value < 0 ? kSmallChunksDefault : value;
     } else if (k == "stream_ch") {
         g_tune.stream_ch = value == 2 ? 2 : 1;
     } else if (k == "xor_wgs") {

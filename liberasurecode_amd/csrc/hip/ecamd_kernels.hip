@@ -78,6 +78,131 @@ template __global__ void gf16_copy_apply_kernel<4>(const ApplyArgs);
 template __global__ void gf16_copy_apply_kernel<8>(const ApplyArgs);
 
 
+// gf16_small_kernel<W>: launches of a few thousand 16-byte chunks (per-call objects of a few KiB:
+// one stripe, fragments at a uniform pitch).  Same split tables and chunk arithmetic as
+// apply_tile; what differs is the argument block.  ApplyArgs carries ~1.7 KB of per-fragment
+// arrays, read inside apply_tile's rolled loops with a scalar-load round trip each -- at one tile
+// those dependent kernel-argument fetches are most of the launch (kernel arguments in host memory,
+// HIP_FORCE_DEV_KERNARG=0: 9.7 -> 19.3 us; tools/small_kernel_probe.py).  SmallArgs is ~100 bytes
+// fetched up front, and every fragment address is base + j * pitch in registers.
+template <int W, int G>
+__global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int D = W / 2;
+    constexpr int EB = 2 * W;
+    constexpr int TB = 512 * EB;  // table bytes per input
+    constexpr int NW = G / 2;                // 16-bit words per lane
+    constexpr int ND = G >= 4 ? G / 4 : 1;  // dwords per lane (G = 2: the low half of one)
+    const int K = a.ncols;
+    const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    auto load = [](const uint8_t* p, int rem, uint32_t (&x)[ND]) {
+        if constexpr (G == 16) {
+            const uint4 v = load_tail(p, rem);
+            x[0] = v.x;
+            x[1] = v.y;
+            x[2] = v.z;
+            x[3] = v.w;
+        } else if (rem >= G) {
+            x[0] = G == 4 ? *reinterpret_cast<const uint32_t*>(p) : *reinterpret_cast<const uint16_t*>(p);
+        } else {
+            x[0] = 0u;
+            for (int i = 0; i < rem; i++) x[0] |= static_cast<uint32_t>(p[i]) << (8 * i);
+        }
+    };
+    // the first lane-group's first four inputs are in flight while the tables stage
+    uint32_t cur[4][ND], nxt[4][ND];
+    auto fetch4 = [&](int64_t cc, int j0, uint32_t (&x)[4][ND]) {
+        const int64_t s = cc / a.cpf;
+        const int64_t off = (cc - s * a.cpf) * G;
+        const int rem = a.bs - off < G ? static_cast<int>(a.bs - off) : G;
+        const uint8_t* in = a.in + s * a.in_stride + off;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (j0 + i < K) load(in + (j0 + i) * a.in_pitch, rem, x[i]);
+    };
+    if (c < a.nchunks) fetch4(c, 0, cur);
+    const int tbytes = K * TB;
+    for (int o = static_cast<int>(threadIdx.x) * 16; o < tbytes; o += static_cast<int>(blockDim.x) * 16)
+        *reinterpret_cast<uint4*>(lds + o) = load16(a.tables + o);
+    __syncthreads();
+
+    for (; c < a.nchunks; c += step) {
+        uint32_t acc[NW][D];
+#pragma unroll
+        for (int w = 0; w < NW; w++)
+#pragma unroll
+            for (int d = 0; d < D; d++) acc[w][d] = 0u;
+        for (int j0 = 0; j0 < K; j0 += 4) {
+            if (j0 + 4 < K) fetch4(c, j0 + 4, nxt);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (j0 + i >= K) break;
+                const uint8_t* tl = lds + static_cast<size_t>(j0 + i) * TB;
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    const uint32_t v = cur[i][w >> 1] >> ((w & 1) * 16);
+                    uint32_t e0[D], e1[D];
+                    lds_entry<D>(tl + (v & 0xffu) * EB, e0);
+                    lds_entry<D>(tl + 256 * EB + ((v >> 8) & 0xffu) * EB, e1);
+#pragma unroll
+                    for (int d = 0; d < D; d++) acc[w][d] = xor3(acc[w][d], e0[d], e1[d]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int d = 0; d < ND; d++) cur[i][d] = nxt[i][d];
+        }
+        const int64_t s = c / a.cpf;
+        const int64_t off = (c - s * a.cpf) * G;
+        const int rem = a.bs - off < G ? static_cast<int>(a.bs - off) : G;
+        uint8_t* out = a.out + s * a.out_stride + off;
+#pragma unroll
+        for (int r = 0; r < W; r++) {
+            if (r >= a.nrows) break;
+            uint32_t o[ND];
+            if constexpr (G == 2) {
+                o[0] = (r & 1) ? (acc[0][r >> 1] >> 16) : (acc[0][r >> 1] & 0xffffu);
+            } else {
+#pragma unroll
+                for (int d = 0; d < ND; d++) {
+                    const uint32_t A = acc[2 * d][r >> 1], B = acc[2 * d + 1][r >> 1];
+                    o[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
+                }
+            }
+            uint8_t* q = out + r * a.out_pitch;
+            if (a.accumulate) {
+                uint32_t prev[ND];
+                load(q, rem, prev);
+#pragma unroll
+                for (int d = 0; d < ND; d++) o[d] ^= prev[d];
+            }
+            if constexpr (G == 16) {
+                store_tail(q, make_uint4(o[0], o[1], o[2], o[3]), rem);
+            } else if (rem >= G) {
+                if constexpr (G == 4)
+                    *reinterpret_cast<uint32_t*>(q) = o[0];
+                else
+                    *reinterpret_cast<uint16_t*>(q) = static_cast<uint16_t>(o[0]);
+            } else {
+                for (int i = 0; i < rem; i++) q[i] = static_cast<uint8_t>(o[0] >> (8 * i));
+            }
+        }
+        if (c + step < a.nchunks) fetch4(c + step, 0, cur);
+    }
+}
+template __global__ void gf16_small_kernel<2, 16>(const SmallArgs);
+template __global__ void gf16_small_kernel<4, 16>(const SmallArgs);
+template __global__ void gf16_small_kernel<8, 16>(const SmallArgs);
+template __global__ void gf16_small_kernel<2, 4>(const SmallArgs);
+template __global__ void gf16_small_kernel<4, 4>(const SmallArgs);
+template __global__ void gf16_small_kernel<8, 4>(const SmallArgs);
+template __global__ void gf16_small_kernel<2, 2>(const SmallArgs);
+template __global__ void gf16_small_kernel<4, 2>(const SmallArgs);
+template __global__ void gf16_small_kernel<8, 2>(const SmallArgs);
+
 #define ECAMD_INST(W, P, N, B) \
     template __global__ void gf16_apply_kernel<W, P, N, B>(const ApplyArgs);
 #define ECAMD_INST2(P, N, B) ECAMD_INST(2, P, N, B) ECAMD_INST(4, P, N, B) ECAMD_INST(8, P, N, B)

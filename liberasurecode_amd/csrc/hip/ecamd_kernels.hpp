@@ -47,6 +47,20 @@ struct ApplyArgs {
                                       //   strided layout (heterogeneous decode groups); null = s
 };
 
+// gf16_small_kernel: one pass over fragments at a uniform pitch (input j of stripe s at
+// in + s * in_stride + j * in_pitch, output r likewise), for launches of a few chunks.
+struct SmallArgs {
+    const uint8_t* tables;
+    const uint8_t* in;
+    uint8_t* out;
+    int64_t in_stride, out_stride;
+    int64_t in_pitch, out_pitch;
+    int64_t bs;
+    int64_t cpf;      // G-byte lane groups per fragment (G = 16 or 4 bytes per lane)
+    int64_t nchunks;  // cpf * stripes
+    int ncols, nrows, accumulate;
+};
+
 // gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).
 constexpr int kStreamGroups = 5;
 
@@ -63,6 +77,8 @@ struct FillArgs {
 
 template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
+template <int W, int G>
+__global__ void gf16_small_kernel(const SmallArgs a);
 template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);
 template <int W, int KG, int CH, bool PF, bool NIB>

@@ -373,8 +373,49 @@ def tune():
     yield d.ecamd_tune
     for key, val in ((b"stream", 1), (b"stream_ch", 1), (b"stream_pf", 0), (b"stream_nib", 0),
                      (b"stream_order", 0), (b"stream_hybrid", 1), (b"multi_list", 1), (b"xor_wgs", 0),
-                     (b"bitslice", 1)):
+                     (b"bitslice", 1), (b"small_chunks", -1), (b"small_lane", 4)):
         d.ecamd_tune(key, val)
+
+
+@pytest.mark.parametrize("small", [(0, 4), (1 << 20, 4), (1 << 20, 16), (1 << 20, 2)])
+@pytest.mark.parametrize("S", [1, 3])
+@pytest.mark.parametrize("bs", [1, 15, 16, 17, 416, 1000, 4097, 16384 + 48])
+@pytest.mark.parametrize("R,K", [(1, 1), (2, 5), (4, 10), (3, 4), (8, 20), (5, 45), (9, 25)])
+def test_small_kernel_shapes(tune, R, K, bs, S, small):
+    """gf16_small_kernel (launches of few chunks: per-call objects) and, with small_chunks 0, the
+    stream kernel's tail path on the same shapes, against the numpy GF(2^16) reference: ragged
+    fragments, several stripes, 2 / 4 / 8-output passes, K = 45 in column passes (accumulate); the
+    small kernel with 4 bytes (default), 16 and 2 bytes per lane."""
+    tune(b"small_chunks", small[0])
+    tune(b"small_lane", small[1])
+    rng = np.random.default_rng(bs * 7 + R * 100 + K + S)
+    coeff = rng.integers(0, 65536, size=(R, K))
+    frags = rng.integers(0, 256, size=(S, K + R, bs), dtype=np.uint8)
+    lay = _upload(frags)
+    D.GF16Map(coeff).apply(lay, list(range(K)), list(range(K, K + R)))
+    out = lay.download_stripes()
+    for s in range(S):
+        want = gfnp.apply_map(coeff, [frags[s, j] for j in range(K)])
+        for r in range(R):
+            assert (out[s, K + r] == want[r]).all(), (s, r)
+        assert (out[s, :K] == frags[s, :K]).all()
+
+
+def test_small_kernel_nonuniform_offsets(tune):
+    """Inputs in a permuted order (no uniform pitch): the small launch declines, the result stays
+    exact; the same map with the inputs in order takes it."""
+    K, R, bs = 6, 3, 700
+    rng = np.random.default_rng(5)
+    coeff = rng.integers(0, 65536, size=(R, K))
+    frags = rng.integers(0, 256, size=(1, K + R, bs), dtype=np.uint8)
+    order = [3, 0, 5, 1, 4, 2]
+    for ins in (order, list(range(K))):
+        lay = _upload(frags)
+        D.GF16Map(coeff).apply(lay, ins, list(range(K, K + R)))
+        out = lay.download_stripes()
+        want = gfnp.apply_map(coeff, [frags[0, j] for j in ins])
+        for r in range(R):
+            assert (out[0, K + r] == want[r]).all(), (ins, r)
 
 
 @pytest.mark.parametrize("R,K", [(1, 1), (2, 4), (2, 5), (4, 10), (4, 13), (7, 16), (8, 20), (3, 21)])
