@@ -244,7 +244,8 @@ struct Tuning {
     Knob stream_ch{1};      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     Knob small_chunks{kSmallChunksDefault};  // strided launches of at most this many 16-byte chunks
                             //   per output row at a uniform pitch: gf16_small_kernel (0 = never)
-    Knob small_lane{4};     //   gf16_small_kernel: bytes per lane (2, 4 or 16)
+    Knob small_lane{0};     //   gf16_small_kernel: bytes per lane (2, 4 or 16; 0: 2 when one workgroup
+                            //   covers the pass that way, else 4 -- DESIGN.md §6)
     Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = by shape, see
                             // launch_xor)
     Knob grid_mult{0};      // stream launches: workgroups per resident slot (0: 2 for 4-output
@@ -622,13 +623,9 @@ bool small_launch(const ApplyArgs& a, int64_t bs, int nstripes)
            uniform(a.out_base, a.out_stride, a.out_off, a.nrows);
 }
 
-int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
-                 hipStream_t st)
+SmallArgs small_args(const ApplyArgs& a, int64_t bs, int nstripes, int lane)
 {
-    const int lane = g_tune.small_lane;
-    const int width = p.width;
     SmallArgs s{};
-    s.tables = tables + p.offset;
     s.in = a.in_base + a.in_off[0];
     s.out = a.out_base + a.out_off[0];
     s.in_stride = a.in_stride;
@@ -641,6 +638,18 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
     s.ncols = a.ncols;
     s.nrows = a.nrows;
     s.accumulate = a.accumulate;
+    for (int r = 0; r < kMaxRows; r++) s.masks[r] = r < a.nrows ? a.masks[r] : 0u;
+    return s;
+}
+
+int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
+                 hipStream_t st)
+{
+    const int lane = g_tune.small_lane ? static_cast<int>(g_tune.small_lane)
+                                       : ((bs + 1) / 2 * nstripes <= 256 ? 2 : 4);
+    const int width = p.width;
+    SmallArgs s = small_args(a, bs, nstripes, lane);
+    s.tables = tables + p.offset;
     const dim3 grid(static_cast<unsigned>((s.nchunks + 255) / 256)), block(256);
     const size_t lds = p.bytes;
 #define SMALL_(W)                                                                                 \
@@ -657,6 +666,14 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
         SMALL_(8)
     }
 #undef SMALL_
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int launch_xor_small(const ApplyArgs& a, int64_t bs, int nstripes, hipStream_t st)
+{
+    const SmallArgs s = small_args(a, bs, nstripes, 4);
+    hipLaunchKernelGGL(xor_small_kernel, dim3(static_cast<unsigned>((s.nchunks + 255) / 256)), dim3(256), 0, st, s);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1229,6 +1246,11 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
             for (int r = 0; r < a.nrows; r++) {
                 a.out_off[r] = out_off[row0 + r];
                 a.masks[r] = col0 < 32 ? (masks[row0 + r] >> col0) : 0u;
+            }
+            if (!PTRS && !copy_off && small_launch(a, bs, nstripes)) {
+                int rc = launch_xor_small(a, bs, nstripes, st);
+                if (rc) return rc;
+                continue;
             }
             Geometry g;
             const bool use_stream = !PTRS && g_tune.stream && stream_offsets(a, bs);
@@ -2348,7 +2370,7 @@ int ecamd_tune(const char* key, int value)
     } else if (k == "stream") {
         g_tune.stream = value != 0;
     } else if (k == "small_lane") {
-        g_tune.small_lane = value == 16 ? 16 : value == 2 ? 2 : 4;
+        g_tune.small_lane = value == 16 || value == 4 || value == 2 ? value : 0;
     } else if (k == "small_chunks") {
         g_tune.small_chunks = value < 0 ? kSmallChunksDefault : value;
     } else if (k == "stream_ch") {

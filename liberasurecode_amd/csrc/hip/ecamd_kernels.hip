@@ -252,6 +252,56 @@ __device__ __forceinline__ void xor_tile(const ApplyArgs& a, uint32_t s, int64_t
     }
 }
 
+// xor_small_kernel: flat XOR launches of a few chunks (per-call objects), 4-byte lanes, on the
+// compact SmallArgs (see gf16_small_kernel); the masks are scalars read once.
+__global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
+{
+    const int K = a.ncols;
+    const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.nchunks; c += step) {
+        const int64_t s = c / a.cpf;
+        const int64_t off = (c - s * a.cpf) * 4;
+        const int rem = a.bs - off < 4 ? static_cast<int>(a.bs - off) : 4;
+        auto load = [rem](const uint8_t* p) -> uint32_t {
+            if (rem >= 4) return *reinterpret_cast<const uint32_t*>(p);
+            uint32_t x = 0u;
+            for (int i = 0; i < rem; i++) x |= static_cast<uint32_t>(p[i]) << (8 * i);
+            return x;
+        };
+        const uint8_t* in = a.in + s * a.in_stride + off;
+        uint32_t acc[kMaxRows];
+#pragma unroll
+        for (int r = 0; r < kMaxRows; r++) acc[r] = 0u;
+        uint32_t cur[4], nxt[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) cur[i] = i < K ? load(in + i * a.in_pitch) : 0u;
+        for (int j0 = 0; j0 < K; j0 += 4) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) nxt[i] = j0 + 4 + i < K ? load(in + (j0 + 4 + i) * a.in_pitch) : 0u;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int r = 0; r < kMaxRows; r++)
+                    acc[r] ^= cur[i] & (0u - ((a.masks[r] >> ((j0 + i) & 31)) & 1u));
+#pragma unroll
+            for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+        }
+        uint8_t* out = a.out + s * a.out_stride + off;
+#pragma unroll
+        for (int r = 0; r < kMaxRows; r++) {
+            if (r >= a.nrows) break;
+            uint8_t* q = out + r * a.out_pitch;
+            uint32_t v = acc[r];
+            if (a.accumulate) v ^= load(q);
+            if (rem >= 4) {
+                *reinterpret_cast<uint32_t*>(q) = v;
+            } else {
+                for (int i = 0; i < rem; i++) q[i] = static_cast<uint8_t>(v >> (8 * i));
+            }
+        }
+    }
+}
+
 template <int W, bool PTRS>
 __global__ void __launch_bounds__(256) xor_apply_kernel(const ApplyArgs a)
 {

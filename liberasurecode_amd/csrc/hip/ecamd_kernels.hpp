@@ -59,6 +59,7 @@ struct SmallArgs {
     int64_t cpf;      // G-byte lane groups per fragment (G = 16 or 4 bytes per lane)
     int64_t nchunks;  // cpf * stripes
     int ncols, nrows, accumulate;
+    uint32_t masks[kMaxRows];  // xor_small_kernel: inputs of output r
 };
 
 // gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).
@@ -79,6 +80,7 @@ template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
 template <int W, int G>
 __global__ void gf16_small_kernel(const SmallArgs a);
+__global__ void xor_small_kernel(const SmallArgs a);
 template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);
 template <int W, int KG, int CH, bool PF, bool NIB>

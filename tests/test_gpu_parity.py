@@ -373,11 +373,11 @@ def tune():
     yield d.ecamd_tune
     for key, val in ((b"stream", 1), (b"stream_ch", 1), (b"stream_pf", 0), (b"stream_nib", 0),
                      (b"stream_order", 0), (b"stream_hybrid", 1), (b"multi_list", 1), (b"xor_wgs", 0),
-                     (b"bitslice", 1), (b"small_chunks", -1), (b"small_lane", 4)):
+                     (b"bitslice", 1), (b"small_chunks", -1), (b"small_lane", 0)):
         d.ecamd_tune(key, val)
 
 
-@pytest.mark.parametrize("small", [(0, 4), (1 << 20, 4), (1 << 20, 16), (1 << 20, 2)])
+@pytest.mark.parametrize("small", [(0, 0), (1 << 20, 0), (1 << 20, 4), (1 << 20, 16), (1 << 20, 2)])
 @pytest.mark.parametrize("S", [1, 3])
 @pytest.mark.parametrize("bs", [1, 15, 16, 17, 416, 1000, 4097, 16384 + 48])
 @pytest.mark.parametrize("R,K", [(1, 1), (2, 5), (4, 10), (3, 4), (8, 20), (5, 45), (9, 25)])
@@ -385,7 +385,7 @@ def test_small_kernel_shapes(tune, R, K, bs, S, small):
     """gf16_small_kernel (launches of few chunks: per-call objects) and, with small_chunks 0, the
     stream kernel's tail path on the same shapes, against the numpy GF(2^16) reference: ragged
     fragments, several stripes, 2 / 4 / 8-output passes, K = 45 in column passes (accumulate); the
-    small kernel with 4 bytes (default), 16 and 2 bytes per lane."""
+    small kernel with 2 / 4 bytes per lane by size (default), 4, 16 and 2."""
     tune(b"small_chunks", small[0])
     tune(b"small_lane", small[1])
     rng = np.random.default_rng(bs * 7 + R * 100 + K + S)
@@ -416,6 +416,29 @@ def test_small_kernel_nonuniform_offsets(tune):
         want = gfnp.apply_map(coeff, [frags[0, j] for j in ins])
         for r in range(R):
             assert (out[0, K + r] == want[r]).all(), (ins, r)
+
+
+@pytest.mark.parametrize("small", [0, 1 << 20])
+@pytest.mark.parametrize("bs", [1, 3, 4, 17, 416, 4097])
+@pytest.mark.parametrize("R,K", [(1, 1), (3, 6), (4, 10), (10, 32)])
+def test_xor_small_kernel(tune, R, K, bs, small):
+    """xor_small_kernel (flat XOR launches of few chunks) and the stream kernel on the same shapes,
+    2 stripes: ragged fragments, more than 8 outputs (row groups), 32 inputs (the masks' width)."""
+    tune(b"small_chunks", small)
+    rng = np.random.default_rng(bs * 3 + R * 50 + K)
+    S = 2
+    frags = rng.integers(0, 256, size=(S, K + R, bs), dtype=np.uint8)
+    masks = [int(m) | 1 << (r % K) for r, m in enumerate(rng.integers(0, 1 << min(K, 62), size=R, dtype=np.int64))]
+    masks = [m & 0xFFFFFFFF for m in masks]
+    lay = _upload(frags)
+    D.xor_apply(masks, lay, list(range(K)), list(range(K, K + R)))
+    out = lay.download_stripes()
+    for r, mk in enumerate(masks):
+        want = np.zeros((S, bs), dtype=np.uint8)
+        for j in range(K):
+            if mk >> j & 1:
+                want ^= frags[:, j]
+        assert (out[:, K + r] == want).all(), r
 
 
 @pytest.mark.parametrize("R,K", [(1, 1), (2, 4), (2, 5), (4, 10), (4, 13), (7, 16), (8, 20), (3, 21)])
