@@ -1107,8 +1107,11 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
     // bytes of each fragment the bitsliced kernel covered, per group of 8 output rows (the LDS-table
     // row widths 2 / 4 / 8 divide 8, so a pass lies in one group)
     std::vector<int64_t> bs_done(static_cast<size_t>((map->R + 7) / 8), 0);
+    // launches small enough for gf16_small_kernel skip the bitsliced one: a per-call 64 KiB object
+    // (6.5 KiB fragments) paid a 12 us one-tile bitsliced launch and a 12 us small launch for the rest
+    const bool small = (bs_all + 15) / 16 * nstripes <= g_tune.small_chunks;
     if constexpr (!PTRS) {
-        for (int g = 0; g * 8 < map->R; g++) {
+        for (int g = 0; g * 8 < map->R && !small; g++) {
             int brc = 0;
             bs_done[static_cast<size_t>(g)] = launch_bitslice(map, g * 8, std::min(8, map->R - g * 8), base_args, in_off, out_off,
                                          bs_all, nstripes, st, &brc);
