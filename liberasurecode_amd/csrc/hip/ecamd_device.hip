@@ -178,9 +178,9 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // measured best on MI355X ("Tuning").
 // A launch knob: written by ecamd_tune from any thread, read by launches on others (each launch
 // reads each knob once; every setting gives bit-identical results, only the launch shape changes).
-// gf16_small_kernel for launches up to 1024 chunks (16 KiB per fragment, one stripe):
+// gf16_small_kernel for launches up to 4096 chunks (64 KiB per fragment, one stripe):
 // DESIGN.md §6 (per-call objects of a few KiB).
-constexpr int kSmallChunksDefault = 1024;
+constexpr int kSmallChunksDefault = 4096;
 
 struct Knob {
     std::atomic<int> v;

@@ -26,9 +26,11 @@ def sync_compile(request):
     d = _lib.dev()
     d.ecamd_tune(b"bitslice", 2)  # wait for the compile: every launch below takes the JIT kernel
     d.ecamd_tune(b"bitslice_depth", request.param)
+    d.ecamd_tune(b"small_chunks", 0)  # small batches would otherwise take the small-launch kernel
     yield d
     d.ecamd_tune(b"bitslice", 1)
     d.ecamd_tune(b"bitslice_depth", DEFAULT_DEPTH)
+    d.ecamd_tune(b"small_chunks", -1)
 
 
 DEFAULT_DEPTH = 0

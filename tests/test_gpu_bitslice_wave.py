@@ -33,7 +33,9 @@ def form(request):
     d.ecamd_tune(b"bs_wave_depth", depth)
     d.ecamd_tune(b"bs_grid", grid)
     d.ecamd_tune(b"bs_narrow_min_k", 1)  # 1-2-output maps too, whatever k
+    d.ecamd_tune(b"small_chunks", 0)  # small batches would otherwise take the small-launch kernel
     yield d
+    d.ecamd_tune(b"small_chunks", -1)
     for k, v in KNOBS.items():
         d.ecamd_tune(k.encode(), v)
 
