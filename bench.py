@@ -282,7 +282,10 @@ def profile_summary(cfg):
 
 
 def _profile_world(command):
-    """--gpus N of the profiled command line (1 when absent)."""
+    """--gpus N of the profiled command line (1 when absent); None when the summary names no bench.py
+    command -- such a summary is never quoted as this run's trace."""
+    if "bench.py" not in command:
+        return None
     parts = command.split()
     for i, p in enumerate(parts[:-1]):
         if p == "--gpus":

@@ -52,6 +52,11 @@ int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
  * written (a permutation of 0..K+R-1; NULL = identity). */
 int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int order, int wave_contig,
                      void *base, int64_t bs, int K, int R, int nstripes, const int *frag, void *stream);
+/* The same with the codec's launch shapes: wgs_per_cu <= 0 gives one workgroup per tile (the
+ * dispatcher hands tiles out, as ecamd_bs_kernel's bs_grid form), and cap_per_cu > 0 limits the
+ * resident workgroups per CU with a dynamic LDS share of 160 KiB / cap (the codec's per-CU caps). */
+int ecamd_probe_mix4(int lp, int sp, int ch, int threads, int wgs_per_cu, int cap_per_cu, int wave_contig,
+                     void *base, int64_t bs, int K, int R, int nstripes, const int *frag, void *stream);
 
 /* VALU / LDS issue-cost probe: grid = CUs x wgs_per_cu workgroups of 256 lanes, each lane `iters`
  * rounds of 8 independent instructions of form op (0 v_xor_b32, 1 v_bitop3_b32, 2 SDWA byte-select

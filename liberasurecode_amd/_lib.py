@@ -182,6 +182,9 @@ def probe():
         _proto(p, "ecamd_probe_mix3", C.c_int,
                [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int,
                 C.c_int, C.c_int, IP, VP])
+        _proto(p, "ecamd_probe_mix4", C.c_int,
+               [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int,
+                C.c_int, C.c_int, IP, VP])
         _proto(p, "ecamd_probe_valu", C.c_int, [C.c_int, C.c_int, C.c_int, VP])
         _probe = p
     return _probe

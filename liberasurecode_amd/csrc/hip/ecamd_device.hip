@@ -181,6 +181,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // gf16_small_kernel for launches up to 4096 chunks (64 KiB per fragment, one stripe):
 // DESIGN.md §6 (per-call objects of a few KiB).
 constexpr int kSmallChunksDefault = 4096;
+constexpr int kMultiStreamsMax = 4;  // decode_multi fan-out: the caller's stream + 3 pool streams
 
 struct Knob {
     std::atomic<int> v;
@@ -252,6 +253,8 @@ struct Tuning {
                             //   passes of at most 64 tiles per slot, else 1; tools/grid_sweep.py,
                             //   tools/c3_size_sweep.py)
     Knob multi_list{1};     // heterogeneous decode: stripe-list stream launches (else pointer tables)
+    Knob multi_streams{1};  //   its per-pattern launches spread over this many streams (1: all on the
+                            //   caller's; the others fork from it and join back, decode_multi_pool)
     Knob bitslice{1};       // 8-output passes: run-time compiled bitsliced kernel (ecamd_jit.hip);
                             //   1 once compiled (LDS tables meanwhile), 2 wait for the compile, 0 off
     Knob bitslice_min_rows{5};   // fewest outputs of a row group that take the bitsliced kernel
@@ -1108,10 +1111,27 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
     // row widths 2 / 4 / 8 divide 8, so a pass lies in one group)
     std::vector<int64_t> bs_done(static_cast<size_t>((map->R + 7) / 8), 0);
     // launches small enough for gf16_small_kernel skip the bitsliced one: a per-call 64 KiB object
-    // (6.5 KiB fragments) paid a 12 us one-tile bitsliced launch and a 12 us small launch for the rest
-    const bool small = (bs_all + 15) / 16 * nstripes <= g_tune.small_chunks;
+    // (6.5 KiB fragments) paid a 12 us one-tile bitsliced launch and a 12 us small launch for the rest.
+    // Only when small_launch() takes EVERY pass of the row group: a pass it declines (permuted survivors,
+    // unaligned bases) would otherwise get the stream kernel over the whole fragment
+    auto group_small = [&](int g) {
+        if ((bs_all + 15) / 16 * nstripes > g_tune.small_chunks) return false;
+        bool any = false;
+        for (const auto& p : map->passes) {
+            if (p.row0 / 8 != g) continue;
+            ApplyArgs a = base_args;
+            a.ncols = p.ncols;
+            a.nrows = std::min(p.width, map->R - p.row0);
+            for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[p.col0 + j];
+            for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[p.row0 + r];
+            if (!small_launch(a, bs_all, nstripes)) return false;
+            any = true;
+        }
+        return any;
+    };
     if constexpr (!PTRS) {
-        for (int g = 0; g * 8 < map->R && !small; g++) {
+        for (int g = 0; g * 8 < map->R; g++) {
+            if (group_small(g)) continue;
             int brc = 0;
             bs_done[static_cast<size_t>(g)] = launch_bitslice(map, g * 8, std::min(8, map->R - g * 8), base_args, in_off, out_off,
                                          bs_all, nstripes, st, &brc);
@@ -1727,19 +1747,44 @@ void stream_use_end(int dev, void* stream)
 int stream_scratch(int dev, void* stream, int slot, size_t words, uint32_t** out)
 {
     if (slot < 0 || slot >= kStreamScratchSlots) return fail(ECAMD_EINVAL, "scratch slot %d", slot);
-    std::lock_guard<std::mutex> lk(g_ctx_mu);
-    StreamCtx& c = ctx_of(dev, stream);
-    uint32_t*& p = c.scratch[slot];
-    size_t& n = c.scratch_words[slot];
-    if (n < words) {
-        if (p) {  // calls on one stream are ordered: the old slot is free once the stream drains
-            HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-            HIP_TRY(hipFree(p));
-            p = nullptr;
-            n = 0;
+    const size_t want = std::max<size_t>(words, 1);
+    // Growing a slot drains this stream and frees the old buffer: done with g_ctx_mu RELEASED, so framed
+    // calls on other streams never wait behind this one (the slot is taken out of the context first;
+    // the caller is inside a StreamUse, so the context itself is not released meanwhile)
+    uint32_t* old = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        StreamCtx& c = ctx_of(dev, stream);
+        if (c.scratch_words[slot] >= words && c.scratch[slot]) {
+            *out = c.scratch[slot];
+            return 0;
         }
-        HIP_TRY(hipMalloc(&p, std::max<size_t>(words, 1) * sizeof(uint32_t)));
-        n = std::max<size_t>(words, 1);
+        old = c.scratch[slot];
+        c.scratch[slot] = nullptr;
+        c.scratch_words[slot] = 0;
+    }
+    if (old) {  // calls on one stream are ordered: the old slot is free once the stream drains
+        HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+        HIP_TRY(hipFree(old));
+    }
+    uint32_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, want * sizeof(uint32_t)));
+    uint32_t* spare = nullptr;  // another thread on the same stream installed one meanwhile
+    {
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        StreamCtx& c = ctx_of(dev, stream);
+        if (c.scratch[slot] && c.scratch_words[slot] >= want) {
+            spare = p;
+            p = c.scratch[slot];
+        } else {
+            spare = c.scratch[slot];
+            c.scratch[slot] = p;
+            c.scratch_words[slot] = want;
+        }
+    }
+    if (spare) {
+        HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+        HIP_TRY(hipFree(spare));
     }
     *out = p;
     return 0;
@@ -2384,6 +2429,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.grid_mult = std::max(0, std::min(value, 64));
     } else if (k == "multi_list") {
         g_tune.multi_list = value;
+    } else if (k == "multi_streams") {
+        g_tune.multi_streams = value < 1 ? 1 : std::min(value, kMultiStreamsMax);
     } else if (k == "bitslice") {
         g_tune.bitslice = value;
     } else if (k == "bitslice_min_rows") {
@@ -2642,6 +2689,47 @@ int ecamd_xor_apply_ptrs(const uint32_t* masks, int R, int K, const void* const*
                             static_cast<hipStream_t>(stream));
 }
 
+}  // extern "C"
+
+namespace {
+// decode_multi's fan-out: a heterogeneous batch runs one launch per erasure pattern, each over only that
+// pattern's stripes -- short launches, each with its own ramp and tail.  With knob multi_streams N > 1
+// the launches go round-robin to the caller's stream and N - 1 pool streams of the device, which wait
+// for everything the caller's stream holds (fork event) and are waited for at the end (one event each):
+// the dispatcher then overlaps one launch's tail with the next one's start.  The pool mutex is held from
+// the fork to the join, so two callers never interleave their record / wait pairs on its events.
+struct MultiPool {
+    std::mutex mu;
+    hipStream_t s[kMultiStreamsMax] = {};
+    hipEvent_t done[kMultiStreamsMax] = {};
+    hipEvent_t fork = nullptr;
+    bool ready = false;
+};
+
+MultiPool& multi_pool(int dev)
+{
+    static std::mutex m;
+    static auto& pools = *new std::map<int, MultiPool>();  // never destroyed: no HIP call at exit
+    std::lock_guard<std::mutex> lk(m);
+    return pools[dev];
+}
+
+// Creates the pool's streams and events once (pool.mu held); false when HIP refuses.
+bool multi_pool_ready(MultiPool& p)
+{
+    if (p.ready) return true;
+    bool ok = hipEventCreateWithFlags(&p.fork, hipEventDisableTiming) == hipSuccess;
+    for (int i = 1; ok && i < kMultiStreamsMax; i++)
+        ok = hipStreamCreateWithFlags(&p.s[i], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&p.done[i], hipEventDisableTiming) == hipSuccess;
+    (void)hipGetLastError();
+    p.ready = ok;
+    return ok;
+}
+}  // namespace
+
+extern "C" {
+
 int ecamd_rs_encode(int k, int m, void* base, int64_t stripe_stride, int64_t frag_stride,
                     int64_t blocksize, int nstripes, void* stream)
 {
@@ -2714,6 +2802,29 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
     if (rc) return rc;
     auto* d_table = static_cast<uint8_t**>(up.dev);
     auto* d_list = static_cast<const int32_t*>(up.dev);
+    // knob multi_streams: the launches of the patterns round-robin over the caller's stream and pool
+    // streams forked from it (MultiPool); the pool streams join back before the upload is released
+    int nonempty = 0;
+    for (const auto& g : groups) nonempty += g.first.empty() ? 0 : 1;
+    const int fan = use_list ? std::min<int>(static_cast<int>(g_tune.multi_streams), nonempty) : 1;
+    MultiPool* pool = fan > 1 ? &multi_pool(dev) : nullptr;
+    std::unique_lock<std::mutex> plk;
+    if (pool) {
+        plk = std::unique_lock<std::mutex>(pool->mu);
+        if (!multi_pool_ready(*pool)) {
+            plk.unlock();
+            pool = nullptr;
+        } else {
+            bool ok = hipEventRecord(pool->fork, static_cast<hipStream_t>(stream)) == hipSuccess;
+            for (int i = 1; ok && i < fan; i++) ok = hipStreamWaitEvent(pool->s[i], pool->fork, 0) == hipSuccess;
+            if (!ok) {  // nothing launched on the pool yet: run everything on the caller's stream
+                (void)hipGetLastError();
+                plk.unlock();
+                pool = nullptr;
+            }
+        }
+    }
+    int turn = 0;
     size_t at = 0;
     for (const auto& g : groups) {
         const int G = static_cast<int>(g.second.size());
@@ -2744,14 +2855,25 @@ int ecamd_rs_decode_multi(int k, int m, const int* missing, int missing_stride,
             a.out_base = static_cast<uint8_t*>(base);
             a.in_stride = a.out_stride = stripe_stride;
             a.stripe_list = sl;
+            const int lane = pool ? turn++ % fan : 0;
             rc = launch_gf16<false>(e->map.get(), a, in_off.data(), out_off.data(), blocksize, G,
-                                    static_cast<hipStream_t>(stream));
+                                    lane ? pool->s[lane] : static_cast<hipStream_t>(stream));
         } else {
             rc = ecamd_map_apply_ptrs(e->map.get(), reinterpret_cast<const void* const*>(t), row,
                                       e->inputs.data(), reinterpret_cast<void* const*>(t), row,
                                       e->outputs.data(), blocksize, G, stream);
         }
         if (rc) break;
+    }
+    if (pool) {  // join: the caller's stream waits for every pool stream's launches (also after an error)
+        for (int i = 1; i < fan; i++) {
+            if (hipEventRecord(pool->done[i], pool->s[i]) != hipSuccess ||
+                hipStreamWaitEvent(static_cast<hipStream_t>(stream), pool->done[i], 0) != hipSuccess) {
+                (void)hipGetLastError();
+                if (!rc) rc = fail(ECAMD_EHIP, "decode_multi: joining the pool streams failed");
+            }
+        }
+        plk.unlock();
     }
     const int rc2 = up.end(stream);
     return rc ? rc : rc2;
@@ -3094,6 +3216,9 @@ int ecamd_rs_kernel_form(int k, int m, const int* missing, int dest, int rebuild
     auto rank = [](int form) { return form == ECAMD_FORM_UNAVAILABLE ? 3 : form == ECAMD_FORM_COMPILING ? 2
                                                                         : form == ECAMD_FORM_BITSLICED ? 1 : 0; };
     int form = ECAMD_FORM_TABLES;
+    // one stripe of plain fragments this short takes gf16_small_kernel (launch_gf16's group_small): no
+    // bitsliced launch, and no compile started for one
+    if ((blocksize + 15) / 16 <= g_tune.small_chunks) return form;
     for (int row0 = 0; row0 < R && K > 0; row0 += 8) {
         const int nrows = std::min(8, R - row0);
         BsForm f;

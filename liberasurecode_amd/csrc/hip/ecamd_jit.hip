@@ -538,7 +538,11 @@ int bitslice_prebuild(const std::vector<int>& coeff, int R, int K, int depth, bo
         const std::string co = dir + "/" + object_name(e) + ".co";
         std::string code;
         if (!read_file(co, code)) {
-            const std::string req_path = co + ".req." + std::to_string(getpid());
+            // unique per call: prebuild.py runs several of these threads at once, and two of them (or a
+            // cap retry) may resolve to the same code object; ecamd_jitc renames its output into place
+            static std::atomic<unsigned> seq{0};
+            const std::string req_path = co + ".req." + std::to_string(getpid()) + "." +
+                                         std::to_string(seq.fetch_add(1, std::memory_order_relaxed));
             {
                 std::ofstream f(req_path);
                 f << request_of(e);

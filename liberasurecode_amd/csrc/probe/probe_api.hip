@@ -172,6 +172,16 @@ int ecamd_probe_mix2(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
 int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int order, int wave_contig,
                      void* base, int64_t bs, int K, int R, int nstripes, const int* frag, void* stream)
 {
+    return ecamd_probe_mix4(lp, sp, ch, threads, std::max(1, wgs_per_cu), -order - 1, wave_contig, base, bs, K, R,
+                            nstripes, frag, stream);
+}
+
+// cap_per_cu < 0 carries mix3's tile order (-order - 1) with no cap; >= 0 is the per-CU cap (order 0)
+int ecamd_probe_mix4(int lp, int sp, int ch, int threads, int wgs_per_cu, int cap_per_cu, int wave_contig,
+                     void* base, int64_t bs, int K, int R, int nstripes, const int* frag, void* stream)
+{
+    const int order = cap_per_cu < 0 ? -cap_per_cu - 1 : 0;
+    const int cap = cap_per_cu < 0 ? 0 : cap_per_cu;
     int dev = 0;
     int rc = ensure_device(&dev);
     if (rc) return rc;
@@ -190,19 +200,21 @@ int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
     }
     a.tiles_per_stripe = static_cast<uint32_t>(bs / span);
     a.ntiles = a.tiles_per_stripe * static_cast<uint32_t>(nstripes);
-    const int grid = static_cast<int>(std::min<int64_t>(a.ntiles,
-                                                        static_cast<int64_t>(cu_count(dev)) * std::max(1, wgs_per_cu)));
+    const int grid = wgs_per_cu <= 0 ? static_cast<int>(a.ntiles)
+                                     : static_cast<int>(std::min<int64_t>(
+                                           a.ntiles, static_cast<int64_t>(cu_count(dev)) * wgs_per_cu));
+    const size_t lds = cap > 0 ? (static_cast<size_t>(160 * 1024) / static_cast<size_t>(cap)) & ~size_t(511) : 0;
     hipStream_t st = static_cast<hipStream_t>(stream);
     bool launched = false;
-#define ECAMD_MIX(LP, SP)                                                                         \
-    if (!launched && lp == LP && sp == SP) {                                                      \
-        if (ch == 1)                                                                              \
-            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 1>), dim3(grid), dim3(threads), 0, st, a); \
-        else if (ch == 2)                                                                         \
-            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 2>), dim3(grid), dim3(threads), 0, st, a); \
-        else                                                                                      \
-            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 4>), dim3(grid), dim3(threads), 0, st, a); \
-        launched = true;                                                                          \
+#define ECAMD_MIX(LP, SP)                                                                           \
+    if (!launched && lp == LP && sp == SP) {                                                        \
+        if (ch == 1)                                                                                \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 1>), dim3(grid), dim3(threads), lds, st, a); \
+        else if (ch == 2)                                                                           \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 2>), dim3(grid), dim3(threads), lds, st, a); \
+        else                                                                                        \
+            hipLaunchKernelGGL((mix_probe_kernel<LP, SP, 4>), dim3(grid), dim3(threads), lds, st, a); \
+        launched = true;                                                                            \
     }
     ECAMD_MIX_POLICIES(ECAMD_MIX)
 #undef ECAMD_MIX

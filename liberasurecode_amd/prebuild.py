@@ -22,16 +22,50 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 JIT_DIR = os.path.join(HERE, "lib", "jit")
 
 # (k, m, missing or None, dest, rebuild_parity): the operations of BASELINE.json configs[1..4] that
-# bench.py times, plus __graft_entry__.smoke()'s (rs_vand, k = 10, m = 4).
+# bench.py times, plus __graft_entry__.smoke()'s (rs_vand, k = 10, m = 4) ...
 C3_LOST = [[0, 1, 2, 3], [0, 5, 10, 13]]
 C5_LOST = [list(range(8)), [0, 2, 4, 6, 20, 22, 24, 26]]
-OPS = (
+BENCH_OPS = (
     [(4, 2, None, -1, 1), (4, 2, [0, 1], -1, 1), (4, 2, [0, 4], -1, 1)]  # C2
     + [(10, 4, None, -1, 1)] + [(10, 4, p, -1, 1) for p in C3_LOST]  # C3 (and C4's shards)
     + [(10, 4, [d], d, 0) for d in (3, 12)] + [(10, 4, [0, 5, 10, 13], 13, 0)]  # C3 reconstruct, smoke
     + [(20, 8, None, -1, 1)] + [(20, 8, p, -1, 1) for p in C5_LOST]  # C5
     + [(20, 8, C5_LOST[0], d, 0) for d in C5_LOST[0]]  # C5: 8 single-destination reconstructs
+    + [(10, 4, p, -1, 1) for p in ([4, 5, 6, 7], [2, 3, 8, 9])]  # tools/multi_bench.py's other patterns
 )
+
+
+# ... and the maps real rebuild traffic uses: for each BASELINE code, every single-loss
+# decode (the API's liberasurecode_decode asks rebuild_parity 1, frontend.cpp rs_decode) and every
+# single-destination reconstruct with that one fragment lost (Swift's reconstructor,
+# liberasurecode_reconstruct_fragment); for Swift's default (10, 4) every 2-, 3- and 4-loss decode as
+# well -- all 1,470 erasure patterns (≈3 min on 8 cores, ≈39 MB of code objects; DESIGN.md §4 "Shipped
+# kernels").  ECAMD_PREBUILD_FULL=0 stops at the 2-loss decodes (≈25 s, ≈3 MB).  Maps that take the LDS
+# tables by shape (k = 4's 1-2-output maps) build nothing.
+def rebuild_ops(full=False):
+    from itertools import combinations
+    ops = []
+    for k, m in ((10, 4), (4, 2), (20, 8)):
+        n = k + m
+        ops += [(k, m, [f], -1, 1) for f in range(n)]
+        ops += [(k, m, [f], f, 0) for f in range(n)]
+    ops += [(10, 4, list(c), -1, 1) for c in combinations(range(14), 2)]
+    if full:
+        ops += [(10, 4, list(c), -1, 1) for r in (3, 4) for c in combinations(range(14), r)]
+    return ops
+
+
+def all_ops(full=None):
+    if full is None:
+        full = os.environ.get("ECAMD_PREBUILD_FULL", "1") != "0"
+    seen, out = set(), []
+    for op in list(BENCH_OPS) + rebuild_ops(full):
+        key = (op[0], op[1], tuple(op[2]) if op[2] is not None else None, op[3], op[4])
+        if key not in seen:
+            seen.add(key)
+            out.append(op)
+    return out
+
 # (backend, k, m, hd): the CHKSUM_CRC32 framed encode's codec-and-checksum kernel, one per code whatever
 # the object size -- Swift's default rs_vand (10, 4) (whole objects and 1 MiB segments alike), the
 # other BASELINE codes, and flat_xor_hd (3, 3, 3)
@@ -42,7 +76,7 @@ def _ints(v):
     return (C.c_int * (len(v) + 1))(*(list(v) + [-1]))
 
 
-def prebuild(arch="gfx950", jobs=8, verbose=False):
+def prebuild(arch="gfx950", jobs=8, verbose=False, full=None):
     lib = C.CDLL(os.path.join(HERE, "lib", "libecamd.so"))
     lib.ecamd_bitslice_prebuild.restype = C.c_int
     lib.ecamd_bitslice_prebuild.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_char_p]
@@ -67,7 +101,7 @@ def prebuild(arch="gfx950", jobs=8, verbose=False):
         return op, rc
 
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        results = list(ex.map(one, list(OPS) + [("frame",) + c for c in FRAME_CODES]))
+        results = list(ex.map(one, all_ops(full) + [("frame",) + c for c in FRAME_CODES]))
     bad = [(op, rc) for op, rc in results if rc < 0]
     if verbose:
         for op, rc in results:

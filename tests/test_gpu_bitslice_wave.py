@@ -120,3 +120,34 @@ def test_narrow_knob_off_keeps_tables():
         for key, v in KNOBS.items():
             d.ecamd_tune(key.encode(), v)
         lay.buf.free()
+
+
+@pytest.mark.parametrize("streams", [1, 4])
+def test_decode_multi_patterns_bitsliced(streams):
+    """ecamd_rs_decode_multi over a heterogeneous (10, 4) batch -- the four patterns tools/multi_bench.py
+    times plus ones no build ships ({1,2,3,4}, {5,9,11}) and single / 2-loss ones -- every group on the
+    bitsliced kernel (knob bitslice 2 compiles what is not shipped), stripe lists in the default
+    one-wave form, byte-exact against the oracle's decode of each stripe; knob multi_streams 4 spreads
+    the per-pattern launches over the caller's stream and 3 forked pool streams."""
+    d = _lib.dev()
+    d.ecamd_tune(b"bitslice", 2)
+    d.ecamd_tune(b"multi_streams", streams)
+    d.ecamd_tune(b"small_chunks", 0)
+    try:
+        k, m, bs, S = 10, 4, 4096 * 3, 48
+        pats = [[0, 1, 2, 3], [4, 5, 6, 7], [0, 5, 10, 13], [2, 3, 8, 9], [1, 2, 3, 4], [6], [2, 7], [5, 9, 11]]
+        per = [pats[s % len(pats)] for s in range(S)]
+        lay, want = _batch(k, m, bs, S, 41)
+        host = want.copy()
+        for s, p in enumerate(per):
+            host[s, p] = 0xC3
+        lay.upload_stripes(host)
+        n0 = _launches()
+        D.rs_decode_multi(k, m, per, lay)
+        assert _launches() - n0 >= len(pats)
+        assert (lay.download_stripes() == want).all()
+        lay.buf.free()
+    finally:
+        d.ecamd_tune(b"multi_streams", 1)
+        d.ecamd_tune(b"small_chunks", -1)
+        d.ecamd_tune(b"bitslice", 1)

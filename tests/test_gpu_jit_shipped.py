@@ -64,6 +64,12 @@ def test_fresh_process_runs_shipped_bitsliced_at_first_launch(tmp_path):
     assert out["decode_other_form"] == COMPILING and out["decode_other_bitsliced_launches"] == 0, out
     assert out["encode_exact"] and out["decode_shipped_exact"] and out["decode_other_exact"], out
     assert out["frame_bitsliced_launches"] > 0 and out["frame_exact"], out  # ecamd_frame_prebuild
+    for name in ("reconstruct6", "decode_2_7"):  # rebuild traffic's maps, never benched (prebuild.rebuild_ops)
+        assert out[name + "_form"] == BITSLICED and out[name + "_bitsliced_launches"] > 0, out
+        assert out[name + "_exact"], out
+    # a small one-stripe operation: gf16_small_kernel, reported as such (no compile started for it)
+    assert out["small16k_form"] == TABLES and out["small16k_bitsliced_launches"] == 0, out
+    assert out["small16k_exact"], out
 
 
 def test_without_helper_shipped_maps_still_bitsliced(tmp_path):
@@ -74,13 +80,16 @@ def test_without_helper_shipped_maps_still_bitsliced(tmp_path):
     assert out["decode_other_form"] == UNAVAILABLE and out["decode_other_bitsliced_launches"] == 0, out
     assert out["encode_exact"] and out["decode_shipped_exact"] and out["decode_other_exact"], out
     assert out["frame_bitsliced_launches"] > 0 and out["frame_exact"], out
+    for name in ("reconstruct6", "decode_2_7"):
+        assert out[name + "_form"] == BITSLICED and out[name + "_bitsliced_launches"] > 0, out
+        assert out[name + "_exact"], out
 
 
 def test_without_helper_or_shipped_objects_tables_serve(tmp_path):
     out = _run(tmp_path, _copy_libs(tmp_path, False))
-    for name in ("encode", "decode_shipped", "decode_other", "frame"):
+    for name in ("encode", "decode_shipped", "decode_other", "frame", "reconstruct6", "decode_2_7"):
         assert out[name + "_bitsliced_launches"] == 0, out
-    for name in ("encode", "decode_shipped", "decode_other"):
+    for name in ("encode", "decode_shipped", "decode_other", "reconstruct6", "decode_2_7"):
         assert out[name + "_form"] == UNAVAILABLE, out
         assert out[name + "_exact"], out
     assert out["frame_exact"], out

@@ -183,18 +183,21 @@ def test_long_batch_split_into_launches():
     lay.buf.free()
 
 
+@pytest.mark.parametrize("streams", [1, 3])
 @pytest.mark.parametrize("tiles_per_slot", [0, 1])
 @pytest.mark.parametrize("k,m,bs,S", [(10, 4, 65536 + 6, 64), (4, 2, 4096, 200), (20, 8, 8192, 40)])
-def test_decode_multi_heterogeneous(k, m, bs, S, tiles_per_slot):
+def test_decode_multi_heterogeneous(k, m, bs, S, tiles_per_slot, streams):
     """Every stripe lost its own set of fragments (including none, all-parity and
     m-missing cases); one call rebuilds them all, each equal to the oracle's decode of that
     stripe on the same (inconsistent, garbage-filled) buffers.  tiles_per_slot 1: the stripe-list
     launches split into several."""
     _lib.check(_lib.dev().ecamd_tune(b"tiles_per_slot", tiles_per_slot), "tune")
+    _lib.check(_lib.dev().ecamd_tune(b"multi_streams", streams), "tune")  # per-pattern launches on 3 streams
     try:
         _decode_multi_case(k, m, bs, S)
     finally:
         _lib.dev().ecamd_tune(b"tiles_per_slot", 0)
+        _lib.dev().ecamd_tune(b"multi_streams", 1)
 
 
 def _decode_multi_case(k, m, bs, S):

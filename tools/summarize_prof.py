@@ -83,6 +83,8 @@ def main():
                     help="label:kernel-substring:first:count -- stats over dispatches [first, "
                          "first+count) of that kernel in dispatch order (repeatable)")
     args = ap.parse_args()
+    if not args.command.strip():  # bench.py quotes a summary only for the command it names
+        ap.error("--command: the exact profiled command line is required")
     g = os.path.join(ROOT, "gpurun_out")
     pre = f"prof_{{}}_{args.cfg}"
     out = {"config": args.cfg, "round": args.round, "command": args.command,
