@@ -95,6 +95,18 @@ void ecamd_map_destroy(ecamd_map *map);
 int ecamd_map_apply_strided(const ecamd_map *map, const void *in_base, int64_t in_stripe_stride,
                             const int64_t *in_off, void *out_base, int64_t out_stripe_stride,
                             const int64_t *out_off, int64_t blocksize, int nstripes, void *stream);
+/* ecamd_map_apply_strided for ONE stripe, plus the CRC32 of every input and output fragment over its
+ * `blocksize` bytes -- zlib's crc32, or the legacy liberasurecode_crc32_alt when legacy != 0 -- written
+ * to crc_out[0 .. K + R) (inputs first; device or pinned host memory), all in ONE launch of the
+ * small-launch kernel.  Returns 0 when done, 1 when the shape does not fuse (nothing launched: more
+ * than 4096 16-byte chunks per fragment, several passes, tables and staged fragments over the LDS, ...;
+ * the caller runs ecamd_map_apply_strided and ecamd_crc32), < 0 on error.  The per-call CHKSUM_CRC32
+ * encode's checksums (src/erasurecode_postprocessing.c:37-69) without two more launches. */
+int ecamd_map_apply_strided_crc(const ecamd_map *map, const void *in_base, const int64_t *in_off, void *out_base,
+                                const int64_t *out_off, int64_t blocksize, int legacy, uint32_t *crc_out,
+                                void *stream);
+/* Launches of ecamd_map_apply_strided_crc that fused the checksums (tests pin which path ran). */
+long long ecamd_small_crc_launches(void);
 
 /* Pointer tables in device memory: input j of stripe s is d_in_ptrs[s*in_row + in_col[j]],
  * output r is d_out_ptrs[s*out_row + out_col[r]] (in_col / out_col are host arrays). */

@@ -16,9 +16,11 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../host/bitslice.hpp"
+#include "../host/crc.hpp"
 #include "../host/gf16.hpp"
 #include "../host/tables.hpp"
 #include "ecamd.h"
@@ -245,6 +247,9 @@ struct Tuning {
     Knob stream_ch{1};      //   16-byte chunks per lane (1, 2; W = 8 always 1)
     Knob small_chunks{kSmallChunksDefault};  // strided launches of at most this many 16-byte chunks
                             //   per output row at a uniform pitch: gf16_small_kernel (0 = never)
+    Knob small_crc_dbg{0};  //   development A/B of the fused small-launch CRC (SmallArgs::crc_dbg)
+    Knob small_stage{1};    //   gf16_small_kernel: stage the inputs into LDS with 16-byte loads first
+                            //   (one stripe, 16-byte pitch; 1 = whenever the LDS holds them, 0 = never)
     Knob small_lane{0};     //   gf16_small_kernel: bytes per lane (2, 4 or 16; 0: 2 when one workgroup
                             //   covers the pass that way, else 4 -- DESIGN.md §6)
     Knob xor_wgs{0};        // xor_stream_kernel: 256-thread workgroups per CU (0 = by shape, see
@@ -645,8 +650,18 @@ SmallArgs small_args(const ApplyArgs& a, int64_t bs, int nstripes, int lane)
     return s;
 }
 
+// The fused checksum of a small launch (gf16_small_kernel CRC): the device image, where the CRCs go,
+// the partials' scratch and the machine.
+struct SmallCrcReq {
+    const uint32_t* img[2];  // build_small_crc_image for 2- and 4-byte lanes
+    uint32_t* out;
+    uint32_t* part;
+    bool legacy;
+};
+
+// ECAMD_EINVAL (nothing launched) when `crc` is given and the launch cannot fuse it.
 int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
-                 hipStream_t st)
+                 hipStream_t st, const SmallCrcReq* crc = nullptr)
 {
     const int lane = g_tune.small_lane ? static_cast<int>(g_tune.small_lane)
                                        : ((bs + 1) / 2 * nstripes <= 256 ? 2 : 4);
@@ -654,12 +669,49 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
     SmallArgs s = small_args(a, bs, nstripes, lane);
     s.tables = tables + p.offset;
     const dim3 grid(static_cast<unsigned>((s.nchunks + 255) / 256)), block(256);
-    const size_t lds = p.bytes;
-#define SMALL_(W)                                                                                 \
-    switch (lane) {                                                                               \
-    case 2: hipLaunchKernelGGL((gf16_small_kernel<W, 2>), grid, block, lds, st, s); break;          \
-    case 16: hipLaunchKernelGGL((gf16_small_kernel<W, 16>), grid, block, lds, st, s); break;        \
-    default: hipLaunchKernelGGL((gf16_small_kernel<W, 4>), grid, block, lds, st, s); break;         \
+    // staged inputs (gf16_small_kernel ST): one stripe, inputs at a 16-byte pitch from a 16-byte
+    // aligned base, the workgroup's 256 * lane bytes of every input beside the tables in LDS
+    const size_t stage = static_cast<size_t>(crc ? a.ncols + a.nrows : a.ncols) * 256 * lane +
+                         (crc ? static_cast<size_t>(small_crc_words(lane)) * 4 : 0);
+    const bool st_in = (g_tune.small_stage || crc) && nstripes == 1 && (s.in_pitch % 16) == 0 && aligned16(s.in) &&
+                       p.bytes + stage <= kLdsBytes &&
+                       (a.ncols - 1) * s.in_pitch + bs < (int64_t(1) << 31);
+    const size_t lds = p.bytes + (st_in ? stage : 0);
+    if (crc) {
+        // the region-shift maps reach 63 regions past a workgroup's: at most 64 workgroups
+        if (!st_in || (lane != 2 && lane != 4) || a.accumulate || grid.x > 64) return ECAMD_EINVAL;
+        s.crc_img = crc->img[lane == 2 ? 0 : 1];
+        const SmallCrcConst k = small_crc_const(crc->legacy, static_cast<uint64_t>(bs),
+                                                static_cast<uint64_t>(grid.x) * 256 * lane - static_cast<uint64_t>(bs));
+        s.crc_out = crc->out;
+        s.crc_dbg = static_cast<int>(g_tune.small_crc_dbg);
+        s.crc_part = crc->part;
+        std::copy(k.minv, k.minv + 32, s.crc_minv);
+        s.crc_c = k.c;
+#define SMALLC_(W)                                                                                          \
+    if (lane == 2)                                                                                          \
+        hipLaunchKernelGGL((gf16_small_kernel<W, 2, true, true>), grid, block, lds, st, s);                 \
+    else                                                                                                    \
+        hipLaunchKernelGGL((gf16_small_kernel<W, 4, true, true>), grid, block, lds, st, s);
+        if (width == 2) {
+            SMALLC_(2)
+        } else if (width == 4) {
+            SMALLC_(4)
+        } else {
+            SMALLC_(8)
+        }
+#undef SMALLC_
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+#define SMALL_(W)                                                                                           \
+    switch (lane * 2 + (st_in ? 1 : 0)) {                                                                   \
+    case 4: hipLaunchKernelGGL((gf16_small_kernel<W, 2, false>), grid, block, lds, st, s); break;          \
+    case 5: hipLaunchKernelGGL((gf16_small_kernel<W, 2, true>), grid, block, lds, st, s); break;           \
+    case 32: hipLaunchKernelGGL((gf16_small_kernel<W, 16, false>), grid, block, lds, st, s); break;        \
+    case 33: hipLaunchKernelGGL((gf16_small_kernel<W, 16, true>), grid, block, lds, st, s); break;         \
+    case 9: hipLaunchKernelGGL((gf16_small_kernel<W, 4, true>), grid, block, lds, st, s); break;           \
+    default: hipLaunchKernelGGL((gf16_small_kernel<W, 4, false>), grid, block, lds, st, s); break;         \
     }
     if (width == 2) {
         SMALL_(2)
@@ -1769,6 +1821,8 @@ int stream_scratch(int dev, void* stream, int slot, size_t words, uint32_t** out
     }
     uint32_t* p = nullptr;
     HIP_TRY(hipMalloc(&p, want * sizeof(uint32_t)));
+    // zeroed once: the small-launch CRC's counter must start at 0 (it resets itself after every launch)
+    HIP_TRY(hipMemsetAsync(p, 0, want * sizeof(uint32_t), static_cast<hipStream_t>(stream)));
     uint32_t* spare = nullptr;  // another thread on the same stream installed one meanwhile
     {
         std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -2419,6 +2473,10 @@ int ecamd_tune(const char* key, int value)
         g_tune.stream = value != 0;
     } else if (k == "small_lane") {
         g_tune.small_lane = value == 16 || value == 4 || value == 2 ? value : 0;
+    } else if (k == "small_crc_dbg") {
+        g_tune.small_crc_dbg = value < 0 ? 0 : value;
+    } else if (k == "small_stage") {
+        g_tune.small_stage = value < 0 ? 1 : value != 0;
     } else if (k == "small_chunks") {
         g_tune.small_chunks = value < 0 ? kSmallChunksDefault : value;
     } else if (k == "stream_ch") {
@@ -2626,6 +2684,77 @@ int ecamd_map_apply_strided(const ecamd_map* map, const void* in_base, int64_t i
     return launch_gf16<false>(map, a, in_off, out_off, blocksize, nstripes,
                               static_cast<hipStream_t>(stream));
 }
+
+}  // extern "C"
+
+namespace {
+std::atomic<long long> g_small_crc_launches{0};
+
+// The fused small-launch CRC image of (dev, machine, lane bytes G) (host/crc.hpp build_small_crc_image).
+int small_crc_image(int dev, bool legacy, int G, const uint32_t** out)
+{
+    static std::mutex mu;
+    static auto& images = *new std::map<std::tuple<int, bool, int>, uint32_t*>();  // never freed: no HIP call at exit
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = images.find({dev, legacy, G});
+    if (it == images.end()) {
+        const std::vector<uint32_t> w = build_small_crc_image(CrcMachine(legacy), G);
+        if (w.size() != static_cast<size_t>(small_crc_words(G))) return fail(ECAMD_EINVAL, "small CRC image layout");
+        uint32_t* d = nullptr;
+        HIP_TRY(hipMalloc(&d, w.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(d, w.data(), w.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        it = images.emplace(std::make_tuple(dev, legacy, G), d).first;
+    }
+    *out = it->second;
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int ecamd_map_apply_strided_crc(const ecamd_map* map, const void* in_base, const int64_t* in_off, void* out_base,
+                                const int64_t* out_off, int64_t blocksize, int legacy, uint32_t* crc_out,
+                                void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!map || !in_off || !out_off || !crc_out) return fail(ECAMD_EINVAL, "null argument");
+    if (blocksize <= 0) return 1;
+    bool ok = aligned16(in_base) && aligned16(out_base);
+    for (int j = 0; j < map->K; j++) ok = ok && (in_off[j] % 16) == 0;
+    for (int r = 0; r < map->R; r++) ok = ok && (out_off[r] % 16) == 0;
+    if (!ok) return fail(ECAMD_EINVAL, "fragment addresses must be 16-byte aligned");
+    // one pass over every input and output row (the small kernel's single launch)
+    if (map->passes.size() != 1 || map->K + map->R > 64) return 1;
+    const auto& p = map->passes[0];
+    if (p.col0 != 0 || p.ncols != map->K || p.row0 != 0 || std::min(p.width, map->R) != map->R) return 1;
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(in_base);
+    a.out_base = static_cast<uint8_t*>(out_base);
+    a.tables = map->d_tables + p.offset;
+    a.bs = blocksize;
+    a.ncols = p.ncols;
+    a.nrows = map->R;
+    for (int j = 0; j < p.ncols; j++) a.in_off[j] = in_off[j];
+    for (int r = 0; r < a.nrows; r++) a.out_off[r] = out_off[r];
+    if (!small_launch(a, blocksize, 1)) return 1;
+    SmallCrcReq req{};
+    req.out = crc_out;
+    req.legacy = legacy != 0;
+    if ((rc = small_crc_image(dev, req.legacy, 2, &req.img[0])) || (rc = small_crc_image(dev, req.legacy, 4, &req.img[1])))
+        return rc;
+    StreamUse use(dev, stream);
+    const size_t wgs = static_cast<size_t>((blocksize + 511) / 512 + 1);  // >= the launch's workgroups
+    if ((rc = stream_scratch(dev, stream, kSmallCrcScratchSlot, 16 + static_cast<size_t>(map->K + map->R) * wgs,
+                             &req.part)))
+        return rc;
+    rc = launch_small(a, p, blocksize, 1, map->d_tables, static_cast<hipStream_t>(stream), &req);
+    if (rc == 0) g_small_crc_launches.fetch_add(1, std::memory_order_relaxed);
+    return rc == ECAMD_EINVAL ? 1 : rc;
+}
+
+long long ecamd_small_crc_launches(void) { return g_small_crc_launches.load(std::memory_order_relaxed); }
 
 int ecamd_map_apply_ptrs(const ecamd_map* map, const void* const* d_in_ptrs, int in_row,
                          const int* in_col, void* const* d_out_ptrs, int out_row,

@@ -54,7 +54,10 @@ int side_join(int dev, void* stream);
 // Device scratch of `words` 32-bit words in slot 0..kStreamScratchSlots-1 of (dev, stream); calls
 // on one stream are ordered, so reuse is safe (slot 1 holds values that must outlive a CRC pass on
 // the same stream, whose partials use slot 0).
-constexpr int kStreamScratchSlots = 4;
+// Slot 4: the small-launch fused CRC's counter and partials (ecamd_map_apply_strided_crc).  A slot is
+// zeroed when it is (re)allocated.
+constexpr int kStreamScratchSlots = 5;
+constexpr int kSmallCrcScratchSlot = 4;
 int stream_scratch(int dev, void* stream, int slot, size_t words, uint32_t** out);
 // A framed call in progress on (dev, stream): its context is not released until the call has
 // returned and its work on the stream has completed.

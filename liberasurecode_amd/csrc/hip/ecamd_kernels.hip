@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ecamd_crc_dev.hpp"
 #include "ecamd_isa.hpp"
 #include "ecamd_kernels.hpp"
 
@@ -85,9 +86,27 @@ template __global__ void gf16_copy_apply_kernel<8>(const ApplyArgs);
 // those dependent kernel-argument fetches are most of the launch (kernel arguments in host memory,
 // HIP_FORCE_DEV_KERNARG=0: 9.7 -> 19.3 us; tools/small_kernel_probe.py).  SmallArgs is ~100 bytes
 // fetched up front, and every fragment address is base + j * pitch in registers.
-template <int W, int G>
+//
+// ST (staged inputs): the workgroup first copies its share of every input -- 256 * G bytes of each
+// fragment, one stripe -- into LDS with 16-byte buffer loads, all issued before one wait, and the lanes
+// read their G bytes from there.  Meant for inputs in pinned HOST memory (the per-call path with no H2D
+// DMA, ECAMD_PERCALL_ZEROCOPY_MODE bit 0): there each load instruction is a PCIe round trip, and
+// K dependent 2-4-byte loads per lane cost far more than one burst of wide ones.
+//
+// CRC (with ST, G = 2 or 4, one pass, one stripe): the payload CRC32 of every input and output fragment
+// in the same launch -- the per-call CHKSUM_CRC32 encode's checksums without the two launches of
+// ecamd_crc32.  The outputs join the staged inputs in LDS.  r0(X||Y) = A^|Y| r0(X) ^
+// r0(Y), so r0 of a region is the XOR over its 16-byte pieces l of A^(16 (NP - 1 - l)) r0(piece l):
+// lane l looks up r0 of its piece and its position map (two rounds of independent LDS lookups), the
+// wave XOR-reduces, and each wave works on up to 4 fragments at once.  A workgroup's region r0 goes
+// past the regions after it with the binary maps A^(REGION 2^i); the last workgroup to finish (a
+// self-resetting counter) XORs them: S = r0 of the fragment zero-extended to gridDim * REGION bytes,
+// then r0 = A^-zext S and crc = ~(A^len ~0 ^ r0) with host constants (crc_minv, crc_c).  Bytes past
+// bs are zero in LDS.
+template <int W, int G, bool ST, bool CRC>
 __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
 {
+    static_assert(!CRC || (ST && (G == 2 || G == 4)), "fused CRC: staged inputs, 2- or 4-byte lanes");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int D = W / 2;
     constexpr int EB = 2 * W;
@@ -113,20 +132,103 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
     };
     // the first lane-group's first four inputs are in flight while the tables stage
     uint32_t cur[4][ND], nxt[4][ND];
+    constexpr int REGION = 256 * G;  // ST: bytes of each input this workgroup stages
+    uint8_t* const stg = lds + K * TB;
+    const int64_t c0 = static_cast<int64_t>(blockIdx.x) * blockDim.x;
     auto fetch4 = [&](int64_t cc, int j0, uint32_t (&x)[4][ND]) {
         const int64_t s = cc / a.cpf;
         const int64_t off = (cc - s * a.cpf) * G;
         const int rem = a.bs - off < G ? static_cast<int>(a.bs - off) : G;
-        const uint8_t* in = a.in + s * a.in_stride + off;
+        if constexpr (ST) {  // one stripe, one chunk per lane: this lane's bytes of the staged region
+            const uint8_t* in = stg + (cc - c0) * G;
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (j0 + i < K) load(in + (j0 + i) * a.in_pitch, rem, x[i]);
+            for (int i = 0; i < 4; i++)
+                if (j0 + i < K) load(in + (j0 + i) * REGION, rem, x[i]);
+        } else {
+            const uint8_t* in = a.in + s * a.in_stride + off;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (j0 + i < K) load(in + (j0 + i) * a.in_pitch, rem, x[i]);
+        }
     };
-    if (c < a.nchunks) fetch4(c, 0, cur);
-    const int tbytes = K * TB;
-    for (int o = static_cast<int>(threadIdx.x) * 16; o < tbytes; o += static_cast<int>(blockDim.x) * 16)
-        *reinterpret_cast<uint4*>(lds + o) = load16(a.tables + o);
+    if constexpr (ST) {
+        // fragment j's bytes [c0 * G, c0 * G + REGION) as 16-byte pieces; bytes past bs are staged but
+        // never read.  The range ends at the last input's last 16-byte granule (the buffer unit checks
+        // whole dwords; a granule never crosses a page), so nothing past it is touched
+        const int64_t base = c0 * G;
+        const int64_t left = a.bs - base;
+        const int nseg = static_cast<int>(((left < REGION ? left : REGION) + 15) / 16);
+        const auto rin = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(a.in), 0, static_cast<int>((K - 1) * a.in_pitch + ((a.bs + 15) & ~int64_t(15))),
+            0x00020000);
+        // CRC: the whole region, zeros past bs (the checksum's zero extension).  Up to 8 loads per
+        // thread are in flight before the first LDS store: each is a PCIe round trip from host memory
+        const int nq = CRC ? REGION / 16 : nseg;
+        const int total = K * nq;
+        for (int i0 = static_cast<int>(threadIdx.x); i0 < total; i0 += 8 * static_cast<int>(blockDim.x)) {
+            u32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int idx = i0 + u * static_cast<int>(blockDim.x);
+                const int j = idx / nq, q = idx - j * nq;
+                v[u] = u32x4{0u, 0u, 0u, 0u};
+                if (idx < total && q < nseg)
+                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<int>(j * a.in_pitch + base + q * 16),
+                                                                 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int idx = i0 + u * static_cast<int>(blockDim.x);
+                if (idx >= total) break;
+                const int j = idx / nq, q = idx - j * nq;
+                if constexpr (CRC) {
+                    const int64_t keep = left - q * 16;  // bytes of this piece inside the fragment
+                    if (keep < 16) {
+#pragma unroll
+                        for (int d = 0; d < 4; d++) {
+                            const int64_t kd = keep - 4 * d;
+                            const uint32_t m = kd >= 4 ? 0xffffffffu : kd <= 0 ? 0u : (1u << (8 * kd)) - 1u;
+                            v[u][d] &= m;
+                        }
+                    }
+                }
+                *reinterpret_cast<u32x4*>(stg + j * REGION + q * 16) = v[u];
+            }
+        }
+    } else if (c < a.nchunks) {
+        fetch4(c, 0, cur);
+    }
+    // tables (and the CRC image) into LDS, 8 loads per thread in flight
+    auto stage = [&](uint8_t* dst, const uint8_t* src, int bytes) {
+        const int step = static_cast<int>(blockDim.x) * 16;
+        for (int o0 = static_cast<int>(threadIdx.x) * 16; o0 < bytes; o0 += 8 * step) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (o0 + u * step < bytes) v[u] = load16(src + o0 + u * step);
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (o0 + u * step < bytes) *reinterpret_cast<uint4*>(dst + o0 + u * step) = v[u];
+        }
+    };
+    stage(lds, a.tables, K * TB);
+    // CRC: the checksum image after the staged inputs and outputs
+    uint32_t* const cimg = reinterpret_cast<uint32_t*>(stg + (K + a.nrows) * REGION);
+    if constexpr (CRC)
+        if (!(a.crc_dbg & 2))
+            stage(reinterpret_cast<uint8_t*>(cimg), reinterpret_cast<const uint8_t*>(a.crc_img), small_crc_words(G) * 4);
     __syncthreads();
+    if constexpr (ST)
+        if (c < a.nchunks) fetch4(c, 0, cur);
+    if constexpr (CRC)  // a lane past the last chunk: its slot of every output region holds zeros
+        if (c >= a.nchunks)
+            for (int r = 0; r < a.nrows; r++) {
+                uint8_t* q = stg + (K + r) * REGION + (c - c0) * G;
+                if constexpr (G == 4)
+                    *reinterpret_cast<uint32_t*>(q) = 0u;
+                else
+                    *reinterpret_cast<uint16_t*>(q) = 0;
+            }
 
     for (; c < a.nchunks; c += step) {
         uint32_t acc[NW][D];
@@ -172,6 +274,14 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
                     o[d] = (r & 1) ? ((A >> 16) | (B & 0xffff0000u)) : ((A & 0xffffu) | (B << 16));
                 }
             }
+            if constexpr (CRC) {  // the output's bytes (zeros past bs) beside the staged inputs
+                const uint32_t m = rem >= G ? (G == 4 ? 0xffffffffu : 0xffffu) : (1u << (8 * rem)) - 1u;
+                uint8_t* l = stg + (K + r) * REGION + (c - c0) * G;
+                if constexpr (G == 4)
+                    *reinterpret_cast<uint32_t*>(l) = o[0] & m;
+                else
+                    *reinterpret_cast<uint16_t*>(l) = static_cast<uint16_t>(o[0] & m);
+            }
             uint8_t* q = out + r * a.out_pitch;
             if (a.accumulate) {
                 uint32_t prev[ND];
@@ -192,16 +302,89 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
         }
         if (c + step < a.nchunks) fetch4(c + step, 0, cur);
     }
+    if constexpr (CRC) {
+        using namespace crcdev;
+        constexpr int NP = REGION / 16;  // 16-byte pieces of a region: 32 or 64
+        const uint32_t* const pos = cimg + kSmallCrcPieceWords;  // A^(16 (NP - 1 - l)), l < NP
+        const uint32_t* const wgs = pos + NP * 128;             // A^(REGION 2^i), i < 6
+        const int lane = static_cast<int>(threadIdx.x) & 63, wave = static_cast<int>(threadIdx.x) >> 6;
+        const int nw = static_cast<int>(blockDim.x) >> 6;
+        const int nfr = K + a.nrows;
+        const int nwg = static_cast<int>(gridDim.x);
+        const int after = nwg - 1 - static_cast<int>(blockIdx.x);  // regions after this workgroup's
+        __syncthreads();  // every lane's outputs are in LDS
+        auto finish = [&](int f, uint32_t S) {  // S = r0 of fragment f zero-extended: the CRC
+            uint32_t r0 = 0;
+#pragma unroll
+            for (int b = 0; b < 32; b++)
+                if ((S >> b) & 1u) r0 ^= a.crc_minv[b];
+            a.crc_out[f] = ~(a.crc_c ^ r0);
+        };
+        for (int f0 = wave; f0 < nfr; f0 += 4 * nw) {
+            uint32_t s[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {  // up to 4 fragments per wave at once: independent lookups
+                const int f = f0 + i * nw;
+                s[i] = 0;
+                if (f < nfr && lane < NP && !(a.crc_dbg & 1)) {
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(stg + f * REGION + lane * 16);
+                    s[i] = lmap<4>(pos + lane * 128, piece_r0<1>(cimg, v));
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 6; t++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) s[i] ^= __shfl_xor(s[i], 1 << t);
+            // every lane now holds the 4 totals: lane i finishes fragment f0 + i * nw, in parallel
+            if (lane < 4) {
+                const int f = f0 + lane * nw;
+                uint32_t x = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
+                if (f < nfr) {
+                    if (nwg == 1) {
+                        finish(f, x);
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 6; b++)
+                            if ((after >> b) & 1) x = lmap<4>(wgs + 128 * b, x);
+                        __hip_atomic_store(a.crc_part + 16 + f * nwg + blockIdx.x, x, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        }
+        if (nwg > 1) {
+            __shared__ int last;
+            __threadfence();  // this workgroup's partials before its count
+            __syncthreads();
+            if (threadIdx.x == 0)
+                last = atomicInc(reinterpret_cast<unsigned*>(a.crc_part), static_cast<unsigned>(nwg - 1)) ==
+                       static_cast<unsigned>(nwg - 1);  // wraps to 0: ready for the next launch
+            __syncthreads();
+            if (last) {
+                __threadfence();
+                for (int f = static_cast<int>(threadIdx.x); f < nfr; f += static_cast<int>(blockDim.x)) {
+                    uint32_t S = 0;
+                    for (int w = 0; w < nwg; w++)
+                        S ^= __hip_atomic_load(a.crc_part + 16 + f * nwg + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    finish(f, S);
+                }
+            }
+        }
+    }
 }
-template __global__ void gf16_small_kernel<2, 16>(const SmallArgs);
-template __global__ void gf16_small_kernel<4, 16>(const SmallArgs);
-template __global__ void gf16_small_kernel<8, 16>(const SmallArgs);
-template __global__ void gf16_small_kernel<2, 4>(const SmallArgs);
-template __global__ void gf16_small_kernel<4, 4>(const SmallArgs);
-template __global__ void gf16_small_kernel<8, 4>(const SmallArgs);
-template __global__ void gf16_small_kernel<2, 2>(const SmallArgs);
-template __global__ void gf16_small_kernel<4, 2>(const SmallArgs);
-template __global__ void gf16_small_kernel<8, 2>(const SmallArgs);
+#define ECAMD_SMALL(G, ST)                                                 \
+    template __global__ void gf16_small_kernel<2, G, ST>(const SmallArgs); \
+    template __global__ void gf16_small_kernel<4, G, ST>(const SmallArgs); \
+    template __global__ void gf16_small_kernel<8, G, ST>(const SmallArgs);
+ECAMD_SMALL(16, false) ECAMD_SMALL(4, false) ECAMD_SMALL(2, false)
+ECAMD_SMALL(16, true) ECAMD_SMALL(4, true) ECAMD_SMALL(2, true)
+#undef ECAMD_SMALL
+#define ECAMD_SMALL_CRC(G)                                                       \
+    template __global__ void gf16_small_kernel<2, G, true, true>(const SmallArgs); \
+    template __global__ void gf16_small_kernel<4, G, true, true>(const SmallArgs); \
+    template __global__ void gf16_small_kernel<8, G, true, true>(const SmallArgs);
+ECAMD_SMALL_CRC(4) ECAMD_SMALL_CRC(2)
+#undef ECAMD_SMALL_CRC
 
 #define ECAMD_INST(W, P, N, B) \
     template __global__ void gf16_apply_kernel<W, P, N, B>(const ApplyArgs);

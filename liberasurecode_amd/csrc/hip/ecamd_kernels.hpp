@@ -60,6 +60,16 @@ struct SmallArgs {
     int64_t nchunks;  // cpf * stripes
     int ncols, nrows, accumulate;
     uint32_t masks[kMaxRows];  // xor_small_kernel: inputs of output r
+    // gf16_small_kernel CRC (fused payload checksums, one stripe): the CRC32 of every input and output
+    // fragment over bs bytes into crc_out[0 .. ncols + nrows) (inputs first); crc_img the fused image
+    // (host/crc.hpp build_fused_crc_image, mb 1), crc_part device scratch: word 0 a self-resetting
+    // counter (zero before the first launch), partials from word 16; crc_minv / crc_c: SmallCrcConst
+    const uint32_t* crc_img;
+    uint32_t* crc_out;
+    uint32_t* crc_part;
+    uint32_t crc_minv[32];
+    uint32_t crc_c;
+    int crc_dbg;  // development A/B (knob small_crc_dbg): 1 skip the epilogue's lookups, 2 skip the image staging
 };
 
 // gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).
@@ -78,8 +88,13 @@ struct FillArgs {
 
 template <int W, bool PTRS, bool NT, bool NIB>
 __global__ void gf16_apply_kernel(const ApplyArgs a);
-template <int W, int G>
+template <int W, int G, bool ST, bool CRC = false>
 __global__ void gf16_small_kernel(const SmallArgs a);
+// Words of the fused small-launch CRC image for G-byte lanes (host/crc.hpp build_small_crc_image): piece
+// tables (byte tables for a piece's dword 0, nibble tables for dwords 1-3), 16 G position maps, 6
+// region-shift maps (nibble fields, 128 words each).
+constexpr int kSmallCrcPieceWords = 1024 + 3 * 128;
+constexpr int small_crc_words(int G) { return kSmallCrcPieceWords + (16 * G + 6) * 128; }
 __global__ void xor_small_kernel(const SmallArgs a);
 template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);

@@ -3,6 +3,9 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include <cstring>
 
@@ -38,6 +41,70 @@ Mat32 zero_shift(const CrcMachine& m, uint64_t nbytes)
         nbytes >>= 1;
     }
     return acc;
+}
+
+Mat32 mat_inverse(const Mat32& a)
+{
+    // Gauss-Jordan over GF(2) on rows: row i of a (bit i of every column) beside row i of I
+    uint32_t row[32], inv[32];
+    for (int i = 0; i < 32; i++) {
+        row[i] = 0;
+        for (int b = 0; b < 32; b++) row[i] |= ((a.col[b] >> i) & 1u) << b;
+        inv[i] = 1u << i;
+    }
+    for (int c = 0; c < 32; c++) {
+        int p = c;
+        while (p < 32 && !((row[p] >> c) & 1u)) p++;
+        if (p == 32) return Mat32{};  // singular (never for a CRC zero-byte step)
+        std::swap(row[p], row[c]);
+        std::swap(inv[p], inv[c]);
+        for (int r = 0; r < 32; r++)
+            if (r != c && ((row[r] >> c) & 1u)) {
+                row[r] ^= row[c];
+                inv[r] ^= inv[c];
+            }
+    }
+    Mat32 out;
+    for (int b = 0; b < 32; b++) {
+        out.col[b] = 0;
+        for (int i = 0; i < 32; i++) out.col[b] |= ((inv[i] >> b) & 1u) << i;
+    }
+    return out;
+}
+
+std::vector<uint32_t> build_small_crc_image(const CrcMachine& m, int G)
+{
+    const int region = 256 * G, np = region / 16;
+    const CrcImage pieces = build_crc_image(m, 5, 4, 4, false);  // byte tables for dword 0, nibbles after
+    const size_t pw = 4 * 256 + 3 * 8 * 16;
+    std::vector<uint32_t> w(pw + static_cast<size_t>(np + 6) * 128, 0);
+    std::copy(pieces.words.begin(), pieces.words.begin() + static_cast<std::ptrdiff_t>(pw), w.begin());
+    for (int l = 0; l < np; l++)
+        field_tables(zero_shift(m, 16ull * static_cast<uint64_t>(np - 1 - l)), 4, w.data() + pw + 128 * l);
+    for (int i = 0; i < 6; i++)
+        field_tables(zero_shift(m, static_cast<uint64_t>(region) << i), 4, w.data() + pw + 128 * (np + i));
+    return w;
+}
+
+SmallCrcConst small_crc_const(bool legacy, uint64_t len, uint64_t zext)
+{
+    static std::mutex mu;
+    static auto& cache = *new std::map<std::tuple<bool, uint64_t, uint64_t>, SmallCrcConst>();
+    static const CrcMachine machines[2] = {CrcMachine(false), CrcMachine(true)};
+    const auto key = std::make_tuple(legacy, len, zext);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    const CrcMachine& m = machines[legacy ? 1 : 0];
+    SmallCrcConst k{};
+    const Mat32 inv = mat_inverse(zero_shift(m, zext));
+    std::copy(inv.col, inv.col + 32, k.minv);
+    k.c = zero_shift(m, len).apply(~0u);
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() > 65536) cache.clear();
+    return cache.emplace(key, k).first->second;
 }
 
 void field_tables(const Mat32& M, int B, uint32_t* out)

@@ -52,6 +52,24 @@ struct Mat32 {
 };
 Mat32 mat_mul(const Mat32& a, const Mat32& b);  // a after b
 Mat32 zero_shift(const CrcMachine& m, uint64_t nbytes);  // A^nbytes
+Mat32 mat_inverse(const Mat32& a);  // a^-1 (the zero-byte step is invertible: the polynomial has x^0)
+
+// Constants of the small-launch kernel's fused checksum (gf16_small_kernel CRC): it forms r0 of each
+// fragment zero-extended by `zext` bytes, S = A^zext r0(M); then r0(M) = minv S with minv = A^-zext, and
+// crc(M) = ~(c ^ r0(M)) with c = A^len ~0.  Cached per (machine, len, zext): O(log) matrix products
+// once, a lookup afterwards.
+// The small-launch kernel's checksum image for G-byte lanes (REGION = 256 * G bytes of a fragment per
+// workgroup, NP = REGION / 16 pieces): the piece tables of build_fused_crc_image (mb 1: byte tables for
+// dword 0, nibble tables for dwords 1-3; 1408 words), then NP position maps A^(16 (NP - 1 - l)) taking
+// piece l's r0 to the end of the region, then 6 maps A^(REGION 2^i) taking a region's r0 past the
+// regions after it -- all as 4-bit field tables (128 words each).
+std::vector<uint32_t> build_small_crc_image(const CrcMachine& m, int G);
+
+struct SmallCrcConst {
+    uint32_t minv[32];
+    uint32_t c;
+};
+SmallCrcConst small_crc_const(bool legacy, uint64_t len, uint64_t zext);
 
 // Field tables of a linear map for B-bit index fields: out[f * 2^B + v] = M(v << (f * B)),
 // f = 0 .. 32/B - 1.

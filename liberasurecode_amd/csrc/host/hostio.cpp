@@ -136,6 +136,26 @@ int64_t zerocopy_bytes()
     return v;
 }
 
+// ECAMD_PERCALL_ZEROCOPY_IN_KIB (default 64): one-chunk calls whose fragments are at most this many KiB
+// let the kernel read its inputs from the pinned slab (no H2D DMA): the small-launch kernel's sizes
+// (<= 4096 16-byte chunks), which stage them through LDS with 16-byte loads -- RS(10,4) 4 / 16 / 64 / 256
+// KiB encodes 22.3 / 28.0 / 31.6 / 42.0 -> 21.5 / 23.4 / 24.9 / 34.0 us (profiles/r06_lat_zc.json).
+int64_t zerocopy_in_bytes()
+{
+    static const int64_t v = [] {
+        const char* env = std::getenv("ECAMD_PERCALL_ZEROCOPY_IN_KIB");
+        const long kib = env ? std::atol(env) : 64;
+        return static_cast<int64_t>(std::max(0L, kib)) << 10;
+    }();
+    return v;
+}
+
+// ECAMD_PERCALL_FUSE_CRC=0: never fold the CRC32s into the codec launch (A/B switch)
+const bool g_fuse_crc = [] {
+    const char* env = std::getenv("ECAMD_PERCALL_FUSE_CRC");
+    return !(env && std::strcmp(env, "0") == 0);
+}();
+
 int zerocopy_mode()
 {
     static const int v = [] {
@@ -352,7 +372,10 @@ void release(Staging* st)
 
 // Kernel launcher for one chunk: inputs at d + j*pitch, outputs at d + (K+r)*pitch.
 // Inputs at din + j*pitch, outputs at dout + (K+r)*pitch.
-using Launch = int (*)(const void* ctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream);
+// crc_dst (may be null): where a launcher that can fold the payload CRC32s into its kernel
+// (ecamd_map_apply_strided_crc) writes them, all inputs then all outputs; *fused says whether it did.
+using Launch = int (*)(const void* ctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream,
+                       uint32_t* crc_dst, bool legacy, bool* fused);
 
 int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, int64_t bs,
                 const void* ctx, Launch launch)
@@ -364,17 +387,24 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     const int64_t padded = (bs + 127) / 128 * 128;
     chunk = std::min(chunk, padded);
     int rc = 0;
-    // Below ~16 KiB of fragments the extra launch + copy costs more than zlib on the host
-    // (4 KiB object: 47 vs 38 us); the frontend then falls back to the CPU for the missing entries.
-    const bool want_crc = t_crc.armed && nfr <= 64 && bs * nfr >= (16 << 10);
+    // CRC32 of every fragment (ecamd_percall_crc_arm), from 16 KiB of fragments (below, zlib on the host
+    // answers sooner; the frontend falls back to the CPU): a one-chunk call first offers it to the codec
+    // launch, which folds it into the small-launch kernel when it can (ecamd_map_apply_strided_crc);
+    // otherwise a separate ecamd_crc32 pass.
+    const bool crc_armed = t_crc.armed && nfr <= 64;
+    const bool crc_pass_ok = crc_armed && bs * nfr >= (16 << 10);
+    const bool want_crc = crc_pass_ok;
     Staging* st = acquire(dev, chunk * nfr + 256, &rc);  // last 256 B of each slab: chunk CRCs
     if (!st) return rc;
     const int64_t crc_off = st->cap - 256;
-    std::vector<uint32_t> crc(want_crc ? nfr : 0, 0u);
+    std::vector<uint32_t> crc(crc_armed ? nfr : 0, 0u);
     const int64_t nchunks = (bs + chunk - 1) / chunk;
     const bool zero_copy = nchunks == 1 && chunk * nfr <= zerocopy_bytes();
-    // which side works on the pinned slab itself (ECAMD_PERCALL_ZEROCOPY_MODE, bit 0 inputs, bit 1 outputs)
-    const bool zc_in = zero_copy && (zerocopy_mode() & 1), zc_out = zero_copy && (zerocopy_mode() & 2);
+    // which side works on the pinned slab itself (ECAMD_PERCALL_ZEROCOPY_MODE, bit 0 inputs, bit 1
+    // outputs; inputs also for fragments of at most ECAMD_PERCALL_ZEROCOPY_IN_KIB, the small-launch
+    // kernel's sizes, whose inputs it stages through LDS with wide loads)
+    const bool zc_in = zero_copy && ((zerocopy_mode() & 1) || bs <= zerocopy_in_bytes());
+    const bool zc_out = zero_copy && (zerocopy_mode() & 2);
     // inputs packed straight into host-writable device memory (no H2D DMA), outputs into the pinned slab
     const bool bar = zc_out && !zc_in && !want_crc && nchunks == 1 && K * chunk <= std::min(bar_bytes(), kBarSlabBytes);
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
@@ -452,16 +482,21 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
             std::atomic_thread_fence(std::memory_order_seq_cst);
         else if (!zc_in)
             rc = ecamd_memcpy_async(sl.d_buf, sl.h_pin, (K - 1) * chunk + n, 0, sl.stream);
-        if (rc == 0) rc = launch(ctx, win, work, chunk, n, sl.stream);
-        if (rc == 0 && want_crc && zc_in && !zc_out)  // the CRC pass reads every fragment from the device slab
+        auto* d_crc = reinterpret_cast<uint32_t*>(work + crc_off);
+        bool fused = false;
+        // fused only from 16 KiB of fragments as well: below, the fused epilogue (~5 us of kernel time)
+        // costs more than zlib on the host (4 KiB RS(10,4) encode 27.8 vs 24.7 us, profiles/r06_lat_crc.json)
+        if (rc == 0)
+            rc = launch(ctx, win, work, chunk, n, sl.stream, crc_pass_ok && nchunks == 1 ? d_crc : nullptr,
+                        t_crc.legacy, &fused);
+        if (rc == 0 && want_crc && !fused && zc_in && !zc_out)  // the CRC pass reads every fragment from the device slab
             rc = ecamd_memcpy_async(work, win, K * chunk, 0, sl.stream);
         if (rc == 0 && !zc_out)
             rc = ecamd_memcpy_async(sl.h_pin + K * chunk, sl.d_buf + K * chunk,
                                     (R - 1) * chunk + n, 1, sl.stream);
         if (rc == 0 && want_crc) {
-            auto* d_crc = reinterpret_cast<uint32_t*>(work + crc_off);
-            rc = ecamd_crc32(t_crc.legacy ? 1 : 0, work, 0, chunk, static_cast<int>(nfr), n,
-                             1, d_crc, sl.stream);
+            if (!fused)
+                rc = ecamd_crc32(t_crc.legacy ? 1 : 0, work, 0, chunk, static_cast<int>(nfr), n, 1, d_crc, sl.stream);
             if (rc == 0 && !zc_out)
                 rc = ecamd_memcpy_async(sl.h_pin + crc_off, d_crc, nfr * 4, 1, sl.stream);
         }
@@ -484,12 +519,22 @@ struct MapCtx {
     int K, R;
 };
 
-int launch_map(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream)
+int launch_map(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream,
+               uint32_t* crc_dst, bool legacy, bool* fused)
 {
     const MapCtx* c = static_cast<const MapCtx*>(vctx);
     std::vector<int64_t> io(c->K), oo(c->R);
     for (int j = 0; j < c->K; j++) io[j] = j * pitch;
     for (int r = 0; r < c->R; r++) oo[r] = (c->K + r) * pitch;
+    *fused = false;
+    if (crc_dst && g_fuse_crc) {  // the codec launch with the checksums folded in, when the shape allows
+        const int rc = ecamd_map_apply_strided_crc(c->map, din, io.data(), dout, oo.data(), bytes, legacy ? 1 : 0,
+                                                   crc_dst, stream);
+        if (rc <= 0) {
+            *fused = rc == 0;
+            return rc;
+        }
+    }
     return ecamd_map_apply_strided(c->map, din, 0, io.data(), dout, 0, oo.data(), bytes, 1, stream);
 }
 
@@ -498,8 +543,10 @@ struct XorCtx {
     int K, R;
 };
 
-int launch_xor(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream)
+int launch_xor(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream,
+               uint32_t* /*crc_dst*/, bool /*legacy*/, bool* fused)
 {
+    *fused = false;  // xor_small_kernel has no checksum epilogue: the separate pass (or the host) serves
     const XorCtx* c = static_cast<const XorCtx*>(vctx);
     std::vector<int64_t> io(c->K), oo(c->R);
     for (int j = 0; j < c->K; j++) io[j] = j * pitch;

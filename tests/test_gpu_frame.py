@@ -3,6 +3,7 @@ zlib / legacy CRC32 on the device against the oracle, and whole fragments (80-by
 payload) against the framing restatement of tests/ec_api.py (pinned to the reference's
 known-answer headers, test/liberasurecode_test.c:2239-2315) with parity from the oracles."""
 import os
+import subprocess
 import sys
 import zlib
 
@@ -340,12 +341,30 @@ def test_frame_decode_join_matches_split(F, k, m, missing):
     _lib.dev().ecamd_tune(b"frame_unfused", 0)
 
 
-@pytest.mark.parametrize("bs", [1000, 65536, (1 << 20) + 6, 3 * (1 << 20)])
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("bs", [100, 1000, 65536, (1 << 20) + 6, 3 * (1 << 20)])
 @pytest.mark.parametrize("legacy", [0, 1])
-def test_percall_crc_handoff(F, bs, legacy):
+def test_percall_crc_handoff(F, bs, legacy, fuse):
     """ecamd_percall_crc_*: while armed, the per-call host path checksums every input and output
     fragment on the GPU (chunk CRCs combined on the host); each equals zlib / the legacy CRC of
-    the final bytes.  This is what liberasurecode.so.1 stamps into the headers."""
+    the final bytes.  This is what liberasurecode.so.1 stamps into the headers.  From 16 KiB of
+    fragments (the host's zlib below); fragments of at most 64 KiB fold the checksums into the
+    small-launch codec kernel (ecamd_map_apply_strided_crc); with that off (fuse "0", run in a child:
+    ECAMD_PERCALL_FUSE_CRC is read once) the separate ecamd_crc32 pass serves them."""
+    if fuse == "0":
+        here = os.path.dirname(os.path.abspath(__file__))
+        env = dict(os.environ, ECAMD_PERCALL_FUSE_CRC="0",
+                   PYTHONPATH=os.pathsep.join([os.path.dirname(here), here, os.environ.get("PYTHONPATH", "")]))
+        r = subprocess.run([sys.executable, "-c", f"import test_gpu_frame as t; t._crc_handoff({bs}, {legacy}, False)"],
+                           cwd=os.path.dirname(os.path.abspath(__file__)), env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return
+    _crc_handoff(bs, legacy, True)
+
+
+def _crc_handoff(bs, legacy, fused):
+    import torch  # noqa: F401  (one HIP runtime per process: torch's)
     import ctypes as C
     from liberasurecode_amd import _lib
     d = _lib.dev()

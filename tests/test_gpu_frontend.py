@@ -362,3 +362,39 @@ def test_decode_direct_matches_general_path():
     assert res["11"] == res["10"] == res["00"]
     assert all(ok for _, _, _, ok in res["11"] if ok is not None), [x for x in res["11"] if x[3] is False][:5]
     assert sum(1 for _, rc, _, ok in res["11"] if ok) > 100
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+@pytest.mark.parametrize("km", [(10, 4), (4, 2), (20, 8)])
+def test_percall_crc_fused(monkeypatch, km, legacy):
+    """The per-call CHKSUM_CRC32 encode with the payload checksums folded into the small-launch codec
+    kernel (ecamd_map_apply_strided_crc: one launch, inputs staged through LDS, one workgroup or a
+    cross-workgroup Horner) -- every fragment byte-equal to the restated framing over zlib / the legacy
+    CRC, at sizes from 1 byte to past the small-launch limit (64 KiB fragments), with the fused-launch
+    counter proving the path (from 16 KiB of fragments; the host's zlib below); (20, 8) does not fit the
+    LDS and must take the separate pass / host."""
+    import torch  # noqa: F401  (one HIP runtime per process: torch's)
+    from liberasurecode_amd import _lib
+    k, m = km
+    d = _lib.dev()
+    cnt = d.ecamd_small_crc_launches
+    cnt.restype = C.c_longlong
+    if legacy:
+        monkeypatch.setenv("LIBERASURECODE_WRITE_LEGACY_CRC", "1")
+    desc = E.create(E.EC_BACKEND_LIBERASURECODE_RS_VAND, k, m, hd=m, ct=E.CHKSUM_CRC32)
+    fused = 0
+    for size in (1, 15, 100, 1000, 4096, 4097, 5121, 16384, 16400, 65536 + 3, 200000, 262144, 640000, 655361,
+                 1 << 20):
+        data = payload_bytes(size, size + k)
+        n0 = cnt()
+        rc, dp, pp, flen = E.encode(desc, data)
+        assert rc == 0
+        fused += cnt() - n0
+        frags = E.fragments(dp, k, flen) + E.fragments(pp, m, flen)
+        E.lib().liberasurecode_encode_cleanup(desc, dp, pp)
+        assert frags == rs_expected(k, m, data, E.CHKSUM_CRC32, legacy=legacy), (size, legacy)
+    E.lib().liberasurecode_instance_destroy(desc)
+    if km == (20, 8):
+        assert fused == 0
+    else:
+        assert fused >= 5, fused  # the sizes with >= 16 KiB of fragments, each at most 64 KiB

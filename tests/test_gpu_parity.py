@@ -376,11 +376,12 @@ def tune():
     yield d.ecamd_tune
     for key, val in ((b"stream", 1), (b"stream_ch", 1), (b"stream_pf", 0), (b"stream_nib", 0),
                      (b"stream_order", 0), (b"stream_hybrid", 1), (b"multi_list", 1), (b"xor_wgs", 0),
-                     (b"bitslice", 1), (b"small_chunks", -1), (b"small_lane", 0)):
+                     (b"bitslice", 1), (b"small_chunks", -1), (b"small_lane", 0), (b"small_stage", -1)):
         d.ecamd_tune(key, val)
 
 
-@pytest.mark.parametrize("small", [(0, 0), (1 << 20, 0), (1 << 20, 4), (1 << 20, 16), (1 << 20, 2)])
+@pytest.mark.parametrize("small", [(0, 0, 1), (1 << 20, 0, 1), (1 << 20, 0, 0), (1 << 20, 4, 1), (1 << 20, 16, 1),
+                                   (1 << 20, 16, 0), (1 << 20, 2, 1), (1 << 20, 2, 0)])
 @pytest.mark.parametrize("S", [1, 3])
 @pytest.mark.parametrize("bs", [1, 15, 16, 17, 416, 1000, 4097, 16384 + 48])
 @pytest.mark.parametrize("R,K", [(1, 1), (2, 5), (4, 10), (3, 4), (8, 20), (5, 45), (9, 25)])
@@ -388,9 +389,11 @@ def test_small_kernel_shapes(tune, R, K, bs, S, small):
     """gf16_small_kernel (launches of few chunks: per-call objects) and, with small_chunks 0, the
     stream kernel's tail path on the same shapes, against the numpy GF(2^16) reference: ragged
     fragments, several stripes, 2 / 4 / 8-output passes, K = 45 in column passes (accumulate); the
-    small kernel with 2 / 4 bytes per lane by size (default), 4, 16 and 2."""
+    small kernel with 2 / 4 bytes per lane by size (default), 4, 16 and 2, its one-stripe launches
+    with the inputs staged into LDS first (small_stage 1, default) and read in place (0)."""
     tune(b"small_chunks", small[0])
     tune(b"small_lane", small[1])
+    tune(b"small_stage", small[2])
     rng = np.random.default_rng(bs * 7 + R * 100 + K + S)
     coeff = rng.integers(0, 65536, size=(R, K))
     frags = rng.integers(0, 256, size=(S, K + R, bs), dtype=np.uint8)

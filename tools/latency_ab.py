@@ -1,29 +1,45 @@
 #!/usr/bin/env python3
-"""A/B of per-call latency settings (round 3): tools/latency_bench.py --codec own in child processes,
+"""A/B of per-call latency settings: tools/latency_bench.py --codec own in child processes,
 interleaved rounds -- the copy helpers' batch threshold (ECAMD_COPY_MIN_KIB, default 2048) at 256 KiB
 and 1 MiB, and the helpers off.  Earlier forms of this tool compared the round-2 host path, the
 recycled buffers and polling the staging streams (profiles/r03_latency_ab1..4.log).
-One JSON line per (setting, round, checksum, size) with the median encode / decode latency."""
+One JSON line per (setting, round, checksum, size) with the median encode / decode latency.
+usage: latency_ab.py [rounds] [set: copy | zc] [latency_bench.py args]"""
 import json
 import os
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SETTINGS = {"default": {},
-            "copy_min_256k": {"ECAMD_COPY_MIN_KIB": "256"},
-            "copy_min_1m": {"ECAMD_COPY_MIN_KIB": "1024"},
-            "no-helpers": {"ECAMD_COPY_THREADS": "0"}}
+SETS = {
+    "copy": {"default": {},
+             "copy_min_256k": {"ECAMD_COPY_MIN_KIB": "256"},
+             "copy_min_1m": {"ECAMD_COPY_MIN_KIB": "1024"},
+             "no-helpers": {"ECAMD_COPY_THREADS": "0"}},
+    # round 6: inputs read from the pinned slab by the kernel (ZEROCOPY_MODE 3, no H2D DMA), with the
+    # small kernel's inputs staged into LDS by 16-byte loads (small_stage 1) or read in place (0)
+    "zc": {"default": {},
+           "mode3_staged": {"ECAMD_PERCALL_ZEROCOPY_MODE": "3"},
+           "mode3_inplace": {"ECAMD_PERCALL_ZEROCOPY_MODE": "3", "ECAMD_TUNE": "small_stage=0"},
+           "mode2_inplace": {"ECAMD_TUNE": "small_stage=0"}},
+    # round 6: the CRC32 encode's checksums folded into the small-launch kernel (default) or the
+    # separate two-launch ecamd_crc32 pass / host zlib (FUSE_CRC 0); round 5's defaults for reference
+    "crc": {"default": {},
+            "no_fuse": {"ECAMD_PERCALL_FUSE_CRC": "0"},
+            "r05_defaults": {"ECAMD_PERCALL_FUSE_CRC": "0", "ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0"}},
+}
 
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    SETTINGS = SETS[sys.argv[2] if len(sys.argv) > 2 else "copy"]
+    extra = sys.argv[3:]  # passed to latency_bench.py (e.g. --max-size 262144)
     for rnd in range(rounds):
         names = list(SETTINGS)
         for name in names[rnd % len(names):] + names[:rnd % len(names)]:  # rotated every round
             env = SETTINGS[name]
             r = subprocess.run([sys.executable, os.path.join(HERE, "latency_bench.py"), "--codec", "own",
-                                "--reps", "25"], capture_output=True, text=True, timeout=600,
+                                "--reps", "25"] + extra, capture_output=True, text=True, timeout=600,
                                env=dict(os.environ, **env))
             if r.returncode != 0:
                 sys.stderr.write(r.stderr[-2000:])

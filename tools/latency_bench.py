@@ -81,7 +81,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=25)
     ap.add_argument("--codec", default="both", choices=["both", "own", "ref"])
+    ap.add_argument("--max-size", type=int, default=0, help="skip object sizes above this (0: all)")
     args = ap.parse_args()
+    if args.max_size:
+        SIZES[:] = [x for x in SIZES if x <= args.max_size]
     if args.codec in ("own", "ref"):
         measure(args.codec, args.reps)
         return
