@@ -107,6 +107,13 @@ int ecamd_map_apply_strided_crc(const ecamd_map *map, const void *in_base, const
                                 void *stream);
 /* Launches of ecamd_map_apply_strided_crc that fused the checksums (tests pin which path ran). */
 long long ecamd_small_crc_launches(void);
+/* Completion flag of the calling thread's next operation (the per-call path, host/hostio.cpp): when the
+ * small-launch kernel that ends it runs (gf16_small_kernel), it stores `value` to *flag -- pinned host
+ * memory -- after every output and checksum store of the operation is visible system-wide, so the host
+ * can poll the flag instead of synchronizing the stream.  ecamd_done_flag_taken() says whether the
+ * operation took it (1) or not (0: other kernels; synchronize as usual) and disarms. */
+void ecamd_done_flag_arm(uint32_t *flag, uint32_t value);
+int ecamd_done_flag_taken(void);
 
 /* Pointer tables in device memory: input j of stripe s is d_in_ptrs[s*in_row + in_col[j]],
  * output r is d_out_ptrs[s*out_row + out_col[r]] (in_col / out_col are host arrays). */
@@ -286,6 +293,9 @@ int ecamd_synchronize(void);
 int ecamd_stream_create(void **stream);
 /* Also releases the library's per-stream context of that stream (side stream, scratch). */
 int ecamd_stream_destroy(void *stream);
+/* hipStreamDestroy on the library's own HIP runtime WITHOUT releasing its context -- what a caller that
+ * destroys a stream behind the library's back does (tests: the contexts stay bounded anyway). */
+int ecamd_stream_destroy_unmanaged(void *stream);
 int ecamd_stream_synchronize(void *stream);
 /* 0 when all work on stream is complete, 1 while some is pending, ECAMD_EHIP on error. */
 int ecamd_stream_query(void *stream);

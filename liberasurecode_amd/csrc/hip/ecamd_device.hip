@@ -416,6 +416,8 @@ struct Tuning {
     Knob frame_crc_wave_pf{kCrcWave.pf};
     Knob frame_crc_wave_mb{4};      //   piece dwords on byte tables (the rest on nibble tables)
     Knob frame_crc_wave_mix{0};     //   no scheduling barrier between an input's CRC lookups and its network
+    Knob frame_crc_wave_l1{0};      //   a piece's last dword through its byte tables in global memory (the
+                                    //   vector L1 as a second lookup engine beside the LDS; round 6 A/B)
     Knob frame_crc_wave_strict{0};  // tests: a framed CRC32 encode the one-wave crc form declines fails
     Knob scatter_lanes{0};  // ecamd_scatter_fragments: one copy lane per destination device for
                             //   peers (0), for every destination incl. local ones (1, exercises the
@@ -471,6 +473,7 @@ int dev_tune(const char* key)
     if (k == "frame_crc_wave_strict") return g_tune.frame_crc_wave_strict;
     if (k == "frame_crc_wave_mix") return g_tune.frame_crc_wave_mix;
     if (k == "frame_crc_wave_mb") return g_tune.frame_crc_wave_mb;
+    if (k == "frame_crc_wave_l1") return g_tune.frame_crc_wave_l1;
     if (k == "frame_tail_bs") return g_tune.frame_tail_bs;
     if (k == "frame_tail_fork") return g_tune.frame_tail_fork;
     if (k == "frame_tail_tiles") return g_tune.frame_tail_tiles;
@@ -659,9 +662,19 @@ struct SmallCrcReq {
     bool legacy;
 };
 
-// ECAMD_EINVAL (nothing launched) when `crc` is given and the launch cannot fuse it.
+// The calling thread's armed completion flag (ecamd_done_flag_arm): taken by its next small launch that
+// ends an operation.
+struct DoneFlag {
+    uint32_t* flag = nullptr;
+    uint32_t value = 0;
+    bool taken = false;
+};
+thread_local DoneFlag t_done;
+
+// ECAMD_EINVAL (nothing launched) when `crc` is given and the launch cannot fuse it.  `last`: this launch
+// ends the operation (the completion flag may be attached to it).
 int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
-                 hipStream_t st, const SmallCrcReq* crc = nullptr)
+                 hipStream_t st, const SmallCrcReq* crc = nullptr, bool last = false)
 {
     const int lane = g_tune.small_lane ? static_cast<int>(g_tune.small_lane)
                                        : ((bs + 1) / 2 * nstripes <= 256 ? 2 : 4);
@@ -677,6 +690,24 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
                        p.bytes + stage <= kLdsBytes &&
                        (a.ncols - 1) * s.in_pitch + bs < (int64_t(1) << 31);
     const size_t lds = p.bytes + (st_in ? stage : 0);
+    // completion flag: several workgroups count in the stream's scratch slot (its context held in use
+    // until this launch is enqueued, so it is not released meanwhile)
+    std::unique_ptr<StreamUse> use;
+    if (last && t_done.flag && !t_done.taken) {
+        if (grid.x > 1 && !crc) {
+            int dev = 0;
+            uint32_t* scr = nullptr;
+            if (hipGetDevice(&dev) == hipSuccess) {
+                use = std::make_unique<StreamUse>(dev, st);
+                if (stream_scratch(dev, st, kSmallCrcScratchSlot, 16, &scr) == 0) s.done_ctr = scr + 1;
+            }
+            (void)hipGetLastError();
+        }
+        if (grid.x == 1 || crc || s.done_ctr) {
+            s.done = t_done.flag;
+            s.done_val = t_done.value;
+        }
+    }
     if (crc) {
         // the region-shift maps reach 63 regions past a workgroup's: at most 64 workgroups
         if (!st_in || (lane != 2 && lane != 4) || a.accumulate || grid.x > 64) return ECAMD_EINVAL;
@@ -702,6 +733,7 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
         }
 #undef SMALLC_
         HIP_TRY(hipGetLastError());
+        if (s.done) t_done.taken = true;
         return 0;
     }
 #define SMALL_(W)                                                                                           \
@@ -722,6 +754,7 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
     }
 #undef SMALL_
     HIP_TRY(hipGetLastError());
+    if (s.done) t_done.taken = true;
     return 0;
 }
 
@@ -1211,7 +1244,7 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             }
         }
         if (!PTRS && small_launch(a, bs, nstripes)) {
-            int rc = launch_small(a, p, bs, nstripes, map->d_tables, st);
+            int rc = launch_small(a, p, bs, nstripes, map->d_tables, st, nullptr, &p == &map->passes.back());
             if (rc) return rc;
             continue;
         }
@@ -2581,6 +2614,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.frame_crc_wave_mb = value <= 0 ? 4 : std::min(value, 4);
     } else if (k == "frame_crc_wave_mix") {
         g_tune.frame_crc_wave_mix = value > 0 ? 1 : 0;
+    } else if (k == "frame_crc_wave_l1") {
+        g_tune.frame_crc_wave_l1 = value > 0 ? 1 : 0;
     } else if (k == "frame_crc_wave_strict") {
         g_tune.frame_crc_wave_strict = value > 0 ? 1 : 0;
     } else if (k == "frame_crc_wave_wpe") {
@@ -2749,12 +2784,21 @@ int ecamd_map_apply_strided_crc(const ecamd_map* map, const void* in_base, const
     if ((rc = stream_scratch(dev, stream, kSmallCrcScratchSlot, 16 + static_cast<size_t>(map->K + map->R) * wgs,
                              &req.part)))
         return rc;
-    rc = launch_small(a, p, blocksize, 1, map->d_tables, static_cast<hipStream_t>(stream), &req);
+    rc = launch_small(a, p, blocksize, 1, map->d_tables, static_cast<hipStream_t>(stream), &req, true);
     if (rc == 0) g_small_crc_launches.fetch_add(1, std::memory_order_relaxed);
     return rc == ECAMD_EINVAL ? 1 : rc;
 }
 
 long long ecamd_small_crc_launches(void) { return g_small_crc_launches.load(std::memory_order_relaxed); }
+
+void ecamd_done_flag_arm(uint32_t* flag, uint32_t value) { t_done = DoneFlag{flag, value, false}; }
+
+int ecamd_done_flag_taken(void)
+{
+    const int taken = t_done.taken ? 1 : 0;
+    t_done = DoneFlag{};
+    return taken;
+}
 
 int ecamd_map_apply_ptrs(const ecamd_map* map, const void* const* d_in_ptrs, int in_row,
                          const int* in_col, void* const* d_out_ptrs, int out_row,
@@ -3242,6 +3286,12 @@ int ecamd_stream_create(void** stream)
 int ecamd_stream_destroy(void* stream)
 {
     ecamd::stream_forget(stream);
+    HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return 0;
+}
+
+int ecamd_stream_destroy_unmanaged(void* stream)
+{
     HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
     return 0;
 }

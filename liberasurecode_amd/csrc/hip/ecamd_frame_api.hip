@@ -441,7 +441,7 @@ int crc_wave_form(const Code& c, int64_t cover)
     if (c.m > 4) cw = std::min(cw, 8);  // (5-8 outputs: built for 2 waves per SIMD)
     const int nibw = 4 - std::clamp(dev_tune("frame_crc_wave_mb"), 1, 4);  // piece dwords on nibble tables
     return dev_tune("frame_crc_wave_pos") | 8 | 32 | (cw << 6) | (dev_tune("frame_crc_wave_mix") ? 1024 : 0) |
-           (nibw << 11);
+           (nibw << 11) | (nibw == 0 && dev_tune("frame_crc_wave_l1") ? 8192 : 0);
 }
 int crc_wave_mb(int wf) { return 4 - ((wf >> 11) & 3); }  // byte-table dwords per piece of the form wf
 int crc_wave_groups(int64_t tps)

@@ -321,8 +321,10 @@ void stop_children_at_exit()
 // of the request, the target and the generator: the same in the shipped and the per-user cache).
 std::string request_of(const BsEntry& e)
 {
-    // (+ 16: crc_mix, + 32 * dwords of a piece on nibble tables)
-    const int cw = (e.crc & 32) ? ((e.crc >> 6) & 15) | ((e.crc & 1024) ? 16 : 0) | (((e.crc >> 11) & 3) << 5) : 0;
+    // (+ 16: crc_mix, + 32 * dwords of a piece on nibble tables, + 128: the last dword's lookups via L1)
+    const int cw = (e.crc & 32) ? ((e.crc >> 6) & 15) | ((e.crc & 1024) ? 16 : 0) | (((e.crc >> 11) & 3) << 5) |
+                                      ((e.crc & 8192) ? 128 : 0)
+                                : 0;
     return bitslice_request(e.coeff, e.R, e.K, kCaps[e.cap_index], e.depth, e.copy, e.crc > 0,
                             e.crc > 0 ? (e.crc & 7) : 1, (e.crc & 8) != 0, (e.crc & 16) != 0, e.wave, &e.shifts,
                             e.prefetch, e.wave || e.occ.threads || cw ? &e.occ : nullptr, cw);

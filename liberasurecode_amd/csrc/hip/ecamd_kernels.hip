@@ -354,7 +354,12 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
         }
         if (nwg > 1) {
             __shared__ int last;
-            __threadfence();  // this workgroup's partials before its count
+            // this workgroup's partials (and, with a completion flag, its output stores, system-wide)
+            // before its count
+            if (a.done)
+                __threadfence_system();
+            else
+                __threadfence();
             __syncthreads();
             if (threadIdx.x == 0)
                 last = atomicInc(reinterpret_cast<unsigned*>(a.crc_part), static_cast<unsigned>(nwg - 1)) ==
@@ -368,6 +373,25 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
                         S ^= __hip_atomic_load(a.crc_part + 16 + f * nwg + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     finish(f, S);
                 }
+                if (a.done) {  // every workgroup's stores are visible: the checksums, then the flag
+                    __threadfence_system();
+                    __syncthreads();
+                    if (threadIdx.x == 0)
+                        __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+            return;
+        }
+    }
+    if (a.done) {  // one workgroup, or no checksum: the completion flag after every output store
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const bool last = gridDim.x == 1 || atomicInc(reinterpret_cast<unsigned*>(a.done_ctr), gridDim.x - 1) ==
+                                                    gridDim.x - 1;  // wraps to 0 for the next launch
+            if (last) {
+                __threadfence_system();
+                __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     }

@@ -70,6 +70,13 @@ struct SmallArgs {
     uint32_t crc_minv[32];
     uint32_t crc_c;
     int crc_dbg;  // development A/B (knob small_crc_dbg): 1 skip the epilogue's lookups, 2 skip the image staging
+    // completion flag (ecamd_done_flag_arm): once every output (and checksum) store of the launch is
+    // visible system-wide, done_val is stored to *done (pinned host memory) -- the per-call path polls it
+    // instead of synchronizing the stream.  Several workgroups: the last one to finish stores it (counter
+    // done_ctr, self-resetting, zero before the first launch; with CRC the checksum's last workgroup).
+    uint32_t* done;
+    uint32_t* done_ctr;
+    uint32_t done_val;
 };
 
 // gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).

@@ -325,6 +325,12 @@ __device__ __forceinline__ u32 piece_r0m(const u32* t, u32 a, u32 b, u32 c, u32 
     const u32 rd = lmap4(n + 128 * (3 - MB), d);
     return x3(ra, rb, rc) ^ rd;
 }
+// byte tables, dword 3's read from global memory g (the vector L1 as a second lookup engine; same layout)
+__device__ __forceinline__ u32 piece_r0g(const u32* t, const u32* g, u32 a, u32 b, u32 c, u32 d)
+{
+    const u32 rd = lmap8(g + 3072, d);
+    return x3(lmap8(t, a), lmap8(t + 1024, b), lmap8(t + 2048, c)) ^ rd;
+}
 // the same through nibble tables: dword w's 8 fields at tab + 128 w (conflict-free 16-entry tables)
 __device__ __forceinline__ u32 piece_r0n(const u32* t, u32 a, u32 b, u32 c, u32 d)
 {
@@ -471,14 +477,18 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         const int maps = NP * PW;                         // gap, levels, A^1024, then the lane tables
         const int words = maps + 8 * 128 + kBsCrcLaneWords;
         constexpr int CS1 = kBsCrcWaveStep;
-        const std::string pfn = MB == 4 ? std::string("piece_r0") : "piece_r0m<" + std::to_string(MB) + ">";
+        const std::string pfn = MB == 4 ? std::string(style.crc_l1 ? "piece_r0g" : "piece_r0")
+                                        : "piece_r0m<" + std::to_string(MB) + ">";
+        // crc_l1: dword 3's byte tables read from the image in global memory (gimg, same offsets as ctab)
+        const std::string gext = MB == 4 && style.crc_l1 ? "gimg + " : "";
         auto crc1 = [&](int f, const char* x) {
             s << "            {\n";
             for (int c0 = 0; c0 < 4; c0 += NP) {
                 s << "                " << (c0 ? "cs = lmap4(gap, cs)" : "u32 cs = 0u");
                 for (int c = c0; c < c0 + NP; c++)
-                    s << " ^ " << pfn << "(ctab + " << (c % NP) * PW << ", " << x << c << "[0], " << x << c << "[1], " << x
-                      << c << "[2], " << x << c << "[3])";
+                    s << " ^ " << pfn << "(ctab + " << (c % NP) * PW << ", "
+                      << (gext.empty() ? std::string() : gext + std::to_string((c % NP) * PW) + ", ") << x << c << "[0], "
+                      << x << c << "[1], " << x << c << "[2], " << x << c << "[3])";
                 s << ";\n";
             }
             s << "                cs = wave_xor(lane_shift(lanes, cs, lofs));\n"
@@ -497,6 +507,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
           << ";\n"
              "    const u32 lane = threadIdx.x & 63u;\n"
              "    const u32 lofs = lane * 4u;\n"
+             "    const u32* gimg = a.crc_img;\n"
              "    const u32 wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n"
              // the first crc_q workgroups take crc_per tiles per wave, the rest one: long runs (one
              // table fill each) first, single tiles for an even finish
@@ -1032,10 +1043,12 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
     // BsOcc::wmin, bits 15-18 BsOcc::wmax, bit 19 BsOcc::barrier (bit 7 then unused); plain maps in
     // the multi-wave form, bits 20-21: lanes per workgroup (1 = 128, 2 = 512; 0 = 256); bit 22 the
     // crc variant in one-wave tiles (with the lane fold; bits 11-19 its occupancy as for bit 6), bits
-    // 23-26 its waves per workgroup, bit 27 its crc_mix, bits 28-29 its piece dwords on nibble tables
+    // 23-26 its waves per workgroup, bit 27 its crc_mix, bits 28-29 its piece dwords on nibble tables,
+    // bit 30 a piece's last dword looked up in global memory (with byte tables only)
     const int cw = crc ? std::clamp(crc_wave & 15, 0, 15) : 0;  // (+ 16: crc_mix, + 32 * nibble dwords)
     const int cmix = cw && (crc_wave & 16) ? 1 : 0;
     const int cnib = cw ? (crc_wave >> 5) & 3 : 0;
+    const int cl1 = cw && !cnib && (crc_wave & 128) ? 1 : 0;
     if (cw) {  // (the one-wave crc form always folds with the lane tables, on byte piece tables)
         crc_lane = true;
         crc_nib = false;
@@ -1057,7 +1070,7 @@ std::string bitslice_request(const std::vector<int>& coeff, int R, int K, int ca
               (crc && crc_nib ? 32 : 0) | (pf << 8) |
               (!wave && !cw ? 0 : (wave ? 64 : 0) | (std::clamp(o.wmin, 1, 8) << 11) |
                                       (std::clamp(o.wmax, o.wmin, 8) << 15) | (o.barrier ? 1 << 19 : 0)) |
-              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) | (cmix << 27) | (cnib << 28) : 0))
+              (tcode << 20) | (cw ? (1 << 22) | (cw << 23) | (cmix << 27) | (cnib << 28) | (cl1 << 30) : 0))
           << "\n";
         if (shifted)  // version 3: the per-input byte shifts of the copy-through inputs
             for (int j = 0; j < K; j++)
@@ -1079,13 +1092,14 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (!(s >> magic >> version) || magic != "ecamd-bitslice-request" || version < 1 || version > 3) return false;
     if (!(s >> R >> K >> cap >> depth) || R <= 0 || R > kBsMaxR || K <= 0 || K > kBsMaxK || cap < 0 || cap > 96)
         return false;
-    if (version >= 2 && (!(s >> cp) || cp < 0 || cp >= (1 << 30) || (cp & 12) == 12))
+    if (version >= 2 && (!(s >> cp) || cp < 0 || (cp & 12) == 12))
         return false;
     const int cw = (cp >> 22) & 1 ? (cp >> 23) & 15 : 0;  // one-wave crc form: waves per workgroup
     if (((cp >> 22) & 1) ? (!cw || (cp & (1 | 2 | 16 | 32)) != (1 | 2 | 16)) : (cp >> 23) != 0)
         return false;
     if (!cw && (cp >> 27)) return false;
-    if (crc_wave) *crc_wave = cw | (((cp >> 27) & 1) << 4) | (((cp >> 28) & 3) << 5);
+    if (((cp >> 30) & 1) && ((cp >> 28) & 3)) return false;  // global-memory lookups: byte tables only
+    if (crc_wave) *crc_wave = cw | (((cp >> 27) & 1) << 4) | (((cp >> 28) & 3) << 5) | (((cp >> 30) & 1) << 7);
     const int tcode = (cp >> 20) & 3;  // lanes per workgroup of the multi-wave plain form
     if (tcode == 3 || (tcode && ((cp & (1 | 2 | 64)) || depth != 0))) return false;
     const int wmin = (cp >> 11) & 15, wmax = (cp >> 15) & 15;  // one-wave occupancy (0: bit 7 / by R)

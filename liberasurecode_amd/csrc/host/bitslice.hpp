@@ -109,6 +109,10 @@ struct BitsliceStyle {
     // one-wave crc form: a piece's first crc_mb dwords through byte tables, the rest through
     // conflict-free nibble tables (build_fused_crc_image_pos mb)
     int crc_mb = 4;
+    // one-wave crc form with byte tables: dword 3 of each piece looked up in the image in global memory
+    // (through the vector L1) instead of LDS -- a second lookup engine for the random-index lookups
+    // whose LDS bank conflicts bound the form (round 6 A/B, knob frame_crc_wave_l1)
+    bool crc_l1 = false;
 };
 // LDS words of the CRC image the crc variant reads (host/crc.hpp build_fused_crc_image_pos: byte
 // piece tables per position, chain step 4096 B): npos x 4 x 1024 piece words + gap + 6 butterfly

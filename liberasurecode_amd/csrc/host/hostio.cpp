@@ -238,6 +238,7 @@ struct Slot {
 struct Staging {
     Slot slot[2];
     int64_t cap = 0;  // bytes per slab
+    uint32_t seq = 0;  // completion-flag values handed out (per context: one caller at a time)
     int device = 0;   // every stream, event and buffer of this context lives there
     ~Staging()
     {
@@ -323,6 +324,7 @@ int grow(Staging* st, int64_t bytes)
         int rc = ecamd_host_alloc(&p, bytes);
         if (rc) return rc;
         s.h_pin = static_cast<char*>(p);
+        std::memset(s.h_pin + bytes - 512, 0, 512);  // the completion flag and chunk CRC words
         rc = ecamd_malloc(&p, bytes);
         if (rc) return rc;
         s.d_buf = static_cast<char*>(p);
@@ -370,6 +372,27 @@ void release(Staging* st)
     g_pool[st->device].push_back(st);
 }
 
+// The completion-flag word of a slab (ecamd_done_flag_arm): 512 bytes before its end, apart from the
+// chunk CRCs in the last 256.
+uint32_t* done_word(char* h_pin, int64_t cap) { return reinterpret_cast<uint32_t*>(h_pin + cap - 512); }
+
+// ECAMD_PERCALL_DONE_FLAG=0: synchronize the stream instead of polling the completion flag (A/B switch)
+const bool g_done_flag = [] {
+    const char* env = std::getenv("ECAMD_PERCALL_DONE_FLAG");
+    return !(env && std::strcmp(env, "0") == 0);
+}();
+constexpr int kDonePollUs = 200;  // then block in hipStreamSynchronize (a busy GPU, or a fault)
+
+// Polls the flag word for `value` (the GPU writes it to pinned host memory); false after kDonePollUs.
+bool poll_done(const uint32_t* flag, uint32_t value)
+{
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(kDonePollUs);
+    for (int i = 0;; i++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == value) return true;
+        if ((i & 63) == 63 && std::chrono::steady_clock::now() > until) return false;
+    }
+}
+
 // Kernel launcher for one chunk: inputs at d + j*pitch, outputs at d + (K+r)*pitch.
 // Inputs at din + j*pitch, outputs at dout + (K+r)*pitch.
 // crc_dst (may be null): where a launcher that can fold the payload CRC32s into its kernel
@@ -394,7 +417,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     const bool crc_armed = t_crc.armed && nfr <= 64;
     const bool crc_pass_ok = crc_armed && bs * nfr >= (16 << 10);
     const bool want_crc = crc_pass_ok;
-    Staging* st = acquire(dev, chunk * nfr + 256, &rc);  // last 256 B of each slab: chunk CRCs
+    Staging* st = acquire(dev, chunk * nfr + 512, &rc);  // last 512 B of each slab: done flag, chunk CRCs
     if (!st) return rc;
     const int64_t crc_off = st->cap - 256;
     std::vector<uint32_t> crc(crc_armed ? nfr : 0, 0u);
@@ -408,6 +431,11 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     // inputs packed straight into host-writable device memory (no H2D DMA), outputs into the pinned slab
     const bool bar = zc_out && !zc_in && !want_crc && nchunks == 1 && K * chunk <= std::min(bar_bytes(), kBarSlabBytes);
     int64_t pending[2] = {-1, -1};  // chunk index in flight per slot
+    // completion flag (one-chunk calls whose outputs land in the pinned slab): the kernel that ends the
+    // operation stores a per-call value into the slab's flag word once its stores are visible; the
+    // caller polls it instead of synchronizing the stream (falls back to that after kDonePollUs)
+    bool flagged[2] = {false, false};
+    uint32_t flag_val[2] = {0, 0};
     std::vector<void*> cdst(static_cast<size_t>(nfr));
     std::vector<const void*> csrc(static_cast<size_t>(nfr));
     std::vector<int64_t> clen(static_cast<size_t>(nfr));
@@ -416,7 +444,10 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     std::vector<int64_t> plen;
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
-        int r = wait_stream(st->slot[s].stream, chunk * nfr >= kSpinMinBytes);
+        int r = 0;
+        if (!(flagged[s] && poll_done(done_word(st->slot[s].h_pin, st->cap), flag_val[s])))
+            r = wait_stream(st->slot[s].stream, chunk * nfr >= kSpinMinBytes);
+        flagged[s] = false;
         if (r) return r;
         const int64_t off = pending[s] * chunk;
         const int64_t n = std::min(chunk, bs - off);
@@ -486,9 +517,17 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         bool fused = false;
         // fused only from 16 KiB of fragments as well: below, the fused epilogue (~5 us of kernel time)
         // costs more than zlib on the host (4 KiB RS(10,4) encode 27.8 vs 24.7 us, profiles/r06_lat_crc.json)
+        const bool arm = g_done_flag && zc_out && nchunks == 1;
+        if (arm) {
+            flag_val[s] = ++st->seq;
+            ecamd_done_flag_arm(done_word(sl.h_pin, st->cap), flag_val[s]);
+        }
         if (rc == 0)
             rc = launch(ctx, win, work, chunk, n, sl.stream, crc_pass_ok && nchunks == 1 ? d_crc : nullptr,
                         t_crc.legacy, &fused);
+        // the flag ends the call only when nothing follows the codec launch on the stream: a separate
+        // CRC pass (want_crc, not fused) does
+        if (arm) flagged[s] = ecamd_done_flag_taken() != 0 && rc == 0 && !(want_crc && !fused);
         if (rc == 0 && want_crc && !fused && zc_in && !zc_out)  // the CRC pass reads every fragment from the device slab
             rc = ecamd_memcpy_async(work, win, K * chunk, 0, sl.stream);
         if (rc == 0 && !zc_out)

@@ -76,6 +76,7 @@ int main(int argc, char** argv)
     style.crc_wave = crc_wave & 15;
     style.crc_mix = (crc_wave & 16) != 0;
     style.crc_mb = 4 - ((crc_wave >> 5) & 3);
+    style.crc_l1 = (crc_wave >> 7) & 1;
     style.waves = wave || crc_wave ? occ.wmin : 0;  // one-wave forms: the request's occupancy (0: by R)
     style.waves_max = wave || crc_wave ? occ.wmax : 0;
     style.input_barrier = (wave || crc_wave) && occ.barrier;

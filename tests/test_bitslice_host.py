@@ -199,20 +199,21 @@ def test_jitc_prefetch_flag(tmp_path):
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs hiprtc")
-@pytest.mark.parametrize("pos,mb,mix,shifted", [(2, 4, 0, False), (1, 4, 0, False), (4, 4, 0, False), (2, 3, 1, False),
-                                                 (2, 4, 0, True)])
-def test_jitc_crc_wave_form(tmp_path, pos, mb, mix, shifted):
+@pytest.mark.parametrize("pos,mb,mix,shifted,l1", [(2, 4, 0, False, 0), (1, 4, 0, False, 0), (4, 4, 0, False, 0),
+                                                    (2, 3, 1, False, 0), (2, 4, 0, True, 0), (2, 4, 0, False, 1)])
+def test_jitc_crc_wave_form(tmp_path, pos, mb, mix, shifted, l1):
     """Flag bit 22 (round 5): the crc variant in one-wave 4 KiB tiles -- workgroups of W waves (bits
     23-26) sharing one table image of `pos` position sets for pieces 1 KiB apart (bits 2-3), byte
     piece tables for the first mb dwords (bits 28-29: 4 - mb), the lane-shift fold (bit 4), the next
     input prefetched (bits 8-10), occupancy in bits 11-18, bit 27 no barrier between lookups and
-    network.  The kernel builds without scratch, its static LDS is the image (the piece sets, 4 KiB of
-    maps, 32 KiB of lane tables), the tile loop carries no atomics; malformed requests are refused."""
+    network, bit 30 (round 6) dword 3 of each piece looked up in the image in global memory.  The kernel
+    builds without scratch, its static LDS is the image (the piece sets, 4 KiB of maps, 32 KiB of lane
+    tables), the tile loop carries no atomics; malformed requests are refused."""
     G = orc.generator(10, 4)
     rows = "\n".join(" ".join(str(c) for c in G[100 + 10 * r:100 + 10 * (r + 1)]) for r in range(4)) + "\n"
     pcode = {1: 0, 2: 1, 4: 2}[pos]
     flags = (1 | 2 | (pcode << 2) | 16 | (4 << 8) | (3 << 11) | (3 << 15) | (1 << 22) | (4 << 23) | (mix << 27) |
-             ((4 - mb) << 28))
+             ((4 - mb) << 28) | (l1 << 30))
     shifts = [(j * 104858) % 16 for j in range(10)]
     head = (f"ecamd-bitslice-request 3\n4 10 40 0\n{flags}\n" + " ".join(map(str, shifts)) + "\n") if shifted \
         else f"ecamd-bitslice-request 2\n4 10 40 0\n{flags}\n"
@@ -228,6 +229,7 @@ def test_jitc_crc_wave_form(tmp_path, pos, mb, mix, shifted):
     assert "__launch_bounds__(256)" in src and "amdgpu_waves_per_eu(3, 3)" in src
     assert "atomic" not in src
     assert ("piece_r0m<" in src) == (mb < 4)
+    assert ("piece_r0g(ctab" in src) == bool(l1)
     assert ("rlg<10>(" in src) == shifted
     notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", str(out)], capture_output=True,
                            text=True).stdout
@@ -237,6 +239,7 @@ def test_jitc_crc_wave_form(tmp_path, pos, mb, mix, shifted):
     for f in (flags & ~2 & ~1,                      # the form without crc
               flags & ~(15 << 23),                  # no waves per workgroup
               flags | 32,                           # nibble-table variant bit
-              (flags & ~(1 << 22) & ~(15 << 23)) | (1 << 27)):  # bit 27 without the form
+              (flags & ~(1 << 22) & ~(15 << 23)) | (1 << 27),  # bit 27 without the form
+              flags | (1 << 28) | (1 << 30)):       # global-memory lookups with nibble tables
         bad.write_text(f"ecamd-bitslice-request 2\n4 10 40 0\n{f}\n" + rows)
         assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2

@@ -937,8 +937,10 @@ def test_stream_contexts_bounded(F):
     import ctypes
     from liberasurecode_amd import _lib
     from liberasurecode_amd.device import Stream
-    hip = ctypes.CDLL("libamdhip64.so")
     d = _lib.dev()
+    # hipStreamDestroy behind the library's back, on the library's own HIP runtime (a ctypes load of
+    # "libamdhip64.so" may open another copy than the one libecamd and torch share, by test order)
+    d.ecamd_stream_destroy_unmanaged.argtypes = [ctypes.c_void_p]
     be = ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND
     k, m, size = 10, 4, 1 << 20
     objs = _objects(1, size, 4242)
@@ -958,7 +960,7 @@ def test_stream_contexts_bounded(F):
             s.destroy()
         else:
             s.synchronize()
-            assert hip.hipStreamDestroy(ctypes.c_void_p(s.handle)) == 0
+            assert d.ecamd_stream_destroy_unmanaged(ctypes.c_void_p(s.handle)) == 0
             s.handle = None
         peak = max(peak, d.ecamd_stream_contexts())
     assert peak <= 17, peak  # the cap (16) + the context being created
@@ -1014,7 +1016,7 @@ def test_stream_contexts_threaded(F):
     ("xor", 3, 3, 3 * 104858 - 4), ("rs", 20, 8, 20 * 40000), ("rs", 12, 6, 12 * 65536),
     ("rs", 10, 4, 10 * 23 * 4096), ("rs", 4, 2, 4 * 4096)])
 @pytest.mark.parametrize("form", [(6, 2, 4, 0, 4), (4, 1, 1, 2, 3), (12, 4, 3, 0, 4), (6, 2, 1, 4, 2), (4, 2, 1, 4, 1),
-                                  (4, 2, 1, 3, 4)])
+                                  (4, 2, 1, 3, 4), (4, 2, 1, 2, 4, 1)])
 @pytest.mark.parametrize("legacy", [False, True])
 def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypatch):
     """CHKSUM_CRC32 framed encode on the crc variant in one-wave 4 KiB tiles (knobs frame_crc_wave =
@@ -1042,13 +1044,15 @@ def test_frame_encode_crc_wave_matches(F, be, k, m, size, form, legacy, monkeypa
             _lib.check(d.ecamd_tune(b"frame_crc_wave_pf", form[3]), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_big", 60 if form[2] > 1 else 0), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_mb", form[4]), "tune")
+            # form[5]: a piece's last dword looked up in global memory (knob frame_crc_wave_l1, round 6 A/B)
+            _lib.check(d.ecamd_tune(b"frame_crc_wave_l1", form[5] if len(form) > 5 else 0), "tune")
             _lib.check(d.ecamd_tune(b"frame_crc_wave_strict", 1 if w else 0), "tune")
             fb = F.FrameBatch(code, k, m, size, S, hd=hd)
             fb.encode(_upload_objects(objs, fb.obj_stride))
             out.append(fb.fragments())
     finally:
         for kn in (b"frame_crc_wave", b"frame_crc_wave_pos", b"frame_crc_wave_per", b"frame_crc_wave_pf",
-                   b"frame_crc_wave_big", b"frame_crc_wave_mb", b"frame_crc_wave_strict"):
+                   b"frame_crc_wave_big", b"frame_crc_wave_mb", b"frame_crc_wave_strict", b"frame_crc_wave_l1"):
             d.ecamd_tune(kn, -1)
         d.ecamd_tune(b"bitslice", 1)
     assert np.array_equal(out[0], out[1])

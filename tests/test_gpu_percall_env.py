@@ -4,7 +4,8 @@ pinned slab for every size (ECAMD_PERCALL_ZEROCOPY_MODE 3) or only its outputs (
 everywhere: ZEROCOPY_IN_KIB 0), inputs AND outputs by DMA (mode 0 / ZEROCOPY_KIB 0), the kernel
 writing its outputs to device memory while reading the slab (mode 1: the CRC pass then copies the
 inputs to the device slab), inputs packed through the PCIe BAR (ECAMD_PERCALL_BAR_KIB), and the
-checksum pass unfused (ECAMD_PERCALL_FUSE_CRC 0) -- RS(10,4) encode / decode / reconstruct at 4 KiB,
+checksum pass unfused (ECAMD_PERCALL_FUSE_CRC 0), the stream synchronized instead of the kernel's
+completion flag polled (ECAMD_PERCALL_DONE_FLAG 0) -- RS(10,4) encode / decode / reconstruct at 4 KiB,
 64 KiB and 1 MiB with CHKSUM_NONE and CRC32, byte-exact against the restated framing, and every
 setting's output digest equal to the default's."""
 import json
@@ -26,6 +27,7 @@ SETTINGS = {
     "zerocopy_off": {"ECAMD_PERCALL_ZEROCOPY_KIB": "0"},
     "bar_64k": {"ECAMD_PERCALL_BAR_KIB": "64", "ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0"},
     "crc_unfused": {"ECAMD_PERCALL_FUSE_CRC": "0"},
+    "stream_sync": {"ECAMD_PERCALL_DONE_FLAG": "0"},
 }
 
 

@@ -26,7 +26,10 @@ SETS = {
     # separate two-launch ecamd_crc32 pass / host zlib (FUSE_CRC 0); round 5's defaults for reference
     "crc": {"default": {},
             "no_fuse": {"ECAMD_PERCALL_FUSE_CRC": "0"},
-            "r05_defaults": {"ECAMD_PERCALL_FUSE_CRC": "0", "ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0"}},
+            "r05_defaults": {"ECAMD_PERCALL_FUSE_CRC": "0", "ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0",
+                             "ECAMD_PERCALL_DONE_FLAG": "0"}},
+    # round 6: the small kernel's completion flag polled (default) or the stream synchronized
+    "flag": {"default": {}, "stream_sync": {"ECAMD_PERCALL_DONE_FLAG": "0"}},
 }
 
 
