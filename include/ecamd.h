@@ -105,7 +105,13 @@ int ecamd_map_apply_strided(const ecamd_map *map, const void *in_base, int64_t i
 int ecamd_map_apply_strided_crc(const ecamd_map *map, const void *in_base, const int64_t *in_off, void *out_base,
                                 const int64_t *out_off, int64_t blocksize, int legacy, uint32_t *crc_out,
                                 void *stream);
-/* Launches of ecamd_map_apply_strided_crc that fused the checksums (tests pin which path ran). */
+/* The same for a flat-XOR map (masks as ecamd_xor_apply_strided, at most 8 outputs): one launch of the
+ * small-launch XOR kernel with the checksums folded in; 0 done, 1 not fused (nothing launched), < 0 error. */
+int ecamd_xor_apply_strided_crc(const uint32_t *masks, int R, int K, const void *in_base, const int64_t *in_off,
+                                void *out_base, const int64_t *out_off, int64_t blocksize, int legacy,
+                                uint32_t *crc_out, void *stream);
+/* Launches of ecamd_map_apply_strided_crc / ecamd_xor_apply_strided_crc that fused the checksums (tests
+ * pin which path ran). */
 long long ecamd_small_crc_launches(void);
 /* Completion flag of the calling thread's next operation (the per-call path, host/hostio.cpp): when the
  * small-launch kernel that ends it runs (gf16_small_kernel), it stores `value` to *flag -- pinned host

@@ -671,6 +671,27 @@ struct DoneFlag {
 };
 thread_local DoneFlag t_done;
 
+// Attaches the thread's armed completion flag to a small launch of `grid` workgroups that ends its
+// operation: several workgroups count in the stream's scratch slot (its context held in `use` until the
+// launch is enqueued, so it is not released meanwhile); a fused checksum counts with its own counter.
+void attach_done(SmallArgs& s, unsigned grid, bool crc, hipStream_t st, std::unique_ptr<StreamUse>& use)
+{
+    if (!t_done.flag || t_done.taken) return;
+    if (grid > 1 && !crc) {
+        int dev = 0;
+        uint32_t* scr = nullptr;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            use = std::make_unique<StreamUse>(dev, st);
+            if (stream_scratch(dev, st, kSmallCrcScratchSlot, 16, &scr) == 0) s.done_ctr = scr + 1;
+        }
+        (void)hipGetLastError();
+    }
+    if (grid == 1 || crc || s.done_ctr) {
+        s.done = t_done.flag;
+        s.done_val = t_done.value;
+    }
+}
+
 // ECAMD_EINVAL (nothing launched) when `crc` is given and the launch cannot fuse it.  `last`: this launch
 // ends the operation (the completion flag may be attached to it).
 int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
@@ -690,24 +711,8 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
                        p.bytes + stage <= kLdsBytes &&
                        (a.ncols - 1) * s.in_pitch + bs < (int64_t(1) << 31);
     const size_t lds = p.bytes + (st_in ? stage : 0);
-    // completion flag: several workgroups count in the stream's scratch slot (its context held in use
-    // until this launch is enqueued, so it is not released meanwhile)
     std::unique_ptr<StreamUse> use;
-    if (last && t_done.flag && !t_done.taken) {
-        if (grid.x > 1 && !crc) {
-            int dev = 0;
-            uint32_t* scr = nullptr;
-            if (hipGetDevice(&dev) == hipSuccess) {
-                use = std::make_unique<StreamUse>(dev, st);
-                if (stream_scratch(dev, st, kSmallCrcScratchSlot, 16, &scr) == 0) s.done_ctr = scr + 1;
-            }
-            (void)hipGetLastError();
-        }
-        if (grid.x == 1 || crc || s.done_ctr) {
-            s.done = t_done.flag;
-            s.done_val = t_done.value;
-        }
-    }
+    if (last) attach_done(s, grid.x, crc != nullptr, st, use);
     if (crc) {
         // the region-shift maps reach 63 regions past a workgroup's: at most 64 workgroups
         if (!st_in || (lane != 2 && lane != 4) || a.accumulate || grid.x > 64) return ECAMD_EINVAL;
@@ -758,11 +763,38 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
     return 0;
 }
 
-int launch_xor_small(const ApplyArgs& a, int64_t bs, int nstripes, hipStream_t st)
+// `last`: this launch ends the operation (the completion flag may be attached).  ECAMD_EINVAL (nothing
+// launched) when `crc` is given and the launch cannot fuse it.
+int launch_xor_small(const ApplyArgs& a, int64_t bs, int nstripes, hipStream_t st, bool last = false,
+                     const SmallCrcReq* crc = nullptr)
 {
-    const SmallArgs s = small_args(a, bs, nstripes, 4);
-    hipLaunchKernelGGL(xor_small_kernel, dim3(static_cast<unsigned>((s.nchunks + 255) / 256)), dim3(256), 0, st, s);
+    SmallArgs s = small_args(a, bs, nstripes, 4);
+    const unsigned grid = static_cast<unsigned>((s.nchunks + 255) / 256);
+    // staged inputs (xor_small_kernel ST), as launch_small: one stripe, a 16-byte pitch and base, 1 KiB per input
+    const bool st_in = (g_tune.small_stage || crc) && nstripes == 1 && (s.in_pitch % 16) == 0 && aligned16(s.in) &&
+                       (a.ncols - 1) * s.in_pitch + bs < (int64_t(1) << 31);
+    if (crc) {
+        if (!st_in || a.accumulate || grid > 64) return ECAMD_EINVAL;
+        const SmallCrcConst k = small_crc_const(crc->legacy, static_cast<uint64_t>(bs),
+                                                static_cast<uint64_t>(grid) * 1024 - static_cast<uint64_t>(bs));
+        s.crc_img = crc->img[1];
+        s.crc_out = crc->out;
+        s.crc_part = crc->part;
+        std::copy(k.minv, k.minv + 32, s.crc_minv);
+        s.crc_c = k.c;
+    }
+    std::unique_ptr<StreamUse> use;
+    if (last) attach_done(s, grid, crc != nullptr, st, use);
+    const size_t stage = static_cast<size_t>(crc ? a.ncols + a.nrows : a.ncols) * 1024 +
+                         (crc ? static_cast<size_t>(small_crc_words(4)) * 4 : 0);
+    if (crc)
+        hipLaunchKernelGGL((xor_small_kernel<true, true>), dim3(grid), dim3(256), stage, st, s);
+    else if (st_in)
+        hipLaunchKernelGGL((xor_small_kernel<true, false>), dim3(grid), dim3(256), stage, st, s);
+    else
+        hipLaunchKernelGGL((xor_small_kernel<false, false>), dim3(grid), dim3(256), 0, st, s);
     HIP_TRY(hipGetLastError());
+    if (s.done) t_done.taken = true;
     return 0;
 }
 
@@ -1356,7 +1388,7 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                 a.masks[r] = col0 < 32 ? (masks[row0 + r] >> col0) : 0u;
             }
             if (!PTRS && !copy_off && small_launch(a, bs, nstripes)) {
-                int rc = launch_xor_small(a, bs, nstripes, st);
+                int rc = launch_xor_small(a, bs, nstripes, st, row0 + kMaxRows >= R && col0 + 32 >= K);
                 if (rc) return rc;
                 continue;
             }
@@ -2785,6 +2817,45 @@ int ecamd_map_apply_strided_crc(const ecamd_map* map, const void* in_base, const
                              &req.part)))
         return rc;
     rc = launch_small(a, p, blocksize, 1, map->d_tables, static_cast<hipStream_t>(stream), &req, true);
+    if (rc == 0) g_small_crc_launches.fetch_add(1, std::memory_order_relaxed);
+    return rc == ECAMD_EINVAL ? 1 : rc;
+}
+
+int ecamd_xor_apply_strided_crc(const uint32_t* masks, int R, int K, const void* in_base, const int64_t* in_off,
+                                void* out_base, const int64_t* out_off, int64_t blocksize, int legacy,
+                                uint32_t* crc_out, void* stream)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (!masks || !in_off || !out_off || !crc_out || R <= 0 || K <= 0 || K > 32)
+        return fail(ECAMD_EINVAL, "bad xor map R=%d K=%d", R, K);
+    if (blocksize <= 0 || R > kMaxRows || K + R > 64) return 1;  // one launch of at most 8 outputs
+    bool ok = aligned16(in_base) && aligned16(out_base);
+    for (int j = 0; j < K; j++) ok = ok && (in_off[j] % 16) == 0;
+    for (int r = 0; r < R; r++) ok = ok && (out_off[r] % 16) == 0;
+    if (!ok) return fail(ECAMD_EINVAL, "fragment addresses must be 16-byte aligned");
+    ApplyArgs a{};
+    a.in_base = static_cast<const uint8_t*>(in_base);
+    a.out_base = static_cast<uint8_t*>(out_base);
+    a.bs = blocksize;
+    a.ncols = K;
+    a.nrows = R;
+    for (int j = 0; j < K; j++) a.in_off[j] = in_off[j];
+    for (int r = 0; r < R; r++) {
+        a.out_off[r] = out_off[r];
+        a.masks[r] = masks[r];
+    }
+    if (!small_launch(a, blocksize, 1)) return 1;
+    SmallCrcReq req{};
+    req.out = crc_out;
+    req.legacy = legacy != 0;
+    if ((rc = small_crc_image(dev, req.legacy, 4, &req.img[1]))) return rc;
+    StreamUse use(dev, stream);
+    const size_t wgs = static_cast<size_t>((blocksize + 1023) / 1024 + 1);
+    if ((rc = stream_scratch(dev, stream, kSmallCrcScratchSlot, 16 + static_cast<size_t>(K + R) * wgs, &req.part)))
+        return rc;
+    rc = launch_xor_small(a, blocksize, 1, static_cast<hipStream_t>(stream), true, &req);
     if (rc == 0) g_small_crc_launches.fetch_add(1, std::memory_order_relaxed);
     return rc == ECAMD_EINVAL ? 1 : rc;
 }

@@ -79,6 +79,163 @@ template __global__ void gf16_copy_apply_kernel<4>(const ApplyArgs);
 template __global__ void gf16_copy_apply_kernel<8>(const ApplyArgs);
 
 
+// Staged inputs of a small launch (one stripe): the K fragments' bytes [c0 * G, c0 * G + region) into
+// stg + j * region as 16-byte pieces, up to 8 loads per thread in flight before the first LDS store (from
+// pinned host memory each load is a PCIe round trip).  The range ends at the last input's last 16-byte
+// granule (the buffer unit checks whole dwords; a granule never crosses a page).  ZERO: the whole region,
+// zeros past bs (a checksum's zero extension); else only up to bs (bytes past bs staged, never read).
+template <bool ZERO>
+__device__ __forceinline__ void small_stage_inputs(uint8_t* stg, const SmallArgs& a, int K, int64_t base, int region)
+{
+    const int64_t left = a.bs - base;
+    const int nseg = static_cast<int>(((left < region ? left : region) + 15) / 16);
+    const auto rin = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(a.in), 0, static_cast<int>((K - 1) * a.in_pitch + ((a.bs + 15) & ~int64_t(15))),
+        0x00020000);
+    const int nq = ZERO ? region / 16 : nseg;
+    const int total = K * nq;
+    for (int i0 = static_cast<int>(threadIdx.x); i0 < total; i0 += 8 * static_cast<int>(blockDim.x)) {
+        u32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int idx = i0 + u * static_cast<int>(blockDim.x);
+            const int j = idx / nq, q = idx - j * nq;
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (idx < total && q < nseg)
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<int>(j * a.in_pitch + base + q * 16), 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int idx = i0 + u * static_cast<int>(blockDim.x);
+            if (idx >= total) break;
+            const int j = idx / nq, q = idx - j * nq;
+            if constexpr (ZERO) {
+                const int64_t keep = left - q * 16;  // bytes of this piece inside the fragment
+                if (keep < 16) {
+#pragma unroll
+                    for (int d = 0; d < 4; d++) {
+                        const int64_t kd = keep - 4 * d;
+                        const uint32_t m = kd >= 4 ? 0xffffffffu : kd <= 0 ? 0u : (1u << (8 * kd)) - 1u;
+                        v[u][d] &= m;
+                    }
+                }
+            }
+            *reinterpret_cast<u32x4*>(stg + j * region + q * 16) = v[u];
+        }
+    }
+}
+
+// The completion flag of a small launch (SmallArgs::done), after every output store of every workgroup
+// is visible system-wide: one workgroup stores it, several count first (done_ctr, self-resetting).
+__device__ __forceinline__ void small_done(const SmallArgs& a)
+{
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const bool last = gridDim.x == 1 ||
+                          atomicInc(reinterpret_cast<unsigned*>(a.done_ctr), gridDim.x - 1) == gridDim.x - 1;
+        if (last) {
+            __threadfence_system();
+            __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// The fused checksum epilogue of a small launch (gf16_small_kernel / xor_small_kernel CRC): the K inputs
+// and nrows outputs of this workgroup's region are in LDS at stg + f * REGION (zeros past bs), the image
+// of build_small_crc_image at cimg.  r0(X||Y) = A^|Y| r0(X) ^ r0(Y), so r0 of a region is the XOR over
+// its 16-byte pieces l of A^(16 (NP - 1 - l)) r0(piece l): lane l looks up r0 of its piece and its
+// position map (two rounds of independent LDS lookups), the wave XOR-reduces, and each wave works on up
+// to 4 fragments at once.  A workgroup's region r0 goes past the regions after it with the binary maps
+// A^(REGION 2^i); the last workgroup to finish (a self-resetting counter) XORs them: S = r0 of the fragment
+// zero-extended to gridDim * REGION bytes, then r0 = A^-zext S and crc = ~(A^len ~0 ^ r0) with host
+// constants (crc_minv, crc_c).  With several workgroups it also stores the completion flag and returns
+// true (the caller stores it otherwise).
+template <int REGION>
+__device__ bool small_crc_epilogue(const SmallArgs& a, const uint8_t* stg, const uint32_t* cimg, int K)
+{
+    using namespace crcdev;
+    constexpr int NP = REGION / 16;  // 16-byte pieces of a region: 32 or 64
+    const uint32_t* const pos = cimg + kSmallCrcPieceWords;  // A^(16 (NP - 1 - l)), l < NP
+    const uint32_t* const wgs = pos + NP * 128;             // A^(REGION 2^i), i < 6
+    const int lane = static_cast<int>(threadIdx.x) & 63, wave = static_cast<int>(threadIdx.x) >> 6;
+    const int nw = static_cast<int>(blockDim.x) >> 6;
+    const int nfr = K + a.nrows;
+    const int nwg = static_cast<int>(gridDim.x);
+    const int after = nwg - 1 - static_cast<int>(blockIdx.x);  // regions after this workgroup's
+    __syncthreads();  // every lane's outputs are in LDS
+    auto finish = [&](int f, uint32_t S) {  // S = r0 of fragment f zero-extended: the CRC
+        uint32_t r0 = 0;
+#pragma unroll
+        for (int b = 0; b < 32; b++)
+            if ((S >> b) & 1u) r0 ^= a.crc_minv[b];
+        a.crc_out[f] = ~(a.crc_c ^ r0);
+    };
+    for (int f0 = wave; f0 < nfr; f0 += 4 * nw) {
+        uint32_t s[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {  // up to 4 fragments per wave at once: independent lookups
+            const int f = f0 + i * nw;
+            s[i] = 0;
+            if (f < nfr && lane < NP && !(a.crc_dbg & 1)) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(stg + f * REGION + lane * 16);
+                s[i] = lmap<4>(pos + lane * 128, piece_r0<1>(cimg, v));
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 6; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) s[i] ^= __shfl_xor(s[i], 1 << t);
+        // every lane now holds the 4 totals: lane i finishes fragment f0 + i * nw, in parallel
+        if (lane < 4) {
+            const int f = f0 + lane * nw;
+            uint32_t x = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
+            if (f < nfr) {
+                if (nwg == 1) {
+                    finish(f, x);
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 6; b++)
+                        if ((after >> b) & 1) x = lmap<4>(wgs + 128 * b, x);
+                    __hip_atomic_store(a.crc_part + 16 + f * nwg + blockIdx.x, x, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+    }
+    if (nwg > 1) {
+        __shared__ int last;
+        // this workgroup's partials (and, with a completion flag, its output stores, system-wide)
+        // before its count
+        if (a.done)
+            __threadfence_system();
+        else
+            __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0)
+            last = atomicInc(reinterpret_cast<unsigned*>(a.crc_part), static_cast<unsigned>(nwg - 1)) ==
+                   static_cast<unsigned>(nwg - 1);  // wraps to 0: ready for the next launch
+        __syncthreads();
+        if (last) {
+            __threadfence();
+            for (int f = static_cast<int>(threadIdx.x); f < nfr; f += static_cast<int>(blockDim.x)) {
+                uint32_t S = 0;
+                for (int w = 0; w < nwg; w++)
+                    S ^= __hip_atomic_load(a.crc_part + 16 + f * nwg + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                finish(f, S);
+            }
+            if (a.done) {  // every workgroup's stores are visible: the checksums, then the flag
+                __threadfence_system();
+                __syncthreads();
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        return true;
+    }
+    return false;
+}
+
 // gf16_small_kernel<W>: launches of a few thousand 16-byte chunks (per-call objects of a few KiB:
 // one stripe, fragments at a uniform pitch).  Same split tables and chunk arithmetic as
 // apply_tile; what differs is the argument block.  ApplyArgs carries ~1.7 KB of per-fragment
@@ -152,49 +309,7 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
         }
     };
     if constexpr (ST) {
-        // fragment j's bytes [c0 * G, c0 * G + REGION) as 16-byte pieces; bytes past bs are staged but
-        // never read.  The range ends at the last input's last 16-byte granule (the buffer unit checks
-        // whole dwords; a granule never crosses a page), so nothing past it is touched
-        const int64_t base = c0 * G;
-        const int64_t left = a.bs - base;
-        const int nseg = static_cast<int>(((left < REGION ? left : REGION) + 15) / 16);
-        const auto rin = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(a.in), 0, static_cast<int>((K - 1) * a.in_pitch + ((a.bs + 15) & ~int64_t(15))),
-            0x00020000);
-        // CRC: the whole region, zeros past bs (the checksum's zero extension).  Up to 8 loads per
-        // thread are in flight before the first LDS store: each is a PCIe round trip from host memory
-        const int nq = CRC ? REGION / 16 : nseg;
-        const int total = K * nq;
-        for (int i0 = static_cast<int>(threadIdx.x); i0 < total; i0 += 8 * static_cast<int>(blockDim.x)) {
-            u32x4 v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int idx = i0 + u * static_cast<int>(blockDim.x);
-                const int j = idx / nq, q = idx - j * nq;
-                v[u] = u32x4{0u, 0u, 0u, 0u};
-                if (idx < total && q < nseg)
-                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<int>(j * a.in_pitch + base + q * 16),
-                                                                 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int idx = i0 + u * static_cast<int>(blockDim.x);
-                if (idx >= total) break;
-                const int j = idx / nq, q = idx - j * nq;
-                if constexpr (CRC) {
-                    const int64_t keep = left - q * 16;  // bytes of this piece inside the fragment
-                    if (keep < 16) {
-#pragma unroll
-                        for (int d = 0; d < 4; d++) {
-                            const int64_t kd = keep - 4 * d;
-                            const uint32_t m = kd >= 4 ? 0xffffffffu : kd <= 0 ? 0u : (1u << (8 * kd)) - 1u;
-                            v[u][d] &= m;
-                        }
-                    }
-                }
-                *reinterpret_cast<u32x4*>(stg + j * REGION + q * 16) = v[u];
-            }
-        }
+        small_stage_inputs<CRC>(stg, a, K, c0 * G, REGION);
     } else if (c < a.nchunks) {
         fetch4(c, 0, cur);
     }
@@ -302,99 +417,9 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
         }
         if (c + step < a.nchunks) fetch4(c + step, 0, cur);
     }
-    if constexpr (CRC) {
-        using namespace crcdev;
-        constexpr int NP = REGION / 16;  // 16-byte pieces of a region: 32 or 64
-        const uint32_t* const pos = cimg + kSmallCrcPieceWords;  // A^(16 (NP - 1 - l)), l < NP
-        const uint32_t* const wgs = pos + NP * 128;             // A^(REGION 2^i), i < 6
-        const int lane = static_cast<int>(threadIdx.x) & 63, wave = static_cast<int>(threadIdx.x) >> 6;
-        const int nw = static_cast<int>(blockDim.x) >> 6;
-        const int nfr = K + a.nrows;
-        const int nwg = static_cast<int>(gridDim.x);
-        const int after = nwg - 1 - static_cast<int>(blockIdx.x);  // regions after this workgroup's
-        __syncthreads();  // every lane's outputs are in LDS
-        auto finish = [&](int f, uint32_t S) {  // S = r0 of fragment f zero-extended: the CRC
-            uint32_t r0 = 0;
-#pragma unroll
-            for (int b = 0; b < 32; b++)
-                if ((S >> b) & 1u) r0 ^= a.crc_minv[b];
-            a.crc_out[f] = ~(a.crc_c ^ r0);
-        };
-        for (int f0 = wave; f0 < nfr; f0 += 4 * nw) {
-            uint32_t s[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {  // up to 4 fragments per wave at once: independent lookups
-                const int f = f0 + i * nw;
-                s[i] = 0;
-                if (f < nfr && lane < NP && !(a.crc_dbg & 1)) {
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(stg + f * REGION + lane * 16);
-                    s[i] = lmap<4>(pos + lane * 128, piece_r0<1>(cimg, v));
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < 6; t++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) s[i] ^= __shfl_xor(s[i], 1 << t);
-            // every lane now holds the 4 totals: lane i finishes fragment f0 + i * nw, in parallel
-            if (lane < 4) {
-                const int f = f0 + lane * nw;
-                uint32_t x = lane == 0 ? s[0] : lane == 1 ? s[1] : lane == 2 ? s[2] : s[3];
-                if (f < nfr) {
-                    if (nwg == 1) {
-                        finish(f, x);
-                    } else {
-#pragma unroll
-                        for (int b = 0; b < 6; b++)
-                            if ((after >> b) & 1) x = lmap<4>(wgs + 128 * b, x);
-                        __hip_atomic_store(a.crc_part + 16 + f * nwg + blockIdx.x, x, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-            }
-        }
-        if (nwg > 1) {
-            __shared__ int last;
-            // this workgroup's partials (and, with a completion flag, its output stores, system-wide)
-            // before its count
-            if (a.done)
-                __threadfence_system();
-            else
-                __threadfence();
-            __syncthreads();
-            if (threadIdx.x == 0)
-                last = atomicInc(reinterpret_cast<unsigned*>(a.crc_part), static_cast<unsigned>(nwg - 1)) ==
-                       static_cast<unsigned>(nwg - 1);  // wraps to 0: ready for the next launch
-            __syncthreads();
-            if (last) {
-                __threadfence();
-                for (int f = static_cast<int>(threadIdx.x); f < nfr; f += static_cast<int>(blockDim.x)) {
-                    uint32_t S = 0;
-                    for (int w = 0; w < nwg; w++)
-                        S ^= __hip_atomic_load(a.crc_part + 16 + f * nwg + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    finish(f, S);
-                }
-                if (a.done) {  // every workgroup's stores are visible: the checksums, then the flag
-                    __threadfence_system();
-                    __syncthreads();
-                    if (threadIdx.x == 0)
-                        __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-            }
-            return;
-        }
-    }
-    if (a.done) {  // one workgroup, or no checksum: the completion flag after every output store
-        __threadfence_system();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const bool last = gridDim.x == 1 || atomicInc(reinterpret_cast<unsigned*>(a.done_ctr), gridDim.x - 1) ==
-                                                    gridDim.x - 1;  // wraps to 0 for the next launch
-            if (last) {
-                __threadfence_system();
-                __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-    }
+    if constexpr (CRC)
+        if (small_crc_epilogue<REGION>(a, stg, cimg, K)) return;
+    if (a.done) small_done(a);  // one workgroup, or no checksum: the flag after every output store
 }
 #define ECAMD_SMALL(G, ST)                                                 \
     template __global__ void gf16_small_kernel<2, G, ST>(const SmallArgs); \
@@ -460,11 +485,34 @@ __device__ __forceinline__ void xor_tile(const ApplyArgs& a, uint32_t s, int64_t
 }
 
 // xor_small_kernel: flat XOR launches of a few chunks (per-call objects), 4-byte lanes, on the
-// compact SmallArgs (see gf16_small_kernel); the masks are scalars read once.
+// compact SmallArgs (see gf16_small_kernel); the masks are scalars read once.  ST: the workgroup's 1 KiB of
+// every input staged into LDS first (small_stage_inputs; one stripe, one chunk per lane), as the RS kernel
+// does for inputs in pinned host memory; the completion flag (SmallArgs::done) after the outputs.
+// CRC (with ST): the fused checksums of every input and output (small_crc_epilogue), as gf16_small_kernel.
+template <bool ST, bool CRC>
 __global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
 {
+    static_assert(!CRC || ST, "fused CRC: staged inputs");
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int REGION = 256 * 4;
     const int K = a.ncols;
     const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t c0 = static_cast<int64_t>(blockIdx.x) * blockDim.x;
+    uint32_t* const cimg = reinterpret_cast<uint32_t*>(lds + (K + a.nrows) * REGION);
+    if constexpr (ST) {
+        small_stage_inputs<CRC>(lds, a, K, c0 * 4, REGION);
+        if constexpr (CRC) {
+            const int bytes = small_crc_words(4) * 4, stp = static_cast<int>(blockDim.x) * 16;
+            for (int o = static_cast<int>(threadIdx.x) * 16; o < bytes; o += stp)
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(cimg) + o) =
+                    load16(reinterpret_cast<const uint8_t*>(a.crc_img) + o);
+            const int64_t c = c0 + threadIdx.x;  // a lane past the last chunk: zeros in its output slots
+            if (c >= a.nchunks)
+                for (int r = 0; r < a.nrows; r++)
+                    *reinterpret_cast<uint32_t*>(lds + (K + r) * REGION + threadIdx.x * 4) = 0u;
+        }
+        __syncthreads();
+    }
     for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.nchunks; c += step) {
         const int64_t s = c / a.cpf;
         const int64_t off = (c - s * a.cpf) * 4;
@@ -475,16 +523,17 @@ __global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
             for (int i = 0; i < rem; i++) x |= static_cast<uint32_t>(p[i]) << (8 * i);
             return x;
         };
-        const uint8_t* in = a.in + s * a.in_stride + off;
+        const uint8_t* in = ST ? lds + (c - c0) * 4 : a.in + s * a.in_stride + off;
+        const int64_t ipitch = ST ? REGION : a.in_pitch;
         uint32_t acc[kMaxRows];
 #pragma unroll
         for (int r = 0; r < kMaxRows; r++) acc[r] = 0u;
         uint32_t cur[4], nxt[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) cur[i] = i < K ? load(in + i * a.in_pitch) : 0u;
+        for (int i = 0; i < 4; i++) cur[i] = i < K ? load(in + i * ipitch) : 0u;
         for (int j0 = 0; j0 < K; j0 += 4) {
 #pragma unroll
-            for (int i = 0; i < 4; i++) nxt[i] = j0 + 4 + i < K ? load(in + (j0 + 4 + i) * a.in_pitch) : 0u;
+            for (int i = 0; i < 4; i++) nxt[i] = j0 + 4 + i < K ? load(in + (j0 + 4 + i) * ipitch) : 0u;
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
@@ -500,6 +549,9 @@ __global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
             uint8_t* q = out + r * a.out_pitch;
             uint32_t v = acc[r];
             if (a.accumulate) v ^= load(q);
+            if constexpr (CRC)  // the output's bytes (zeros past bs) beside the staged inputs
+                *reinterpret_cast<uint32_t*>(lds + (K + r) * REGION + (c - c0) * 4) =
+                    v & (rem >= 4 ? 0xffffffffu : (1u << (8 * rem)) - 1u);
             if (rem >= 4) {
                 *reinterpret_cast<uint32_t*>(q) = v;
             } else {
@@ -507,7 +559,13 @@ __global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
             }
         }
     }
+    if constexpr (CRC)
+        if (small_crc_epilogue<REGION>(a, lds, cimg, K)) return;
+    if (a.done) small_done(a);
 }
+template __global__ void xor_small_kernel<false, false>(const SmallArgs);
+template __global__ void xor_small_kernel<true, false>(const SmallArgs);
+template __global__ void xor_small_kernel<true, true>(const SmallArgs);
 
 template <int W, bool PTRS>
 __global__ void __launch_bounds__(256) xor_apply_kernel(const ApplyArgs a)

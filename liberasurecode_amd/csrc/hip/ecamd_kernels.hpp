@@ -102,6 +102,7 @@ __global__ void gf16_small_kernel(const SmallArgs a);
 // region-shift maps (nibble fields, 128 words each).
 constexpr int kSmallCrcPieceWords = 1024 + 3 * 128;
 constexpr int small_crc_words(int G) { return kSmallCrcPieceWords + (16 * G + 6) * 128; }
+template <bool ST, bool CRC = false>
 __global__ void xor_small_kernel(const SmallArgs a);
 template <int W>
 __global__ void gf16_copy_apply_kernel(const ApplyArgs a);

@@ -400,8 +400,11 @@ bool poll_done(const uint32_t* flag, uint32_t value)
 using Launch = int (*)(const void* ctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream,
                        uint32_t* crc_dst, bool legacy, bool* fused);
 
+// staged_in: the launcher's small kernel stages its inputs through LDS with wide loads (gf16_small_kernel,
+// xor_small_kernel; reading 2-4-byte lanes in place over PCIe costs more than the DMA), so small calls may
+// leave the inputs in the pinned slab.
 int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, int64_t bs,
-                const void* ctx, Launch launch)
+                const void* ctx, Launch launch, bool staged_in)
 {
     const int64_t nfr = K + R;
     // The chunk is also the fragment pitch in the slab: a multiple of 128 puts every fragment
@@ -426,7 +429,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     // which side works on the pinned slab itself (ECAMD_PERCALL_ZEROCOPY_MODE, bit 0 inputs, bit 1
     // outputs; inputs also for fragments of at most ECAMD_PERCALL_ZEROCOPY_IN_KIB, the small-launch
     // kernel's sizes, whose inputs it stages through LDS with wide loads)
-    const bool zc_in = zero_copy && ((zerocopy_mode() & 1) || bs <= zerocopy_in_bytes());
+    const bool zc_in = zero_copy && ((zerocopy_mode() & 1) || (staged_in && bs <= zerocopy_in_bytes()));
     const bool zc_out = zero_copy && (zerocopy_mode() & 2);
     // inputs packed straight into host-writable device memory (no H2D DMA), outputs into the pinned slab
     const bool bar = zc_out && !zc_in && !want_crc && nchunks == 1 && K * chunk <= std::min(bar_bytes(), kBarSlabBytes);
@@ -583,13 +586,21 @@ struct XorCtx {
 };
 
 int launch_xor(const void* vctx, char* din, char* dout, int64_t pitch, int64_t bytes, void* stream,
-               uint32_t* /*crc_dst*/, bool /*legacy*/, bool* fused)
+               uint32_t* crc_dst, bool legacy, bool* fused)
 {
-    *fused = false;  // xor_small_kernel has no checksum epilogue: the separate pass (or the host) serves
+    *fused = false;
     const XorCtx* c = static_cast<const XorCtx*>(vctx);
     std::vector<int64_t> io(c->K), oo(c->R);
     for (int j = 0; j < c->K; j++) io[j] = j * pitch;
     for (int r = 0; r < c->R; r++) oo[r] = (c->K + r) * pitch;
+    if (crc_dst && g_fuse_crc) {  // the XOR launch with the checksums folded in, when the shape allows
+        const int rc = ecamd_xor_apply_strided_crc(c->masks.data(), c->R, c->K, din, io.data(), dout, oo.data(),
+                                                   bytes, legacy ? 1 : 0, crc_dst, stream);
+        if (rc <= 0) {
+            *fused = rc == 0;
+            return rc;
+        }
+    }
     return ecamd_xor_apply_strided(c->masks.data(), c->R, c->K, din, 0, io.data(), dout, 0, oo.data(),
                                    bytes, 1, stream);
 }
@@ -615,7 +626,7 @@ int ecamd_host_map_apply(const int* coeff, int R, int K, const void* const* in,
     if (!mh) return note_exec(rc ? rc : ECAMD_EINVAL);
     MapCtx ctx{mh->map, K, R};
     return note_exec(run_chunked(dev, K, R, reinterpret_cast<const char* const*>(in),
-                                 reinterpret_cast<char* const*>(out), blocksize, &ctx, launch_map));
+                                 reinterpret_cast<char* const*>(out), blocksize, &ctx, launch_map, true));
 }
 
 int ecamd_host_xor_apply(const uint64_t* sources, int R, int nbuf, const void* const* bufs,
@@ -653,7 +664,7 @@ int ecamd_host_xor_apply(const uint64_t* sources, int R, int nbuf, const void* c
     DeviceScope scope(dev);
     if (scope.rc) return note_exec(scope.rc);
     return note_exec(run_chunked(dev, ctx.K, R, in.data(), reinterpret_cast<char* const*>(out),
-                                 blocksize, &ctx, launch_xor));
+                                 blocksize, &ctx, launch_xor, true));
 }
 
 int ecamd_percall_crc_arm(int legacy)

@@ -424,15 +424,17 @@ def test_small_kernel_nonuniform_offsets(tune):
             assert (out[0, K + r] == want[r]).all(), (ins, r)
 
 
+@pytest.mark.parametrize("S,stage", [(2, 1), (1, 1), (1, 0)])
 @pytest.mark.parametrize("small", [0, 1 << 20])
 @pytest.mark.parametrize("bs", [1, 3, 4, 17, 416, 4097])
 @pytest.mark.parametrize("R,K", [(1, 1), (3, 6), (4, 10), (10, 32)])
-def test_xor_small_kernel(tune, R, K, bs, small):
+def test_xor_small_kernel(tune, R, K, bs, small, S, stage):
     """xor_small_kernel (flat XOR launches of few chunks) and the stream kernel on the same shapes,
-    2 stripes: ragged fragments, more than 8 outputs (row groups), 32 inputs (the masks' width)."""
+    1 and 2 stripes: ragged fragments, more than 8 outputs (row groups), 32 inputs (the masks' width);
+    one-stripe launches with the inputs staged into LDS (small_stage 1, default) or read in place."""
     tune(b"small_chunks", small)
+    tune(b"small_stage", stage)
     rng = np.random.default_rng(bs * 3 + R * 50 + K)
-    S = 2
     frags = rng.integers(0, 256, size=(S, K + R, bs), dtype=np.uint8)
     masks = [int(m) | 1 << (r % K) for r, m in enumerate(rng.integers(0, 1 << min(K, 62), size=R, dtype=np.int64))]
     masks = [m & 0xFFFFFFFF for m in masks]

@@ -30,6 +30,9 @@ SETS = {
                              "ECAMD_PERCALL_DONE_FLAG": "0"}},
     # round 6: the small kernel's completion flag polled (default) or the stream synchronized
     "flag": {"default": {}, "stream_sync": {"ECAMD_PERCALL_DONE_FLAG": "0"}},
+    # round 6, both changes of the per-call path at once against round 5's (inputs by DMA, stream synchronised)
+    "r06": {"default": {}, "r05_path": {"ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0", "ECAMD_PERCALL_DONE_FLAG": "0",
+                                        "ECAMD_PERCALL_FUSE_CRC": "0"}},
 }
 
 

@@ -28,11 +28,15 @@ def pct(xs, q):
     return xs[min(len(xs) - 1, int(q * len(xs)))]
 
 
+BACKEND = {"rs": None, "xor": None}  # set in main: (backend id, k, m, hd)
+
+
 def measure(codec, reps):
     import ec_api
+    be, k, m, hd = BACKEND["cur"]
     out = []
     for ct in (ec_api.CHKSUM_NONE, ec_api.CHKSUM_CRC32):
-        desc = ec_api.create(ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND, 10, 4, ct=ct)
+        desc = ec_api.create(be, k, m, hd=hd, ct=ct)
         assert desc > 0, desc
         for size in SIZES:
             data = os.urandom(size)
@@ -43,9 +47,9 @@ def measure(codec, reps):
                 rc, d, p, flen = ec_api.encode(desc, data)
                 t1 = time.perf_counter()
                 assert rc == 0
-                frags = ec_api.fragments(d, 10, flen) + ec_api.fragments(p, 4, flen)
+                frags = ec_api.fragments(d, k, flen) + ec_api.fragments(p, m, flen)
                 ec_api.lib().liberasurecode_encode_cleanup(desc, d, p)
-                avail = frags[4:]
+                avail = frags[min(m, hd - 1 if hd else m):]
                 t1b = time.perf_counter()
                 rc, got = ec_api.decode(desc, avail, flen)
                 t2 = time.perf_counter()
@@ -82,7 +86,13 @@ def main():
     ap.add_argument("--reps", type=int, default=25)
     ap.add_argument("--codec", default="both", choices=["both", "own", "ref"])
     ap.add_argument("--max-size", type=int, default=0, help="skip object sizes above this (0: all)")
+    ap.add_argument("--backend", default="rs", choices=["rs", "xor"],
+                    help="rs: liberasurecode_rs_vand (10, 4); xor: flat_xor_hd (10, 6, 4), hd - 1 = 3 data lost")
     args = ap.parse_args()
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ec_api
+    BACKEND["cur"] = ((ec_api.EC_BACKEND_LIBERASURECODE_RS_VAND, 10, 4, 0) if args.backend == "rs"
+                      else (ec_api.EC_BACKEND_FLAT_XOR_HD, 10, 6, 4))
     if args.max_size:
         SIZES[:] = [x for x in SIZES if x <= args.max_size]
     if args.codec in ("own", "ref"):
@@ -92,7 +102,8 @@ def main():
     env = dict(os.environ, LD_LIBRARY_PATH=ref_dir + (":" + os.environ["LD_LIBRARY_PATH"]
                                                       if os.environ.get("LD_LIBRARY_PATH") else ""))
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--codec", "ref", "--reps",
-                        str(args.reps)], env=env, capture_output=True, text=True, timeout=900)
+                        str(args.reps), "--backend", args.backend, "--max-size", str(args.max_size)], env=env,
+                       capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
     ref = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     for x in ref:
