@@ -15,7 +15,9 @@ Ranks come from torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*
 `--gpus N` > 1 is given without them, bench.py starts the N rank processes itself before anything
 touches the GPU (fresh child processes, no exec) and relays rank 0's line.
 
-Extra fields: "roofline" (the dominant kernel, HIP-event timed per launch on its launch stream; peak =
+Extra fields: "roofline" (the dominant kernel, per launch from the HIP event pair around the timed
+steps on their launch stream -- gaps between launches count; the encode / decode split comes from
+PASS_SPLIT_STEPS untimed steps after the region, whose extra events would perturb it; peak =
 8 TB/s spec, plus a live copy probe; "trace" = the same figure from the committed rocprofv3 kernel
 trace of this command), "cpu_baseline" (the reference codec compiled from its sources -- or the
 oracle restatement when that build is absent -- on the host's usable cores; at every N, timed by
@@ -36,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+PASS_SPLIT_STEPS = 5  # untimed steps after the timed region that time the encode / decode passes apart
 # second decode pattern per config, data and parity mixed
 MIXED_PATTERNS = {"c3": [0, 5, 10, 13], "c2": [0, 4], "c5": [0, 2, 4, 6, 20, 22, 24, 26]}
 GIB = float(1 << 30)
@@ -534,17 +537,14 @@ def main():
                          f"(bitsliced launches {bs_enc} / {bs_dec}); the per-launch roofline would be misstated")
     bs_per_pass = bs_enc
 
-    ev = [(D.Event(), D.Event(), D.Event()) for _ in range(args.steps)]
+    # The timed steps carry ONE event pair (around all of them): events recorded between the passes
+    # are markers the command processor serialises on, and cost ~1% of the value at C3
+    # (profiles/r06_gap_ab.json).  The encode / decode split is timed afterwards, outside the region.
+    ev_all = (D.Event(), D.Event())
 
-    def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
+    def step():
         D.rs_encode(k, m, lay, stream=stream)
-        if i is not None:
-            ev[i][1].record(stream)
         D.rs_decode(k, m, missing, lay, stream=stream)
-        if i is not None:
-            ev[i][2].record(stream)
 
     # Settle: the GPU leaves its idle clocks only after tens of ms of sustained load (C3 at warm-up
     # 2 / 5 / 20 / 80 steps: 0.70 / 0.72 / 0.739 / 0.741 of 8 TB/s, profiles/r02_warmup_sweep.log),
@@ -565,13 +565,25 @@ def main():
     sync_all()
     co.barrier()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
+    ev_all[0].record(stream)
+    for _ in range(args.steps):
+        step()
+    ev_all[1].record(stream)
     sync_all()
     elapsed = time.perf_counter() - t0
     elapsed = co.reduce([elapsed], op="max")[0]
     co.barrier()
 
+    region_ms = ev_all[0].elapsed_ms(ev_all[1])
+    # encode / decode split: PASS_SPLIT_STEPS more steps with an event between the passes (untimed)
+    ev = [(D.Event(), D.Event(), D.Event()) for _ in range(PASS_SPLIT_STEPS)]
+    for a, b, c in ev:
+        a.record(stream)
+        D.rs_encode(k, m, lay, stream=stream)
+        b.record(stream)
+        D.rs_decode(k, m, missing, lay, stream=stream)
+        c.record(stream)
+    stream.synchronize()
     enc_ms = [a.elapsed_ms(b) for a, b, _ in ev]
     dec_ms = [b.elapsed_ms(c) for _, b, c in ev]
     obj_bytes = S * k * F  # object bytes per batch on this rank
@@ -586,8 +598,8 @@ def main():
     bitsliced = bs_per_pass > 0
     per_pass = bs_per_pass if bitsliced else dispatches_per_pass(k, width, F, S, torch.cuda.get_device_properties(
         torch.cuda.current_device()).multi_processor_count)
-    pass_ms = (sum(enc_ms) + sum(dec_ms)) / (2 * args.steps)
-    launch_ms = pass_ms / per_pass  # HIP events bracket whole passes: gaps between launches count
+    pass_ms = region_ms / (2 * args.steps)
+    launch_ms = pass_ms / per_pass  # HIP events bracket the timed steps: gaps between launches count
     # algorithmic HBM bytes per launch: k inputs read + outputs written, per stripe
     algo_bytes = S * (2 * k + m + len(missing)) * F // 2 // per_pass
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
@@ -688,8 +700,11 @@ def main():
                          "per_rank_frac": [round(algo_bytes / (x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                            for x in per_rank_launch_ms],
                          "dispatches_per_pass": per_pass,
+                         "timed_region_event_ms": round(region_ms, 4),
                          "encode_pass_ms": round(sum(enc_ms) / len(enc_ms), 4),
                          "decode_pass_ms": round(sum(dec_ms) / len(dec_ms), 4),
+                         "pass_split": f"{PASS_SPLIT_STEPS} untimed steps after the region, "
+                                       "an event between the passes",
                          "copy_peak_measured": round(copy_gbs, 1),
                          "copy_peak_rank": 0,
                          "copy_probes": copy_probes,

@@ -6,7 +6,8 @@ timestamps), plus -- for the bench's dominant kernel -- the same statistics over
 only: the bench launches it `--pre` times before the settle steps (2: an encode and a decode, which
 also compile any bitsliced kernel the config needs), twice per settle step (`--settle`, bench.py's
 untimed clock ramp-up), twice per warm-up step, twice per timed step,
-then for the untimed mixed-pattern decodes; the timed launches are dispatches
+then twice per untimed pass-split step (bench.PASS_SPLIT_STEPS) and for the untimed mixed-pattern
+decodes; the timed launches are dispatches
 [pre + 2*(settle + warmup), pre + 2*(settle + warmup) + 2*steps) of that kernel in dispatch order
 (times --per-pass when a pass is several launches).  bench.py reads
 "timed_avg_ns" to put the trace-derived roofline fraction beside its HIP-event one.
