@@ -306,6 +306,7 @@ struct Tuning {
                                   //   stores after its network and the next input's loads, from the planes
                                   //   transposed back (BitsliceStyle prefetch 1): C5 framed encode 0.660 ->
                                   //   0.670, decode-join of 8 data 0.629 -> 0.710 (profiles/r04_late_copy_ab.log)
+    Knob bs_copy_ring{0};         // one-wave copy-through maps read through an LDS ring of 2 / 4 inputs (0: registers)
     Knob bs_realign{1};           // bitsliced copy-through / crc kernels reading object chunks at offsets that are not
                                   //   multiples of 16: 1 = aligned loads + the neighbour lane's chunk (DPP),
                                   //   realigned in registers (BitsliceStyle::in_shift); 0 = unaligned loads
@@ -480,6 +481,7 @@ int dev_tune(const char* key)
     if (k == "frame_xor_copy") return g_tune.frame_xor_copy;
     if (k == "frame_join_align") return g_tune.frame_join_align;
     if (k == "bs_realign") return g_tune.bs_realign;
+    if (k == "bs_copy_ring") return g_tune.bs_copy_ring;
     if (k == "bs_late_copy") return g_tune.bs_late_copy;
     if (k == "bs_prefetch") return g_tune.bs_prefetch;
     if (k == "frame_crc_pos") return g_tune.frame_crc_pos;
@@ -1098,9 +1100,12 @@ bool bs_form(int nrows, int K, bool copy, bool unaligned, BsForm& f)
     if (nrows < g_tune.bitslice_min_rows && !narrow) return false;
     // LDS ring (depth 2 / 4) or register loads: bs_wave_depth for one-wave plain maps, bitslice_depth
     // for 16 KiB tiles; copy-through maps always load into registers
-    f.depth = copy ? 0 : static_cast<int>(f.wave ? g_tune.bs_wave_depth : g_tune.bitslice_depth);
-    f.prefetch = !copy ? (f.wave && f.depth == 0 ? static_cast<int>(g_tune.bs_plain_prefetch) : 0)
-                       : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
+    // (one-wave copy-through maps: an LDS ring only with knob bs_copy_ring, a development A/B)
+    f.depth = copy ? (f.wave ? static_cast<int>(g_tune.bs_copy_ring) : 0)
+                   : static_cast<int>(f.wave ? g_tune.bs_wave_depth : g_tune.bitslice_depth);
+    f.prefetch = f.depth ? 0
+                 : !copy ? (f.wave ? static_cast<int>(g_tune.bs_plain_prefetch) : 0)
+                         : f.wave ? static_cast<int>(g_tune.bs_prefetch) : static_cast<int>(g_tune.bs_late_copy);
     f.occ = wave_occ(nrows, copy);
     if (!f.wave) {  // multi-wave form: its workgroup size (plain register form only; bs_tile_threads)
         f.occ = BsOcc{};
@@ -2530,6 +2535,8 @@ int ecamd_tune(const char* key, int value)
         g_tune.bs_prefetch = value < 0 ? 2 : value == 2 || value == 4 ? value : 0;  // < 0: the default (2)
     } else if (k == "bs_late_copy") {
         g_tune.bs_late_copy = value < 0 ? 1 : value > 0 ? 1 : 0;  // < 0: the default (1)
+    } else if (k == "bs_copy_ring") {
+        g_tune.bs_copy_ring = value >= 4 ? 4 : value >= 2 ? 2 : 0;
     } else if (k == "bs_realign") {
         g_tune.bs_realign = value < 0 ? 1 : value != 0;  // < 0: the default (1)
     } else if (k == "frame_unfused") {

@@ -294,12 +294,15 @@ const std::string& generator_fingerprint()
         wave_pf.prefetch = 4;
         shifted.in_shift = {6};
         crc_shifted.in_shift = {10};
+        BitsliceStyle copy_ring = shifted;  // the one-wave copy-through LDS ring (knob bs_copy_ring)
+        copy_ring.threads = 64;
+        copy_ring.waves = 2;
         fp = bitslice_source(tiny, 0) + bitslice_source(tiny, 2) + bitslice_source(tiny, 0, copy) +
              bitslice_source(tiny, 0, crc) + bitslice_source(tiny, 0, lane) + bitslice_source(tiny5, 0, crc) +
              bitslice_source(tiny5, 0, nib) + bitslice_source(tiny, 0, wave) + bitslice_source(tiny, 0, shifted) +
              bitslice_source(tiny, 0, crc_shifted) + bitslice_source(tiny5, 0, wave_pf) +
              bitslice_source(tiny, 2, wave_ring) + bitslice_source(tiny, 0, wave_occ) +
-             bitslice_source(tiny, 0, crc_wave) + kBsNetworkVersion;
+             bitslice_source(tiny, 0, crc_wave) + bitslice_source(tiny, 2, copy_ring) + kBsNetworkVersion;
     });
     return fp;
 }
@@ -451,8 +454,10 @@ std::vector<int> normalize(const std::vector<int>& coeff, int R, int K, int& dep
     }
     copy = copy || crc;
     wave = wave && !crc;
-    depth = copy ? 0 : bitslice_depth(depth, K);  // one-wave tiles: the LDS ring only in plain maps
-    prefetch = (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
+    // the LDS ring: plain maps, and copy-through maps in one-wave tiles (not the crc variant)
+    depth = crc || (copy && !wave) ? 0 : bitslice_depth(depth, K);
+    prefetch = depth ? 0
+               : (wave || crc) && (prefetch == 2 || prefetch == 4) ? prefetch
                : (crc & 32) && prefetch == 3 ? 3  // the one-wave crc form: two inputs ahead
                : (copy && !crc && !wave && prefetch == 1) ? 1 : 0;
     if (crc & 32) {  // the one-wave crc form keeps its occupancy (waves per SIMD, cap, barrier)

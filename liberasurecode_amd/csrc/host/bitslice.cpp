@@ -365,7 +365,7 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
                                                                                 : bitslice_waves_per_simd(net.R, style.crc);
     // one-wave tiles: the plain / copy-through register form, and the plain LDS-ring form
     const int T = CW ? 64 * CW
-                  : (!style.crc && (!D || !style.copy_through) && style.threads == 64) ? 64
+                  : (!style.crc && style.threads == 64) ? 64
                   : (!style.crc && !D && !style.copy_through && (style.threads == 128 || style.threads == 512))
                       ? style.threads
                       : 256;
@@ -375,6 +375,21 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
     // occupancy CAP -- the compiler raises the kernel descriptor's VGPR count until no more than max
     // waves fit (max 2: 176 VGPRs whatever the code uses).  style.waves_max 0: max = min.
     const int wmax = style.waves_max > 0 ? std::max(style.waves_max, wpe) : wpe;
+    // one-wave LDS ring with realigned inputs: the 16-byte window D bytes into the aligned pair (lo, hi)
+    // read back from the ring (emitted for that form only)
+    bool ring_shift = false;
+    if (D && T == 64)
+        for (int j = 0; j < net.K && j < static_cast<int>(style.in_shift.size()); j++)
+            ring_shift = ring_shift || (style.in_shift[static_cast<size_t>(j)] & 15);
+    if (ring_shift)
+        s << "template <int D>\n__device__ __forceinline__ v4u rl2(v4u lo, v4u hi)\n{\n"
+             "    const u32 w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};\n"
+             "    constexpr int dw = D >> 2, by = D & 3;\n"
+             "    if constexpr (by == 0)\n        return v4u{w[dw], w[dw + 1], w[dw + 2], w[dw + 3]};\n"
+             "    else\n        return v4u{__builtin_amdgcn_alignbyte(w[dw + 1], w[dw], by), "
+             "__builtin_amdgcn_alignbyte(w[dw + 2], w[dw + 1], by),\n"
+             "                   __builtin_amdgcn_alignbyte(w[dw + 3], w[dw + 2], by), "
+             "__builtin_amdgcn_alignbyte(w[dw + 4], w[dw + 3], by)};\n}\n";
     s << "extern \"C\" __global__ void __launch_bounds__(" << T << ") __attribute__((amdgpu_waves_per_eu(" << wpe << ", "
       << wmax << ")))\n"
          "ecamd_bs_kernel(ecamd_bs_args a)\n{\n";
@@ -898,11 +913,18 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
         // LDS-DMA load each: lane l's 16 bytes land at slot + c*1024 + l*16) into a ring of D slots,
         // D - 1 inputs ahead of the network, so the next input's loads are in flight while the current
         // network runs -- without the 16 VGPRs per input a register prefetch holds across it.  The
-        // code is straight-line per tile, so each wait is exact: before input j's reads at most
-        // 4*min(D - 1, K - 1 - j) loads may still be outstanding (vmcnt retires in issue order; the
-        // previous tile's output stores, issued earlier, are retired by the same wait).  A slot is
-        // refilled only after the reads of its previous input returned (lgkmcnt(0) before each network).
-        s << "    __shared__ __attribute__((aligned(16))) u8 ring[" << D << " * 4096];\n"
+        // code is straight-line per tile, so each wait is exact: before input j's reads, the vector-
+        // memory operations issued after its last load may still be outstanding (vmcnt retires in
+        // issue order; the previous tile's output stores, issued earlier, are retired by the same
+        // wait).  A slot is refilled only after the reads of its previous input returned (lgkmcnt(0)
+        // before each network).
+        // Copy-through (framed encode / decode-join): each input's 4 chunks are stored to its copy
+        // slot from the registers read back.  Realigned inputs (in_shift d != 0): the slot holds the
+        // ALIGNED 4 KiB under the tile's windows plus the 16 bytes after it (one more load, by lane 0
+        // only -- the other lanes' offsets are out of range and land zeros in the slot's 1 KiB pad);
+        // lane l reads the aligned pair at l*16 and l*16 + 16 of each chunk and realigns it (rl2<d>).
+        const int SLOT = ring_shift ? 5120 : 4096;
+        s << "    __shared__ __attribute__((aligned(16))) u8 ring[" << D << " * " << SLOT << "];\n"
              "    typedef __attribute__((address_space(3))) u8 lds_u8;\n"
              "    const u32 wring = (u32)(unsigned long)(lds_u8*)ring;\n"
              "    const u32 lane = threadIdx.x * 16u;\n"
@@ -916,28 +938,72 @@ std::string bitslice_source(const BitsliceNet& net, int depth, BitsliceStyle sty
              "            (void*)(a.in_base + (i64)s * a.in_stride), 0, (int)a.in_records, 0x00020000);\n"
              "        const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(\n"
              "            (void*)(a.out_base + (i64)s * a.out_stride), 0, (int)a.out_records, 0x00020000);\n";
+        if (style.copy_through) {
+            s << "        const __amdgpu_buffer_rsrc_t rcopy = __builtin_amdgcn_make_buffer_rsrc(\n"
+                 "            (void*)(a.copy_base + (i64)s * a.copy_stride), 0, (int)a.copy_records, 0x00020000);\n";
+            for (int j = 0; j < net.K; j++)
+                s << "        const i32 cofs" << j << " = a.copy_idx[" << j << "] == 0xff ? (i32)0x80000000u : (i32)(a.copy_idx["
+                  << j << "] * a.copy_step);\n";
+        }
+        // vector-memory operations of one tile in issue order: the input a load belongs to, -1 a store
+        std::vector<int> vmem;
         // (the chunk's byte offset goes into the scalar offset: the instruction's immediate offset
         // would move the LDS destination too)
         auto issue1 = [&](int j) {
-            for (int c = 0; c < 4; c++)
+            const int d = shift_of(j);
+            const std::string base = "a.in_off[" + std::to_string(j) + "]" + (d ? " - " + std::to_string(d) : std::string());
+            for (int c = 0; c < 4; c++) {
                 s << "        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (__attribute__((address_space(3))) void*)(unsigned "
                      "long)(wring + "
-                  << (j % D) * 4096 + c * 1024 << "u), 16, off, a.in_off[" << j << "] + " << c * 1024 << ", 0, 2);\n";
+                  << (j % D) * SLOT + c * 1024 << "u), 16, off, " << base << " + " << c * 1024 << ", 0, 2);\n";
+                vmem.push_back(j);
+            }
+            if (d) {
+                s << "        __builtin_amdgcn_raw_ptr_buffer_load_lds(rin, (__attribute__((address_space(3))) void*)(unsigned "
+                     "long)(wring + "
+                  << (j % D) * SLOT + 4096 << "u), 16, threadIdx.x == 0u ? off + " << base
+                  << " + 4096 : (i32)0x80000000u, 0, 0, 2);\n";
+                vmem.push_back(j);
+            }
+        };
+        auto pending_after = [&](int j) {  // operations issued after input j's last load
+            int n = 0;
+            for (size_t i = vmem.size(); i-- > 0 && vmem[i] != j;) n++;
+            return n;
         };
         acc_init();
         for (int q = 0; q < D - 1 && q < net.K; q++) issue1(q);
         for (int j = 0; j < net.K; j++) {
+            const int d = shift_of(j);
             s << "        {  // input " << j << "\n";
             if (j + D - 1 < net.K) issue1(j + D - 1);
-            s << "            asm volatile(\"s_waitcnt vmcnt(" << 4 * std::min(D - 1, net.K - 1 - j) << ")\" ::: \"memory\");\n"
-              << "            const u32 rd = wring + " << (j % D) * 4096 << "u + lane;\n"
+            s << "            asm volatile(\"s_waitcnt vmcnt(" << std::min(pending_after(j), 63) << ")\" ::: \"memory\");\n"
+              << "            const u32 rd = wring + " << (j % D) * SLOT << "u + lane;\n"
               << "            v4u q0, q1, q2, q3;\n"
               << "            asm volatile(\"ds_read_b128 %0, %1\" : \"=v\"(q0) : \"v\"(rd) : \"memory\");\n"
               << "            asm volatile(\"ds_read_b128 %0, %1 offset:1024\" : \"=v\"(q1) : \"v\"(rd) : \"memory\");\n"
               << "            asm volatile(\"ds_read_b128 %0, %1 offset:2048\" : \"=v\"(q2) : \"v\"(rd) : \"memory\");\n"
-              << "            asm volatile(\"ds_read_b128 %0, %1 offset:3072\" : \"=v\"(q3) : \"v\"(rd) : \"memory\");\n"
-              << "            asm volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(q0), \"+v\"(q1), \"+v\"(q2), \"+v\"(q3));\n"
-              << "            u32 P[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],\n"
+              << "            asm volatile(\"ds_read_b128 %0, %1 offset:3072\" : \"=v\"(q3) : \"v\"(rd) : \"memory\");\n";
+            if (d)
+                s << "            v4u h0, h1, h2, h3;\n"
+                  << "            asm volatile(\"ds_read_b128 %0, %1 offset:16\" : \"=v\"(h0) : \"v\"(rd) : \"memory\");\n"
+                  << "            asm volatile(\"ds_read_b128 %0, %1 offset:1040\" : \"=v\"(h1) : \"v\"(rd) : \"memory\");\n"
+                  << "            asm volatile(\"ds_read_b128 %0, %1 offset:2064\" : \"=v\"(h2) : \"v\"(rd) : \"memory\");\n"
+                  << "            asm volatile(\"ds_read_b128 %0, %1 offset:3088\" : \"=v\"(h3) : \"v\"(rd) : \"memory\");\n"
+                  << "            asm volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(q0), \"+v\"(q1), \"+v\"(q2), \"+v\"(q3), "
+                     "\"+v\"(h0), \"+v\"(h1), \"+v\"(h2), \"+v\"(h3));\n"
+                  << "            q0 = rl2<" << d << ">(q0, h0);\n            q1 = rl2<" << d << ">(q1, h1);\n"
+                  << "            q2 = rl2<" << d << ">(q2, h2);\n            q3 = rl2<" << d << ">(q3, h3);\n";
+            else
+                s << "            asm volatile(\"s_waitcnt lgkmcnt(0)\" : \"+v\"(q0), \"+v\"(q1), \"+v\"(q2), \"+v\"(q3));\n";
+            if (style.copy_through) {
+                for (int c = 0; c < 4; c++) {
+                    s << "            __builtin_amdgcn_raw_buffer_store_b128(q" << c << ", rcopy, cofs" << j << " + off + "
+                      << c * 1024 << ", 0, 2);  // copy-through\n";
+                    vmem.push_back(-1);
+                }
+            }
+            s << "            u32 P[16] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3],\n"
               << "                         q2[0], q2[1], q2[2], q2[3], q3[0], q3[1], q3[2], q3[3]};\n";
             network(j);
             // every network completes before the next input's reads: without it the compiler sinks
@@ -1106,8 +1172,8 @@ bool bitslice_parse_request(const std::string& text, std::vector<int>& coeff, in
     if (wmin > 8 || wmax > 8 || (wmax && wmax < wmin) ||
         ((wmin || wmax || ((cp >> 19) & 1)) && ((!(cp & 64) && !cw) || (cp & 128))))
         return false;
-    if (version >= 2 && depth != 0 && ((cp & ~(128 | (511 << 11))) != 64 || (depth != 2 && depth != 4) || cw))
-        return false;  // copy / crc: register loads; plain one-wave tiles: registers or an LDS ring
+    if (version >= 2 && depth != 0 && (((cp & ~(128 | (511 << 11))) | 1) != 65 || (depth != 2 && depth != 4) || cw))
+        return false;  // crc: register loads; plain / copy-through one-wave tiles: registers or an LDS ring
     if (tcode && cw) return false;
     if (occ) {
         occ->wmin = wmin ? wmin : (cp & 128) ? 2 : 0;

@@ -176,6 +176,39 @@ def test_jitc_realign_lane_experiment(tmp_path):
     assert loads["1"] < loads["0"], loads
 
 
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so") or not shutil.which("/opt/rocm/bin/hipcc"),
+                    reason="needs hiprtc and hipcc")
+@pytest.mark.parametrize("depth", [2, 4])
+def test_jitc_copy_ring_form(tmp_path, depth):
+    """Round 6 (knob bs_copy_ring): the one-wave copy-through form reads its inputs through
+    an LDS ring of `depth` slots; realigned inputs get the aligned 4 KiB + 16 B of the tile per slot (one
+    more LDS-DMA load, by lane 0) and realign on the LDS read (rl2<d>).  Builds without scratch; the ring
+    is refused for the 16 KiB-tile copy form and the crc variant."""
+    G = orc.generator(10, 4)
+    shifts = [(j * 104858) % 16 for j in range(10)]
+    rows = "\n".join(" ".join(str(c) for c in G[100 + 10 * r:100 + 10 * (r + 1)]) for r in range(4)) + "\n"
+    wave_copy = 1 | 64 | (2 << 11) | (2 << 15)
+    req = tmp_path / "ring.req"
+    req.write_text(f"ecamd-bitslice-request 3\n4 10 0 {depth} {wave_copy}\n" + " ".join(map(str, shifts)) + "\n" + rows)
+    out = tmp_path / "ring.co"
+    env = dict(os.environ, ECAMD_JIT_KEEP_SOURCE="1")
+    r = subprocess.run([JITC, str(req), str(out)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    src = (tmp_path / "ring.hip").read_text()
+    assert f"ring[{depth} * 5120]" in src and "rl2<10>(" in src and "threadIdx.x == 0u ?" in src
+    assert src.count("// copy-through") == 40  # 4 chunks of each of the 10 inputs
+    hip = tmp_path / "k.hip"
+    hip.write_text("#include <hip/hip_runtime.h>\n" + src)
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S",
+                        "-o", str(tmp_path / "k.s"), str(hip)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "ScratchSize: 0" in (tmp_path / "k.s").read_text()
+    bad = tmp_path / "bad.req"
+    for flags in (1, 1 | 2 | 16 | (1 << 22) | (2 << 23)):  # 16 KiB-tile copy form; the one-wave crc variant
+        bad.write_text(f"ecamd-bitslice-request 2\n4 10 0 {depth} {flags}\n" + rows)
+        assert subprocess.run([JITC, str(bad), str(tmp_path / "bad.co")], capture_output=True).returncode == 2
+
+
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/lib/libhiprtc.so"), reason="needs hiprtc")
 def test_jitc_prefetch_flag(tmp_path):
     """Flag bits 8-10 (round 4): the one-wave form loads the first 2 / 4 chunks of the next input before

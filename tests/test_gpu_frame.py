@@ -552,9 +552,13 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         # the LDS tables, and the split-then-encode path
         # (+ frame_tail_bs: the payloads' rest past the whole tiles by split + plain encode, or not;
         # + bs_prefetch: the copy-through kernel's next-input loads ahead of its copy stores, 0 / 2 / 4;
-        # + frame_tail_fork: the rest on the side stream by default (1-4 KiB, no checksum), never, always)
-        for padded, mode, tail, pf, fork in ((1, 2, 1, 2, 1), (1, 0, 1, 2, 1), (0, 1, 1, 2, 1), (1, 2, 0, 2, 0),
-                                             (1, 2, 1, 0, 1), (1, 2, 1, 4, 1), (1, 2, 1, 2, 0), (1, 2, 1, 2, 2)):
+        # + frame_tail_fork: the rest on the side stream by default (1-4 KiB, no checksum), never, always;
+        # + bs_copy_ring 2 / 4: the inputs through an LDS ring, realigned on the LDS read)
+        for padded, mode, tail, pf, fork, ring in ((1, 2, 1, 2, 1, 0), (1, 0, 1, 2, 1, 0), (0, 1, 1, 2, 1, 0),
+                                                   (1, 2, 0, 2, 0, 0), (1, 2, 1, 0, 1, 0), (1, 2, 1, 4, 1, 0),
+                                                   (1, 2, 1, 2, 0, 0), (1, 2, 1, 2, 2, 0), (1, 2, 1, 2, 1, 2),
+                                                   (1, 2, 1, 2, 1, 4)):
+            _lib.check(_lib.dev().ecamd_tune(b"bs_copy_ring", ring), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_tail_bs", tail), "tune")
@@ -569,6 +573,7 @@ def test_frame_encode_padded_copy_matches_split(F, k, m, size, ct):
         _lib.dev().ecamd_tune(b"frame_tail_bs", 1)
         _lib.dev().ecamd_tune(b"bs_prefetch", -1)
         _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
+        _lib.dev().ecamd_tune(b"bs_copy_ring", 0)
     assert all(np.array_equal(o, out[2]) for o in out)
     want = expected_stripe(be, k, m, 0, objs[1], ct)
     assert all(out[0][1, i].tobytes() == want[i] for i in range(k + m))
@@ -592,9 +597,12 @@ def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
     try:
         # (frame_copy_padded, bitslice, bs_prefetch): the one-wave bitsliced decode-join (copy-through,
         # next input's loads ahead of the copy stores: 2 default, 0, 4), the LDS tables, decode + join;
-        # frame_tail_fork: the LDS-table rest beside the bitsliced launch by default (1-4 KiB), never, always
-        for padded, mode, pf, fork in ((1, 2, 2, 1), (1, 2, 0, 1), (1, 2, 4, 1), (1, 0, 2, 1), (1, 2, 2, 0),
-                                       (1, 2, 2, 2), (0, 1, 2, 1)):
+        # frame_tail_fork: the LDS-table rest beside the bitsliced launch by default (1-4 KiB), never, always;
+        # bs_copy_ring 2 / 4: the bitsliced decode-join's inputs through an LDS ring
+        for padded, mode, pf, fork, ring in ((1, 2, 2, 1, 0), (1, 2, 0, 1, 0), (1, 2, 4, 1, 0), (1, 0, 2, 1, 0),
+                                             (1, 2, 2, 0, 0), (1, 2, 2, 2, 0), (1, 2, 2, 1, 2), (1, 2, 2, 1, 4),
+                                             (0, 1, 2, 1, 0)):
+            _lib.check(_lib.dev().ecamd_tune(b"bs_copy_ring", ring), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"frame_copy_padded", padded), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bitslice", mode), "tune")
             _lib.check(_lib.dev().ecamd_tune(b"bs_prefetch", pf), "tune")
@@ -609,6 +617,7 @@ def test_frame_decode_padded_join_matches_split(F, k, m, size, missing):
         _lib.dev().ecamd_tune(b"bitslice", 1)
         _lib.dev().ecamd_tune(b"bs_prefetch", -1)
         _lib.dev().ecamd_tune(b"frame_tail_fork", -1)
+        _lib.dev().ecamd_tune(b"bs_copy_ring", 0)
     assert all(np.array_equal(g, got[-1]) for g in got)
     for s in range(S):
         assert got[0][s, :size].tobytes() == objs[s]

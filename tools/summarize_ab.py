@@ -3,7 +3,7 @@
 for profiles/: per case and variant the median, min and max of a metric over the rounds, variants
 sorted best first.  The raw log stays in gpurun_out/ (VERDICT r05 #7).
 
-usage: summarize_ab.py OUT.json LOG --case KEY --variant KEY[,KEY2] --metric KEY --command TEXT
+usage: summarize_ab.py OUT.json LOG --case KEY[,KEY2] --variant KEY[,KEY2] --metric KEY --command TEXT
                        [--lower-is-better] [--note TEXT]"""
 import argparse
 import json
@@ -29,12 +29,12 @@ def main():
         if not line.startswith("{"):
             continue
         r = json.loads(line)
-        if a.metric not in r or a.case not in r:
+        if a.metric not in r or any(c not in r for c in a.case.split(",")):
             continue
         v = next((f"{k}={r[k]}" for k in vkeys if k in r), None)
         if v is None:
             continue
-        table.setdefault(str(r[a.case]), {}).setdefault(v, []).append(r[a.metric])
+        table.setdefault("/".join(str(r[c]) for c in a.case.split(",")), {}).setdefault(v, []).append(r[a.metric])
     out = {"source": a.log, "command": a.command, "metric": a.metric, "note": a.note, "cases": {}}
     for case, vs in table.items():
         rows = [{"variant": v, "median": round(statistics.median(x), 4), "min": min(x), "max": max(x), "n": len(x)}
