@@ -117,9 +117,22 @@ long long ecamd_small_crc_launches(void);
  * small-launch kernel that ends it runs (gf16_small_kernel), it stores `value` to *flag -- pinned host
  * memory -- after every output and checksum store of the operation is visible system-wide, so the host
  * can poll the flag instead of synchronizing the stream.  ecamd_done_flag_taken() says whether the
- * operation took it (1) or not (0: other kernels; synchronize as usual) and disarms. */
+ * operation took it (1), posted it to the resident small server (2: wait with ecamd_small_server_wait,
+ * not on the stream, which it never touched) or not (0: other kernels; synchronize as usual) and disarms. */
 void ecamd_done_flag_arm(uint32_t *flag, uint32_t value);
 int ecamd_done_flag_taken(void);
+/* The same, and the operation may be posted to the calling thread's resident small server (small_server_kernel,
+ * DESIGN.md §6) instead of launched when it is ONE small launch with staged inputs: mode 1 any such launch,
+ * 2 only one with the checksums fused (a separate checksum pass would follow on the stream); 0 as
+ * ecamd_done_flag_arm.  The caller guarantees nothing it enqueued earlier on the stream is still pending. */
+void ecamd_done_flag_arm_server(uint32_t *flag, uint32_t value, int mode);
+/* Waits for a served operation's flag; relaunches the server if it exited before the request (its idle
+ * time).  0, or < 0 after 10 s or a HIP error. */
+int ecamd_small_server_wait(const uint32_t *flag, uint32_t value);
+/* Operations posted to small servers, and server kernels launched (first use, after idle exits, variant
+ * switches, relaunches in ecamd_small_server_wait), in this process (tests pin which path ran). */
+long long ecamd_small_server_posts(void);
+long long ecamd_small_server_launches(void);
 
 /* Pointer tables in device memory: input j of stripe s is d_in_ptrs[s*in_row + in_col[j]],
  * output r is d_out_ptrs[s*out_row + out_col[r]] (in_col / out_col are host arrays). */

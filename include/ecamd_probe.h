@@ -55,6 +55,12 @@ int ecamd_probe_mix3(int lp, int sp, int ch, int threads, int wgs_per_cu, int or
 /* The same with the codec's launch shapes: wgs_per_cu <= 0 gives one workgroup per tile (the
  * dispatcher hands tiles out, as ecamd_bs_kernel's bs_grid form), and cap_per_cu > 0 limits the
  * resident workgroups per CU with a dynamic LDS share of 160 KiB / cap (the codec's per-CU caps). */
+/* Mailbox round trip (round 6): one wave polls a word in coherent pinned host memory for requests
+ * 1..n posted by this thread, optionally reads `payload` bytes of the mailbox, and acks each; the host
+ * times post -> ack.  out_us: mean, min, median, 90th percentile (first request excluded), in us.  The
+ * wave exits after n requests, on stop, or after idle_us with no request. */
+int ecamd_probe_mailbox(int n, int payload, int idle_us, double *out_us);
+
 int ecamd_probe_mix4(int lp, int sp, int ch, int threads, int wgs_per_cu, int cap_per_cu, int wave_contig,
                      void *base, int64_t bs, int K, int R, int nstripes, const int *frag, void *stream);
 

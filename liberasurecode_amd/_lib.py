@@ -186,6 +186,7 @@ def probe():
                [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, VP, C.c_int64, C.c_int,
                 C.c_int, C.c_int, IP, VP])
         _proto(p, "ecamd_probe_valu", C.c_int, [C.c_int, C.c_int, C.c_int, VP])
+        _proto(p, "ecamd_probe_mailbox", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)])
         _probe = p
     return _probe
 

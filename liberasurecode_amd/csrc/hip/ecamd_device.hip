@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <numeric>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdlib>
@@ -670,6 +671,10 @@ struct DoneFlag {
     uint32_t* flag = nullptr;
     uint32_t value = 0;
     bool taken = false;
+    // the resident small server (ecamd_done_flag_arm_server): 1 any small launch that is the whole
+    // operation may be posted to it, 2 only a fused-checksum one; served: it was
+    int server = 0;
+    bool served = false;
 };
 thread_local DoneFlag t_done;
 
@@ -694,10 +699,183 @@ void attach_done(SmallArgs& s, unsigned grid, bool crc, hipStream_t st, std::uni
     }
 }
 
+// ---- The resident small server (small_server_kernel) ----
+// A per-call operation that is ONE small launch -- its inputs and outputs in the pinned slab, nothing else
+// on its stream -- is posted to a mailbox instead of launched: the caller thread's server (kSmallServerWgs
+// workgroups of one variant, on a stream of its own) polls it, runs the same body, and stores the same
+// completion flag.  Host-side launch latency (~4-6 us of hipLaunchKernel) and the kernel's start (~5 us)
+// leave the call; the mailbox round trip is ~5 us (tools/mailbox_probe.py).  The server exits idle_us
+// after its last request, on stop (thread exit), or to switch variants; a post after its exit is noticed
+// by ecamd_small_server_wait, which relaunches it with the request pending (that server skips it if its
+// flag is already set).  Its counters and checksum partials are its own scratch, zeroed at creation.
+struct SmallServer {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    SmallServerBox* box = nullptr;  // coherent pinned host memory
+    uint32_t* scratch = nullptr;    // device: word 1 the done counter, from word 64 the checksum partials
+    uint32_t variant = 0;           // of the launched kernel
+    uint32_t post = 0, prev = 0, seq = 0;
+    bool running = false;
+    std::chrono::steady_clock::time_point last{};
+};
+constexpr size_t kServerScratchWords = 64 + 16 + 64 * kSmallServerWgs;  // partials: 16 + (K + R) * workgroups
+constexpr int kMaxSmallServers = 8;
+constexpr size_t kServerLds = kLdsBytes - 1024;  // the server's dynamic LDS (its static share is < 1 KiB)
+std::mutex g_srv_mu;
+auto& g_srv_free = *new std::vector<SmallServer*>();  // idle servers of exited threads (never freed)
+std::atomic<long long> g_srv_posts{0}, g_srv_launches{0};
+int g_srv_count = 0;
+
+// ECAMD_PERCALL_SERVER_IDLE_US: how long a server polls without a request (default 2000 us)
+int64_t server_idle_us()
+{
+    static const int64_t v = [] {
+        const char* e = std::getenv("ECAMD_PERCALL_SERVER_IDLE_US");
+        const long long x = e ? std::atoll(e) : 2000;
+        return static_cast<int64_t>(std::clamp<long long>(x, 50, 1000000));
+    }();
+    return v;
+}
+
+struct ServerHold {
+    SmallServer* s = nullptr;
+    ~ServerHold()
+    {
+        if (!s) return;
+        if (std::getenv("ECAMD_SRV_TRACE"))  // DEBUG
+            std::fprintf(stderr, "srv-trace gpu: args %.2f us body %.2f us over %u\n",
+                         s->box->pad[2] ? s->box->pad[0] / 100.0 / s->box->pad[2] : 0.0,
+                         s->box->pad[2] ? s->box->pad[1] / 100.0 / s->box->pad[2] : 0.0, s->box->pad[2]);
+        __atomic_store_n(&s->box->stop, 1u, __ATOMIC_RELEASE);  // its workgroups exit at their next poll
+        std::lock_guard<std::mutex> lk(g_srv_mu);
+        g_srv_free.push_back(s);
+    }
+};
+thread_local ServerHold t_srv;
+
+SmallServer* thread_server(int dev)
+{
+    if (t_srv.s) return t_srv.s->dev == dev ? t_srv.s : nullptr;
+    std::unique_lock<std::mutex> lk(g_srv_mu);
+    for (size_t i = 0; i < g_srv_free.size(); i++) {
+        SmallServer* sv = g_srv_free[i];
+        if (sv->dev != dev) continue;
+        g_srv_free.erase(g_srv_free.begin() + static_cast<std::ptrdiff_t>(i));
+        lk.unlock();
+        if (hipStreamSynchronize(sv->st) != hipSuccess) {  // its kernel saw stop
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        __atomic_store_n(&sv->box->stop, 0u, __ATOMIC_RELEASE);
+        sv->running = false;
+        t_srv.s = sv;
+        return sv;
+    }
+    if (g_srv_count >= kMaxSmallServers) return nullptr;
+    g_srv_count++;
+    lk.unlock();
+    auto sv = std::make_unique<SmallServer>();
+    sv->dev = dev;
+    bool ok = hipHostMalloc(reinterpret_cast<void**>(&sv->box), sizeof(SmallServerBox),
+                            hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess;
+    ok = ok && hipMalloc(&sv->scratch, kServerScratchWords * 4) == hipSuccess &&
+         hipMemset(sv->scratch, 0, kServerScratchWords * 4) == hipSuccess &&
+         hipStreamCreateWithFlags(&sv->st, hipStreamNonBlocking) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        if (sv->box) (void)hipHostFree(sv->box);
+        if (sv->scratch) (void)hipFree(sv->scratch);
+        std::lock_guard<std::mutex> lk2(g_srv_mu);
+        g_srv_count--;
+        return nullptr;
+    }
+    std::memset(sv->box, 0, sizeof(SmallServerBox));
+    t_srv.s = sv.release();
+    return t_srv.s;
+}
+
+int server_launch(SmallServer* sv, uint32_t variant, uint32_t post0, bool dup)
+{
+    SmallServerArgs a{sv->box, post0, dup ? 1u : 0u, static_cast<uint64_t>(server_idle_us()) * 100u};
+    const void* k = nullptr;
+    switch (variant) {
+#define SV_(W, G, C)                                                                                     \
+    case (W) | ((G) << 4) | ((C) << 8):                                                                  \
+        k = reinterpret_cast<const void*>(&small_server_kernel<(W) | ((G) << 4) | ((C) << 8)>);          \
+        break;
+        SV_(2, 2, 0) SV_(4, 2, 0) SV_(8, 2, 0) SV_(2, 4, 0) SV_(4, 4, 0) SV_(8, 4, 0)
+        SV_(2, 2, 1) SV_(4, 2, 1) SV_(8, 2, 1) SV_(2, 4, 1) SV_(4, 4, 1) SV_(8, 4, 1)
+#undef SV_
+    case kSmallServerXor: k = reinterpret_cast<const void*>(&small_server_kernel<kSmallServerXor>); break;
+    case kSmallServerXor | (1u << 8):
+        k = reinterpret_cast<const void*>(&small_server_kernel<kSmallServerXor | (1u << 8)>);
+        break;
+    default: return fail(ECAMD_EINVAL, "small server variant %u", variant);
+    }
+    HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kServerLds)));
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(k, dim3(kSmallServerWgs), dim3(256), args, kServerLds, sv->st));
+    sv->running = true;
+    sv->variant = variant;
+    g_srv_launches.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+
+// Posts the small launch `s` (variant, nblk workgroups, lds bytes) to the calling thread's server: 0 posted,
+// 1 not taken (the caller launches it), < 0 an error.
+int server_post(SmallArgs& s, uint32_t variant, unsigned nblk, size_t lds, bool crc)
+{
+    if (nblk == 0 || nblk > static_cast<unsigned>(kSmallServerWgs) || lds > kServerLds) return 1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    SmallServer* sv = thread_server(dev);
+    if (!sv) return 1;
+    s.done_ctr = sv->scratch + 1;
+    if (crc) s.crc_part = sv->scratch + 64;
+    const auto now = std::chrono::steady_clock::now();
+    bool launch = !sv->running || sv->variant != variant;
+    if (!launch && now - sv->last > std::chrono::microseconds(server_idle_us() / 2)) {
+        const hipError_t q = hipStreamQuery(sv->st);  // past half its idle time: did it exit?
+        if (q == hipSuccess)
+            launch = true;
+        else if (q != hipErrorNotReady)
+            return fail(ECAMD_EHIP, "small server: %s", hipGetErrorString(q));
+    }
+    if (launch) {
+        if (sv->running && sv->variant != variant) {  // another variant: stop it first
+            __atomic_store_n(&sv->box->stop, 1u, __ATOMIC_RELEASE);
+            HIP_TRY(hipStreamSynchronize(sv->st));
+            __atomic_store_n(&sv->box->stop, 0u, __ATOMIC_RELEASE);
+        }
+        const int rc = server_launch(sv, variant, sv->post, false);
+        if (rc) return rc;
+    }
+    std::memcpy(&sv->box->args, &s, sizeof(SmallArgs));
+    sv->box->variant = variant;
+    sv->seq = sv->seq % 0xffffffu + 1u;
+    sv->prev = sv->post;
+    sv->post = (sv->seq << 8) | nblk;
+    __atomic_store_n(&sv->box->post, sv->post, __ATOMIC_RELEASE);  // after the arguments (x86: stores in order)
+    sv->last = now;
+    g_srv_posts.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+
+// Whether a small launch may go to the server: armed for it, the whole operation, staged inputs.
+bool server_wanted(bool crc, bool only, bool st_in, int nstripes, const SmallArgs& s)
+{
+    return only && st_in && nstripes == 1 && s.done && !t_done.taken &&
+           (t_done.server == 1 || (t_done.server == 2 && crc));
+}
+
 // ECAMD_EINVAL (nothing launched) when `crc` is given and the launch cannot fuse it.  `last`: this launch
-// ends the operation (the completion flag may be attached to it).
+// ends the operation (the completion flag may be attached to it); `only`: it is the whole operation (then
+// it may be posted to the resident small server).
 int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int nstripes, const uint8_t* tables,
-                 hipStream_t st, const SmallCrcReq* crc = nullptr, bool last = false)
+                 hipStream_t st, const SmallCrcReq* crc = nullptr, bool last = false, bool only = false)
 {
     const int lane = g_tune.small_lane ? static_cast<int>(g_tune.small_lane)
                                        : ((bs + 1) / 2 * nstripes <= 256 ? 2 : 4);
@@ -726,6 +904,14 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
         s.crc_part = crc->part;
         std::copy(k.minv, k.minv + 32, s.crc_minv);
         s.crc_c = k.c;
+        if (server_wanted(true, only, st_in, nstripes, s)) {
+            const int r = server_post(s, static_cast<uint32_t>(width | (lane << 4) | 256), grid.x, lds, true);
+            if (r < 0) return r;
+            if (r == 0) {
+                t_done.taken = t_done.served = true;
+                return 0;
+            }
+        }
 #define SMALLC_(W)                                                                                          \
     if (lane == 2)                                                                                          \
         hipLaunchKernelGGL((gf16_small_kernel<W, 2, true, true>), grid, block, lds, st, s);                 \
@@ -742,6 +928,14 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
         HIP_TRY(hipGetLastError());
         if (s.done) t_done.taken = true;
         return 0;
+    }
+    if ((lane == 2 || lane == 4) && server_wanted(false, only, st_in, nstripes, s)) {
+        const int r = server_post(s, static_cast<uint32_t>(width | (lane << 4)), grid.x, lds, false);
+        if (r < 0) return r;
+        if (r == 0) {
+            t_done.taken = t_done.served = true;
+            return 0;
+        }
     }
 #define SMALL_(W)                                                                                           \
     switch (lane * 2 + (st_in ? 1 : 0)) {                                                                   \
@@ -768,7 +962,7 @@ int launch_small(const ApplyArgs& a, const ecamd_map::Pass& p, int64_t bs, int n
 // `last`: this launch ends the operation (the completion flag may be attached).  ECAMD_EINVAL (nothing
 // launched) when `crc` is given and the launch cannot fuse it.
 int launch_xor_small(const ApplyArgs& a, int64_t bs, int nstripes, hipStream_t st, bool last = false,
-                     const SmallCrcReq* crc = nullptr)
+                     const SmallCrcReq* crc = nullptr, bool only = false)
 {
     SmallArgs s = small_args(a, bs, nstripes, 4);
     const unsigned grid = static_cast<unsigned>((s.nchunks + 255) / 256);
@@ -789,6 +983,14 @@ int launch_xor_small(const ApplyArgs& a, int64_t bs, int nstripes, hipStream_t s
     if (last) attach_done(s, grid, crc != nullptr, st, use);
     const size_t stage = static_cast<size_t>(crc ? a.ncols + a.nrows : a.ncols) * 1024 +
                          (crc ? static_cast<size_t>(small_crc_words(4)) * 4 : 0);
+    if (server_wanted(crc != nullptr, only, st_in, nstripes, s)) {
+        const int r = server_post(s, kSmallServerXor | (crc ? 256u : 0u), grid, stage, crc != nullptr);
+        if (r < 0) return r;
+        if (r == 0) {
+            t_done.taken = t_done.served = true;
+            return 0;
+        }
+    }
     if (crc)
         hipLaunchKernelGGL((xor_small_kernel<true, true>), dim3(grid), dim3(256), stage, st, s);
     else if (st_in)
@@ -1281,7 +1483,8 @@ int launch_gf16(const ecamd_map* map, ApplyArgs base_args, const int64_t* in_off
             }
         }
         if (!PTRS && small_launch(a, bs, nstripes)) {
-            int rc = launch_small(a, p, bs, nstripes, map->d_tables, st, nullptr, &p == &map->passes.back());
+            int rc = launch_small(a, p, bs, nstripes, map->d_tables, st, nullptr, &p == &map->passes.back(),
+                                  map->passes.size() == 1 && done == 0);
             if (rc) return rc;
             continue;
         }
@@ -1393,7 +1596,8 @@ int launch_xor(const uint32_t* masks, int R, int K, ApplyArgs base_args, const i
                 a.masks[r] = col0 < 32 ? (masks[row0 + r] >> col0) : 0u;
             }
             if (!PTRS && !copy_off && small_launch(a, bs, nstripes)) {
-                int rc = launch_xor_small(a, bs, nstripes, st, row0 + kMaxRows >= R && col0 + 32 >= K);
+                int rc = launch_xor_small(a, bs, nstripes, st, row0 + kMaxRows >= R && col0 + 32 >= K, nullptr,
+                                          R <= kMaxRows && K <= 32);
                 if (rc) return rc;
                 continue;
             }
@@ -2823,7 +3027,7 @@ int ecamd_map_apply_strided_crc(const ecamd_map* map, const void* in_base, const
     if ((rc = stream_scratch(dev, stream, kSmallCrcScratchSlot, 16 + static_cast<size_t>(map->K + map->R) * wgs,
                              &req.part)))
         return rc;
-    rc = launch_small(a, p, blocksize, 1, map->d_tables, static_cast<hipStream_t>(stream), &req, true);
+    rc = launch_small(a, p, blocksize, 1, map->d_tables, static_cast<hipStream_t>(stream), &req, true, true);
     if (rc == 0) g_small_crc_launches.fetch_add(1, std::memory_order_relaxed);
     return rc == ECAMD_EINVAL ? 1 : rc;
 }
@@ -2862,7 +3066,7 @@ int ecamd_xor_apply_strided_crc(const uint32_t* masks, int R, int K, const void*
     const size_t wgs = static_cast<size_t>((blocksize + 1023) / 1024 + 1);
     if ((rc = stream_scratch(dev, stream, kSmallCrcScratchSlot, 16 + static_cast<size_t>(K + R) * wgs, &req.part)))
         return rc;
-    rc = launch_xor_small(a, blocksize, 1, static_cast<hipStream_t>(stream), true, &req);
+    rc = launch_xor_small(a, blocksize, 1, static_cast<hipStream_t>(stream), true, &req, true);
     if (rc == 0) g_small_crc_launches.fetch_add(1, std::memory_order_relaxed);
     return rc == ECAMD_EINVAL ? 1 : rc;
 }
@@ -2871,11 +3075,47 @@ long long ecamd_small_crc_launches(void) { return g_small_crc_launches.load(std:
 
 void ecamd_done_flag_arm(uint32_t* flag, uint32_t value) { t_done = DoneFlag{flag, value, false}; }
 
+void ecamd_done_flag_arm_server(uint32_t* flag, uint32_t value, int mode)
+{
+    t_done = DoneFlag{flag, value, false};
+    t_done.server = mode == 1 || mode == 2 ? mode : 0;
+}
+
 int ecamd_done_flag_taken(void)
 {
-    const int taken = t_done.taken ? 1 : 0;
+    const int taken = t_done.served ? 2 : t_done.taken ? 1 : 0;
     t_done = DoneFlag{};
     return taken;
+}
+
+long long ecamd_small_server_posts(void) { return g_srv_posts.load(std::memory_order_relaxed); }
+long long ecamd_small_server_launches(void) { return g_srv_launches.load(std::memory_order_relaxed); }
+
+int ecamd_small_server_wait(const uint32_t* flag, uint32_t value)
+{
+    SmallServer* sv = t_srv.s;
+    if (!sv) return fail(ECAMD_EINVAL, "small server wait: no server on this thread");
+    using clk = std::chrono::steady_clock;
+    const auto deadline = clk::now() + std::chrono::seconds(10);
+    auto check = clk::now() + std::chrono::microseconds(50);
+    for (int i = 0;; i++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == value) return 0;
+        if ((i & 63) != 63) continue;
+        const auto now = clk::now();
+        if (now > check) {
+            const hipError_t q = hipStreamQuery(sv->st);
+            if (q == hipSuccess) {  // the server exited before this request: run it again, request pending
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == value) return 0;
+                const int rc = server_launch(sv, sv->variant, sv->prev, true);
+                if (rc) return rc;
+                sv->last = now;
+            } else if (q != hipErrorNotReady) {
+                return fail(ECAMD_EHIP, "small server: %s", hipGetErrorString(q));
+            }
+            check = now + std::chrono::microseconds(50);
+        }
+        if (now > deadline) return fail(ECAMD_EHIP, "small server: no completion within 10 s");
+    }
 }
 
 int ecamd_map_apply_ptrs(const ecamd_map* map, const void* const* d_in_ptrs, int in_row,

@@ -89,8 +89,14 @@ __device__ __forceinline__ void small_stage_inputs(uint8_t* stg, const SmallArgs
 {
     const int64_t left = a.bs - base;
     const int nseg = static_cast<int>(((left < region ? left : region) + 15) / 16);
+    // (uniform by construction; readfirstlane says so to the compiler when the argument block is in LDS --
+    // the resident server -- so the loads below need no per-lane resource loop)
+    const uint64_t ip = reinterpret_cast<uint64_t>(a.in);
+    const uint64_t ipu = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ip))) |
+                         (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ip >> 32)))) << 32);
     const auto rin = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.in), 0, static_cast<int>((K - 1) * a.in_pitch + ((a.bs + 15) & ~int64_t(15))),
+        reinterpret_cast<void*>(ipu), 0,
+        __builtin_amdgcn_readfirstlane(static_cast<int>((K - 1) * a.in_pitch + ((a.bs + 15) & ~int64_t(15)))),
         0x00020000);
     const int nq = ZERO ? region / 16 : nseg;
     const int total = K * nq;
@@ -127,13 +133,15 @@ __device__ __forceinline__ void small_stage_inputs(uint8_t* stg, const SmallArgs
 
 // The completion flag of a small launch (SmallArgs::done), after every output store of every workgroup
 // is visible system-wide: one workgroup stores it, several count first (done_ctr, self-resetting).
-__device__ __forceinline__ void small_done(const SmallArgs& a)
+// (bid / nblk: this workgroup's index and the launch's workgroups -- blockIdx / gridDim, or a request of
+// the resident small server, small_server_kernel)
+__device__ __forceinline__ void small_done(const SmallArgs& a, int bid, int nblk)
 {
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
-        const bool last = gridDim.x == 1 ||
-                          atomicInc(reinterpret_cast<unsigned*>(a.done_ctr), gridDim.x - 1) == gridDim.x - 1;
+        const unsigned n = static_cast<unsigned>(nblk);
+        const bool last = n == 1 || atomicInc(reinterpret_cast<unsigned*>(a.done_ctr), n - 1) == n - 1;
         if (last) {
             __threadfence_system();
             __hip_atomic_store(a.done, a.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -151,8 +159,12 @@ __device__ __forceinline__ void small_done(const SmallArgs& a)
 // zero-extended to gridDim * REGION bytes, then r0 = A^-zext S and crc = ~(A^len ~0 ^ r0) with host
 // constants (crc_minv, crc_c).  With several workgroups it also stores the completion flag and returns
 // true (the caller stores it otherwise).
-template <int REGION>
-__device__ bool small_crc_epilogue(const SmallArgs& a, const uint8_t* stg, const uint32_t* cimg, int K)
+// SRV: the resident server's form (small_server_kernel: the argument block in LDS, not in kernel arguments)
+// -- the final maps' 32 words are read in a rolled loop, which keeps the compiler from holding them (and
+// the rest of the block) in registers across the epilogue.
+template <int REGION, bool SRV = false>
+__device__ __forceinline__ bool small_crc_epilogue(const SmallArgs& a, const uint8_t* stg, const uint32_t* cimg, int K, int bid,
+                                   int nblk)
 {
     using namespace crcdev;
     constexpr int NP = REGION / 16;  // 16-byte pieces of a region: 32 or 64
@@ -161,14 +173,20 @@ __device__ bool small_crc_epilogue(const SmallArgs& a, const uint8_t* stg, const
     const int lane = static_cast<int>(threadIdx.x) & 63, wave = static_cast<int>(threadIdx.x) >> 6;
     const int nw = static_cast<int>(blockDim.x) >> 6;
     const int nfr = K + a.nrows;
-    const int nwg = static_cast<int>(gridDim.x);
-    const int after = nwg - 1 - static_cast<int>(blockIdx.x);  // regions after this workgroup's
+    const int nwg = nblk;
+    const int after = nwg - 1 - bid;  // regions after this workgroup's
     __syncthreads();  // every lane's outputs are in LDS
     auto finish = [&](int f, uint32_t S) {  // S = r0 of fragment f zero-extended: the CRC
         uint32_t r0 = 0;
+        if constexpr (SRV) {
+#pragma unroll 1
+            for (int b = 0; b < 32; b++)
+                if ((S >> b) & 1u) r0 ^= a.crc_minv[b];
+        } else {
 #pragma unroll
-        for (int b = 0; b < 32; b++)
-            if ((S >> b) & 1u) r0 ^= a.crc_minv[b];
+            for (int b = 0; b < 32; b++)
+                if ((S >> b) & 1u) r0 ^= a.crc_minv[b];
+        }
         a.crc_out[f] = ~(a.crc_c ^ r0);
     };
     for (int f0 = wave; f0 < nfr; f0 += 4 * nw) {
@@ -197,7 +215,7 @@ __device__ bool small_crc_epilogue(const SmallArgs& a, const uint8_t* stg, const
 #pragma unroll
                     for (int b = 0; b < 6; b++)
                         if ((after >> b) & 1) x = lmap<4>(wgs + 128 * b, x);
-                    __hip_atomic_store(a.crc_part + 16 + f * nwg + blockIdx.x, x, __ATOMIC_RELAXED,
+                    __hip_atomic_store(a.crc_part + 16 + f * nwg + bid, x, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
@@ -260,19 +278,18 @@ __device__ bool small_crc_epilogue(const SmallArgs& a, const uint8_t* stg, const
 // self-resetting counter) XORs them: S = r0 of the fragment zero-extended to gridDim * REGION bytes,
 // then r0 = A^-zext S and crc = ~(A^len ~0 ^ r0) with host constants (crc_minv, crc_c).  Bytes past
 // bs are zero in LDS.
-template <int W, int G, bool ST, bool CRC>
-__global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
+template <int W, int G, bool ST, bool CRC, bool SRV = false>
+__device__ __forceinline__ void gf16_small_body(const SmallArgs& a, uint8_t* lds, int bid, int nblk)
 {
     static_assert(!CRC || (ST && (G == 2 || G == 4)), "fused CRC: staged inputs, 2- or 4-byte lanes");
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int D = W / 2;
     constexpr int EB = 2 * W;
     constexpr int TB = 512 * EB;  // table bytes per input
     constexpr int NW = G / 2;                // 16-bit words per lane
     constexpr int ND = G >= 4 ? G / 4 : 1;  // dwords per lane (G = 2: the low half of one)
     const int K = a.ncols;
-    const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t step = static_cast<int64_t>(nblk) * blockDim.x;
+    int64_t c = static_cast<int64_t>(bid) * blockDim.x + threadIdx.x;
     auto load = [](const uint8_t* p, int rem, uint32_t (&x)[ND]) {
         if constexpr (G == 16) {
             const uint4 v = load_tail(p, rem);
@@ -291,7 +308,7 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
     uint32_t cur[4][ND], nxt[4][ND];
     constexpr int REGION = 256 * G;  // ST: bytes of each input this workgroup stages
     uint8_t* const stg = lds + K * TB;
-    const int64_t c0 = static_cast<int64_t>(blockIdx.x) * blockDim.x;
+    const int64_t c0 = static_cast<int64_t>(bid) * blockDim.x;
     auto fetch4 = [&](int64_t cc, int j0, uint32_t (&x)[4][ND]) {
         const int64_t s = cc / a.cpf;
         const int64_t off = (cc - s * a.cpf) * G;
@@ -418,8 +435,14 @@ __global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
         if (c + step < a.nchunks) fetch4(c + step, 0, cur);
     }
     if constexpr (CRC)
-        if (small_crc_epilogue<REGION>(a, stg, cimg, K)) return;
-    if (a.done) small_done(a);  // one workgroup, or no checksum: the flag after every output store
+        if (small_crc_epilogue<REGION, SRV>(a, stg, cimg, K, bid, nblk)) return;
+    if (a.done) small_done(a, bid, nblk);  // one workgroup, or no checksum: the flag after every output store
+}
+template <int W, int G, bool ST, bool CRC>
+__global__ void __launch_bounds__(256) gf16_small_kernel(const SmallArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    gf16_small_body<W, G, ST, CRC>(a, lds, static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x));
 }
 #define ECAMD_SMALL(G, ST)                                                 \
     template __global__ void gf16_small_kernel<2, G, ST>(const SmallArgs); \
@@ -489,15 +512,14 @@ __device__ __forceinline__ void xor_tile(const ApplyArgs& a, uint32_t s, int64_t
 // every input staged into LDS first (small_stage_inputs; one stripe, one chunk per lane), as the RS kernel
 // does for inputs in pinned host memory; the completion flag (SmallArgs::done) after the outputs.
 // CRC (with ST): the fused checksums of every input and output (small_crc_epilogue), as gf16_small_kernel.
-template <bool ST, bool CRC>
-__global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
+template <bool ST, bool CRC, bool SRV = false>
+__device__ __forceinline__ void xor_small_body(const SmallArgs& a, uint8_t* lds, int bid, int nblk)
 {
     static_assert(!CRC || ST, "fused CRC: staged inputs");
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int REGION = 256 * 4;
     const int K = a.ncols;
-    const int64_t step = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    const int64_t c0 = static_cast<int64_t>(blockIdx.x) * blockDim.x;
+    const int64_t step = static_cast<int64_t>(nblk) * blockDim.x;
+    const int64_t c0 = static_cast<int64_t>(bid) * blockDim.x;
     uint32_t* const cimg = reinterpret_cast<uint32_t*>(lds + (K + a.nrows) * REGION);
     if constexpr (ST) {
         small_stage_inputs<CRC>(lds, a, K, c0 * 4, REGION);
@@ -513,7 +535,7 @@ __global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
         }
         __syncthreads();
     }
-    for (int64_t c = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; c < a.nchunks; c += step) {
+    for (int64_t c = c0 + threadIdx.x; c < a.nchunks; c += step) {
         const int64_t s = c / a.cpf;
         const int64_t off = (c - s * a.cpf) * 4;
         const int rem = a.bs - off < 4 ? static_cast<int>(a.bs - off) : 4;
@@ -560,12 +582,101 @@ __global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
         }
     }
     if constexpr (CRC)
-        if (small_crc_epilogue<REGION>(a, lds, cimg, K)) return;
-    if (a.done) small_done(a);
+        if (small_crc_epilogue<REGION, SRV>(a, lds, cimg, K, bid, nblk)) return;
+    if (a.done) small_done(a, bid, nblk);
+}
+template <bool ST, bool CRC>
+__global__ void __launch_bounds__(256) xor_small_kernel(const SmallArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    xor_small_body<ST, CRC>(a, lds, static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x));
 }
 template __global__ void xor_small_kernel<false, false>(const SmallArgs);
 template __global__ void xor_small_kernel<true, false>(const SmallArgs);
 template __global__ void xor_small_kernel<true, true>(const SmallArgs);
+
+// small_server_kernel: the resident form of the per-call small launches.  Lane 0 of each
+// workgroup polls the mailbox (system-scope acquire loads of the host-written post word, s_sleep between
+// them); a new post names its sequence and workgroup count, and workgroups below that count read the
+// argument block and variant (one word per lane, into LDS) and run the same body a launch would, with
+// (blockIdx, post's count) for (blockIdx, gridDim) -- the completion flag, checksums and counters as in
+// a launch.  The others only note the post.  Every workgroup exits on stop, or idle_ticks after its last
+// post: the grid always drains on its own.  The host writes a request only after the previous one's
+// flag, so no participating workgroup can see its arguments change under it.
+template <uint32_t V>
+__global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs sa)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int kArgWords = static_cast<int>(sizeof(SmallArgs) / 4);
+    __shared__ __attribute__((aligned(16))) uint32_t argw[kArgWords + 4];
+    __shared__ uint32_t cmd[2];
+    uint32_t last = sa.post0;
+    bool check = sa.dup_check != 0;
+    const int bid = static_cast<int>(blockIdx.x);
+    uint32_t dbg_args = 0, dbg_body = 0, dbg_n = 0;  // DEBUG (temporary)
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t p = last, go = 0;
+            for (;;) {
+                p = __hip_atomic_load(&sa.box->post, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (p != last) {
+                    go = 1;
+                    break;
+                }
+                if (__hip_atomic_load(&sa.box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > sa.idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            cmd[0] = p;
+            cmd[1] = go;
+        }
+        __syncthreads();
+        const uint32_t p = cmd[0];
+        if (!cmd[1]) return;
+        last = p;
+        const int nblk = static_cast<int>(p & 0xffu);
+        const uint64_t tA = __builtin_amdgcn_s_memrealtime();  // DEBUG
+        uint64_t tB = tA;
+        if (bid < nblk) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(&sa.box->args);
+            for (int i = static_cast<int>(threadIdx.x); i < kArgWords; i += static_cast<int>(blockDim.x))
+                argw[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (threadIdx.x == 0) argw[kArgWords] = __hip_atomic_load(&sa.box->variant, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __syncthreads();
+            const SmallArgs& a = *reinterpret_cast<const SmallArgs*>(argw);
+            const uint32_t v = argw[kArgWords];
+            tB = __builtin_amdgcn_s_memrealtime();  // DEBUG
+            bool skip = false;
+            if (check && a.done)  // a relaunch: the previous server may have finished this request
+                skip = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.done_val;
+            if (!skip && v == V) {  // (a request of another variant is never posted to this server)
+                constexpr int W = V & 15, G = (V >> 4) & 15;
+                constexpr bool C = ((V >> 8) & 1) != 0;
+                if constexpr ((V & kSmallServerXor) != 0)
+                    xor_small_body<true, C, true>(a, lds, bid, nblk);
+                else
+                    gf16_small_body<W, G, true, C, true>(a, lds, bid, nblk);
+            }
+        }
+        check = false;
+        __syncthreads();  // argw, cmd and the LDS are reused by the next request
+        if (bid == 0 && threadIdx.x == 0 && nblk > 0) {  // DEBUG
+            dbg_args += static_cast<uint32_t>(tB - tA);
+            dbg_body += static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() - tB);
+            dbg_n++;
+            __hip_atomic_store(&sa.box->pad[0], dbg_args, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&sa.box->pad[1], dbg_body, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&sa.box->pad[2], dbg_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+#define SRV_(W, G, C) template __global__ void small_server_kernel<(W) | ((G) << 4) | ((C) << 8)>(const SmallServerArgs);
+SRV_(2, 2, 0) SRV_(4, 2, 0) SRV_(8, 2, 0) SRV_(2, 4, 0) SRV_(4, 4, 0) SRV_(8, 4, 0)
+SRV_(2, 2, 1) SRV_(4, 2, 1) SRV_(8, 2, 1) SRV_(2, 4, 1) SRV_(4, 4, 1) SRV_(8, 4, 1)
+#undef SRV_
+template __global__ void small_server_kernel<kSmallServerXor>(const SmallServerArgs);
+template __global__ void small_server_kernel<kSmallServerXor | (1u << 8)>(const SmallServerArgs);
 
 template <int W, bool PTRS>
 __global__ void __launch_bounds__(256) xor_apply_kernel(const ApplyArgs a)

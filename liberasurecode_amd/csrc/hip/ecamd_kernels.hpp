@@ -79,6 +79,27 @@ struct SmallArgs {
     uint32_t done_val;
 };
 
+// The resident small server (small_server_kernel): the per-call path's small launches posted to a
+// mailbox in coherent pinned host memory instead of launched -- one per caller thread, kSmallServerWgs
+// workgroups polling it until idle_ticks of the 100 MHz constant clock pass without a request.
+struct SmallServerBox {
+    uint32_t post;      // (sequence << 8) | workgroups of the request, stored last by the host
+    uint32_t stop;      // host: every workgroup exits at its next poll
+    uint32_t variant;   // kSmallServerXor | CRC << 8 | G << 4 | W (gf16_small_body / xor_small_body)
+    uint32_t pad[13];
+    SmallArgs args;     // the request's argument block (its scratch the server's own)
+};
+struct SmallServerArgs {
+    SmallServerBox* box;
+    uint32_t post0;      // the post word already handled: a different one is a request
+    uint32_t dup_check;  // relaunched while a request was pending: skip it if its flag is already set
+    uint64_t idle_ticks;
+};
+constexpr int kSmallServerWgs = 16;
+constexpr uint32_t kSmallServerXor = 1u << 12;
+template <uint32_t V>
+__global__ void small_server_kernel(const SmallServerArgs sa);
+
 // gf16_stream_kernel handles up to kStreamGroups*4 inputs per launch (fully unrolled).
 constexpr int kStreamGroups = 5;
 

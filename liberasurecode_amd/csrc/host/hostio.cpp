@@ -381,6 +381,21 @@ const bool g_done_flag = [] {
     const char* env = std::getenv("ECAMD_PERCALL_DONE_FLAG");
     return !(env && std::strcmp(env, "0") == 0);
 }();
+// ECAMD_PERCALL_SERVER=1: post one-launch calls to the resident small server (ecamd_done_flag_arm_server)
+// instead of launching their small kernel (off by default: DESIGN.md §6, profiles/r06_lat_server.json)
+const bool g_server = [] {
+    const char* env = std::getenv("ECAMD_PERCALL_SERVER");
+    return env && std::strcmp(env, "1") == 0;
+}();
+struct Trace {  // DEBUG
+    double launch = 0, wait = 0;
+    long n = 0;
+    ~Trace()
+    {
+        if (std::getenv("ECAMD_SRV_TRACE") && n)
+            std::fprintf(stderr, "srv-trace host: launch %.2f us wait %.2f us over %ld\n", launch / n, wait / n, n);
+    }
+} g_trace;
 constexpr int kDonePollUs = 200;  // then block in hipStreamSynchronize (a busy GPU, or a fault)
 
 // Polls the flag word for `value` (the GPU writes it to pinned host memory); false after kDonePollUs.
@@ -438,6 +453,7 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     // operation stores a per-call value into the slab's flag word once its stores are visible; the
     // caller polls it instead of synchronizing the stream (falls back to that after kDonePollUs)
     bool flagged[2] = {false, false};
+    bool served[2] = {false, false};  // posted to the resident small server: its stream, not the slot's
     uint32_t flag_val[2] = {0, 0};
     std::vector<void*> cdst(static_cast<size_t>(nfr));
     std::vector<const void*> csrc(static_cast<size_t>(nfr));
@@ -448,9 +464,16 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
         int r = 0;
-        if (!(flagged[s] && poll_done(done_word(st->slot[s].h_pin, st->cap), flag_val[s])))
+        const auto tw0 = std::chrono::steady_clock::now();  // DEBUG
+        if (served[s]) {
+            const uint32_t* fw = done_word(st->slot[s].h_pin, st->cap);
+            if (!poll_done(fw, flag_val[s])) r = ecamd_small_server_wait(fw, flag_val[s]);
+        } else if (!(flagged[s] && poll_done(done_word(st->slot[s].h_pin, st->cap), flag_val[s]))) {
             r = wait_stream(st->slot[s].stream, chunk * nfr >= kSpinMinBytes);
-        flagged[s] = false;
+        }
+        g_trace.wait += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
+        g_trace.n++;
+        flagged[s] = served[s] = false;
         if (r) return r;
         const int64_t off = pending[s] * chunk;
         const int64_t n = std::min(chunk, bs - off);
@@ -523,14 +546,24 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         const bool arm = g_done_flag && zc_out && nchunks == 1;
         if (arm) {
             flag_val[s] = ++st->seq;
-            ecamd_done_flag_arm(done_word(sl.h_pin, st->cap), flag_val[s]);
+            // the resident small server may take the launch when nothing else of this call is on the stream
+            // (inputs read from the slab itself: no copy before it) -- with a checksum wanted, only a fused one
+            // (a separate pass after it would run on the stream, unordered with the server)
+            const int srv = g_server && zc_in && rc == 0 ? (want_crc ? 2 : 1) : 0;
+            ecamd_done_flag_arm_server(done_word(sl.h_pin, st->cap), flag_val[s], srv);
         }
+        const auto tl0 = std::chrono::steady_clock::now();  // DEBUG
         if (rc == 0)
             rc = launch(ctx, win, work, chunk, n, sl.stream, crc_pass_ok && nchunks == 1 ? d_crc : nullptr,
                         t_crc.legacy, &fused);
+        g_trace.launch += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tl0).count();
         // the flag ends the call only when nothing follows the codec launch on the stream: a separate
         // CRC pass (want_crc, not fused) does
-        if (arm) flagged[s] = ecamd_done_flag_taken() != 0 && rc == 0 && !(want_crc && !fused);
+        if (arm) {
+            const int taken = ecamd_done_flag_taken();
+            flagged[s] = taken != 0 && rc == 0 && !(want_crc && !fused);
+            served[s] = taken == 2;
+        }
         if (rc == 0 && want_crc && !fused && zc_in && !zc_out)  // the CRC pass reads every fragment from the device slab
             rc = ecamd_memcpy_async(work, win, K * chunk, 0, sl.stream);
         if (rc == 0 && !zc_out)

@@ -37,6 +37,7 @@ __global__ void launch_probe_kernel(uint32_t* sink, const uint8_t* src, int byte
 template <int U>
 __global__ void bw_probe_kernel(uint8_t* dst, const uint8_t* src, int64_t bytes, int kind,
                                 uint32_t* sink);
+__global__ void mailbox_probe_kernel(uint32_t* mb, int n, int payload, uint64_t idle_ticks);
 __global__ void stream_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, int64_t n);
 
 template <int OP>

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <vector>
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -271,6 +273,63 @@ int ecamd_probe_unaligned(int mode, int shift, void* dst, const void* src, int64
     default: hipLaunchKernelGGL(unaligned_probe_kernel<5>, grid, block, 0, st, d, s, bytes, shift); break;
     }
     HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+
+int ecamd_probe_mailbox(int n, int payload, int idle_us, double* out_us)
+{
+    int dev = 0;
+    int rc = ensure_device(&dev);
+    if (rc) return rc;
+    if (n < 1 || n > 100000 || payload < 0 || payload > 256 || idle_us < 1 || idle_us > 100000 || !out_us)
+        return fail(-22, "mailbox probe: n 1..100000, payload 0..256, idle_us 1..100000");
+    uint32_t* mb = nullptr;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&mb), 4096, hipHostMallocCoherent | hipHostMallocMapped));
+    for (int i = 0; i < 1024; i++) mb[i] = 0;
+    hipStream_t st = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipLaunchKernelGGL(mailbox_probe_kernel, dim3(1), dim3(64), 0, st, mb, n, payload,
+                       static_cast<uint64_t>(idle_us) * 100u);
+    hipError_t le = hipGetLastError();
+    std::vector<double> us;
+    us.reserve(static_cast<size_t>(n));
+    int failed = le != hipSuccess ? -5 : 0;
+    // the first request waits for the wave to start: a generous bound, later ones idle_us
+    for (int i = 1; i <= n && !failed; i++) {
+        volatile uint32_t* ack = mb + 1;
+        const auto t0 = std::chrono::steady_clock::now();
+        __atomic_store_n(mb, static_cast<uint32_t>(i), __ATOMIC_RELEASE);
+        for (;;) {
+            if (*ack == static_cast<uint32_t>(i)) break;
+            const double el = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            if (el > (i == 1 ? 2e6 : static_cast<double>(idle_us))) {
+                failed = -62;
+                break;
+            }
+        }
+        us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        // a gap between requests, as between calls
+        const auto g0 = std::chrono::steady_clock::now();
+        while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - g0).count() < 2.0) {
+        }
+    }
+    __atomic_store_n(mb + 2, 1u, __ATOMIC_RELEASE);  // stop: the wave exits at its next poll
+    hipError_t se = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    (void)hipHostFree(mb);
+    if (le != hipSuccess) return fail(-5, "mailbox probe launch: %s", hipGetErrorString(le));
+    if (se != hipSuccess) return fail(-5, "mailbox probe sync: %s", hipGetErrorString(se));
+    if (failed) return fail(failed, "mailbox probe: no ack within the bound");
+    std::vector<double> s(us.begin() + 1, us.end());
+    if (s.empty()) s = us;
+    std::sort(s.begin(), s.end());
+    double sum = 0;
+    for (double v : s) sum += v;
+    out_us[0] = sum / static_cast<double>(s.size());
+    out_us[1] = s.front();
+    out_us[2] = s[s.size() / 2];
+    out_us[3] = s[s.size() * 9 / 10];
     return 0;
 }
 

@@ -403,4 +403,40 @@ template __global__ void launch_probe_kernel<2, 0>(uint32_t*, const uint8_t*, in
 template __global__ void launch_probe_kernel<0, 1024>(uint32_t*, const uint8_t*, int);
 template __global__ void launch_probe_kernel<0, 4096>(uint32_t*, const uint8_t*, int);
 
+
+// Mailbox round trip (round 6, the resident-server question of DESIGN.md §10): one wave polls a word in
+// pinned host memory (system-scope acquire loads, s_sleep between them) for request i = 1..n, optionally
+// reads `payload` bytes of the mailbox after it (the argument block a server would fetch), and stores
+// the ack word.  Every wave exits: after request n, when the host sets stop, or after idle_ticks of the
+// 100 MHz constant clock (s_memrealtime) with no new request.
+__global__ void __launch_bounds__(64) mailbox_probe_kernel(uint32_t* mb, int n, int payload, uint64_t idle_ticks)
+{
+    const int lane = static_cast<int>(threadIdx.x);
+    uint32_t sum = 0;
+    for (int i = 1; i <= n; i++) {
+        uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool got = false;
+        for (;;) {
+            const uint32_t seq = __hip_atomic_load(mb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint32_t stop = __hip_atomic_load(mb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (stop) break;
+            if (seq == static_cast<uint32_t>(i)) {
+                got = true;
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (!got) break;
+        if (payload > 0 && lane * 4 < payload)
+            sum += __hip_atomic_load(mb + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        sum = __builtin_amdgcn_readfirstlane(sum);
+        if (lane == 0) {
+            __hip_atomic_store(mb + 3, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+            __hip_atomic_store(mb + 1, static_cast<uint32_t>(i), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 }  // namespace ecamd

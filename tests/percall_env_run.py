@@ -4,11 +4,19 @@ the parent put in the environment (they are read once per process).  RS(10,4) an
 objects of 4 KiB,
 64 KiB and 1 MiB (+5 bytes), CHKSUM_NONE and CHKSUM_CRC32: every fragment compared with the restated
 framing over the oracle codec (test_gpu_frontend.rs_expected), a decode of 4 lost data fragments and a
-reconstruct of a lost parity.  Prints one JSON line {"ok": true, "digest": sha256 of all outputs}."""
+reconstruct of a lost parity.  Prints one JSON line {"ok": true, "digest": sha256 of all outputs, "posts" /
+"server_launches": the resident small server's counters}.
+
+PERCALL_SLEEP_US: a pause after every call (the server's idle exit between calls).  PERCALL_THREADS=N:
+the RS(10,4) calls of 4 KiB and 16 KiB fragments, 30 rounds, in N threads at once (each thread its own
+server, up to the library's limit; the rest launch) -- every result checked, no digest."""
+import ctypes as C
 import hashlib
 import json
 import os
 import sys
+import threading
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
@@ -19,7 +27,63 @@ import ec_api as E  # noqa: E402
 from test_gpu_frontend import payload_bytes, rs_expected, xor_expected  # noqa: E402
 
 
+def _counters():
+    from liberasurecode_amd import _lib
+    d = _lib.dev()
+    out = {}
+    for key, name in (("posts", "ecamd_small_server_posts"), ("server_launches", "ecamd_small_server_launches")):
+        fn = getattr(d, name)
+        fn.restype = C.c_longlong
+        out[key] = fn()
+    return out
+
+
+def _pause():
+    us = int(os.environ.get("PERCALL_SLEEP_US", "0"))
+    if us:
+        time.sleep(us / 1e6)
+
+
+def threads_main(n):
+    k, m = 10, 4
+    errors = []
+    cases = []
+    for ct in (E.CHKSUM_NONE, E.CHKSUM_CRC32):
+        for size in (4096 * k, 16384 * k - 7):
+            data = payload_bytes(size, size + ct)
+            cases.append((ct, data, rs_expected(k, m, data, ct)))
+    descs = {ct: E.create(E.EC_BACKEND_LIBERASURECODE_RS_VAND, k, m, hd=m, ct=ct) for ct in (E.CHKSUM_NONE, E.CHKSUM_CRC32)}
+
+    def work(t):
+        try:
+            for rnd in range(30):
+                for ct, data, want in cases[t % len(cases):] + cases[:t % len(cases)]:
+                    desc = descs[ct]
+                    rc, dp, pp, flen = E.encode(desc, data)
+                    assert rc == 0, ("encode", rc)
+                    frags = E.fragments(dp, k, flen) + E.fragments(pp, m, flen)
+                    E.lib().liberasurecode_encode_cleanup(desc, dp, pp)
+                    assert frags == want, ("fragments", t, rnd, ct, len(data))
+                    rc, out = E.decode(desc, frags[4:], flen, force=1)
+                    assert rc == 0 and out == data, ("decode", t, rnd, ct, len(data), rc)
+                    _pause()
+        except AssertionError as e:  # noqa: PERF203
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(n)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:3]
+    for desc in descs.values():
+        assert E.lib().liberasurecode_instance_destroy(desc) == 0
+    print(json.dumps(dict({"ok": True, "threads": n}, **_counters())))
+
+
 def main():
+    if os.environ.get("PERCALL_THREADS"):
+        return threads_main(int(os.environ["PERCALL_THREADS"]))
     h = hashlib.sha256()
     # liberasurecode_rs_vand (10, 4) and flat_xor_hd (10, 6, 4): 4 / 3 data fragments lost
     for be, k, m, hd, lost in ((E.EC_BACKEND_LIBERASURECODE_RS_VAND, 10, 4, 4, 4), (E.EC_BACKEND_FLAT_XOR_HD, 10, 6, 4, 3)):
@@ -30,6 +94,7 @@ def main():
                 data = payload_bytes(size, size * 3 + ct)
                 rc, dp, pp, flen = E.encode(desc, data)
                 assert rc == 0, ("encode", size, rc)
+                _pause()
                 frags = E.fragments(dp, k, flen) + E.fragments(pp, m, flen)
                 E.lib().liberasurecode_encode_cleanup(desc, dp, pp)
                 want = rs_expected(k, m, data, ct) if be == E.EC_BACKEND_LIBERASURECODE_RS_VAND \
@@ -37,12 +102,13 @@ def main():
                 assert frags == want, ("fragments", be, ct, size)
                 rc, out = E.decode(desc, frags[lost:], flen, force=1)
                 assert rc == 0 and out == data, ("decode", be, ct, size, rc)
+                _pause()
                 rc, rec = E.reconstruct(desc, frags[:k] + frags[k + 1:], flen, k)
                 assert rc == 0 and rec == frags[k], ("reconstruct", be, ct, size, rc)
                 for f in frags:
                     h.update(f)
             assert E.lib().liberasurecode_instance_destroy(desc) == 0
-    print(json.dumps({"ok": True, "digest": h.hexdigest()}))
+    print(json.dumps(dict({"ok": True, "digest": h.hexdigest()}, **_counters())))
 
 
 if __name__ == "__main__":

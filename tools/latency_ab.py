@@ -4,7 +4,7 @@ interleaved rounds -- the copy helpers' batch threshold (ECAMD_COPY_MIN_KIB, def
 and 1 MiB, and the helpers off.  Earlier forms of this tool compared the round-2 host path, the
 recycled buffers and polling the staging streams (profiles/r03_latency_ab1..4.log).
 One JSON line per (setting, round, checksum, size) with the median encode / decode latency.
-usage: latency_ab.py [rounds] [set: copy | zc] [latency_bench.py args]"""
+usage: latency_ab.py [rounds] [set: copy | zc | crc | flag | r06 | server] [latency_bench.py args]"""
 import json
 import os
 import subprocess
@@ -33,6 +33,8 @@ SETS = {
     # round 6, both changes of the per-call path at once against round 5's (inputs by DMA, stream synchronised)
     "r06": {"default": {}, "r05_path": {"ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0", "ECAMD_PERCALL_DONE_FLAG": "0",
                                         "ECAMD_PERCALL_FUSE_CRC": "0"}},
+    # round 6: one-launch calls launched (default) or posted to the resident small server
+    "server": {"default": {}, "server": {"ECAMD_PERCALL_SERVER": "1"}},
 }
 
 
