@@ -278,8 +278,11 @@ __device__ __forceinline__ bool small_crc_epilogue(const SmallArgs& a, const uin
 // self-resetting counter) XORs them: S = r0 of the fragment zero-extended to gridDim * REGION bytes,
 // then r0 = A^-zext S and crc = ~(A^len ~0 ^ r0) with host constants (crc_minv, crc_c).  Bytes past
 // bs are zero in LDS.
+// resident (the server, a request with the previous one's arguments): the tables and checksum image this
+// workgroup staged for it are still in LDS
 template <int W, int G, bool ST, bool CRC, bool SRV = false>
-__device__ __forceinline__ void gf16_small_body(const SmallArgs& a, uint8_t* lds, int bid, int nblk)
+__device__ __forceinline__ void gf16_small_body(const SmallArgs& a, uint8_t* lds, int bid, int nblk,
+                                                bool resident = false)
 {
     static_assert(!CRC || (ST && (G == 2 || G == 4)), "fused CRC: staged inputs, 2- or 4-byte lanes");
     constexpr int D = W / 2;
@@ -343,11 +346,11 @@ __device__ __forceinline__ void gf16_small_body(const SmallArgs& a, uint8_t* lds
                 if (o0 + u * step < bytes) *reinterpret_cast<uint4*>(dst + o0 + u * step) = v[u];
         }
     };
-    stage(lds, a.tables, K * TB);
+    if (!resident) stage(lds, a.tables, K * TB);
     // CRC: the checksum image after the staged inputs and outputs
     uint32_t* const cimg = reinterpret_cast<uint32_t*>(stg + (K + a.nrows) * REGION);
     if constexpr (CRC)
-        if (!(a.crc_dbg & 2))
+        if (!(a.crc_dbg & 2) && !resident)
             stage(reinterpret_cast<uint8_t*>(cimg), reinterpret_cast<const uint8_t*>(a.crc_img), small_crc_words(G) * 4);
     __syncthreads();
     if constexpr (ST)
@@ -513,7 +516,8 @@ __device__ __forceinline__ void xor_tile(const ApplyArgs& a, uint32_t s, int64_t
 // does for inputs in pinned host memory; the completion flag (SmallArgs::done) after the outputs.
 // CRC (with ST): the fused checksums of every input and output (small_crc_epilogue), as gf16_small_kernel.
 template <bool ST, bool CRC, bool SRV = false>
-__device__ __forceinline__ void xor_small_body(const SmallArgs& a, uint8_t* lds, int bid, int nblk)
+__device__ __forceinline__ void xor_small_body(const SmallArgs& a, uint8_t* lds, int bid, int nblk,
+                                               bool resident = false)
 {
     static_assert(!CRC || ST, "fused CRC: staged inputs");
     constexpr int REGION = 256 * 4;
@@ -524,7 +528,7 @@ __device__ __forceinline__ void xor_small_body(const SmallArgs& a, uint8_t* lds,
     if constexpr (ST) {
         small_stage_inputs<CRC>(lds, a, K, c0 * 4, REGION);
         if constexpr (CRC) {
-            const int bytes = small_crc_words(4) * 4, stp = static_cast<int>(blockDim.x) * 16;
+            const int bytes = resident ? 0 : small_crc_words(4) * 4, stp = static_cast<int>(blockDim.x) * 16;
             for (int o = static_cast<int>(threadIdx.x) * 16; o < bytes; o += stp)
                 *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(cimg) + o) =
                     load16(reinterpret_cast<const uint8_t*>(a.crc_img) + o);
@@ -609,18 +613,20 @@ __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int kArgWords = static_cast<int>(sizeof(SmallArgs) / 4);
     __shared__ __attribute__((aligned(16))) uint32_t argw[kArgWords + 4];
-    __shared__ uint32_t cmd[2];
+    __shared__ uint32_t cmd[4];  // post word, go, the request's flag value, its variant
     uint32_t last = sa.post0;
     bool check = sa.dup_check != 0;
+    bool have = false;  // argw (and, for workgroups that took part, the LDS tables) hold the last request's
     const int bid = static_cast<int>(blockIdx.x);
-    uint32_t dbg_args = 0, dbg_body = 0, dbg_n = 0;  // DEBUG (temporary)
     for (;;) {
         if (threadIdx.x == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            uint32_t p = last, go = 0;
-            for (;;) {
-                p = __hip_atomic_load(&sa.box->post, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (p != last) {
+            uint64_t pv = last;
+            uint32_t go = 0;
+            for (;;) {  // the post word and the flag value in one 8-byte load
+                pv = __hip_atomic_load(reinterpret_cast<uint64_t*>(&sa.box->post), __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                if (static_cast<uint32_t>(pv) != last) {
                     go = 1;
                     break;
                 }
@@ -628,55 +634,68 @@ __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs
                 if (__builtin_amdgcn_s_memrealtime() - t0 > sa.idle_ticks) break;
                 __builtin_amdgcn_s_sleep(2);
             }
-            cmd[0] = p;
+            cmd[0] = static_cast<uint32_t>(pv);
             cmd[1] = go;
+            cmd[2] = static_cast<uint32_t>(pv >> 32);
         }
         __syncthreads();
         const uint32_t p = cmd[0];
         if (!cmd[1]) return;
         last = p;
         const int nblk = static_cast<int>(p & 0xffu);
-        const uint64_t tA = __builtin_amdgcn_s_memrealtime();  // DEBUG
-        uint64_t tB = tA;
+        // kSmallServerSame: the host did not rewrite the argument block (the previous request's, but for
+        // the flag value); this workgroup reuses its copy, and its staged tables when it took part
+        const bool reuse = (p & kSmallServerSame) != 0 && have;
         if (bid < nblk) {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(&sa.box->args);
-            for (int i = static_cast<int>(threadIdx.x); i < kArgWords; i += static_cast<int>(blockDim.x))
-                argw[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (threadIdx.x == 0) argw[kArgWords] = __hip_atomic_load(&sa.box->variant, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (!reuse) {
+                // the argument block in 16-byte pieces, one per lane, system-coherent (sc0 | sc1): one PCIe
+                // round trip (past the box's end the buffer unit returns zeros: argw has room for the last piece)
+                static_assert(offsetof(SmallServerBox, args) % 16 == 0, "box layout");
+                const auto rbox = __builtin_amdgcn_make_buffer_rsrc(
+                    sa.box, 0, static_cast<int>(sizeof(SmallServerBox)), 0x00020000);
+                if (threadIdx.x < (sizeof(SmallArgs) + 15) / 16)
+                    *reinterpret_cast<u32x4*>(argw + 4 * threadIdx.x) = __builtin_amdgcn_raw_buffer_load_b128(
+                        rbox, static_cast<int>(offsetof(SmallServerBox, args) + 16 * threadIdx.x), 0, 17);
+                if (threadIdx.x == 0)
+                    cmd[3] = __hip_atomic_load(&sa.box->variant, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) argw[offsetof(SmallArgs, done_val) / 4] = cmd[2];
             __syncthreads();
             const SmallArgs& a = *reinterpret_cast<const SmallArgs*>(argw);
-            const uint32_t v = argw[kArgWords];
-            tB = __builtin_amdgcn_s_memrealtime();  // DEBUG
             bool skip = false;
             if (check && a.done)  // a relaunch: the previous server may have finished this request
                 skip = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.done_val;
-            if (!skip && v == V) {  // (a request of another variant is never posted to this server)
+            if (!skip) {  // the checksum form or not: this kernel's (W, G) or XOR in either (V: its key)
                 constexpr int W = V & 15, G = (V >> 4) & 15;
-                constexpr bool C = ((V >> 8) & 1) != 0;
-                if constexpr ((V & kSmallServerXor) != 0)
-                    xor_small_body<true, C, true>(a, lds, bid, nblk);
-                else
-                    gf16_small_body<W, G, true, C, true>(a, lds, bid, nblk);
+                const bool crc = (cmd[3] & 256u) != 0;
+                if constexpr ((V & kSmallServerXor) != 0) {
+                    if (crc)
+                        xor_small_body<true, true, true>(a, lds, bid, nblk, reuse);
+                    else
+                        xor_small_body<true, false, true>(a, lds, bid, nblk, reuse);
+                } else {
+                    if (crc)
+                        gf16_small_body<W, G, true, true, true>(a, lds, bid, nblk, reuse);
+                    else
+                        gf16_small_body<W, G, true, false, true>(a, lds, bid, nblk, reuse);
+                }
             }
+            have = true;
+        } else {
+            have = false;  // its LDS holds no tables of this request: the next "same" one reloads
         }
         check = false;
         __syncthreads();  // argw, cmd and the LDS are reused by the next request
-        if (bid == 0 && threadIdx.x == 0 && nblk > 0) {  // DEBUG
-            dbg_args += static_cast<uint32_t>(tB - tA);
-            dbg_body += static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() - tB);
-            dbg_n++;
-            __hip_atomic_store(&sa.box->pad[0], dbg_args, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&sa.box->pad[1], dbg_body, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&sa.box->pad[2], dbg_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
     }
 }
-#define SRV_(W, G, C) template __global__ void small_server_kernel<(W) | ((G) << 4) | ((C) << 8)>(const SmallServerArgs);
-SRV_(2, 2, 0) SRV_(4, 2, 0) SRV_(8, 2, 0) SRV_(2, 4, 0) SRV_(4, 4, 0) SRV_(8, 4, 0)
-SRV_(2, 2, 1) SRV_(4, 2, 1) SRV_(8, 2, 1) SRV_(2, 4, 1) SRV_(4, 4, 1) SRV_(8, 4, 1)
-#undef SRV_
+template __global__ void small_server_kernel<2 | (2 << 4)>(const SmallServerArgs);
+template __global__ void small_server_kernel<4 | (2 << 4)>(const SmallServerArgs);
+template __global__ void small_server_kernel<8 | (2 << 4)>(const SmallServerArgs);
+template __global__ void small_server_kernel<2 | (4 << 4)>(const SmallServerArgs);
+template __global__ void small_server_kernel<4 | (4 << 4)>(const SmallServerArgs);
+template __global__ void small_server_kernel<8 | (4 << 4)>(const SmallServerArgs);
 template __global__ void small_server_kernel<kSmallServerXor>(const SmallServerArgs);
-template __global__ void small_server_kernel<kSmallServerXor | (1u << 8)>(const SmallServerArgs);
 
 template <int W, bool PTRS>
 __global__ void __launch_bounds__(256) xor_apply_kernel(const ApplyArgs a)

@@ -381,21 +381,12 @@ const bool g_done_flag = [] {
     const char* env = std::getenv("ECAMD_PERCALL_DONE_FLAG");
     return !(env && std::strcmp(env, "0") == 0);
 }();
-// ECAMD_PERCALL_SERVER=1: post one-launch calls to the resident small server (ecamd_done_flag_arm_server)
-// instead of launching their small kernel (off by default: DESIGN.md §6, profiles/r06_lat_server.json)
+// ECAMD_PERCALL_SERVER=0: launch every small kernel instead of posting one-launch calls to the resident
+// small server (ecamd_done_flag_arm_server; DESIGN.md §6, profiles/r06_lat_server.json)
 const bool g_server = [] {
     const char* env = std::getenv("ECAMD_PERCALL_SERVER");
-    return env && std::strcmp(env, "1") == 0;
+    return !(env && std::strcmp(env, "0") == 0);
 }();
-struct Trace {  // DEBUG
-    double launch = 0, wait = 0;
-    long n = 0;
-    ~Trace()
-    {
-        if (std::getenv("ECAMD_SRV_TRACE") && n)
-            std::fprintf(stderr, "srv-trace host: launch %.2f us wait %.2f us over %ld\n", launch / n, wait / n, n);
-    }
-} g_trace;
 constexpr int kDonePollUs = 200;  // then block in hipStreamSynchronize (a busy GPU, or a fault)
 
 // Polls the flag word for `value` (the GPU writes it to pinned host memory); false after kDonePollUs.
@@ -464,15 +455,12 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
     auto drain = [&](int s) -> int {
         if (pending[s] < 0) return 0;
         int r = 0;
-        const auto tw0 = std::chrono::steady_clock::now();  // DEBUG
         if (served[s]) {
             const uint32_t* fw = done_word(st->slot[s].h_pin, st->cap);
             if (!poll_done(fw, flag_val[s])) r = ecamd_small_server_wait(fw, flag_val[s]);
         } else if (!(flagged[s] && poll_done(done_word(st->slot[s].h_pin, st->cap), flag_val[s]))) {
             r = wait_stream(st->slot[s].stream, chunk * nfr >= kSpinMinBytes);
         }
-        g_trace.wait += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw0).count();
-        g_trace.n++;
         flagged[s] = served[s] = false;
         if (r) return r;
         const int64_t off = pending[s] * chunk;
@@ -552,11 +540,9 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
             const int srv = g_server && zc_in && rc == 0 ? (want_crc ? 2 : 1) : 0;
             ecamd_done_flag_arm_server(done_word(sl.h_pin, st->cap), flag_val[s], srv);
         }
-        const auto tl0 = std::chrono::steady_clock::now();  // DEBUG
         if (rc == 0)
             rc = launch(ctx, win, work, chunk, n, sl.stream, crc_pass_ok && nchunks == 1 ? d_crc : nullptr,
                         t_crc.legacy, &fused);
-        g_trace.launch += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tl0).count();
         // the flag ends the call only when nothing follows the codec launch on the stream: a separate
         // CRC pass (want_crc, not fused) does
         if (arm) {

@@ -5,8 +5,8 @@ everywhere: ZEROCOPY_IN_KIB 0), inputs AND outputs by DMA (mode 0 / ZEROCOPY_KIB
 writing its outputs to device memory while reading the slab (mode 1: the CRC pass then copies the
 inputs to the device slab), inputs packed through the PCIe BAR (ECAMD_PERCALL_BAR_KIB), and the
 checksum pass unfused (ECAMD_PERCALL_FUSE_CRC 0), the stream synchronized instead of the kernel's
-completion flag polled (ECAMD_PERCALL_DONE_FLAG 0), one-launch calls posted to the resident small server
-instead of launched (ECAMD_PERCALL_SERVER 1), and the server exiting between calls (a 50 us idle time and
+completion flag polled (ECAMD_PERCALL_DONE_FLAG 0), one-launch calls launched instead of posted to the
+resident small server (ECAMD_PERCALL_SERVER 0), and the server exiting between calls (a 50 us idle time and
 a 1 ms pause after each call) -- RS(10,4) encode / decode / reconstruct at 4 KiB, 64 KiB and 1 MiB with
 CHKSUM_NONE and CRC32, byte-exact against the restated framing, and every setting's output digest equal to
 the default's.  Plus concurrent callers: 4 threads (a server each) and 12 (more than the library's 8
@@ -31,9 +31,8 @@ SETTINGS = {
     "bar_64k": {"ECAMD_PERCALL_BAR_KIB": "64", "ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0"},
     "crc_unfused": {"ECAMD_PERCALL_FUSE_CRC": "0"},
     "stream_sync": {"ECAMD_PERCALL_DONE_FLAG": "0"},
-    "server": {"ECAMD_PERCALL_SERVER": "1"},
-    "server_idle_exit": {"ECAMD_PERCALL_SERVER": "1", "ECAMD_PERCALL_SERVER_IDLE_US": "50",
-                         "PERCALL_SLEEP_US": "1000"},
+    "server_off": {"ECAMD_PERCALL_SERVER": "0"},
+    "server_idle_exit": {"ECAMD_PERCALL_SERVER_IDLE_US": "50", "PERCALL_SLEEP_US": "1000"},
 }
 
 
@@ -48,28 +47,22 @@ def _run(env_extra):
 @pytest.fixture(scope="module")
 def default_run():
     out = _run({})
-    assert out["posts"] == 0, out  # the server is off by default
+    assert out["posts"] > 0 and out["server_launches"] >= 1, out  # the server served the one-launch calls
     return out
 
 
-@pytest.fixture(scope="module")
-def server_posts():
-    out = _run(SETTINGS["server"])
-    assert out["posts"] > 0 and out["server_launches"] >= 1, out  # the server served the small calls
-    return out["posts"]
-
-
 @pytest.mark.parametrize("name", [n for n in SETTINGS if n != "default"])
-def test_percall_setting_byte_exact(name, default_run, server_posts):
+def test_percall_setting_byte_exact(name, default_run):
     out = _run(SETTINGS[name])
     assert out["ok"] and out["digest"] == default_run["digest"], (name, out)
     if name == "server_idle_exit":  # the server exits between calls: launched again for (nearly) every one
-        assert out["posts"] == server_posts and out["server_launches"] > out["posts"] // 2, out
-    elif name != "server":
-        assert out["posts"] == 0, (name, out)
+        assert out["posts"] == default_run["posts"] and out["server_launches"] > out["posts"] // 2, out
+    elif name in ("server_off", "stream_sync", "zerocopy_off", "zerocopy_mode0", "zerocopy_mode1", "inputs_by_dma",
+                  "bar_64k"):
+        assert out["posts"] == 0, (name, out)  # no call met the server's conditions
 
 
 @pytest.mark.parametrize("threads", [4, 12])
 def test_percall_threads(threads):
-    out = _run({"PERCALL_THREADS": str(threads), "ECAMD_PERCALL_SERVER": "1"})
+    out = _run({"PERCALL_THREADS": str(threads)})
     assert out["ok"] and out["posts"] > 0, out

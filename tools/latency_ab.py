@@ -33,8 +33,8 @@ SETS = {
     # round 6, both changes of the per-call path at once against round 5's (inputs by DMA, stream synchronised)
     "r06": {"default": {}, "r05_path": {"ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0", "ECAMD_PERCALL_DONE_FLAG": "0",
                                         "ECAMD_PERCALL_FUSE_CRC": "0"}},
-    # round 6: one-launch calls launched (default) or posted to the resident small server
-    "server": {"default": {}, "server": {"ECAMD_PERCALL_SERVER": "1"}},
+    # round 6: one-launch calls posted to the resident small server (default) or launched
+    "server": {"default": {}, "launch": {"ECAMD_PERCALL_SERVER": "0"}},
 }
 
 

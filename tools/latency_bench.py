@@ -31,7 +31,7 @@ def pct(xs, q):
 BACKEND = {"rs": None, "xor": None}  # set in main: (backend id, k, m, hd)
 
 
-def measure(codec, reps):
+def measure(codec, reps, repeat=False):
     import ec_api
     be, k, m, hd = BACKEND["cur"]
     out = []
@@ -42,7 +42,25 @@ def measure(codec, reps):
             data = os.urandom(size)
             n = reps if size <= (4 << 20) else max(8, reps // 3)
             enc, dec = [], []
-            for it in range(n + 3):
+            if repeat:  # one operation repeated (a caller encoding, or decoding, object after object)
+                for it in range(n + 3):
+                    t0 = time.perf_counter()
+                    rc, d, p, flen = ec_api.encode(desc, data)
+                    t1 = time.perf_counter()
+                    assert rc == 0
+                    frags = ec_api.fragments(d, k, flen) + ec_api.fragments(p, m, flen)
+                    ec_api.lib().liberasurecode_encode_cleanup(desc, d, p)
+                    if it >= 3:
+                        enc.append(t1 - t0)
+                avail = frags[min(m, hd - 1 if hd else m):]
+                for it in range(n + 3):
+                    t1b = time.perf_counter()
+                    rc, got = ec_api.decode(desc, avail, flen)
+                    t2 = time.perf_counter()
+                    assert rc == 0 and got == data
+                    if it >= 3:
+                        dec.append(t2 - t1b)
+            for it in range(0 if repeat else n + 3):
                 t0 = time.perf_counter()
                 rc, d, p, flen = ec_api.encode(desc, data)
                 t1 = time.perf_counter()
@@ -57,7 +75,7 @@ def measure(codec, reps):
                 if it >= 3:  # first calls: pool / map set-up
                     enc.append(t1 - t0)
                     dec.append(t2 - t1b)  # includes the ctypes copy-out of the decoded object
-            rec = {"codec": codec, "ct": ct, "size": size, "calls": n}
+            rec = {"codec": codec, "ct": ct, "size": size, "calls": n, "order": "repeat" if repeat else "alternate"}
             for name, xs in (("encode", enc), ("decode_4lost", dec)):
                 med = statistics.median(xs)
                 rec[f"{name}_us"] = round(med * 1e6, 1)
@@ -88,6 +106,8 @@ def main():
     ap.add_argument("--max-size", type=int, default=0, help="skip object sizes above this (0: all)")
     ap.add_argument("--backend", default="rs", choices=["rs", "xor"],
                     help="rs: liberasurecode_rs_vand (10, 4); xor: flat_xor_hd (10, 6, 4), hd - 1 = 3 data lost")
+    ap.add_argument("--repeat", action="store_true",
+                    help="time N encodes in a row, then N decodes (default: encode and decode alternate)")
     args = ap.parse_args()
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ec_api
@@ -96,19 +116,20 @@ def main():
     if args.max_size:
         SIZES[:] = [x for x in SIZES if x <= args.max_size]
     if args.codec in ("own", "ref"):
-        measure(args.codec, args.reps)
+        measure(args.codec, args.reps, args.repeat)
         return
     ref_dir = os.path.join(ROOT, "oracle", "_ref")
     env = dict(os.environ, LD_LIBRARY_PATH=ref_dir + (":" + os.environ["LD_LIBRARY_PATH"]
                                                       if os.environ.get("LD_LIBRARY_PATH") else ""))
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--codec", "ref", "--reps",
-                        str(args.reps), "--backend", args.backend, "--max-size", str(args.max_size)], env=env,
+                        str(args.reps), "--backend", args.backend, "--max-size", str(args.max_size)] +
+                       (["--repeat"] if args.repeat else []), env=env,
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-2000:]
     ref = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     for x in ref:
         print(json.dumps(x), flush=True)
-    own = measure("own", args.reps)
+    own = measure("own", args.reps, args.repeat)
     print(json.dumps({"summary": "per-call crossover (1 thread, RS 10+4): largest object size where "
                                  "the reference CPU codec is faster than the GPU drop-in",
                       "encode_crossover_bytes": crossover(own, ref, "encode"),
