@@ -718,8 +718,11 @@ struct SmallServer {
     uint32_t key = 0;  // of the launched kernel: W | G << 4, or kSmallServerXor
     uint32_t post = 0, prev = 0, seq = 0;
     bool running = false;
-    bool have_args = false;  // the box holds the argument block of the last post (this server instance)
-    SmallArgs last_args{};
+    bool have_args[2] = {false, false};  // box slot i holds last_args[i] (this server instance)
+    SmallArgs last_args[2]{};
+    uint32_t last_variant[2] = {0, 0};
+    uint32_t gen[2] = {0, 0};  // slot generations (8 bits in the post word)
+    int last_slot = 0;
     std::chrono::steady_clock::time_point last{};
 };
 constexpr size_t kServerScratchWords = 64 + 16 + 64 * kSmallServerWgs;  // partials: 16 + (K + R) * workgroups
@@ -849,21 +852,31 @@ int server_post(SmallArgs& s, uint32_t variant, unsigned nblk, size_t lds, bool 
         const int rc = server_launch(sv, key, sv->post, false);
         if (rc) return rc;
     }
-    // the previous request's arguments but for the flag value (the common case: one caller repeating one
-    // operation on one size): the box is not rewritten and the server keeps its copy and staged tables
-    SmallArgs cmp = s;
-    cmp.done_val = sv->last_args.done_val;
-    const bool same = !launch && sv->have_args && sv->box->variant == variant &&
-                      std::memcmp(&cmp, &sv->last_args, sizeof(SmallArgs)) == 0;
-    if (!same) {
-        std::memcpy(&sv->box->args, &s, sizeof(SmallArgs));
-        sv->box->variant = variant;
+    // a cached request's arguments but for the flag value (the common case: one caller repeating one
+    // operation, or alternating two, on one size): the slot is not rewritten and the server keeps its copy
+    // (and its staged tables when they are that slot's)
+    if (launch) sv->have_args[0] = sv->have_args[1] = false;  // (a new instance holds no block: new generations)
+    int slot = -1;
+    for (int i = 0; i < 2 && slot < 0; i++) {
+        if (!sv->have_args[i] || sv->last_variant[i] != variant) continue;
+        SmallArgs cmp = s;
+        cmp.done_val = sv->last_args[i].done_val;
+        if (std::memcmp(&cmp, &sv->last_args[i], sizeof(SmallArgs)) == 0) slot = i;
     }
-    sv->last_args = s;
-    sv->have_args = true;
-    sv->seq = sv->seq % 0x7fffffu + 1u;
+    const bool same = slot >= 0;
+    if (!same) {  // the slot not used last
+        slot = sv->last_slot ^ 1;
+        std::memcpy(&sv->box->slot[slot].args, &s, sizeof(SmallArgs));
+        sv->box->variant[slot] = variant;
+        sv->last_args[slot] = s;
+        sv->last_variant[slot] = variant;
+        sv->have_args[slot] = true;
+        sv->gen[slot] = (sv->gen[slot] + 1u) & 0xffu;
+    }
+    sv->last_slot = slot;
+    sv->seq = sv->seq % 0x3fffu + 1u;
     sv->prev = sv->post;
-    sv->post = (sv->seq << 9) | (same ? kSmallServerSame : 0u) | nblk;
+    sv->post = (sv->seq << 18) | (sv->gen[slot] << 10) | (slot ? kSmallServerSlot : 0u) | nblk;
     __atomic_store_n(&sv->box->done_val, s.done_val, __ATOMIC_RELAXED);
     __atomic_store_n(&sv->box->post, sv->post, __ATOMIC_RELEASE);  // after the rest (x86: stores in order)
     sv->last = now;

@@ -611,12 +611,14 @@ template <uint32_t V>
 __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs sa)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    constexpr int kArgWords = static_cast<int>(sizeof(SmallArgs) / 4);
-    __shared__ __attribute__((aligned(16))) uint32_t argw[kArgWords + 4];
-    __shared__ uint32_t cmd[4];  // post word, go, the request's flag value, its variant
+    constexpr int kArgWords = static_cast<int>(sizeof(SmallServerSlot) / 4);
+    __shared__ __attribute__((aligned(16))) uint32_t argw[2][kArgWords];
+    __shared__ uint32_t varw[2];
+    __shared__ uint32_t cmd[3];  // post word, go, the request's flag value
     uint32_t last = sa.post0;
     bool check = sa.dup_check != 0;
-    bool have = false;  // argw (and, for workgroups that took part, the LDS tables) hold the last request's
+    int have[2] = {-1, -1};  // the generation of slot i's block argw[i] holds (-1: none)
+    int tab = -1;            // slot << 8 | generation whose tables (and checksum image) this workgroup's LDS holds
     const int bid = static_cast<int>(blockIdx.x);
     for (;;) {
         if (threadIdx.x == 0) {
@@ -643,47 +645,50 @@ __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs
         if (!cmd[1]) return;
         last = p;
         const int nblk = static_cast<int>(p & 0xffu);
-        // kSmallServerSame: the host did not rewrite the argument block (the previous request's, but for
-        // the flag value); this workgroup reuses its copy, and its staged tables when it took part
-        const bool reuse = (p & kSmallServerSame) != 0 && have;
+        const int sl = (p & kSmallServerSlot) ? 1 : 0;
+        const int gen = static_cast<int>((p >> 10) & 0xffu);
+        // the host rewrites a slot only with a new generation: a workgroup holding that generation's block
+        // reuses its copy (the flag value aside), and its staged tables when they are that block's -- whatever
+        // posts it may have missed while it polled
+        const bool reuse = have[sl] == gen;
+        const bool resident = reuse && tab == (sl << 8 | gen);
         if (bid < nblk) {
             if (!reuse) {
-                // the argument block in 16-byte pieces, one per lane, system-coherent (sc0 | sc1): one PCIe
-                // round trip (past the box's end the buffer unit returns zeros: argw has room for the last piece)
-                static_assert(offsetof(SmallServerBox, args) % 16 == 0, "box layout");
+                // the argument block in 16-byte pieces, one per lane, system-coherent (sc0 | sc1): one PCIe round trip
+                static_assert(offsetof(SmallServerBox, slot) % 16 == 0 && sizeof(SmallServerSlot) % 16 == 0, "box layout");
                 const auto rbox = __builtin_amdgcn_make_buffer_rsrc(
                     sa.box, 0, static_cast<int>(sizeof(SmallServerBox)), 0x00020000);
-                if (threadIdx.x < (sizeof(SmallArgs) + 15) / 16)
-                    *reinterpret_cast<u32x4*>(argw + 4 * threadIdx.x) = __builtin_amdgcn_raw_buffer_load_b128(
-                        rbox, static_cast<int>(offsetof(SmallServerBox, args) + 16 * threadIdx.x), 0, 17);
+                if (threadIdx.x < sizeof(SmallServerSlot) / 16)
+                    *reinterpret_cast<u32x4*>(argw[sl] + 4 * threadIdx.x) = __builtin_amdgcn_raw_buffer_load_b128(
+                        rbox, static_cast<int>(offsetof(SmallServerBox, slot) + sl * sizeof(SmallServerSlot) + 16 * threadIdx.x),
+                        0, 17);
                 if (threadIdx.x == 0)
-                    cmd[3] = __hip_atomic_load(&sa.box->variant, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    varw[sl] = __hip_atomic_load(&sa.box->variant[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             __syncthreads();
-            if (threadIdx.x == 0) argw[offsetof(SmallArgs, done_val) / 4] = cmd[2];
+            if (threadIdx.x == 0) argw[sl][offsetof(SmallArgs, done_val) / 4] = cmd[2];
             __syncthreads();
-            const SmallArgs& a = *reinterpret_cast<const SmallArgs*>(argw);
+            const SmallArgs& a = *reinterpret_cast<const SmallArgs*>(argw[sl]);
             bool skip = false;
             if (check && a.done)  // a relaunch: the previous server may have finished this request
                 skip = __hip_atomic_load(a.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == a.done_val;
             if (!skip) {  // the checksum form or not: this kernel's (W, G) or XOR in either (V: its key)
                 constexpr int W = V & 15, G = (V >> 4) & 15;
-                const bool crc = (cmd[3] & 256u) != 0;
+                const bool crc = (varw[sl] & 256u) != 0;
                 if constexpr ((V & kSmallServerXor) != 0) {
                     if (crc)
-                        xor_small_body<true, true, true>(a, lds, bid, nblk, reuse);
+                        xor_small_body<true, true, true>(a, lds, bid, nblk, resident);
                     else
-                        xor_small_body<true, false, true>(a, lds, bid, nblk, reuse);
+                        xor_small_body<true, false, true>(a, lds, bid, nblk, resident);
                 } else {
                     if (crc)
-                        gf16_small_body<W, G, true, true, true>(a, lds, bid, nblk, reuse);
+                        gf16_small_body<W, G, true, true, true>(a, lds, bid, nblk, resident);
                     else
-                        gf16_small_body<W, G, true, false, true>(a, lds, bid, nblk, reuse);
+                        gf16_small_body<W, G, true, false, true>(a, lds, bid, nblk, resident);
                 }
+                tab = sl << 8 | gen;
             }
-            have = true;
-        } else {
-            have = false;  // its LDS holds no tables of this request: the next "same" one reloads
+            have[sl] = gen;
         }
         check = false;
         __syncthreads();  // argw, cmd and the LDS are reused by the next request

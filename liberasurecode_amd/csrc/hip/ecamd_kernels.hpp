@@ -82,13 +82,16 @@ struct SmallArgs {
 // The resident small server (small_server_kernel): the per-call path's small launches posted to a
 // mailbox in coherent pinned host memory instead of launched -- one per caller thread, kSmallServerWgs
 // workgroups polling it until idle_ticks of the 100 MHz constant clock pass without a request.
+struct alignas(16) SmallServerSlot {
+    SmallArgs args;
+};
 struct alignas(16) SmallServerBox {
-    uint32_t post;      // (sequence << 9) | kSmallServerSame | workgroups of the request, stored last by the host
-    uint32_t done_val;  // the request's completion-flag value (read with post, one 8-byte load)
-    uint32_t stop;      // host: every workgroup exits at its next poll
-    uint32_t variant;   // kSmallServerXor | CRC << 8 | G << 4 | W (gf16_small_body / xor_small_body)
-    uint32_t pad[12];
-    SmallArgs args;     // the request's argument block (its scratch the server's own)
+    uint32_t post;        // sequence << 18 | slot generation << 10 | slot << 9 | workgroups, stored last by the host
+    uint32_t done_val;    // the request's completion-flag value (read with post, one 8-byte load)
+    uint32_t stop;        // host: every workgroup exits at its next poll
+    uint32_t variant[2];  // per slot: kSmallServerXor | CRC << 8 | G << 4 | W (gf16_small_body / xor_small_body)
+    uint32_t pad[11];
+    SmallServerSlot slot[2];  // two argument blocks (an encode and a decode alternating both stay cached)
 };
 struct SmallServerArgs {
     SmallServerBox* box;
@@ -98,7 +101,7 @@ struct SmallServerArgs {
 };
 constexpr int kSmallServerWgs = 16;
 constexpr uint32_t kSmallServerXor = 1u << 12;
-constexpr uint32_t kSmallServerSame = 1u << 8;  // post word: the argument block is the previous request's
+constexpr uint32_t kSmallServerSlot = 1u << 9;  // post word: argument slot 1 (else 0); bits 10-17 its generation
 template <uint32_t V>  // V: W | G << 4, or kSmallServerXor (each with and without the fused checksum)
 __global__ void small_server_kernel(const SmallServerArgs sa);
 
