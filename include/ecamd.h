@@ -133,6 +133,8 @@ int ecamd_small_server_wait(const uint32_t *flag, uint32_t value);
  * switches, relaunches in ecamd_small_server_wait), in this process (tests pin which path ran). */
 long long ecamd_small_server_posts(void);
 long long ecamd_small_server_launches(void);
+/* Posts that wrote a new argument block into one of the server's two slots (the others reused a cached one). */
+long long ecamd_small_server_rewrites(void);
 
 /* Pointer tables in device memory: input j of stripe s is d_in_ptrs[s*in_row + in_col[j]],
  * output r is d_out_ptrs[s*out_row + out_col[r]] (in_col / out_col are host arrays). */

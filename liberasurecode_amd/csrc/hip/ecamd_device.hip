@@ -728,9 +728,10 @@ struct SmallServer {
 constexpr size_t kServerScratchWords = 64 + 16 + 64 * kSmallServerWgs;  // partials: 16 + (K + R) * workgroups
 constexpr int kMaxSmallServers = 8;
 constexpr size_t kServerLds = kLdsBytes - 1024;  // the server's dynamic LDS (its static share is < 1 KiB)
+static_assert(2 * static_cast<size_t>(kSmallServerLdsHalf) <= kServerLds, "two table placements");
 std::mutex g_srv_mu;
 auto& g_srv_free = *new std::vector<SmallServer*>();  // idle servers of exited threads (never freed)
-std::atomic<long long> g_srv_posts{0}, g_srv_launches{0};
+std::atomic<long long> g_srv_posts{0}, g_srv_launches{0}, g_srv_rewrites{0};
 int g_srv_count = 0;
 
 // ECAMD_PERCALL_SERVER_IDLE_US: how long a server polls without a request (default 2000 us)
@@ -872,11 +873,13 @@ int server_post(SmallArgs& s, uint32_t variant, unsigned nblk, size_t lds, bool 
         sv->last_variant[slot] = variant;
         sv->have_args[slot] = true;
         sv->gen[slot] = (sv->gen[slot] + 1u) & 0xffu;
+        g_srv_rewrites.fetch_add(1, std::memory_order_relaxed);
     }
     sv->last_slot = slot;
     sv->seq = sv->seq % 0x3fffu + 1u;
     sv->prev = sv->post;
-    sv->post = (sv->seq << 18) | (sv->gen[slot] << 10) | (slot ? kSmallServerSlot : 0u) | nblk;
+    sv->post = (sv->seq << 18) | (sv->gen[slot] << 10) | (slot ? kSmallServerSlot : 0u) |
+               (lds <= static_cast<size_t>(kSmallServerLdsHalf) ? kSmallServerHalf : 0u) | nblk;
     __atomic_store_n(&sv->box->done_val, s.done_val, __ATOMIC_RELAXED);
     __atomic_store_n(&sv->box->post, sv->post, __ATOMIC_RELEASE);  // after the rest (x86: stores in order)
     sv->last = now;
@@ -3110,6 +3113,7 @@ int ecamd_done_flag_taken(void)
 
 long long ecamd_small_server_posts(void) { return g_srv_posts.load(std::memory_order_relaxed); }
 long long ecamd_small_server_launches(void) { return g_srv_launches.load(std::memory_order_relaxed); }
+long long ecamd_small_server_rewrites(void) { return g_srv_rewrites.load(std::memory_order_relaxed); }
 
 int ecamd_small_server_wait(const uint32_t* flag, uint32_t value)
 {

@@ -618,7 +618,10 @@ __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs
     uint32_t last = sa.post0;
     bool check = sa.dup_check != 0;
     int have[2] = {-1, -1};  // the generation of slot i's block argw[i] holds (-1: none)
-    int tab = -1;            // slot << 8 | generation whose tables (and checksum image) this workgroup's LDS holds
+    // per slot: the generation whose tables (and checksum image) this workgroup's LDS holds where that slot's
+    // requests run (-1: none), and whether they run at 0 over more than half the LDS (not kSmallServerHalf)
+    int tab[2] = {-1, -1};
+    bool whole[2] = {false, false};
     const int bid = static_cast<int>(blockIdx.x);
     for (;;) {
         if (threadIdx.x == 0) {
@@ -651,7 +654,9 @@ __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs
         // reuses its copy (the flag value aside), and its staged tables when they are that block's -- whatever
         // posts it may have missed while it polled
         const bool reuse = have[sl] == gen;
-        const bool resident = reuse && tab == (sl << 8 | gen);
+        const bool half = (p & kSmallServerHalf) != 0;
+        const bool resident = reuse && tab[sl] == gen;
+        uint8_t* const base = half ? lds + sl * kSmallServerLdsHalf : lds;
         if (bid < nblk) {
             if (!reuse) {
                 // the argument block in 16-byte pieces, one per lane, system-coherent (sc0 | sc1): one PCIe round trip
@@ -677,18 +682,26 @@ __global__ void __launch_bounds__(256) small_server_kernel(const SmallServerArgs
                 const bool crc = (varw[sl] & 256u) != 0;
                 if constexpr ((V & kSmallServerXor) != 0) {
                     if (crc)
-                        xor_small_body<true, true, true>(a, lds, bid, nblk, resident);
+                        xor_small_body<true, true, true>(a, base, bid, nblk, resident);
                     else
-                        xor_small_body<true, false, true>(a, lds, bid, nblk, resident);
+                        xor_small_body<true, false, true>(a, base, bid, nblk, resident);
                 } else {
                     if (crc)
-                        gf16_small_body<W, G, true, true, true>(a, lds, bid, nblk, resident);
+                        gf16_small_body<W, G, true, true, true>(a, base, bid, nblk, resident);
                     else
-                        gf16_small_body<W, G, true, false, true>(a, lds, bid, nblk, resident);
+                        gf16_small_body<W, G, true, false, true>(a, base, bid, nblk, resident);
                 }
-                tab = sl << 8 | gen;
+                // a half request overlaps the other slot's tables only when those run at 0 over more than half;
+                // a whole one may overlap them wherever they are
+                if (!half || whole[sl ^ 1]) tab[sl ^ 1] = -1;
+                tab[sl] = gen;
+                whole[sl] = !half;
             }
             have[sl] = gen;
+        } else if (!reuse) {
+            // a rewrite of slot sl this workgroup sits out: its copy is stale from here on (the 8-bit
+            // generation would otherwise match again after 256 rewrites it did not take part in)
+            have[sl] = -1;
         }
         check = false;
         __syncthreads();  // argw, cmd and the LDS are reused by the next request

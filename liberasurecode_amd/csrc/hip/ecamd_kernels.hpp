@@ -86,7 +86,7 @@ struct alignas(16) SmallServerSlot {
     SmallArgs args;
 };
 struct alignas(16) SmallServerBox {
-    uint32_t post;        // sequence << 18 | slot generation << 10 | slot << 9 | workgroups, stored last by the host
+    uint32_t post;        // sequence << 18 | slot generation << 10 | slot << 9 | half << 8 | workgroups, stored last
     uint32_t done_val;    // the request's completion-flag value (read with post, one 8-byte load)
     uint32_t stop;        // host: every workgroup exits at its next poll
     uint32_t variant[2];  // per slot: kSmallServerXor | CRC << 8 | G << 4 | W (gf16_small_body / xor_small_body)
@@ -102,6 +102,10 @@ struct SmallServerArgs {
 constexpr int kSmallServerWgs = 16;
 constexpr uint32_t kSmallServerXor = 1u << 12;
 constexpr uint32_t kSmallServerSlot = 1u << 9;  // post word: argument slot 1 (else 0); bits 10-17 its generation
+// post word: the request's LDS (tables, staging, checksum image) fits in kSmallServerLdsHalf bytes, and it runs
+// at slot * kSmallServerLdsHalf: an encode and a decode alternating both keep their staged tables
+constexpr uint32_t kSmallServerHalf = 1u << 8;
+constexpr int kSmallServerLdsHalf = 79 * 1024;
 template <uint32_t V>  // V: W | G << 4, or kSmallServerXor (each with and without the fused checksum)
 __global__ void small_server_kernel(const SmallServerArgs sa);
 

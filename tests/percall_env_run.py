@@ -81,9 +81,68 @@ def threads_main(n):
     print(json.dumps(dict({"ok": True, "threads": n}, **_counters())))
 
 
+def churn_main():
+    """PERCALL_CHURN=1: the server's cached argument slots and table placements under churn (one thread, one
+    kernel key: W = 4 outputs, 4-byte lanes).  (1) Two large RS(10,4) encodes (6 workgroups), then N one-
+    workgroup encodes of distinct sizes (every one rewrites a slot; N around 512 brings both slots' 8-bit
+    generations back round to the large calls'), then a third large encode -- the workgroups that sat out
+    the small calls must not reuse the large calls' arguments.  (2) RS(10,4) encode and decode alternating
+    (each slot's tables in its half of the LDS), and RS(10,4) encode alternating with an RS(20,8) decode of 4
+    lost data fragments (20 inputs: tables over half the LDS, placed at 0).  Every output checked."""
+    k, m = 10, 4
+    ct = E.CHKSUM_NONE
+    desc = E.create(E.EC_BACKEND_LIBERASURECODE_RS_VAND, k, m, hd=m, ct=ct)
+    desc20 = E.create(E.EC_BACKEND_LIBERASURECODE_RS_VAND, 20, 8, hd=8, ct=ct)
+    assert desc > 0 and desc20 > 0
+    cache = {}
+
+    def enc(d, kk, mm, size):
+        if (kk, size) not in cache:
+            data = payload_bytes(size, size * 7 + kk)
+            cache[(kk, size)] = (data, rs_expected(kk, mm, data, ct))
+        data, want = cache[(kk, size)]
+        rc, dp, pp, flen = E.encode(d, data)
+        assert rc == 0, ("encode", kk, size, rc)
+        frags = E.fragments(dp, kk, flen) + E.fragments(pp, mm, flen)
+        E.lib().liberasurecode_encode_cleanup(d, dp, pp)
+        assert frags == want, ("fragments", kk, size)
+        return data, frags, flen
+
+    def dec(d, data, frags, flen, lost):
+        rc, out = E.decode(d, frags[lost:], flen, force=1)
+        assert rc == 0 and out == data, ("decode", len(data), rc)
+
+    before = _counters()["posts"]
+    small = [k * bs for bs in range(514, 1025, 2)]  # fragments of 514..1024 bytes: one workgroup of 4-byte lanes
+    large = [k * (6000 + 2 * j) for j in range(16)]  # ~6 KiB fragments: 6 workgroups
+    calls = 0
+    for rep, n in enumerate((510, 511, 512, 513, 514)):
+        enc(desc, k, m, large[3 * rep])
+        enc(desc, k, m, large[3 * rep + 1])
+        for i in range(n):
+            enc(desc, k, m, small[i % len(small)])
+        enc(desc, k, m, large[3 * rep + 2])
+        calls += n + 3
+    for size in (k * 700, k * 3000):
+        data, frags, flen = enc(desc, k, m, size)
+        data20, frags20, flen20 = enc(desc20, 20, 8, 2 * size)
+        for _ in range(50):
+            enc(desc, k, m, size)
+            dec(desc, data, frags, flen, 4)
+            enc(desc, k, m, size)
+            dec(desc20, data20, frags20, flen20, 4)
+            calls += 4
+    for d in (desc, desc20):
+        assert E.lib().liberasurecode_instance_destroy(d) == 0
+    out = _counters()
+    print(json.dumps(dict({"ok": True, "calls": calls, "posted": out["posts"] - before}, **out)))
+
+
 def main():
     if os.environ.get("PERCALL_THREADS"):
         return threads_main(int(os.environ["PERCALL_THREADS"]))
+    if os.environ.get("PERCALL_CHURN"):
+        return churn_main()
     h = hashlib.sha256()
     # liberasurecode_rs_vand (10, 4) and flat_xor_hd (10, 6, 4): 4 / 3 data fragments lost
     for be, k, m, hd, lost in ((E.EC_BACKEND_LIBERASURECODE_RS_VAND, 10, 4, 4, 4), (E.EC_BACKEND_FLAT_XOR_HD, 10, 6, 4, 3)):

@@ -66,3 +66,12 @@ def test_percall_setting_byte_exact(name, default_run):
 def test_percall_threads(threads):
     out = _run({"PERCALL_THREADS": str(threads)})
     assert out["ok"] and out["posts"] > 0, out
+
+
+def test_percall_server_slot_churn():
+    """The server's two argument slots and LDS table placements under churn (percall_env_run.churn_main):
+    workgroups that sat out 510-514 rewrites keep no stale arguments; alternating operations keep their
+    tables apart; every output byte-exact, most calls served."""
+    out = _run({"PERCALL_CHURN": "1"})
+    assert out["ok"] and out["posted"] > out["calls"] // 2, out
+
