@@ -31,7 +31,8 @@ def _counters():
     from liberasurecode_amd import _lib
     d = _lib.dev()
     out = {}
-    for key, name in (("posts", "ecamd_small_server_posts"), ("server_launches", "ecamd_small_server_launches")):
+    for key, name in (("posts", "ecamd_small_server_posts"), ("server_launches", "ecamd_small_server_launches"),
+                      ("rewrites", "ecamd_small_server_rewrites")):
         fn = getattr(d, name)
         fn.restype = C.c_longlong
         out[key] = fn()
@@ -123,8 +124,16 @@ def churn_main():
             enc(desc, k, m, small[i % len(small)])
         enc(desc, k, m, large[3 * rep + 2])
         calls += n + 3
+    alt_rewrites = []
     for size in (k * 700, k * 3000):
         data, frags, flen = enc(desc, k, m, size)
+        dec(desc, data, frags, flen, 4)
+        r0 = _counters()["rewrites"]
+        for _ in range(50):  # both argument blocks stay cached in the two slots
+            enc(desc, k, m, size)
+            dec(desc, data, frags, flen, 4)
+            calls += 2
+        alt_rewrites.append(_counters()["rewrites"] - r0)
         data20, frags20, flen20 = enc(desc20, 20, 8, 2 * size)
         for _ in range(50):
             enc(desc, k, m, size)
@@ -135,7 +144,8 @@ def churn_main():
     for d in (desc, desc20):
         assert E.lib().liberasurecode_instance_destroy(d) == 0
     out = _counters()
-    print(json.dumps(dict({"ok": True, "calls": calls, "posted": out["posts"] - before}, **out)))
+    print(json.dumps(dict({"ok": True, "calls": calls, "posted": out["posts"] - before,
+                           "alternating_rewrites": alt_rewrites}, **out)))
 
 
 def main():

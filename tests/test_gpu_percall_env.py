@@ -74,4 +74,7 @@ def test_percall_server_slot_churn():
     tables apart; every output byte-exact, most calls served."""
     out = _run({"PERCALL_CHURN": "1"})
     assert out["ok"] and out["posted"] > out["calls"] // 2, out
+    # 50 alternating encode / decode pairs of one size: no slot rewritten once both blocks are cached (a
+    # server idle exit in between, a stall past 2 ms, costs one rewrite of each; one slot would give 100)
+    assert all(r <= 4 for r in out["alternating_rewrites"]), out
 
