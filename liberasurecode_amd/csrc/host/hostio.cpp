@@ -18,6 +18,8 @@
 #include <mutex>
 #include <vector>
 
+#include <zlib.h>
+
 #include "crc.hpp"
 #include "ecamd.h"
 #include "ecamd_host.h"
@@ -387,6 +389,11 @@ const bool g_server = [] {
     const char* env = std::getenv("ECAMD_PERCALL_SERVER");
     return !(env && std::strcmp(env, "0") == 0);
 }();
+// ECAMD_PERCALL_OVERLAP_CRC=0: leave a small call's input CRC32s to the frontend, after the call (A/B switch)
+const bool g_overlap_crc = [] {
+    const char* env = std::getenv("ECAMD_PERCALL_OVERLAP_CRC");
+    return !(env && std::strcmp(env, "0") == 0);
+}();
 constexpr int kDonePollUs = 200;  // then block in hipStreamSynchronize (a busy GPU, or a fault)
 
 // Polls the flag word for `value` (the GPU writes it to pinned host memory); false after kDonePollUs.
@@ -563,15 +570,41 @@ int run_chunked(int dev, int K, int R, const char* const* in, char* const* out, 
         }
         pending[s] = c;
     }
+    // below crc_pass_ok's size the frontend checksums the fragments with zlib after the call: the inputs'
+    // CRC32s are taken here instead, while the kernel runs (the caller's buffers, which the call only
+    // reads), and reach write_checksum through ecamd_percall_crc_lookup; the outputs' stay the frontend's
+    std::vector<uint32_t> in_crc;
+    if (rc == 0 && crc_armed && !want_crc && !t_crc.legacy && g_overlap_crc) {
+        in_crc.resize(static_cast<size_t>(K));
+        for (int j = 0; j < K; j++)
+            in_crc[j] = static_cast<uint32_t>(::crc32(0, reinterpret_cast<const Bytef*>(in[j]), static_cast<uInt>(bs)));
+    }
     for (int s = 0; s < 2; s++) {
         int r = drain(s);
         if (rc == 0) rc = r;
     }
     release(st);
+    // the outputs' bytes changed: drop what was recorded for them (an earlier call's input, or an output
+    // that is also an input: flat XOR applies in place)
+    auto overlaps_out = [&](const void* p, int64_t len) {
+        const char* a = static_cast<const char*>(p);
+        for (int o = 0; o < R; o++)
+            if (a < out[o] + bs && out[o] < a + len) return true;
+        return false;
+    };
+    if (crc_armed) {
+        auto& e = t_crc.entries;
+        e.erase(std::remove_if(e.begin(), e.end(), [&](const auto& x) { return overlaps_out(x.ptr, x.len); }),
+                e.end());
+    }
     if (rc == 0 && want_crc) {  // outputs after inputs: a lookup takes the latest entry
-        for (int j = 0; j < K; j++) t_crc.entries.push_back({in[j], bs, crc[j]});
+        for (int j = 0; j < K; j++)
+            if (!overlaps_out(in[j], bs)) t_crc.entries.push_back({in[j], bs, crc[j]});
         for (int o = 0; o < R; o++) t_crc.entries.push_back({out[o], bs, crc[K + o]});
     }
+    if (rc == 0 && !in_crc.empty())
+        for (int j = 0; j < K; j++)
+            if (!overlaps_out(in[j], bs)) t_crc.entries.push_back({in[j], bs, in_crc[j]});
     return rc;
 }
 

@@ -168,7 +168,9 @@ def main():
                 E.lib().liberasurecode_encode_cleanup(desc, dp, pp)
                 want = rs_expected(k, m, data, ct) if be == E.EC_BACKEND_LIBERASURECODE_RS_VAND \
                     else xor_expected(k, m, hd, data, ct)
-                assert frags == want, ("fragments", be, ct, size)
+                assert frags == want, ("fragments", be, ct, size,
+                                       [(i, [o for o in range(len(f)) if f[o] != w[o]][:8])
+                                        for i, (f, w) in enumerate(zip(frags, want)) if f != w])
                 rc, out = E.decode(desc, frags[lost:], flen, force=1)
                 assert rc == 0 and out == data, ("decode", be, ct, size, rc)
                 _pause()

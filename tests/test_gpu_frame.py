@@ -348,7 +348,7 @@ def test_percall_crc_handoff(F, bs, legacy, fuse):
     """ecamd_percall_crc_*: while armed, the per-call host path checksums every input and output
     fragment on the GPU (chunk CRCs combined on the host); each equals zlib / the legacy CRC of
     the final bytes.  This is what liberasurecode.so.1 stamps into the headers.  From 16 KiB of
-    fragments (the host's zlib below); fragments of at most 64 KiB fold the checksums into the
+    fragments (below, the inputs' zlib CRC32s are taken on the host during the call); fragments of at most 64 KiB fold the checksums into the
     small-launch codec kernel (ecamd_map_apply_strided_crc); with that off (fuse "0", run in a child:
     ECAMD_PERCALL_FUSE_CRC is read once) the separate ecamd_crc32 pass serves them."""
     if fuse == "0":
@@ -379,11 +379,13 @@ def _crc_handoff(bs, legacy, fused):
     d.ecamd_percall_crc_arm(legacy)
     try:
         assert d.ecamd_host_map_apply(_lib.ints(rows), m, k, inp, out, bs) == 0
-        for buf in data + parity:
+        big = bs * (k + m) >= 16 << 10
+        for i, buf in enumerate(data + parity):
             c = C.c_uint32()
             found = d.ecamd_percall_crc_lookup(buf.ctypes.data, bs, C.byref(c)) == 0
-            # below 16 KiB of fragments the host computes the CRCs (no GPU entry recorded)
-            assert found == (bs * (k + m) >= 16 << 10)
+            # below 16 KiB of fragments no GPU checksum: the inputs' zlib CRC32s are taken on the host while
+            # the kernel runs (not the legacy CRC), the outputs' are left to the caller
+            assert found == (big or (i < k and not legacy)), (i, bs, legacy)
             if found:
                 assert c.value == O.crc32(buf, legacy=bool(legacy))
         c = C.c_uint32()

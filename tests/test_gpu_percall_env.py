@@ -4,7 +4,8 @@ pinned slab for every size (ECAMD_PERCALL_ZEROCOPY_MODE 3) or only its outputs (
 everywhere: ZEROCOPY_IN_KIB 0), inputs AND outputs by DMA (mode 0 / ZEROCOPY_KIB 0), the kernel
 writing its outputs to device memory while reading the slab (mode 1: the CRC pass then copies the
 inputs to the device slab), inputs packed through the PCIe BAR (ECAMD_PERCALL_BAR_KIB), and the
-checksum pass unfused (ECAMD_PERCALL_FUSE_CRC 0), the stream synchronized instead of the kernel's
+checksum pass unfused (ECAMD_PERCALL_FUSE_CRC 0), a small call's input CRC32s left to the frontend
+(ECAMD_PERCALL_OVERLAP_CRC 0), the stream synchronized instead of the kernel's
 completion flag polled (ECAMD_PERCALL_DONE_FLAG 0), one-launch calls launched instead of posted to the
 resident small server (ECAMD_PERCALL_SERVER 0), and the server exiting between calls (a 50 us idle time and
 a 1 ms pause after each call) -- RS(10,4) encode / decode / reconstruct at 4 KiB, 64 KiB and 1 MiB with
@@ -30,6 +31,7 @@ SETTINGS = {
     "zerocopy_off": {"ECAMD_PERCALL_ZEROCOPY_KIB": "0"},
     "bar_64k": {"ECAMD_PERCALL_BAR_KIB": "64", "ECAMD_PERCALL_ZEROCOPY_IN_KIB": "0"},
     "crc_unfused": {"ECAMD_PERCALL_FUSE_CRC": "0"},
+    "crc_overlap_off": {"ECAMD_PERCALL_OVERLAP_CRC": "0"},
     "stream_sync": {"ECAMD_PERCALL_DONE_FLAG": "0"},
     "server_off": {"ECAMD_PERCALL_SERVER": "0"},
     "server_idle_exit": {"ECAMD_PERCALL_SERVER_IDLE_US": "50", "PERCALL_SLEEP_US": "1000"},

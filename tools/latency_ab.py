@@ -4,7 +4,7 @@ interleaved rounds -- the copy helpers' batch threshold (ECAMD_COPY_MIN_KIB, def
 and 1 MiB, and the helpers off.  Earlier forms of this tool compared the round-2 host path, the
 recycled buffers and polling the staging streams (profiles/r03_latency_ab1..4.log).
 One JSON line per (setting, round, checksum, size) with the median encode / decode latency.
-usage: latency_ab.py [rounds] [set: copy | zc | crc | flag | r06 | server] [latency_bench.py args]"""
+usage: latency_ab.py [rounds] [set: copy | zc | crc | flag | r06 | server | ocrc] [latency_bench.py args]"""
 import json
 import os
 import subprocess
@@ -35,6 +35,8 @@ SETS = {
                                         "ECAMD_PERCALL_FUSE_CRC": "0"}},
     # round 6: one-launch calls posted to the resident small server (default) or launched
     "server": {"default": {}, "launch": {"ECAMD_PERCALL_SERVER": "0"}},
+    # round 6: a small CRC32 call's input checksums taken on the host while the kernel runs (default)
+    "ocrc": {"default": {}, "no_overlap": {"ECAMD_PERCALL_OVERLAP_CRC": "0"}},
 }
 
 
